@@ -1,0 +1,77 @@
+"""ctypes binding of libavsr_hip.so (the C-ABI declared in include/avsr_hip.h).
+
+The product path has no fallback: if the library is missing or fails to load, every op
+raises. `torch` is imported first so that the HIP runtime torch ships (same SONAME
+libamdhip64.so.7) is the one the library binds to — one runtime per process.
+"""
+import ctypes
+import os
+
+import torch  # noqa: F401  (must precede the library load: shared HIP runtime)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libavsr_hip.so")
+
+AVSR_F32, AVSR_BF16 = 0, 1
+ACT_NONE, ACT_GELU, ACT_RELU = 0, 1, 2
+
+_c_p = ctypes.c_void_p
+_i64 = ctypes.c_int64
+_f = ctypes.c_float
+_i = ctypes.c_int
+
+
+class GemmParams(ctypes.Structure):
+    _fields_ = [
+        ("M", _i), ("N", _i), ("K", _i), ("batch", _i),
+        ("dtype", _i), ("a_kmajor", _i), ("b_kmajor", _i), ("c_f32", _i),
+        ("A", _c_p), ("lda", _i64), ("strideA", _i64),
+        ("B", _c_p), ("ldb", _i64), ("strideB", _i64),
+        ("C", _c_p), ("ldc", _i64), ("strideC", _i64),
+        ("alpha", _f), ("beta", _f),
+        ("bias", _c_p),
+        ("act", _i), ("epi_bwd", _i),
+        ("preact", _c_p),
+        ("res", _c_p), ("ldr", _i64), ("strideR", _i64),
+        ("gate", _c_p),
+        ("drop_p", _f),
+        ("seed", ctypes.c_uint64),
+    ]
+
+
+# (symbol name, params struct or None for custom signature)
+SYMBOLS = {
+    "avsr_version": ([], ctypes.c_char_p),
+    "avsr_gemm": ([ctypes.POINTER(GemmParams), _c_p], _i),
+}
+
+_lib = None
+
+
+class AvsrLibError(RuntimeError):
+    pass
+
+
+def load():
+    """Load the library (raises AvsrLibError if it is missing: no fallback path)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise AvsrLibError(f"{LIB_PATH} not built: run `python -c 'import __graft_entry__ as g; g.build()'`")
+    lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+    for name, (argtypes, restype) in SYMBOLS.items():
+        fn = getattr(lib, name)
+        fn.argtypes = argtypes
+        fn.restype = restype
+    _lib = lib
+    return lib
+
+
+def check(rc, op):
+    if rc != 0:
+        raise AvsrLibError(f"{op} failed with code {rc}")
+
+
+def stream_ptr(device=None):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)

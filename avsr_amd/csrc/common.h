@@ -1,0 +1,89 @@
+// Shared device helpers for the gfx950 kernels of libavsr_hip.so.
+// Wave = 64 lanes everywhere; bf16 is clang's __bf16 (same bits as torch.bfloat16).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "avsr_hip.h"
+
+typedef __bf16 bf16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+#define AVSR_DEV __device__ __forceinline__
+
+AVSR_DEV float to_f(float x) { return x; }
+AVSR_DEV float to_f(bf16 x) { return (float)x; }
+template <typename T> AVSR_DEV T from_f(float x);
+template <> AVSR_DEV float from_f<float>(float x) { return x; }
+template <> AVSR_DEV bf16 from_f<bf16>(float x) { return (bf16)x; }
+
+// 16-byte vector of T (8 bf16 or 4 f32)
+struct alignas(16) v16 { uint32_t w[4]; };
+
+AVSR_DEV float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+AVSR_DEV float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// ---- counter-based dropout stream: keep(seed, idx) with P(keep) = 1 - p ------------
+// A 2-round Philox-style mix of (seed, idx) -> 32-bit uniform. Identical in forward and
+// backward so no mask is ever stored (the backward recomputes it from the index).
+AVSR_DEV uint32_t mix32(uint64_t seed, uint64_t idx) {
+  uint32_t lo = (uint32_t)idx, hi = (uint32_t)(idx >> 32);
+  uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    uint64_t p0 = (uint64_t)lo * 0xD2511F53u;
+    uint64_t p1 = (uint64_t)hi * 0xCD9E8D57u;
+    uint32_t nlo = (uint32_t)(p1 >> 32) ^ k0 ^ (uint32_t)p0;
+    uint32_t nhi = (uint32_t)(p0 >> 32) ^ k1 ^ (uint32_t)p1;
+    lo = nlo; hi = nhi;
+    k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+  }
+  return lo ^ hi;
+}
+AVSR_DEV float drop_scale(float p, uint64_t seed, uint64_t idx) {
+  // returns 0 for dropped, 1/(1-p) for kept
+  uint32_t thr = (uint32_t)(p * 4294967296.0f);
+  return mix32(seed, idx) >= thr ? 1.0f / (1.0f - p) : 0.0f;
+}
+
+AVSR_DEV float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+AVSR_DEV float gelu_erf_grad(float x) {
+  float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752f));
+  float pdf = 0.39894228040143268f * __expf(-0.5f * x * x);
+  return cdf + x * pdf;
+}
+AVSR_DEV float act_fwd(int act, float h) {
+  return act == AVSR_ACT_GELU ? gelu_erf(h) : (act == AVSR_ACT_RELU ? fmaxf(h, 0.f) : h);
+}
+AVSR_DEV float act_bwd(int act, float h) {
+  return act == AVSR_ACT_GELU ? gelu_erf_grad(h) : (act == AVSR_ACT_RELU ? (h > 0.f ? 1.f : 0.f) : 1.f);
+}
+
+// split an fp32 fragment into bf16 hi + lo parts (parity mode: 3 MFMA products)
+AVSR_DEV void split8(const float* x, bf16x8& hi, bf16x8& lo) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    bf16 h = (bf16)x[j];
+    hi[j] = h;
+    lo[j] = (bf16)(x[j] - (float)h);
+  }
+}
+
+AVSR_DEV f32x16 mfma32(const bf16x8& a, const bf16x8& b, const f32x16& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+#define AVSR_CHECK_LAUNCH() do { hipError_t e_ = hipGetLastError(); if (e_ != hipSuccess) return (int)e_; } while (0)
+
+static inline int avsr_aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
