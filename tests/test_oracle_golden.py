@@ -1,0 +1,71 @@
+"""Pin the CPU oracle (oracle/avsr_oracle.py) to the golden vectors the reference itself
+produced (tests/golden/make_golden.py). CPU only."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import avsr_oracle as O
+from tests.oracle_util import golden_batch, golden_state, load_golden, rel, tiny_cfg
+
+
+@pytest.fixture(scope="module")
+def g():
+    return load_golden()
+
+
+def test_encoder_eval(g):
+    torch.set_num_threads(8)
+    sd = O.to_torch_state(golden_state(g))
+    b = golden_batch(g)
+    with torch.no_grad():
+        x = O.encoder_forward(sd, tiny_cfg(), torch.from_numpy(b["audios"]), torch.from_numpy(b["videos"]), None, False)
+    assert rel(x, g["enc_eval"]) < 1e-4
+
+
+@pytest.fixture(scope="module")
+def train_run(g):
+    torch.set_num_threads(8)
+    sd = O.to_torch_state(golden_state(g), requires_grad=True)
+    b = {k: torch.from_numpy(v) for k, v in golden_batch(g).items()}
+    loss, lc, la, acc, ex = O.e2e_forward(sd, tiny_cfg(), b["videos"], b["audios"], b["video_lengths"], b["labels"], True)
+    loss.backward()
+    return sd, (loss, lc, la, acc), ex
+
+
+def test_train_losses(g, train_run):
+    _, (loss, lc, la, acc), ex = train_run
+    ref = g["loss"]
+    assert abs(loss.item() - ref[0]) / abs(ref[0]) < 1e-5
+    assert abs(lc.item() - ref[1]) / abs(ref[1]) < 1e-5
+    assert abs(la.item() - ref[2]) / abs(ref[2]) < 1e-5
+    assert acc == pytest.approx(ref[3])
+    assert rel(ex["enc"].detach(), g["enc_train"]) < 1e-4
+    assert rel(ex["ctc_logits"].detach().transpose(0, 1), g["ctc_logits"]) < 1e-4
+    assert rel(ex["dec_logits"].detach(), g["dec_logits"]) < 1e-4
+
+
+def test_train_grads(g, train_run):
+    sd, _, _ = train_run
+    for k, n, head in zip(g["grad_keys"], g["grad_norm"], g["grad_head"]):
+        gr = sd[k].grad
+        assert gr is not None, k
+        assert torch.isfinite(gr).all(), k
+        assert abs(gr.double().norm().item() - n) <= 1e-4 * abs(n) + 1e-9, k
+        h = gr.flatten()[:8].numpy()
+        np.testing.assert_allclose(h, head[:len(h)], rtol=2e-3, atol=1e-6 * max(1.0, abs(n)))
+
+
+def test_bn_running_stats(g, train_run):
+    sd, _, _ = train_run
+    for k, row in zip(g["bn_keys"], g["bn_after"]):
+        np.testing.assert_allclose(sd[k].detach().flatten()[:8].numpy(), row, rtol=1e-5, atol=1e-6)
+
+
+def test_decoder_one_step(g):
+    sd = O.to_torch_state(golden_state(g))
+    cfg = tiny_cfg()
+    for b in range(2):
+        x = torch.from_numpy(g[f"dec_enc_{b}"])
+        with torch.no_grad():
+            logp = O.decoder_one_step(sd, cfg, torch.tensor([[5048, 5, 17, 301]]), x.unsqueeze(0))
+        assert rel(logp, g[f"onestep_{b}"]) < 1e-5
