@@ -36,6 +36,23 @@ class GemmParams(ctypes.Structure):
         ("gate", _c_p),
         ("drop_p", _f),
         ("seed", ctypes.c_uint64),
+        ("splitk", _i),
+    ]
+
+
+class ConvParams(ctypes.Structure):
+    _fields_ = [
+        ("dtype", _i),
+        ("nimg", _i), ("hin", _i), ("win", _i), ("cin", _i),
+        ("hout", _i), ("wout", _i), ("cout", _i),
+        ("kh", _i), ("kw", _i), ("sh", _i), ("sw", _i), ("ph", _i), ("pw", _i),
+        ("groups", _i),
+        ("ldx", _i64), ("ldy", _i64),
+        ("x", _c_p), ("w", _c_p), ("y", _c_p),
+        ("dx", _c_p), ("dy", _c_p), ("dw", _c_p),
+        ("stats", _c_p),
+        ("alpha", _f), ("beta", _f),
+        ("splitk", _i),
     ]
 
 
@@ -43,6 +60,10 @@ class GemmParams(ctypes.Structure):
 SYMBOLS = {
     "avsr_version": ([], ctypes.c_char_p),
     "avsr_gemm": ([ctypes.POINTER(GemmParams), _c_p], _i),
+    "avsr_conv_fwd": ([ctypes.POINTER(ConvParams), _c_p], _i),
+    "avsr_conv_bwd_data": ([ctypes.POINTER(ConvParams), _c_p], _i),
+    "avsr_conv_bwd_weight": ([ctypes.POINTER(ConvParams), _c_p], _i),
+    "avsr_conv_stat_tiles": ([ctypes.POINTER(ConvParams)], _i),
 }
 
 _lib = None

@@ -1,0 +1,426 @@
+// Shared MFMA GEMM core for libavsr_hip.so (dense GEMM and implicit-GEMM convolution).
+//
+// Block tile (64*WM) x (64*WN) x 32, 256 threads = 4 waves laid out WM x WN, each wave a
+// 64x64 sub-tile = 2x2 v_mfma_f32_32x32x16_bf16 accumulators (fp32). Operands are staged
+// global -> registers -> LDS, double-buffered with one barrier per K-tile: the next tile's
+// global loads are issued before the current tile's MFMAs. LDS rows are padded by one
+// 16-byte vector (conflict-free ds_read_b128 fragment reads).
+//
+// Operand "loaders" describe how an (R x K) operand view maps to memory:
+//   LdDenseK    elem(r,k) = p[r*ld + k]                     (k contiguous)
+//   LdDenseR    elem(r,k) = p[k*ld + r]                     (r contiguous)
+//   LdConvK     im2col gather of an NHWC activation, k = (kh, kw, c) with c contiguous
+//               (conv forward A operand; with TRANSP, the data-grad A operand over dY)
+//   LdConvR     im2col gather, r = (kh, kw, c) contiguous in c, k = output pixel
+//               (conv weight-grad B operand)
+//   LdWgtR      conv weight [cout][kh][kw][cin] viewed as (r = cin, k = (kh, kw, cout))
+//               (conv data-grad B operand)
+// fp32 storage runs the same tiles on bf16 hi/lo splits (3 MFMA products per step).
+#pragma once
+#include "common.h"
+
+namespace gemmcore {
+
+constexpr int BKE = 32, NT = 256;
+
+template <typename T> struct V { static constexpr int VE = 16 / (int)sizeof(T); static constexpr int ROW = BKE + VE; };
+
+// q = n / d for 0 <= n < 2^31 (Granlund-Montgomery round-up multiplier)
+struct FastDiv {
+  uint32_t d, m, s;
+};
+static inline FastDiv make_fastdiv(uint32_t d) {
+  FastDiv f; f.d = d; uint32_t s = 0;
+  while ((1ull << s) < d) ++s;
+  f.s = s;
+  f.m = (uint32_t)(((1ull << 32) * ((1ull << s) - d)) / d + 1);
+  return f;
+}
+AVSR_DEV uint32_t fdiv(uint32_t n, const FastDiv& f) { return (__umulhi(n, f.m) + n) >> f.s; }
+
+AVSR_DEV void zero(v16& v) { v.w[0] = v.w[1] = v.w[2] = v.w[3] = 0u; }
+
+// ---- convolution geometry (one group) ----------------------------------------------
+struct ConvGeom {
+  int nimg, hin, win, hout, wout;   // forward geometry (input x -> output y)
+  int kh, kw, sh, sw, ph, pw;
+  int cin, cout;                    // channels per group
+  int64_t ldx, ldy;                 // pixel strides (total channels) of x and y
+  FastDiv f_hw_out, f_w_out;        // division by hout*wout, wout
+  FastDiv f_hw_in, f_w_in;          // division by hin*win, win
+  FastDiv f_kw;                     // division by kw
+  int cin_shift, cout_shift;        // log2(cin), log2(cout)
+};
+
+// ---------------------------------------------------------------- dense loaders
+template <typename T, int R> struct LdDenseK {
+  static constexpr bool KMAJ = true;
+  static constexpr int VE = V<T>::VE, VPT = R * BKE / VE / NT;
+  const T* p; int64_t ld; int rext, K;
+  AVSR_DEV void init(int, int) {}
+  AVSR_DEV void load(int r0, int k0, v16 (&reg)[VPT], int tid) const {
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) {
+      int v = tid + i * NT, r = v / (BKE / VE), k = k0 + (v % (BKE / VE)) * VE;
+      if (r0 + r < rext && k < K) reg[i] = *(const v16*)(p + (int64_t)(r0 + r) * ld + k);
+      else zero(reg[i]);
+    }
+  }
+};
+
+template <typename T, int R> struct LdDenseR {
+  static constexpr bool KMAJ = false;
+  static constexpr int VE = V<T>::VE, VPT = R * BKE / VE / NT;
+  const T* p; int64_t ld; int rext, K;
+  AVSR_DEV void init(int, int) {}
+  AVSR_DEV void load(int r0, int k0, v16 (&reg)[VPT], int tid) const {
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) {
+      int v = tid + i * NT, kk = v / (R / VE), rr = r0 + (v % (R / VE)) * VE, k = k0 + kk;
+      if (k < K && rr < rext) reg[i] = *(const v16*)(p + (int64_t)k * ld + rr);
+      else zero(reg[i]);
+    }
+  }
+};
+
+// ---------------------------------------------------------------- conv loaders
+// A operand of conv forward (TRANSP=false: r = output pixel of y, gather x) or of conv
+// data-grad (TRANSP=true: r = input pixel of x, gather dy at ((h+ph-kh)/sh, (w+pw-kw)/sw)).
+// k = (kh, kw, c) with c fastest; c runs over cin (forward) or cout (data-grad).
+template <typename T, int R, bool TRANSP> struct LdConvK {
+  static constexpr bool KMAJ = true;
+  static constexpr int VE = V<T>::VE, VPT = R * BKE / VE / NT;
+  const T* p; ConvGeom g; int rext, K;
+  int pn[VPT], ph_[VPT], pw_[VPT];  // per vector: image*pixels base, h origin, w origin (or -1e6 if row invalid)
+  AVSR_DEV void init(int r0, int tid) {
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) {
+      int v = tid + i * NT, r = r0 + v / (BKE / VE);
+      if (r >= rext) { pn[i] = 0; ph_[i] = -1000000; pw_[i] = 0; continue; }
+      if (!TRANSP) {
+        uint32_t n = fdiv(r, g.f_hw_out); uint32_t rem = r - n * g.f_hw_out.d;
+        uint32_t oh = fdiv(rem, g.f_w_out); uint32_t ow = rem - oh * g.f_w_out.d;
+        pn[i] = n * g.hin * g.win; ph_[i] = oh * g.sh - g.ph; pw_[i] = ow * g.sw - g.pw;
+      } else {
+        uint32_t n = fdiv(r, g.f_hw_in); uint32_t rem = r - n * g.f_hw_in.d;
+        uint32_t h = fdiv(rem, g.f_w_in); uint32_t w = rem - h * g.f_w_in.d;
+        pn[i] = n * g.hout * g.wout; ph_[i] = h + g.ph; pw_[i] = w + g.pw;
+      }
+    }
+  }
+  AVSR_DEV void load(int, int k0, v16 (&reg)[VPT], int tid) const {
+    const int cs = TRANSP ? g.cout_shift : g.cin_shift;
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) {
+      int v = tid + i * NT, k = k0 + (v % (BKE / VE)) * VE;
+      int c = k & ((1 << cs) - 1), khw = k >> cs;
+      int kh = fdiv(khw, g.f_kw), kw = khw - kh * g.f_kw.d;
+      bool ok = k < K;
+      int64_t off;
+      if (!TRANSP) {
+        int ih = ph_[i] + kh, iw = pw_[i] + kw;
+        ok = ok && ih >= 0 && ih < g.hin && iw >= 0 && iw < g.win;
+        off = (int64_t)(pn[i] + ih * g.win + iw) * g.ldx + c;
+      } else {
+        int th = ph_[i] - kh, tw = pw_[i] - kw;
+        int oh = th / g.sh, ow = tw / g.sw;
+        ok = ok && th >= 0 && tw >= 0 && oh * g.sh == th && ow * g.sw == tw && oh < g.hout && ow < g.wout;
+        off = (int64_t)(pn[i] + oh * g.wout + ow) * g.ldy + c;
+      }
+      if (ok) reg[i] = *(const v16*)(p + off);
+      else zero(reg[i]);
+    }
+  }
+};
+
+// B operand of conv weight-grad: r = (kh, kw, cin) (vectors along cin), k = output pixel.
+template <typename T, int R> struct LdConvR {
+  static constexpr bool KMAJ = false;
+  static constexpr int VE = V<T>::VE, VPT = R * BKE / VE / NT;
+  const T* p; ConvGeom g; int rext, K;
+  int rk[VPT], rw[VPT], rc[VPT];   // per vector: kh, kw, c (kh = -1e6 if r invalid)
+  AVSR_DEV void init(int r0, int tid) {
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) {
+      int v = tid + i * NT, r = r0 + (v % (R / VE)) * VE;
+      if (r >= rext) { rk[i] = -1000000; rw[i] = 0; rc[i] = 0; continue; }
+      int c = r & ((1 << g.cin_shift) - 1), khw = r >> g.cin_shift;
+      int kh = fdiv(khw, g.f_kw);
+      rk[i] = kh; rw[i] = khw - kh * g.f_kw.d; rc[i] = c;
+    }
+  }
+  AVSR_DEV void load(int, int k0, v16 (&reg)[VPT], int tid) const {
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) {
+      int v = tid + i * NT, k = k0 + v / (R / VE);
+      bool ok = k < K;
+      uint32_t kk = ok ? k : 0;
+      uint32_t n = fdiv(kk, g.f_hw_out); uint32_t rem = kk - n * g.f_hw_out.d;
+      uint32_t oh = fdiv(rem, g.f_w_out); uint32_t ow = rem - oh * g.f_w_out.d;
+      int ih = (int)oh * g.sh - g.ph + rk[i], iw = (int)ow * g.sw - g.pw + rw[i];
+      ok = ok && ih >= 0 && ih < g.hin && iw >= 0 && iw < g.win;
+      if (ok) reg[i] = *(const v16*)(p + (int64_t)(n * g.hin * g.win + ih * g.win + iw) * g.ldx + rc[i]);
+      else zero(reg[i]);
+    }
+  }
+};
+
+// B operand of conv data-grad: weight stored [cout][kh][kw][cin] (one group), viewed as
+// (r = cin, k = (kh, kw, cout) with cout fastest).
+template <typename T, int R> struct LdWgtR {
+  static constexpr bool KMAJ = false;
+  static constexpr int VE = V<T>::VE, VPT = R * BKE / VE / NT;
+  const T* p; ConvGeom g; int rext, K;
+  AVSR_DEV void init(int, int) {}
+  AVSR_DEV void load(int r0, int k0, v16 (&reg)[VPT], int tid) const {
+    const int ktot = g.kh * g.kw * g.cin;
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) {
+      int v = tid + i * NT, k = k0 + v / (R / VE), rr = r0 + (v % (R / VE)) * VE;
+      int co = k & ((1 << g.cout_shift) - 1), khw = k >> g.cout_shift;
+      if (k < K && rr < rext) reg[i] = *(const v16*)(p + (int64_t)co * ktot + khw * g.cin + rr);
+      else zero(reg[i]);
+    }
+  }
+};
+
+// ---------------------------------------------------------------- LDS staging
+template <typename T, int R, bool KMAJ, int VPT>
+AVSR_DEV void lstore(T* lds, const v16 (&reg)[VPT], int tid) {
+  constexpr int VE = V<T>::VE, ROW = V<T>::ROW;
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    int v = tid + i * NT;
+    if constexpr (KMAJ) {
+      int r = v / (BKE / VE), kv = v % (BKE / VE);
+      *(v16*)(lds + r * ROW + kv * VE) = reg[i];
+    } else {
+      int kk = v / (R / VE), rv = v % (R / VE);
+      const T* vals = (const T*)&reg[i];
+#pragma unroll
+      for (int e = 0; e < VE; ++e) lds[(rv * VE + e) * ROW + kk] = vals[e];
+    }
+  }
+}
+
+template <typename T>
+AVSR_DEV void frag(const T* lds, int rb, int s, int lane, bf16x8& hi, bf16x8& lo) {
+  constexpr int ROW = V<T>::ROW;
+  const T* p = lds + (rb + (lane & 31)) * ROW + s * 16 + 8 * (lane >> 5);
+  if constexpr (sizeof(T) == 2) {
+    hi = *(const bf16x8*)p;
+  } else {
+    f32x4 x0 = *(const f32x4*)p, x1 = *(const f32x4*)(p + 4);
+    float x[8] = {x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
+    split8(x, hi, lo);
+  }
+}
+
+template <typename T, int WM, int WN> struct Tile {
+  static constexpr int BM = 64 * WM, BN = 64 * WN;
+  static constexpr int ML_BYTES = 2 * (BM + BN) * V<T>::ROW * (int)sizeof(T);
+  static constexpr int EP_BYTES = (BM / 2) * (BN + 4) * 4;
+  static constexpr int LDS_BYTES = ML_BYTES > EP_BYTES ? ML_BYTES : EP_BYTES;
+};
+
+// Main loop over K-tiles [kbeg, kend): acc[i][j] is the wave's 2x2 block of 32x32 tiles.
+template <typename T, int WM, int WN, class LA, class LB>
+AVSR_DEV void mainloop(LA& la, LB& lb, int m0, int n0, int kbeg, int kend, f32x16 (&acc)[2][2], char* smem) {
+  using TL = Tile<T, WM, WN>;
+  constexpr int ROW = V<T>::ROW;
+  T* lA = (T*)smem;
+  T* lB = lA + 2 * TL::BM * ROW;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  if (kbeg >= kend) return;
+  la.init(m0, tid);
+  lb.init(n0, tid);
+  v16 ra[LA::VPT], rb[LB::VPT];
+  const int nk = (kend - kbeg + BKE - 1) / BKE;
+  la.load(m0, kbeg, ra, tid);
+  lb.load(n0, kbeg, rb, tid);
+  lstore<T, TL::BM, LA::KMAJ>(lA, ra, tid);
+  lstore<T, TL::BN, LB::KMAJ>(lB, rb, tid);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    const bool more = kt + 1 < nk;
+    if (more) {
+      la.load(m0, kbeg + (kt + 1) * BKE, ra, tid);
+      lb.load(n0, kbeg + (kt + 1) * BKE, rb, tid);
+    }
+    const T* cA = lA + cur * TL::BM * ROW;
+    const T* cB = lB + cur * TL::BN * ROW;
+#pragma unroll
+    for (int s = 0; s < BKE / 16; ++s) {
+      bf16x8 ah[2], al[2], bh[2], bl[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) frag<T>(cA, wm * 64 + i * 32, s, lane, ah[i], al[i]);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) frag<T>(cB, wn * 64 + j * 32, s, lane, bh[j], bl[j]);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          acc[i][j] = mfma32(ah[i], bh[j], acc[i][j]);
+          if constexpr (sizeof(T) == 4) {
+            acc[i][j] = mfma32(ah[i], bl[j], acc[i][j]);
+            acc[i][j] = mfma32(al[i], bh[j], acc[i][j]);
+          }
+        }
+    }
+    if (more) {
+      lstore<T, TL::BM, LA::KMAJ>(lA + (cur ^ 1) * TL::BM * ROW, ra, tid);
+      lstore<T, TL::BN, LB::KMAJ>(lB + (cur ^ 1) * TL::BN * ROW, rb, tid);
+    }
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------- epilogue
+struct Epi {
+  int M, N;
+  void* C; int64_t ldc;
+  float alpha, beta;
+  const float* bias;
+  int act, bwd, atomic;
+  void* preact;
+  const void* res; int64_t ldr;
+  const void* gate;
+  float drop_p; uint64_t seed; uint64_t drop_base;
+  float* stats;        // BN partials: [m_tile][N][3] = (count, mean, M2) of the stored values
+};
+
+// row/col of accumulator register r of tile (i, j)
+AVSR_DEV int acc_row(int wm, int i, int r, int lane) { return wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5); }
+AVSR_DEV int acc_col(int wn, int j, int lane) { return wn * 64 + j * 32 + (lane & 31); }
+
+// apply the elementwise epilogue to NE consecutive columns [col, col+NE) of one row
+template <typename T, typename OutT, int NE>
+AVSR_DEV void epi_elems(const Epi& e, int row, int col, const float* v_in) {
+  OutT* C = (OutT*)e.C;
+  const T* R = (const T*)e.res;
+  T* P = (T*)e.preact;
+  const T* G = (const T*)e.gate;
+  const int64_t off = (int64_t)row * e.ldc + col;
+  if (e.atomic) {
+#pragma unroll
+    for (int q = 0; q < NE; ++q)
+      if (col + q < e.N) atomicAdd((float*)C + off + q, e.alpha * v_in[q]);
+    return;
+  }
+#pragma unroll
+  for (int q = 0; q < NE; ++q) {
+    if (col + q >= e.N) break;
+    float v = e.alpha * v_in[q];
+    const uint64_t didx = e.drop_base + (uint64_t)row * (uint64_t)e.N + col + q;
+    if (!e.bwd) {
+      if (e.bias) v += e.bias[col + q];
+      if (P) P[off + q] = from_f<T>(v);
+      v = act_fwd(e.act, v);
+      if (e.drop_p > 0.f) v *= drop_scale(e.drop_p, e.seed, didx);
+      if (R) v += to_f(R[(int64_t)row * e.ldr + col + q]);
+    } else {
+      if (e.drop_p > 0.f) v *= drop_scale(e.drop_p, e.seed, didx);
+      if (G) v *= act_bwd(e.act, to_f(G[off + q]));
+    }
+    if (e.beta != 0.f) v += e.beta * to_f(C[off + q]);
+    C[off + q] = from_f<OutT>(v);
+  }
+}
+
+// Epilogue: (1) optional BN statistics straight from the accumulators; (2) the tile is
+// staged through LDS in two halves (BM/2 rows each) and written row-major, 4 consecutive
+// columns per thread (coalesced stores, vector residual/gate reads).
+template <typename T, typename OutT, int WM, int WN>
+AVSR_DEV void epilogue(const Epi& e, int m0, int n0, f32x16 (&acc)[2][2], char* smem) {
+  constexpr int BM = 64 * WM, BN = 64 * WN, HR = BM / 2, LDR = BN + 4;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  float* st = (float*)smem;
+  if (e.stats) {
+    // per column: count / mean / M2 of alpha*acc over the tile's valid rows (the stored conv
+    // output: no bias / activation on this path), merged across waves with Chan's formula
+    __syncthreads();
+    float* red = st;  // [WM][BN][3]
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      float s = 0.f, c = 0.f;
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const bool ok = m0 + acc_row(wm, i, r, lane) < e.M;
+          s += ok ? e.alpha * acc[i][j][r] : 0.f;
+          c += ok ? 1.f : 0.f;
+        }
+      s += __shfl_xor(s, 32, 64);
+      c += __shfl_xor(c, 32, 64);
+      const float mean = c > 0.f ? s / c : 0.f;
+      float m2 = 0.f;
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const bool ok = m0 + acc_row(wm, i, r, lane) < e.M;
+          const float d = e.alpha * acc[i][j][r] - mean;
+          m2 += ok ? d * d : 0.f;
+        }
+      m2 += __shfl_xor(m2, 32, 64);
+      if (lane < 32) {
+        const int lc = acc_col(wn, j, lane);
+        red[(wm * BN + lc) * 3 + 0] = c;
+        red[(wm * BN + lc) * 3 + 1] = mean;
+        red[(wm * BN + lc) * 3 + 2] = m2;
+      }
+    }
+    __syncthreads();
+    for (int lc = tid; lc < BN; lc += NT) {
+      const int col = n0 + lc;
+      if (col < e.N) {
+        float n = 0.f, mean = 0.f, m2 = 0.f;
+        for (int w = 0; w < WM; ++w) {
+          const float nb = red[(w * BN + lc) * 3 + 0], mb = red[(w * BN + lc) * 3 + 1], qb = red[(w * BN + lc) * 3 + 2];
+          if (nb > 0.f) {
+            const float nn = n + nb, d = mb - mean;
+            mean += d * nb / nn;
+            m2 += qb + d * d * n * nb / nn;
+            n = nn;
+          }
+        }
+        float* o = e.stats + ((int64_t)(m0 / BM) * e.N + col) * 3;
+        o[0] = n; o[1] = mean; o[2] = m2;
+      }
+    }
+  }
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int lr = wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        st[lr * LDR + wn * 64 + j * 32 + (lane & 31)] = acc[half][j][r];
+      }
+    __syncthreads();
+    for (int c = tid; c < HR * BN / 4; c += NT) {
+      const int lr = c / (BN / 4), lc = (c % (BN / 4)) * 4;
+      const int row = m0 + (lr >> 5) * 64 + half * 32 + (lr & 31);
+      const int col = n0 + lc;
+      if (row < e.M && col < e.N) {
+        const f32x4 v4 = *(const f32x4*)(st + lr * LDR + lc);
+        const float v[4] = {v4[0], v4[1], v4[2], v4[3]};
+        epi_elems<T, OutT, 4>(e, row, col, v);
+      }
+    }
+  }
+}
+
+}  // namespace gemmcore

@@ -25,7 +25,8 @@ def _ptr(t):
 
 def gemm(A, B, C, *, M, N, K, a_kmajor, b_kmajor, lda, ldb, ldc, batch=1,
          strideA=0, strideB=0, strideC=0, alpha=1.0, beta=0.0, bias=None, act=L.ACT_NONE,
-         epi_bwd=False, preact=None, res=None, ldr=None, strideR=0, gate=None, drop_p=0.0, seed=0):
+         epi_bwd=False, preact=None, res=None, ldr=None, strideR=0, gate=None, drop_p=0.0, seed=0,
+         splitk=1):
     """Raw GEMM launch: C[b,m,n] = epi(alpha * sum_k A(b,m,k) B(b,n,k)). See avsr_hip.h."""
     lib = L.load()
     assert A.is_cuda and B.is_cuda and C.is_cuda
@@ -54,6 +55,7 @@ def gemm(A, B, C, *, M, N, K, a_kmajor, b_kmajor, lda, ldb, ldc, batch=1,
     p.strideR = strideR
     p.gate = None if gate is None else gate.data_ptr()
     p.drop_p, p.seed = float(drop_p), int(seed) & 0xFFFFFFFFFFFFFFFF
+    p.splitk = int(splitk)
     L.check(lib.avsr_gemm(ctypes.byref(p), L.stream_ptr()), "avsr_gemm")
     return C
 
@@ -94,3 +96,75 @@ def linear_wgrad(dy, x, dW, *, beta=0.0):
     gemm(dy, x, dW, M=N, N=K, K=M, a_kmajor=False, b_kmajor=False, lda=dy.stride(0), ldb=x.stride(0),
          ldc=dW.stride(0), beta=beta)
     return dW
+
+
+# ---------------------------------------------------------------------------------------
+# Implicit-GEMM convolution (NHWC activations, weights [cout][kh][kw][cin])
+# ---------------------------------------------------------------------------------------
+
+class ConvGeom:
+    """Geometry of one (grouped) 2-D convolution over NHWC tensors."""
+
+    def __init__(self, nimg, hin, win, cin, cout, kh, kw, stride=(1, 1), pad=(0, 0), groups=1,
+                 hout=None, wout=None, ldx=None, ldy=None):
+        self.nimg, self.hin, self.win, self.cin, self.cout = nimg, hin, win, cin, cout
+        self.kh, self.kw = kh, kw
+        self.sh, self.sw = stride
+        self.ph, self.pw = pad
+        self.groups = groups
+        self.hout = hout if hout is not None else (hin + 2 * self.ph - kh) // self.sh + 1
+        self.wout = wout if wout is not None else (win + 2 * self.pw - kw) // self.sw + 1
+        self.ldx = ldx if ldx is not None else groups * cin
+        self.ldy = ldy if ldy is not None else groups * cout
+
+    def params(self, dtype):
+        p = L.ConvParams()
+        p.dtype = dtype
+        p.nimg, p.hin, p.win, p.cin = self.nimg, self.hin, self.win, self.cin
+        p.hout, p.wout, p.cout = self.hout, self.wout, self.cout
+        p.kh, p.kw, p.sh, p.sw, p.ph, p.pw = self.kh, self.kw, self.sh, self.sw, self.ph, self.pw
+        p.groups, p.ldx, p.ldy = self.groups, self.ldx, self.ldy
+        p.alpha, p.beta = 1.0, 0.0
+        return p
+
+    @property
+    def out_pixels(self):
+        return self.nimg * self.hout * self.wout
+
+    @property
+    def in_pixels(self):
+        return self.nimg * self.hin * self.win
+
+
+def conv_stat_tiles(g, dtype=L.AVSR_BF16):
+    p = g.params(dtype)
+    return L.load().avsr_conv_stat_tiles(ctypes.byref(p))
+
+
+def conv_fwd(g, x, w, y, stats=None):
+    """y[pix, co] = conv(x, w); stats: fp32 [tiles, cout, 3] BN partials (groups == 1)."""
+    p = g.params(dtype_code(x))
+    assert x.dtype == w.dtype == y.dtype and x.is_cuda
+    p.x, p.w, p.y = x.data_ptr(), w.data_ptr(), y.data_ptr()
+    p.stats = None if stats is None else stats.data_ptr()
+    L.check(L.load().avsr_conv_fwd(ctypes.byref(p), L.stream_ptr()), "avsr_conv_fwd")
+    return y
+
+
+def conv_bwd_data(g, dy, w, dx, alpha=1.0, beta=0.0):
+    p = g.params(dtype_code(dy))
+    assert dy.dtype == w.dtype == dx.dtype
+    p.dy, p.w, p.dx = dy.data_ptr(), w.data_ptr(), dx.data_ptr()
+    p.alpha, p.beta = alpha, beta
+    L.check(L.load().avsr_conv_bwd_data(ctypes.byref(p), L.stream_ptr()), "avsr_conv_bwd_data")
+    return dx
+
+
+def conv_bwd_weight(g, x, dy, dw, splitk=0):
+    """dw (fp32, [groups*cout, kh, kw, cin]) += wgrad(x, dy)."""
+    p = g.params(dtype_code(x))
+    assert x.dtype == dy.dtype and dw.dtype == torch.float32
+    p.x, p.dy, p.dw = x.data_ptr(), dy.data_ptr(), dw.data_ptr()
+    p.splitk = splitk
+    L.check(L.load().avsr_conv_bwd_weight(ctypes.byref(p), L.stream_ptr()), "avsr_conv_bwd_weight")
+    return dw

@@ -68,9 +68,45 @@ typedef struct {
   const void* gate;          /* backward: pre-activation h (dtype, ld = ldc) or NULL */
   float drop_p;              /* dropout probability (0 = off) */
   uint64_t seed;             /* counter-based dropout stream id */
+  int splitk;                /* >1: K split over blocks, C (fp32) += alpha*acc by atomics */
 } avsr_gemm_params;
 
 int avsr_gemm(const avsr_gemm_params* p, void* stream);
+
+/* ------------------------------------------------------------------------------------
+ * Implicit-GEMM convolution over NHWC activations (no im2col buffer), grouped.
+ *   x [nimg][hin][win][ldx] (group g uses channels g*cin .. g*cin+cin-1)
+ *   y [nimg][hout][wout][ldy] (group g: channels g*cout ..)
+ *   w [groups*cout][kh][kw][cin]  (= torch channels_last physical order)
+ * fwd:         y  = conv(x, w)                          (+ BN partial statistics if stats)
+ * bwd_data:    dx = alpha * conv_transpose(dy, w) (+ beta * dx)
+ * bwd_weight:  dw (fp32) += conv_wgrad(x, dy)   (split-K, fp32 atomics)
+ * Replaces: nn.Conv2d in src/nets/backend/backbones/resnet.py:10-22 (3x3 and 1x1
+ *   downsample, ResNet-18 trunk), nn.Conv3d stem resnet.py:132 (as a 2-D conv over 5
+ *   time-stacked channels, see avsr_stem_pack), and the grouped pos-conv Conv1d
+ *   (k=128, groups 16) of HF:Wav2Vec2PositionalConvEmbedding (:326-369) as a 1-D conv
+ *   (win = wout = kw = 1).
+ * Requirements: cin, cout powers of two >= 8; ldx, ldy multiples of 8; 16-B aligned.
+ * ------------------------------------------------------------------------------------ */
+typedef struct {
+  int dtype;
+  int nimg, hin, win, cin;
+  int hout, wout, cout;
+  int kh, kw, sh, sw, ph, pw;
+  int groups;
+  int64_t ldx, ldy;
+  const void* x; const void* w; void* y;   /* forward operands / output */
+  void* dx; const void* dy; float* dw;     /* backward */
+  float* stats;   /* fwd only: [avsr_conv_stat_tiles()][groups*cout][3] (count, mean, M2) or NULL */
+  float alpha, beta;                       /* bwd_data scaling */
+  int splitk;     /* bwd_weight: 0 = auto */
+} avsr_conv_params;
+
+int avsr_conv_fwd(const avsr_conv_params* p, void* stream);
+int avsr_conv_bwd_data(const avsr_conv_params* p, void* stream);
+int avsr_conv_bwd_weight(const avsr_conv_params* p, void* stream);
+/* number of row tiles the forward partial statistics are split into */
+int avsr_conv_stat_tiles(const avsr_conv_params* p);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,102 @@
+"""Implicit-GEMM convolution kernels vs torch fp64 convolution (NCHW reference)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from avsr_amd import ops
+
+pytestmark = pytest.mark.gpu
+
+
+def _rel(a, b):
+    a = a.detach().double().cpu(); b = b.detach().double().cpu()
+    return ((a - b).abs().max() / b.abs().max().clamp_min(1e-30)).item()
+
+
+CASES = [
+    # nimg, h, w, cin, cout, k, stride, pad
+    (6, 22, 22, 64, 64, 3, 1, 1),
+    (5, 22, 22, 64, 128, 3, 2, 1),
+    (5, 22, 22, 64, 128, 1, 2, 0),
+    (7, 6, 6, 256, 512, 3, 2, 1),
+    (4, 3, 3, 512, 512, 3, 1, 1),
+    (3, 88, 88, 8, 64, 7, 2, 3),      # stem as 2-D conv over 8 packed channels
+]
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("case", CASES)
+def test_conv2d(dev, dtype, case):
+    n, h, w, cin, cout, k, s, p = case
+    g = torch.Generator().manual_seed(n * 100 + cin)
+    x = torch.randn(n, cin, h, w, generator=g)
+    wt = torch.randn(cout, cin, k, k, generator=g) * (cin * k * k) ** -0.5
+    ref = F.conv2d(x.double(), wt.double(), stride=s, padding=p)
+    ho, wo = ref.shape[2], ref.shape[3]
+    geom = ops.ConvGeom(n, h, w, cin, cout, k, k, (s, s), (p, p))
+    xd = x.permute(0, 2, 3, 1).contiguous().to(dev, dtype)
+    wd = wt.permute(0, 2, 3, 1).contiguous().to(dev, dtype)
+    y = torch.empty(n, ho, wo, cout, device=dev, dtype=dtype)
+    tiles = ops.conv_stat_tiles(geom)
+    stats = torch.empty(tiles, cout, 3, device=dev)
+    ops.conv_fwd(geom, xd, wd, y, stats)
+    tol = 3e-5 if dtype == torch.float32 else 2e-2
+    assert _rel(y.permute(0, 3, 1, 2), ref) < tol
+    # BN partial statistics combine to the batch mean / biased variance
+    cnt, mean, m2 = stats[..., 0].double(), stats[..., 1].double(), stats[..., 2].double()
+    tot = cnt.sum(0)
+    gm = (cnt * mean).sum(0) / tot
+    var = (m2 + cnt * (mean - gm) ** 2).sum(0) / tot
+    rm = ref.mean(dim=(0, 2, 3)); rv = ref.var(dim=(0, 2, 3), unbiased=False)
+    assert _rel(gm, rm) < (1e-4 if dtype == torch.float32 else 3e-2) or (gm - rm).abs().max() < 1e-3
+    assert _rel(var, rv) < (1e-4 if dtype == torch.float32 else 3e-2)
+    # data grad and weight grad
+    dyt = torch.randn(n, cout, ho, wo, generator=g)
+    xr = x.double().requires_grad_(); wr = wt.double().requires_grad_()
+    F.conv2d(xr, wr, stride=s, padding=p).backward(dyt.double())
+    dy = dyt.permute(0, 2, 3, 1).contiguous().to(dev, dtype)
+    dx = torch.empty(n, h, w, cin, device=dev, dtype=dtype)
+    ops.conv_bwd_data(geom, dy, wd, dx)
+    assert _rel(dx.permute(0, 3, 1, 2), xr.grad) < tol
+    dw = torch.zeros(cout, k, k, cin, device=dev)
+    ops.conv_bwd_weight(geom, xd, dy, dw)
+    assert _rel(dw.permute(0, 3, 1, 2), wr.grad) < (1e-4 if dtype == torch.float32 else 2e-2)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_posconv_grouped_1d(dev, dtype):
+    """Wav2Vec2PositionalConvEmbedding conv: Conv1d(D, D, k=128, pad=64, groups=16), drop last frame."""
+    B, T, D, G, K = 3, 37, 256, 16, 128
+    cg = D // G
+    g = torch.Generator().manual_seed(9)
+    x = torch.randn(B, T, D, generator=g)
+    wt = torch.randn(D, cg, K, generator=g) * (cg * K) ** -0.5
+    ref = F.conv1d(x.double().transpose(1, 2), wt.double(), padding=K // 2, groups=G)[:, :, :-1].transpose(1, 2)
+    geom = ops.ConvGeom(B, T, 1, cg, cg, K, 1, (1, 1), (K // 2, 0), groups=G, hout=T, wout=1)
+    xd = x.contiguous().to(dev, dtype)
+    wd = wt.permute(0, 2, 1).contiguous().to(dev, dtype)         # [D][K][cg] = [cout][kh][kw=1][cin]
+    y = torch.empty(B, T, D, device=dev, dtype=dtype)
+    ops.conv_fwd(geom, xd, wd, y)
+    tol = 3e-5 if dtype == torch.float32 else 2e-2
+    assert _rel(y, ref) < tol
+    dyt = torch.randn(B, T, D, generator=g)
+    xr = x.double().requires_grad_(); wr = wt.double().requires_grad_()
+    out = F.conv1d(xr.transpose(1, 2), wr, padding=K // 2, groups=G)[:, :, :-1].transpose(1, 2)
+    out.backward(dyt.double())
+    dy = dyt.to(dev, dtype)
+    dx = torch.empty(B, T, D, device=dev, dtype=dtype)
+    ops.conv_bwd_data(geom, dy, wd, dx)
+    assert _rel(dx, xr.grad) < tol
+    dw = torch.zeros(D, K, cg, device=dev)
+    ops.conv_bwd_weight(geom, xd, dy, dw)
+    assert _rel(dw.permute(0, 2, 1), wr.grad) < (1e-4 if dtype == torch.float32 else 2e-2)
+
+
+def test_gemm_splitk(dev):
+    M, N, K = 64, 576, 20000
+    a = torch.randn(K, M, device=dev, dtype=torch.bfloat16)
+    b = torch.randn(K, N, device=dev, dtype=torch.bfloat16)
+    c = torch.zeros(M, N, device=dev)
+    ops.gemm(a, b, c, M=M, N=N, K=K, a_kmajor=False, b_kmajor=False, lda=M, ldb=N, ldc=N, splitk=16)
+    ref = a.double().t() @ b.double()
+    assert _rel(c, ref) < 1e-2

@@ -8,7 +8,7 @@ pytestmark = pytest.mark.gpu
 
 
 def _rel(a, b):
-    a = a.double(); b = b.double()
+    a = a.detach().double().cpu(); b = b.detach().double().cpu()
     return ((a - b).abs().max() / b.abs().max().clamp_min(1e-30)).item()
 
 
