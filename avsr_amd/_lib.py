@@ -56,6 +56,56 @@ class ConvParams(ctypes.Structure):
     ]
 
 
+class LayerNormParams(ctypes.Structure):
+    _fields_ = [
+        ("dtype", _i), ("rows", _i), ("N", _i), ("eps", _f),
+        ("x", _c_p), ("ldx", _i64), ("y", _c_p), ("ldy", _i64),
+        ("gamma", _c_p), ("beta", _c_p), ("mean", _c_p), ("rstd", _c_p),
+        ("dy", _c_p), ("lddy", _i64), ("dx", _c_p), ("lddx", _i64),
+        ("dres", _c_p), ("lddres", _i64), ("dgamma", _c_p), ("dbeta", _c_p),
+    ]
+
+
+class BnFinalizeParams(ctypes.Structure):
+    _fields_ = [
+        ("tiles", _i), ("C", _i), ("partials", _c_p), ("gamma", _c_p), ("beta", _c_p),
+        ("running_mean", _c_p), ("running_var", _c_p), ("momentum", _f), ("eps", _f),
+        ("training", _i), ("mean", _c_p), ("invstd", _c_p), ("scale", _c_p), ("shift", _c_p),
+    ]
+
+
+class BnActParams(ctypes.Structure):
+    _fields_ = [
+        ("dtype", _i), ("M", _i), ("C", _i),
+        ("h", _c_p), ("scale", _c_p), ("shift", _c_p), ("res", _c_p), ("scale2", _c_p), ("shift2", _c_p),
+        ("prelu", _c_p), ("y", _c_p), ("dy", _c_p), ("dz", _c_p),
+        ("mean", _c_p), ("invstd", _c_p), ("mean2", _c_p), ("invstd2", _c_p),
+        ("sums", _c_p), ("dprelu", _c_p), ("dgamma", _c_p), ("dbeta", _c_p), ("dgamma2", _c_p), ("dbeta2", _c_p),
+        ("dh", _c_p), ("dh2", _c_p), ("beta_acc", _f),
+    ]
+
+
+class StemPoolParams(ctypes.Structure):
+    _fields_ = [
+        ("dtype", _i), ("nimg", _i), ("H", _i), ("W", _i), ("C", _i), ("Ho", _i), ("Wo", _i),
+        ("h", _c_p), ("scale", _c_p), ("shift", _c_p), ("prelu", _c_p), ("y", _c_p), ("argmax", _c_p),
+        ("dy", _c_p), ("dz", _c_p), ("mean", _c_p), ("invstd", _c_p),
+        ("sums", _c_p), ("dprelu", _c_p), ("dgamma", _c_p), ("dbeta", _c_p),
+    ]
+
+
+def fill(struct_cls, **kw):
+    """Build a params struct; torch tensors become raw device pointers, None -> NULL."""
+    p = struct_cls()
+    for k, v in kw.items():
+        if v is None:
+            continue
+        if isinstance(v, torch.Tensor):
+            v = v.data_ptr()
+        setattr(p, k, v)
+    return p
+
+
 # (symbol name, params struct or None for custom signature)
 SYMBOLS = {
     "avsr_version": ([], ctypes.c_char_p),
@@ -64,6 +114,16 @@ SYMBOLS = {
     "avsr_conv_bwd_data": ([ctypes.POINTER(ConvParams), _c_p], _i),
     "avsr_conv_bwd_weight": ([ctypes.POINTER(ConvParams), _c_p], _i),
     "avsr_conv_stat_tiles": ([ctypes.POINTER(ConvParams)], _i),
+    "avsr_layernorm_fwd": ([ctypes.POINTER(LayerNormParams), _c_p], _i),
+    "avsr_layernorm_bwd": ([ctypes.POINTER(LayerNormParams), _c_p], _i),
+    "avsr_bn_finalize": ([ctypes.POINTER(BnFinalizeParams), _c_p], _i),
+    "avsr_bn_act_fwd": ([ctypes.POINTER(BnActParams), _c_p], _i),
+    "avsr_bn_act_bwd_reduce": ([ctypes.POINTER(BnActParams), _c_p], _i),
+    "avsr_bn_bwd_apply": ([ctypes.POINTER(BnActParams), _c_p], _i),
+    "avsr_stem_pool_fwd": ([ctypes.POINTER(StemPoolParams), _c_p], _i),
+    "avsr_stem_pool_bwd_reduce": ([ctypes.POINTER(StemPoolParams), _c_p], _i),
+    "avsr_avgpool_fwd": ([_i, _i, _i, _i, _c_p, _c_p, _c_p], _i),
+    "avsr_avgpool_bwd": ([_i, _i, _i, _i, _c_p, _c_p, _c_p], _i),
 }
 
 _lib = None

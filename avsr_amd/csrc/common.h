@@ -87,3 +87,36 @@ AVSR_DEV f32x16 mfma32(const bf16x8& a, const bf16x8& b, const f32x16& c) {
 #define AVSR_CHECK_LAUNCH() do { hipError_t e_ = hipGetLastError(); if (e_ != hipSuccess) return (int)e_; } while (0)
 
 static inline int avsr_aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
+
+// ---- 16-byte vector load/store of VE = 16/sizeof(T) elements as floats ----------------
+template <typename T> struct VecW { static constexpr int VE = 16 / (int)sizeof(T); };
+template <typename T> AVSR_DEV void ldv(const T* p, float* o) {
+  if constexpr (sizeof(T) == 2) {
+    bf16x8 v = *(const bf16x8*)p;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = (float)v[j];
+  } else {
+    f32x4 v = *(const f32x4*)p;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[j] = v[j];
+  }
+}
+template <typename T> AVSR_DEV void stv(T* p, const float* o) {
+  if constexpr (sizeof(T) == 2) {
+    bf16x8 v;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = (bf16)o[j];
+    *(bf16x8*)p = v;
+  } else {
+    f32x4 v;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = o[j];
+    *(f32x4*)p = v;
+  }
+}
+// grid-stride launch size for memory-bound kernels (<= 8 blocks of 256 per CU)
+static inline int avsr_grid(long work, int per_block = 256, int cap = 2048) {
+  long g = (work + per_block - 1) / per_block;
+  if (g < 1) g = 1;
+  return (int)(g < cap ? g : cap);
+}

@@ -92,7 +92,7 @@ static int tile_bm(int M, int N) { return N <= 64 ? 256 : (M <= 64 ? 64 : 128); 
 static void base_epi(Epi& e) {
   e.alpha = 1.f; e.beta = 0.f; e.bias = nullptr; e.act = 0; e.bwd = 0; e.atomic = 0;
   e.preact = nullptr; e.res = nullptr; e.ldr = 0; e.gate = nullptr; e.drop_p = 0.f; e.seed = 0;
-  e.drop_base = 0; e.stats = nullptr;
+  e.drop_base = 0; e.stats = nullptr; e.stats_tiles = 0;
 }
 
 }  // namespace
@@ -116,6 +116,7 @@ extern "C" int avsr_conv_fwd(const avsr_conv_params* p, void* stream) {
   a.splits = 1; a.kchunk = a.K;
   base_epi(a.e);
   a.e.M = a.M; a.e.N = a.N; a.e.C = p->y; a.e.ldc = p->ldy; a.e.stats = p->stats;
+  a.e.stats_tiles = avsr_conv_stat_tiles(p);
   if (a.M == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
   if (p->dtype == AVSR_F32) return by_tile<float, float, K_FWD>(a, p->groups, st);

@@ -86,7 +86,7 @@ extern "C" int avsr_gemm(const avsr_gemm_params* p, void* stream) {
   e.alpha = p->alpha; e.beta = p->beta; e.bias = p->bias;
   e.act = p->act; e.bwd = p->epi_bwd; e.atomic = splits > 1;
   e.preact = p->preact; e.res = p->res; e.ldr = p->ldr; e.gate = p->gate;
-  e.drop_p = p->drop_p; e.seed = p->seed; e.drop_base = 0; e.stats = nullptr;
+  e.drop_p = p->drop_p; e.seed = p->seed; e.drop_base = 0; e.stats = nullptr; e.stats_tiles = 0;
   hipStream_t st = (hipStream_t)stream;
   if (p->K == 0) return AVSR_E_SHAPE;
   if (p->dtype == AVSR_F32) return by_tile<float, float>(p, a, st);

@@ -294,7 +294,8 @@ struct Epi {
   const void* res; int64_t ldr;
   const void* gate;
   float drop_p; uint64_t seed; uint64_t drop_base;
-  float* stats;        // BN partials: [m_tile][N][3] = (count, mean, M2) of the stored values
+  float* stats;        // BN partials: [N][stats_tiles][3] = (count, mean, M2) of the stored values
+  int stats_tiles;
 };
 
 // row/col of accumulator register r of tile (i, j)
@@ -394,7 +395,7 @@ AVSR_DEV void epilogue(const Epi& e, int m0, int n0, f32x16 (&acc)[2][2], char* 
             n = nn;
           }
         }
-        float* o = e.stats + ((int64_t)(m0 / BM) * e.N + col) * 3;
+        float* o = e.stats + ((int64_t)col * e.stats_tiles + m0 / BM) * 3;
         o[0] = n; o[1] = mean; o[2] = m2;
       }
     }

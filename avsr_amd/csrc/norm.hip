@@ -1,0 +1,576 @@
+// LayerNorm, BatchNorm (+PReLU, +residual), stem max-pool and global average pool —
+// forward and backward, for the AVSR hot path (declarations and reference call sites in
+// include/avsr_hip.h). All are HBM-bound: 16-byte vector loads/stores, fp32 statistics,
+// one pass per tensor where the math allows.
+#include "common.h"
+
+namespace {
+
+// =============================================================== LayerNorm
+struct LnArgs {
+  int rows, N; float eps;
+  const void* x; int64_t ldx; void* y; int64_t ldy;
+  const float* gamma; const float* beta; float* mean; float* rstd;
+  const void* dy; int64_t lddy; void* dx; int64_t lddx; const void* dres; int64_t lddres;
+  float* dgamma; float* dbeta;
+};
+
+// one wave per row; lane owns vectors lane, lane+64, ... (VPL of them)
+template <typename T, int VPL>
+__global__ __launch_bounds__(256) void ln_fwd_kernel(LnArgs a) {
+  constexpr int VE = VecW<T>::VE;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= a.rows) return;
+  const T* x = (const T*)a.x + (int64_t)row * a.ldx;
+  float v[VPL][VE];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) {
+    const int c = (lane + i * 64) * VE;
+    if (c < a.N) ldv(x + c, v[i]);
+    else
+#pragma unroll
+      for (int j = 0; j < VE; ++j) v[i][j] = 0.f;
+#pragma unroll
+    for (int j = 0; j < VE; ++j) s += v[i][j];
+  }
+  const float mean = wave_sum(s) / a.N;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) {
+    const int c = (lane + i * 64) * VE;
+    if (c < a.N)
+#pragma unroll
+      for (int j = 0; j < VE; ++j) { const float d = v[i][j] - mean; q += d * d; }
+  }
+  const float rstd = rsqrtf(wave_sum(q) / a.N + a.eps);
+  T* y = (T*)a.y + (int64_t)row * a.ldy;
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) {
+    const int c = (lane + i * 64) * VE;
+    if (c < a.N) {
+      float o[VE];
+#pragma unroll
+      for (int j = 0; j < VE; ++j) o[j] = (v[i][j] - mean) * rstd * a.gamma[c + j] + a.beta[c + j];
+      stv(y + c, o);
+    }
+  }
+  if (lane == 0) { a.mean[row] = mean; a.rstd[row] = rstd; }
+}
+
+// grid-stride over rows (one wave per row at a time); dgamma/dbeta accumulated per lane in
+// registers, then one fp32 atomic per column per wave
+template <typename T, int VPL>
+__global__ __launch_bounds__(256) void ln_bwd_kernel(LnArgs a) {
+  constexpr int VE = VecW<T>::VE;
+  const int lane = threadIdx.x & 63;
+  const int nw = gridDim.x * 4;
+  float dg[VPL][VE], db[VPL][VE];
+#pragma unroll
+  for (int i = 0; i < VPL; ++i)
+#pragma unroll
+    for (int j = 0; j < VE; ++j) { dg[i][j] = 0.f; db[i][j] = 0.f; }
+  for (int row = blockIdx.x * 4 + (threadIdx.x >> 6); row < a.rows; row += nw) {
+    const T* x = (const T*)a.x + (int64_t)row * a.ldx;
+    const T* dy = (const T*)a.dy + (int64_t)row * a.lddy;
+    const float mean = a.mean[row], rstd = a.rstd[row];
+    float xh[VPL][VE], g[VPL][VE];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) {
+      const int c = (lane + i * 64) * VE;
+      if (c < a.N) {
+        float xv[VE], dv[VE];
+        ldv(x + c, xv);
+        ldv(dy + c, dv);
+#pragma unroll
+        for (int j = 0; j < VE; ++j) {
+          xh[i][j] = (xv[j] - mean) * rstd;
+          g[i][j] = dv[j] * a.gamma[c + j];
+          s1 += g[i][j];
+          s2 += g[i][j] * xh[i][j];
+          dg[i][j] += dv[j] * xh[i][j];
+          db[i][j] += dv[j];
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < VE; ++j) { xh[i][j] = 0.f; g[i][j] = 0.f; }
+      }
+    }
+    s1 = wave_sum(s1) / a.N;
+    s2 = wave_sum(s2) / a.N;
+    T* dx = (T*)a.dx + (int64_t)row * a.lddx;
+    const T* dr = a.dres ? (const T*)a.dres + (int64_t)row * a.lddres : nullptr;
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) {
+      const int c = (lane + i * 64) * VE;
+      if (c < a.N) {
+        float o[VE], r[VE];
+        if (dr) ldv(dr + c, r);
+        else
+#pragma unroll
+          for (int j = 0; j < VE; ++j) r[j] = 0.f;
+#pragma unroll
+        for (int j = 0; j < VE; ++j) o[j] = r[j] + rstd * (g[i][j] - s1 - xh[i][j] * s2);
+        stv(dx + c, o);
+      }
+    }
+  }
+  if (a.dgamma) {
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) {
+      const int c = (lane + i * 64) * VE;
+      if (c < a.N)
+#pragma unroll
+        for (int j = 0; j < VE; ++j) { atomicAdd(a.dgamma + c + j, dg[i][j]); atomicAdd(a.dbeta + c + j, db[i][j]); }
+    }
+  }
+}
+
+template <typename T>
+int ln_launch(const avsr_layernorm_params* p, bool bwd, hipStream_t st) {
+  constexpr int VE = VecW<T>::VE;
+  LnArgs a;
+  a.rows = p->rows; a.N = p->N; a.eps = p->eps;
+  a.x = p->x; a.ldx = p->ldx; a.y = p->y; a.ldy = p->ldy; a.gamma = p->gamma; a.beta = p->beta;
+  a.mean = p->mean; a.rstd = p->rstd; a.dy = p->dy; a.lddy = p->lddy; a.dx = p->dx; a.lddx = p->lddx;
+  a.dres = p->dres; a.lddres = p->lddres; a.dgamma = p->dgamma; a.dbeta = p->dbeta;
+  const int vpl = (p->N / VE + 63) / 64;
+  int blocks = (p->rows + 3) / 4;
+  if (bwd) blocks = blocks < 256 ? blocks : 256;
+#define LNL(V)                                                                                   \
+  if (vpl <= V) {                                                                                \
+    if (bwd) hipLaunchKernelGGL((ln_bwd_kernel<T, V>), dim3(blocks), dim3(256), 0, st, a);       \
+    else hipLaunchKernelGGL((ln_fwd_kernel<T, V>), dim3(blocks), dim3(256), 0, st, a);           \
+    AVSR_CHECK_LAUNCH();                                                                         \
+    return 0;                                                                                    \
+  }
+  LNL(1) LNL(2) LNL(4) LNL(8)
+#undef LNL
+  return AVSR_E_SHAPE;
+}
+
+int ln_check(const avsr_layernorm_params* p) {
+  if (!p) return AVSR_E_ARG;
+  const int ve = p->dtype == AVSR_BF16 ? 8 : 4;
+  if (p->N % ve || p->ldx % ve || p->ldy % ve) return AVSR_E_ALIGN;
+  return 0;
+}
+
+// =============================================================== BatchNorm
+__global__ __launch_bounds__(256) void bn_finalize_kernel(avsr_bn_finalize_params a) {
+  const int c = blockIdx.x;
+  __shared__ double sn[256], sm[256], sq[256];
+  double n = 0, mean = 0, m2 = 0;
+  if (a.training) {
+    const float* pp = a.partials + (int64_t)c * a.tiles * 3;
+    for (int t = threadIdx.x; t < a.tiles; t += 256) {
+      const double nb = pp[t * 3 + 0], mb = pp[t * 3 + 1], qb = pp[t * 3 + 2];
+      if (nb > 0) {
+        const double nn = n + nb, d = mb - mean;
+        mean += d * nb / nn;
+        m2 += qb + d * d * n * nb / nn;
+        n = nn;
+      }
+    }
+    sn[threadIdx.x] = n; sm[threadIdx.x] = mean; sq[threadIdx.x] = m2;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+      if (threadIdx.x < o) {
+        const double na = sn[threadIdx.x], nb = sn[threadIdx.x + o];
+        if (nb > 0) {
+          const double nn = na + nb, d = sm[threadIdx.x + o] - sm[threadIdx.x];
+          sm[threadIdx.x] += d * nb / nn;
+          sq[threadIdx.x] += sq[threadIdx.x + o] + d * d * na * nb / nn;
+          sn[threadIdx.x] = nn;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  if (threadIdx.x == 0) {
+    double mu, var;
+    if (a.training) {
+      n = sn[0]; mu = sm[0]; var = n > 0 ? sq[0] / n : 0.0;
+      if (a.running_mean) {
+        const double unb = n > 1 ? sq[0] / (n - 1) : var;
+        a.running_mean[c] = (float)((1.0 - a.momentum) * a.running_mean[c] + a.momentum * mu);
+        a.running_var[c] = (float)((1.0 - a.momentum) * a.running_var[c] + a.momentum * unb);
+      }
+    } else {
+      mu = a.running_mean[c]; var = a.running_var[c];
+    }
+    const float inv = (float)(1.0 / sqrt(var + (double)a.eps));
+    const float g = a.gamma ? a.gamma[c] : 1.f, b = a.beta ? a.beta[c] : 0.f;
+    a.mean[c] = (float)mu; a.invstd[c] = inv;
+    a.scale[c] = g * inv; a.shift[c] = b - (float)mu * g * inv;
+  }
+}
+
+struct BnArgs {
+  int M, C;
+  const void* h; const float* scale; const float* shift;
+  const void* res; const float* scale2; const float* shift2;
+  const float* prelu; void* y;
+  const void* dy; void* dz;
+  const float* mean; const float* invstd; const float* mean2; const float* invstd2;
+  float* sums; float* dprelu; float* dgamma; float* dbeta; float* dgamma2; float* dbeta2;
+  void* dh; void* dh2; float beta_acc;
+};
+
+template <typename T>
+__global__ __launch_bounds__(256) void bn_act_fwd_kernel(BnArgs a) {
+  constexpr int VE = VecW<T>::VE;
+  const int64_t nv = (int64_t)a.M * a.C / VE;
+  for (int64_t v = blockIdx.x * 256 + threadIdx.x; v < nv; v += (int64_t)gridDim.x * 256) {
+    const int c0 = (int)(v % (a.C / VE)) * VE;
+    float h[VE], r[VE], o[VE];
+    ldv((const T*)a.h + v * VE, h);
+    if (a.res) ldv((const T*)a.res + v * VE, r);
+#pragma unroll
+    for (int j = 0; j < VE; ++j) {
+      float z = h[j] * a.scale[c0 + j] + a.shift[c0 + j];
+      if (a.res) z += a.scale2 ? r[j] * a.scale2[c0 + j] + a.shift2[c0 + j] : r[j];
+      o[j] = z > 0.f ? z : z * a.prelu[c0 + j];
+    }
+    stv((T*)a.y + v * VE, o);
+  }
+}
+
+// block-level reduction of per-thread channel partials (thread's channel group is fixed:
+// the grid stride is a multiple of C/VE) followed by one fp32 atomic per channel per block
+template <int VE>
+__device__ void block_chan_reduce(float (&q)[VE], float* lds, int cpv, float* out, int stride) {
+  // lds: [256][VE]
+#pragma unroll
+  for (int j = 0; j < VE; ++j) lds[threadIdx.x * VE + j] = q[j];
+  __syncthreads();
+  if ((int)threadIdx.x < cpv) {
+    float acc[VE];
+#pragma unroll
+    for (int j = 0; j < VE; ++j) acc[j] = 0.f;
+    for (int t = threadIdx.x; t < 256; t += cpv)
+#pragma unroll
+      for (int j = 0; j < VE; ++j) acc[j] += lds[t * VE + j];
+    if (out) {
+      const int c0 = threadIdx.x * VE;
+#pragma unroll
+      for (int j = 0; j < VE; ++j) atomicAdd(out + (int64_t)(c0 + j) * stride, acc[j]);
+    }
+  }
+  __syncthreads();
+}
+
+// MODE 0: dy given per element; MODE 1: stem max-pool — dy gathered through the argmax
+template <typename T, int MODE>
+__global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(BnArgs a, avsr_stem_pool_params sp) {
+  constexpr int VE = VecW<T>::VE;
+  __shared__ float lds[256 * VE];
+  const int cpv = a.C / VE;
+  const int64_t nv = (int64_t)a.M * cpv;
+  float s0[VE], s1[VE], s2[VE], s3[VE];
+#pragma unroll
+  for (int j = 0; j < VE; ++j) { s0[j] = s1[j] = s2[j] = s3[j] = 0.f; }
+  const int64_t tid0 = blockIdx.x * 256 + threadIdx.x;
+  const int c0 = (int)(tid0 % cpv) * VE;
+  for (int64_t v = tid0; v < nv; v += (int64_t)gridDim.x * 256) {
+    float h[VE], r[VE], d[VE];
+    ldv((const T*)a.h + v * VE, h);
+    if (a.res) ldv((const T*)a.res + v * VE, r);
+    if constexpr (MODE == 0) {
+      ldv((const T*)a.dy + v * VE, d);
+    } else {
+      // input pixel (n, ih, iw) of the stem max-pool; windows (oh, ow) with 2*o-1 <= i <= 2*o+1
+      const int64_t pix = v / cpv;
+      const int iw = (int)(pix % sp.W), ih = (int)((pix / sp.W) % sp.H);
+      const int64_t n = pix / ((int64_t)sp.W * sp.H);
+#pragma unroll
+      for (int j = 0; j < VE; ++j) d[j] = 0.f;
+      const int oh0 = (ih + 1) / 2 - 1, ow0 = (iw + 1) / 2 - 1;
+      for (int oh = oh0; oh <= oh0 + 1; ++oh) {
+        if (oh < 0 || oh >= sp.Ho || ih < 2 * oh - 1 || ih > 2 * oh + 1) continue;
+        for (int ow = ow0; ow <= ow0 + 1; ++ow) {
+          if (ow < 0 || ow >= sp.Wo || iw < 2 * ow - 1 || iw > 2 * ow + 1) continue;
+          const int64_t ov = ((n * sp.Ho + oh) * sp.Wo + ow) * cpv + c0 / VE;
+          const uint8_t want = (uint8_t)((ih - 2 * oh + 1) * 3 + (iw - 2 * ow + 1));
+          float g[VE];
+          ldv((const T*)sp.dy + ov * VE, g);
+          const uint8_t* am = sp.argmax + ov * VE;
+#pragma unroll
+          for (int j = 0; j < VE; ++j) d[j] += am[j] == want ? g[j] : 0.f;
+        }
+      }
+    }
+    float dzo[VE];
+#pragma unroll
+    for (int j = 0; j < VE; ++j) {
+      const int c = c0 + j;
+      float z = h[j] * a.scale[c] + a.shift[c];
+      if (a.res) z += a.scale2 ? r[j] * a.scale2[c] + a.shift2[c] : r[j];
+      const float pw = a.prelu[c];
+      const float dz = z > 0.f ? d[j] : d[j] * pw;
+      s3[j] += z > 0.f ? 0.f : d[j] * z;
+      dzo[j] = dz;
+      s0[j] += dz;
+      s1[j] += dz * (h[j] - a.mean[c]) * a.invstd[c];
+      if (a.scale2) s2[j] += dz * (r[j] - a.mean2[c]) * a.invstd2[c];
+    }
+    stv((T*)a.dz + v * VE, dzo);
+  }
+  // channel sums: sums[c][0..2] (scratch for bwd_apply) + gradient accumulators
+  block_chan_reduce<VE>(s0, lds, cpv, a.sums ? a.sums + 0 : nullptr, 3);
+  if (a.dbeta) { block_chan_reduce<VE>(s0, lds, cpv, a.dbeta, 1); }
+  if (a.dbeta2) { block_chan_reduce<VE>(s0, lds, cpv, a.dbeta2, 1); }
+  block_chan_reduce<VE>(s1, lds, cpv, a.sums ? a.sums + 1 : nullptr, 3);
+  if (a.dgamma) block_chan_reduce<VE>(s1, lds, cpv, a.dgamma, 1);
+  if (a.scale2) {
+    block_chan_reduce<VE>(s2, lds, cpv, a.sums ? a.sums + 2 : nullptr, 3);
+    if (a.dgamma2) block_chan_reduce<VE>(s2, lds, cpv, a.dgamma2, 1);
+  }
+  if (a.dprelu) block_chan_reduce<VE>(s3, lds, cpv, a.dprelu, 1);
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(BnArgs a) {
+  constexpr int VE = VecW<T>::VE;
+  const int64_t nv = (int64_t)a.M * a.C / VE;
+  const float invM = 1.f / (float)a.M;
+  for (int64_t v = blockIdx.x * 256 + threadIdx.x; v < nv; v += (int64_t)gridDim.x * 256) {
+    const int c0 = (int)(v % (a.C / VE)) * VE;
+    float dz[VE], h[VE], o[VE];
+    ldv((const T*)a.dz + v * VE, dz);
+    ldv((const T*)a.h + v * VE, h);
+    if (a.beta_acc != 0.f) ldv((const T*)a.dh + v * VE, o);
+#pragma unroll
+    for (int j = 0; j < VE; ++j) {
+      const int c = c0 + j;
+      const float xh = (h[j] - a.mean[c]) * a.invstd[c];
+      const float g = a.scale[c] * (dz[j] - a.sums[c * 3 + 0] * invM - xh * a.sums[c * 3 + 1] * invM);
+      o[j] = a.beta_acc != 0.f ? a.beta_acc * o[j] + g : g;
+    }
+    stv((T*)a.dh + v * VE, o);
+    if (a.dh2) {
+      float r[VE], o2[VE];
+      ldv((const T*)a.res + v * VE, r);
+#pragma unroll
+      for (int j = 0; j < VE; ++j) {
+        const int c = c0 + j;
+        const float xh = (r[j] - a.mean2[c]) * a.invstd2[c];
+        o2[j] = a.scale2[c] * (dz[j] - a.sums[c * 3 + 0] * invM - xh * a.sums[c * 3 + 2] * invM);
+      }
+      stv((T*)a.dh2 + v * VE, o2);
+    }
+  }
+}
+
+BnArgs bn_args(const avsr_bn_act_params* p) {
+  BnArgs a;
+  a.M = p->M; a.C = p->C; a.h = p->h; a.scale = p->scale; a.shift = p->shift; a.res = p->res;
+  a.scale2 = p->scale2; a.shift2 = p->shift2; a.prelu = p->prelu; a.y = p->y; a.dy = p->dy; a.dz = p->dz;
+  a.mean = p->mean; a.invstd = p->invstd; a.mean2 = p->mean2; a.invstd2 = p->invstd2; a.sums = p->sums;
+  a.dprelu = p->dprelu; a.dgamma = p->dgamma; a.dbeta = p->dbeta; a.dgamma2 = p->dgamma2; a.dbeta2 = p->dbeta2;
+  a.dh = p->dh; a.dh2 = p->dh2; a.beta_acc = p->beta_acc;
+  return a;
+}
+
+// =============================================================== stem max-pool
+template <typename T>
+__global__ __launch_bounds__(256) void stem_pool_fwd_kernel(avsr_stem_pool_params p) {
+  constexpr int VE = VecW<T>::VE;
+  const int cpv = p.C / VE;
+  const int64_t nv = (int64_t)p.nimg * p.Ho * p.Wo * cpv;
+  for (int64_t v = blockIdx.x * 256 + threadIdx.x; v < nv; v += (int64_t)gridDim.x * 256) {
+    const int c0 = (int)(v % cpv) * VE;
+    const int64_t pix = v / cpv;
+    const int ow = (int)(pix % p.Wo), oh = (int)((pix / p.Wo) % p.Ho);
+    const int64_t n = pix / ((int64_t)p.Wo * p.Ho);
+    float best[VE];
+    uint8_t idx[VE];
+#pragma unroll
+    for (int j = 0; j < VE; ++j) { best[j] = -INFINITY; idx[j] = 0; }
+    for (int dh = 0; dh < 3; ++dh) {
+      const int ih = 2 * oh - 1 + dh;
+      if (ih < 0 || ih >= p.H) continue;
+      for (int dw = 0; dw < 3; ++dw) {
+        const int iw = 2 * ow - 1 + dw;
+        if (iw < 0 || iw >= p.W) continue;
+        float h[VE];
+        ldv((const T*)p.h + (((n * p.H + ih) * p.W + iw) * p.C + c0), h);
+#pragma unroll
+        for (int j = 0; j < VE; ++j) {
+          const float z = h[j] * p.scale[c0 + j] + p.shift[c0 + j];
+          const float y = z > 0.f ? z : z * p.prelu[c0 + j];
+          if (y > best[j]) { best[j] = y; idx[j] = (uint8_t)(dh * 3 + dw); }
+        }
+      }
+    }
+    stv((T*)p.y + v * VE, best);
+#pragma unroll
+    for (int j = 0; j < VE; ++j) p.argmax[v * VE + j] = idx[j];
+  }
+}
+
+// =============================================================== avg pool
+template <typename T>
+__global__ __launch_bounds__(256) void avgpool_fwd_kernel(int nimg, int P, int C, const T* x, T* y) {
+  constexpr int VE = VecW<T>::VE;
+  const int cpv = C / VE;
+  const int64_t nv = (int64_t)nimg * cpv;
+  for (int64_t v = blockIdx.x * 256 + threadIdx.x; v < nv; v += (int64_t)gridDim.x * 256) {
+    const int64_t n = v / cpv;
+    const int c0 = (int)(v % cpv) * VE;
+    float s[VE], t[VE];
+#pragma unroll
+    for (int j = 0; j < VE; ++j) s[j] = 0.f;
+    for (int q = 0; q < P; ++q) {
+      ldv(x + ((n * P + q) * C + c0), t);
+#pragma unroll
+      for (int j = 0; j < VE; ++j) s[j] += t[j];
+    }
+#pragma unroll
+    for (int j = 0; j < VE; ++j) s[j] /= (float)P;
+    stv(y + v * VE, s);
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void avgpool_bwd_kernel(int nimg, int P, int C, const T* dy, T* dx) {
+  constexpr int VE = VecW<T>::VE;
+  const int cpv = C / VE;
+  const int64_t nv = (int64_t)nimg * P * cpv;
+  for (int64_t v = blockIdx.x * 256 + threadIdx.x; v < nv; v += (int64_t)gridDim.x * 256) {
+    const int64_t n = v / ((int64_t)P * cpv);
+    const int c0 = (int)(v % cpv) * VE;
+    float t[VE];
+    ldv(dy + (n * C + c0), t);
+#pragma unroll
+    for (int j = 0; j < VE; ++j) t[j] /= (float)P;
+    stv(dx + v * VE, t);
+  }
+}
+
+int bn_grid(int64_t nv, int cpv) {
+  // grid stride (blocks*256) must be a multiple of cpv: 256 % cpv == 0 for cpv <= 256 power of 2
+  (void)cpv;
+  return avsr_grid(nv, 256, 2048);
+}
+
+}  // namespace
+
+extern "C" int avsr_layernorm_fwd(const avsr_layernorm_params* p, void* stream) {
+  int rc = ln_check(p);
+  if (rc) return rc;
+  if (p->rows == 0) return 0;
+  if (p->dtype == AVSR_BF16) return ln_launch<bf16>(p, false, (hipStream_t)stream);
+  if (p->dtype == AVSR_F32) return ln_launch<float>(p, false, (hipStream_t)stream);
+  return AVSR_E_DTYPE;
+}
+
+extern "C" int avsr_layernorm_bwd(const avsr_layernorm_params* p, void* stream) {
+  int rc = ln_check(p);
+  if (rc) return rc;
+  if (p->rows == 0) return 0;
+  if (p->dtype == AVSR_BF16) return ln_launch<bf16>(p, true, (hipStream_t)stream);
+  if (p->dtype == AVSR_F32) return ln_launch<float>(p, true, (hipStream_t)stream);
+  return AVSR_E_DTYPE;
+}
+
+extern "C" int avsr_bn_finalize(const avsr_bn_finalize_params* p, void* stream) {
+  if (!p || p->C <= 0) return AVSR_E_ARG;
+  if (p->training && !p->partials) return AVSR_E_ARG;
+  if (!p->training && (!p->running_mean || !p->running_var)) return AVSR_E_ARG;
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3(p->C), dim3(256), 0, (hipStream_t)stream, *p);
+  AVSR_CHECK_LAUNCH();
+  return 0;
+}
+
+static int bn_check(const avsr_bn_act_params* p) {
+  if (!p) return AVSR_E_ARG;
+  const int ve = p->dtype == AVSR_BF16 ? 8 : 4;
+  if (p->C % ve || (p->C / ve) > 256 || (256 % (p->C / ve))) return AVSR_E_SHAPE;
+  return 0;
+}
+
+extern "C" int avsr_bn_act_fwd(const avsr_bn_act_params* p, void* stream) {
+  int rc = bn_check(p);
+  if (rc) return rc;
+  BnArgs a = bn_args(p);
+  const int ve = p->dtype == AVSR_BF16 ? 8 : 4;
+  const int g = bn_grid((int64_t)p->M * p->C / ve, p->C / ve);
+  if (p->dtype == AVSR_BF16) hipLaunchKernelGGL(bn_act_fwd_kernel<bf16>, dim3(g), dim3(256), 0, (hipStream_t)stream, a);
+  else hipLaunchKernelGGL(bn_act_fwd_kernel<float>, dim3(g), dim3(256), 0, (hipStream_t)stream, a);
+  AVSR_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int avsr_bn_act_bwd_reduce(const avsr_bn_act_params* p, void* stream) {
+  int rc = bn_check(p);
+  if (rc) return rc;
+  BnArgs a = bn_args(p);
+  avsr_stem_pool_params sp = {};
+  const int ve = p->dtype == AVSR_BF16 ? 8 : 4;
+  const int g = bn_grid((int64_t)p->M * p->C / ve, p->C / ve);
+  if (p->dtype == AVSR_BF16) hipLaunchKernelGGL((bn_bwd_reduce_kernel<bf16, 0>), dim3(g), dim3(256), 0, (hipStream_t)stream, a, sp);
+  else hipLaunchKernelGGL((bn_bwd_reduce_kernel<float, 0>), dim3(g), dim3(256), 0, (hipStream_t)stream, a, sp);
+  AVSR_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int avsr_bn_bwd_apply(const avsr_bn_act_params* p, void* stream) {
+  int rc = bn_check(p);
+  if (rc) return rc;
+  if (!p->sums || !p->dz || !p->dh) return AVSR_E_ARG;
+  BnArgs a = bn_args(p);
+  const int ve = p->dtype == AVSR_BF16 ? 8 : 4;
+  const int g = bn_grid((int64_t)p->M * p->C / ve, p->C / ve);
+  if (p->dtype == AVSR_BF16) hipLaunchKernelGGL(bn_bwd_apply_kernel<bf16>, dim3(g), dim3(256), 0, (hipStream_t)stream, a);
+  else hipLaunchKernelGGL(bn_bwd_apply_kernel<float>, dim3(g), dim3(256), 0, (hipStream_t)stream, a);
+  AVSR_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int avsr_stem_pool_fwd(const avsr_stem_pool_params* p, void* stream) {
+  if (!p) return AVSR_E_ARG;
+  const int ve = p->dtype == AVSR_BF16 ? 8 : 4;
+  if (p->C % ve) return AVSR_E_SHAPE;
+  const int g = avsr_grid((int64_t)p->nimg * p->Ho * p->Wo * p->C / ve);
+  if (p->dtype == AVSR_BF16) hipLaunchKernelGGL(stem_pool_fwd_kernel<bf16>, dim3(g), dim3(256), 0, (hipStream_t)stream, *p);
+  else hipLaunchKernelGGL(stem_pool_fwd_kernel<float>, dim3(g), dim3(256), 0, (hipStream_t)stream, *p);
+  AVSR_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int avsr_stem_pool_bwd_reduce(const avsr_stem_pool_params* p, void* stream) {
+  if (!p) return AVSR_E_ARG;
+  const int ve = p->dtype == AVSR_BF16 ? 8 : 4;
+  if (p->C % ve || (256 % (p->C / ve))) return AVSR_E_SHAPE;
+  BnArgs a = {};
+  a.M = p->nimg * p->H * p->W; a.C = p->C; a.h = p->h; a.scale = p->scale; a.shift = p->shift;
+  a.prelu = p->prelu; a.dz = p->dz; a.mean = p->mean; a.invstd = p->invstd; a.sums = p->sums;
+  a.dprelu = p->dprelu; a.dgamma = p->dgamma; a.dbeta = p->dbeta;
+  const int g = bn_grid((int64_t)a.M * p->C / ve, p->C / ve);
+  if (p->dtype == AVSR_BF16) hipLaunchKernelGGL((bn_bwd_reduce_kernel<bf16, 1>), dim3(g), dim3(256), 0, (hipStream_t)stream, a, *p);
+  else hipLaunchKernelGGL((bn_bwd_reduce_kernel<float, 1>), dim3(g), dim3(256), 0, (hipStream_t)stream, a, *p);
+  AVSR_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int avsr_avgpool_fwd(int dtype, int nimg, int P, int C, const void* x, void* y, void* stream) {
+  const int ve = dtype == AVSR_BF16 ? 8 : 4;
+  if (C % ve) return AVSR_E_SHAPE;
+  const int g = avsr_grid((int64_t)nimg * C / ve);
+  if (dtype == AVSR_BF16) hipLaunchKernelGGL(avgpool_fwd_kernel<bf16>, dim3(g), dim3(256), 0, (hipStream_t)stream, nimg, P, C, (const bf16*)x, (bf16*)y);
+  else hipLaunchKernelGGL(avgpool_fwd_kernel<float>, dim3(g), dim3(256), 0, (hipStream_t)stream, nimg, P, C, (const float*)x, (float*)y);
+  AVSR_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int avsr_avgpool_bwd(int dtype, int nimg, int P, int C, const void* dy, void* dx, void* stream) {
+  const int ve = dtype == AVSR_BF16 ? 8 : 4;
+  if (C % ve) return AVSR_E_SHAPE;
+  const int g = avsr_grid((int64_t)nimg * P * C / ve);
+  if (dtype == AVSR_BF16) hipLaunchKernelGGL(avgpool_bwd_kernel<bf16>, dim3(g), dim3(256), 0, (hipStream_t)stream, nimg, P, C, (const bf16*)dy, (bf16*)dx);
+  else hipLaunchKernelGGL(avgpool_bwd_kernel<float>, dim3(g), dim3(256), 0, (hipStream_t)stream, nimg, P, C, (const float*)dy, (float*)dx);
+  AVSR_CHECK_LAUNCH();
+  return 0;
+}

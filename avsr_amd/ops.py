@@ -168,3 +168,119 @@ def conv_bwd_weight(g, x, dy, dw, splitk=0):
     p.splitk = splitk
     L.check(L.load().avsr_conv_bwd_weight(ctypes.byref(p), L.stream_ptr()), "avsr_conv_bwd_weight")
     return dw
+
+
+def _call(name, params):
+    L.check(getattr(L.load(), name)(ctypes.byref(params), L.stream_ptr()), name)
+
+
+# ---------------------------------------------------------------------------------------
+# LayerNorm
+# ---------------------------------------------------------------------------------------
+
+def layernorm_fwd(x, gamma, beta, eps, y=None, mean=None, rstd=None):
+    rows, N = x.shape
+    y = torch.empty_like(x) if y is None else y
+    mean = torch.empty(rows, device=x.device) if mean is None else mean
+    rstd = torch.empty(rows, device=x.device) if rstd is None else rstd
+    _call("avsr_layernorm_fwd", L.fill(L.LayerNormParams, dtype=dtype_code(x), rows=rows, N=N, eps=eps,
+                                        x=x, ldx=x.stride(0), y=y, ldy=y.stride(0), gamma=gamma, beta=beta,
+                                        mean=mean, rstd=rstd))
+    return y, mean, rstd
+
+
+def layernorm_bwd(dy, x, gamma, mean, rstd, dx=None, dres=None, dgamma=None, dbeta=None):
+    """dx = dres + LN-backward(dy); dgamma/dbeta (fp32) accumulate."""
+    rows, N = x.shape
+    dx = torch.empty_like(x) if dx is None else dx
+    _call("avsr_layernorm_bwd", L.fill(L.LayerNormParams, dtype=dtype_code(x), rows=rows, N=N, eps=0.0,
+                                        x=x, ldx=x.stride(0), ldy=N, gamma=gamma, mean=mean, rstd=rstd,
+                                        dy=dy, lddy=dy.stride(0), dx=dx, lddx=dx.stride(0),
+                                        dres=dres, lddres=0 if dres is None else dres.stride(0),
+                                        dgamma=dgamma, dbeta=dbeta))
+    return dx
+
+
+# ---------------------------------------------------------------------------------------
+# BatchNorm (+PReLU, +residual) over NHWC rows
+# ---------------------------------------------------------------------------------------
+
+class BnState:
+    """Per-step statistics of one BatchNorm: mean / invstd / folded scale / shift (fp32 [C])."""
+
+    def __init__(self, C, device):
+        buf = torch.empty(4, C, device=device)
+        self.mean, self.invstd, self.scale, self.shift = buf[0], buf[1], buf[2], buf[3]
+
+
+def bn_finalize(st, gamma, beta, running_mean, running_var, *, partials=None, training=True,
+                momentum=0.1, eps=1e-5):
+    C = gamma.shape[0]
+    tiles = 0 if partials is None else partials.shape[1]
+    _call("avsr_bn_finalize", L.fill(L.BnFinalizeParams, tiles=tiles, C=C, partials=partials, gamma=gamma,
+                                      beta=beta, running_mean=running_mean, running_var=running_var,
+                                      momentum=momentum, eps=eps, training=int(training), mean=st.mean,
+                                      invstd=st.invstd, scale=st.scale, shift=st.shift))
+    return st
+
+
+def bn_act_fwd(h, st, prelu, y, res=None, st2=None):
+    M, C = h.shape
+    _call("avsr_bn_act_fwd", L.fill(L.BnActParams, dtype=dtype_code(h), M=M, C=C, h=h, scale=st.scale,
+                                     shift=st.shift, res=res, scale2=None if st2 is None else st2.scale,
+                                     shift2=None if st2 is None else st2.shift, prelu=prelu, y=y))
+    return y
+
+
+def bn_act_bwd(dy, h, st, prelu, dh, *, res=None, st2=None, dh2=None, dz=None, sums=None,
+               dprelu=None, dgamma=None, dbeta=None, dgamma2=None, dbeta2=None, beta_acc=0.0):
+    """Backward of y = prelu(bn(h) + [bn2(res) | res]): returns dz (grad of the residual
+    input when identity) and writes dh (and dh2 for the downsample BN)."""
+    M, C = h.shape
+    dz = torch.empty_like(h) if dz is None else dz
+    sums = torch.zeros(C, 3, device=h.device) if sums is None else sums.zero_()
+    p = L.fill(L.BnActParams, dtype=dtype_code(h), M=M, C=C, h=h, scale=st.scale, shift=st.shift, res=res,
+               scale2=None if st2 is None else st2.scale, shift2=None if st2 is None else st2.shift,
+               prelu=prelu, dy=dy, dz=dz, mean=st.mean, invstd=st.invstd,
+               mean2=None if st2 is None else st2.mean, invstd2=None if st2 is None else st2.invstd,
+               sums=sums, dprelu=dprelu, dgamma=dgamma, dbeta=dbeta, dgamma2=dgamma2, dbeta2=dbeta2,
+               dh=dh, dh2=dh2, beta_acc=beta_acc)
+    _call("avsr_bn_act_bwd_reduce", p)
+    _call("avsr_bn_bwd_apply", p)
+    return dz
+
+
+def stem_pool_fwd(h, nimg, H, W, st, prelu, y, argmax):
+    C = h.shape[-1]
+    _call("avsr_stem_pool_fwd", L.fill(L.StemPoolParams, dtype=dtype_code(h), nimg=nimg, H=H, W=W, C=C,
+                                        Ho=(H + 1) // 2, Wo=(W + 1) // 2, h=h, scale=st.scale, shift=st.shift,
+                                        prelu=prelu, y=y, argmax=argmax))
+    return y
+
+
+def stem_pool_bwd(dy, argmax, h, nimg, H, W, st, prelu, dh, *, dz=None, sums=None, dprelu=None,
+                  dgamma=None, dbeta=None):
+    """Backward through max-pool, PReLU and BN of the stem: writes dh (grad of the conv output)."""
+    C = h.shape[-1]
+    dz = torch.empty_like(h) if dz is None else dz
+    sums = torch.zeros(C, 3, device=h.device) if sums is None else sums.zero_()
+    sp = L.fill(L.StemPoolParams, dtype=dtype_code(h), nimg=nimg, H=H, W=W, C=C, Ho=(H + 1) // 2,
+                Wo=(W + 1) // 2, h=h, scale=st.scale, shift=st.shift, prelu=prelu, argmax=argmax, dy=dy, dz=dz,
+                mean=st.mean, invstd=st.invstd, sums=sums, dprelu=dprelu, dgamma=dgamma, dbeta=dbeta)
+    _call("avsr_stem_pool_bwd_reduce", sp)
+    M = nimg * H * W
+    _call("avsr_bn_bwd_apply", L.fill(L.BnActParams, dtype=dtype_code(h), M=M, C=C, h=h.view(M, C), scale=st.scale,
+                                       shift=st.shift, dz=dz, mean=st.mean, invstd=st.invstd, sums=sums, dh=dh))
+    return dh
+
+
+def avgpool_fwd(x, nimg, P, C, y):
+    L.check(L.load().avsr_avgpool_fwd(dtype_code(x), nimg, P, C, x.data_ptr(), y.data_ptr(), L.stream_ptr()),
+            "avsr_avgpool_fwd")
+    return y
+
+
+def avgpool_bwd(dy, nimg, P, C, dx):
+    L.check(L.load().avsr_avgpool_bwd(dtype_code(dy), nimg, P, C, dy.data_ptr(), dx.data_ptr(), L.stream_ptr()),
+            "avsr_avgpool_bwd")
+    return dx

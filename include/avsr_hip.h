@@ -97,7 +97,7 @@ typedef struct {
   int64_t ldx, ldy;
   const void* x; const void* w; void* y;   /* forward operands / output */
   void* dx; const void* dy; float* dw;     /* backward */
-  float* stats;   /* fwd only: [avsr_conv_stat_tiles()][groups*cout][3] (count, mean, M2) or NULL */
+  float* stats;   /* fwd only: [cout][avsr_conv_stat_tiles()][3] (count, mean, M2) or NULL */
   float alpha, beta;                       /* bwd_data scaling */
   int splitk;     /* bwd_weight: 0 = auto */
 } avsr_conv_params;
@@ -107,6 +107,96 @@ int avsr_conv_bwd_data(const avsr_conv_params* p, void* stream);
 int avsr_conv_bwd_weight(const avsr_conv_params* p, void* stream);
 /* number of row tiles the forward partial statistics are split into */
 int avsr_conv_stat_tiles(const avsr_conv_params* p);
+
+/* ------------------------------------------------------------------------------------
+ * LayerNorm over the last dim (rows of N), fp32 statistics.
+ * fwd: y = (x - mean) * rstd * gamma + beta; stores mean/rstd per row (fp32).
+ * bwd: dx = (dres ? dres : 0) + rstd * (g - mean(g) - xhat * mean(g * xhat)), g = dy * gamma;
+ *      dgamma += sum dy * xhat, dbeta += sum dy   (fp32, atomics)
+ * Replaces: torch.nn.LayerNorm at avhubert.py:184-185/:484 (2048, eps 1e-5),
+ *   HF:Wav2Vec2EncoderLayer layer_norm / final_layer_norm and encoder layer_norm (1e-5),
+ *   src/nets/backend/transformer/layer_norm.py:12-33 (decoder, eps 1e-12).
+ * ------------------------------------------------------------------------------------ */
+typedef struct {
+  int dtype, rows, N;
+  float eps;
+  const void* x; int64_t ldx;
+  void* y; int64_t ldy;
+  const float* gamma; const float* beta;
+  float* mean; float* rstd;                 /* [rows] */
+  const void* dy; int64_t lddy;             /* bwd */
+  void* dx; int64_t lddx;                   /* bwd output */
+  const void* dres; int64_t lddres;         /* bwd: residual gradient added to dx (may alias dx) */
+  float* dgamma; float* dbeta;              /* bwd: fp32 accumulators [N] or NULL */
+} avsr_layernorm_params;
+int avsr_layernorm_fwd(const avsr_layernorm_params* p, void* stream);
+int avsr_layernorm_bwd(const avsr_layernorm_params* p, void* stream);
+
+/* ------------------------------------------------------------------------------------
+ * BatchNorm (NHWC, per-channel) for the ResNet-18 lip frontend, resnet.py:30-164.
+ * finalize: combine conv-epilogue partials (count, mean, M2) -> mean / invstd; scale =
+ *   gamma*invstd, shift = beta - mean*scale; training also updates running stats
+ *   (momentum 0.1, unbiased running_var, as torch.nn.BatchNorm2d/3d). Eval mode builds
+ *   scale/shift from the running statistics.
+ * act_fwd: y = prelu(h*scale + shift + r), r = res (identity) or res*scale2 + shift2
+ *   (downsample BN) or 0;  prelu weight per channel (nn.PReLU(num_parameters=C)).
+ * act_bwd_reduce: z recomputed; dz = dy * prelu'(z) (stored); accumulates per channel
+ *   sum dz, sum dz*xhat (and for the downsample BN), prelu-weight grad sum dy*z*[z<=0];
+ *   also dgamma/dbeta of both BNs.
+ * bwd_apply: dh = scale*(dz - sum dz/M - xhat*sum(dz xhat)/M) (+beta*dh), same for the
+ *   downsample BN into dhd.
+ * ------------------------------------------------------------------------------------ */
+typedef struct {
+  int tiles, C;               /* partial tiles, channels */
+  const float* partials;      /* [C][tiles][3] or NULL (eval) */
+  const float* gamma; const float* beta;
+  float* running_mean; float* running_var;
+  float momentum, eps;
+  int training;
+  float* mean; float* invstd; float* scale; float* shift;   /* [C] outputs */
+} avsr_bn_finalize_params;
+int avsr_bn_finalize(const avsr_bn_finalize_params* p, void* stream);
+
+typedef struct {
+  int dtype, M, C;
+  const void* h;                                   /* conv output (pre-BN) [M][C] */
+  const float* scale; const float* shift;          /* BN of h */
+  const void* res;                                 /* residual [M][C] or NULL */
+  const float* scale2; const float* shift2;        /* BN of res (downsample) or NULL (identity) */
+  const float* prelu;                              /* [C] */
+  void* y;                                         /* fwd output */
+  /* backward */
+  const void* dy; void* dz;
+  const float* mean; const float* invstd;          /* BN of h (for xhat) */
+  const float* mean2; const float* invstd2;        /* BN of res when scale2 */
+  float* sums;    /* [C][5]: sum dz, sum dz*xhat, sum dz*xhat2, prelu grad (fp32, zeroed by caller) */
+  float* dprelu;  /* [C] fp32 grad accumulator */
+  float* dgamma; float* dbeta; float* dgamma2; float* dbeta2;   /* fp32 grad accumulators or NULL */
+  void* dh; void* dh2; float beta_acc;             /* bwd_apply outputs (dh2 for the downsample BN) */
+} avsr_bn_act_params;
+int avsr_bn_act_fwd(const avsr_bn_act_params* p, void* stream);
+int avsr_bn_act_bwd_reduce(const avsr_bn_act_params* p, void* stream);
+int avsr_bn_bwd_apply(const avsr_bn_act_params* p, void* stream);
+
+/* stem: y[n][oh][ow][c] = max_{3x3, s2, p1} prelu(bn(h)) (+argmax index),
+ * resnet.py:132-136 (BatchNorm3d + PReLU + MaxPool3d((1,3,3),(1,2,2),(0,1,1))).
+ * bwd_reduce: routes dy through the argmax and PReLU -> dz [n][h][w][c], with the BN
+ * reductions of avsr_bn_act_bwd_reduce (then avsr_bn_bwd_apply). */
+typedef struct {
+  int dtype, nimg, H, W, C, Ho, Wo;
+  const void* h; const float* scale; const float* shift; const float* prelu;
+  void* y; uint8_t* argmax;
+  const void* dy; void* dz;
+  const float* mean; const float* invstd;
+  float* sums; float* dprelu; float* dgamma; float* dbeta;
+} avsr_stem_pool_params;
+int avsr_stem_pool_fwd(const avsr_stem_pool_params* p, void* stream);
+int avsr_stem_pool_bwd_reduce(const avsr_stem_pool_params* p, void* stream);
+
+/* global average pool over P pixels: y[n][c] = mean_p x[n][p][c] (nn.AdaptiveAvgPool2d(1),
+ * resnet.py:83,121); bwd: dx[n][p][c] = dy[n][c] / P */
+int avsr_avgpool_fwd(int dtype, int nimg, int P, int C, const void* x, void* y, void* stream);
+int avsr_avgpool_bwd(int dtype, int nimg, int P, int C, const void* dy, void* dx, void* stream);
 
 #ifdef __cplusplus
 }

@@ -38,15 +38,16 @@ def test_conv2d(dev, dtype, case):
     wd = wt.permute(0, 2, 3, 1).contiguous().to(dev, dtype)
     y = torch.empty(n, ho, wo, cout, device=dev, dtype=dtype)
     tiles = ops.conv_stat_tiles(geom)
-    stats = torch.empty(tiles, cout, 3, device=dev)
+    stats = torch.empty(cout, tiles, 3, device=dev)
     ops.conv_fwd(geom, xd, wd, y, stats)
     tol = 3e-5 if dtype == torch.float32 else 2e-2
     assert _rel(y.permute(0, 3, 1, 2), ref) < tol
     # BN partial statistics combine to the batch mean / biased variance
     cnt, mean, m2 = stats[..., 0].double(), stats[..., 1].double(), stats[..., 2].double()
-    tot = cnt.sum(0)
-    gm = (cnt * mean).sum(0) / tot
-    var = (m2 + cnt * (mean - gm) ** 2).sum(0) / tot
+    tot = cnt.sum(1, keepdim=True)
+    gm = (cnt * mean).sum(1, keepdim=True) / tot
+    var = ((m2 + cnt * (mean - gm) ** 2).sum(1, keepdim=True) / tot).flatten()
+    gm = gm.flatten()
     rm = ref.mean(dim=(0, 2, 3)); rv = ref.var(dim=(0, 2, 3), unbiased=False)
     assert _rel(gm, rm) < (1e-4 if dtype == torch.float32 else 3e-2) or (gm - rm).abs().max() < 1e-3
     assert _rel(var, rv) < (1e-4 if dtype == torch.float32 else 3e-2)

@@ -1,0 +1,141 @@
+"""LayerNorm / BatchNorm(+PReLU, +residual) / stem max-pool / avg-pool kernels vs torch fp64."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from avsr_amd import ops
+
+pytestmark = pytest.mark.gpu
+
+
+def _rel(a, b):
+    a = a.detach().double().cpu(); b = b.detach().double().cpu()
+    return ((a - b).abs().max() / b.abs().max().clamp_min(1e-30)).item()
+
+
+def _tol(dtype, f32=2e-5, b16=2e-2):
+    return f32 if dtype == torch.float32 else b16
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("N,eps", [(1024, 1e-5), (2048, 1e-5), (256, 1e-12)])
+def test_layernorm(dev, dtype, N, eps):
+    g = torch.Generator().manual_seed(N)
+    rows = 777
+    x = torch.randn(rows, N, generator=g) * 2 + 0.5
+    gam = 1 + 0.1 * torch.randn(N, generator=g)
+    bet = 0.1 * torch.randn(N, generator=g)
+    dy = torch.randn(rows, N, generator=g)
+    dres = torch.randn(rows, N, generator=g)
+    xd = x.to(dev, dtype)
+    y, mean, rstd = ops.layernorm_fwd(xd, gam.to(dev), bet.to(dev), eps)
+    xr = xd.double().cpu().requires_grad_(); gr = gam.double().requires_grad_(); br = bet.double().requires_grad_()
+    ref = F.layer_norm(xr, (N,), gr, br, eps)
+    assert _rel(y, ref) < _tol(dtype, 1e-5)
+    ref.backward(dy.double())
+    dg = torch.zeros(N, device=dev); db = torch.zeros(N, device=dev)
+    dx = ops.layernorm_bwd(dy.to(dev, dtype), xd, gam.to(dev), mean, rstd, dres=dres.to(dev, dtype), dgamma=dg, dbeta=db)
+    assert _rel(dx, xr.grad + dres.double()) < _tol(dtype, 1e-5)
+    assert _rel(dg, gr.grad) < _tol(dtype, 1e-5)
+    assert _rel(db, br.grad) < _tol(dtype, 1e-5)
+
+
+def _partials(h, chunks=7):
+    """(count, mean, M2) per channel per row-chunk, layout [C][tiles][3]."""
+    parts = []
+    for c in h.double().chunk(chunks, 0):
+        n = torch.full((h.shape[1],), float(c.shape[0]), dtype=torch.float64)
+        m = c.mean(0)
+        parts.append(torch.stack([n, m, ((c - m) ** 2).sum(0)], -1))
+    return torch.stack(parts, 1).float()
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("mode", ["plain", "identity", "downsample"])
+def test_bn_act(dev, dtype, mode):
+    g = torch.Generator().manual_seed(11)
+    M, C = 3000, 128
+    h = torch.randn(M, C, generator=g) * 1.5 + 0.3
+    r = torch.randn(M, C, generator=g) * 0.7 - 0.2
+    gam = 1 + 0.1 * torch.randn(C, generator=g); bet = 0.1 * torch.randn(C, generator=g)
+    gam2 = 1 + 0.1 * torch.randn(C, generator=g); bet2 = 0.1 * torch.randn(C, generator=g)
+    a = 0.25 + 0.05 * torch.randn(C, generator=g)
+    rm = 0.1 * torch.randn(C, generator=g); rv = 0.5 + torch.rand(C, generator=g)
+    hd, rd = h.to(dev, dtype), r.to(dev, dtype)
+    st = ops.BnState(C, dev)
+    rmd, rvd = rm.clone().to(dev), rv.clone().to(dev)
+    ops.bn_finalize(st, gam.to(dev), bet.to(dev), rmd, rvd, partials=_partials(hd.float().cpu()).to(dev))
+    st2 = None
+    if mode == "downsample":
+        st2 = ops.BnState(C, dev)
+        ops.bn_finalize(st2, gam2.to(dev), bet2.to(dev), None, None, partials=_partials(rd.float().cpu()).to(dev))
+    y = torch.empty_like(hd)
+    ops.bn_act_fwd(hd, st, a.to(dev), y, res=None if mode == "plain" else rd, st2=st2)
+    # torch reference (train-mode BN, momentum 0.1, unbiased running var)
+    hr = hd.double().cpu().requires_grad_(); rr = rd.double().cpu().requires_grad_()
+    P = [t.double().requires_grad_() for t in (gam, bet, gam2, bet2, a)]
+    rm2, rv2 = rm.double().clone(), rv.double().clone()
+    z = F.batch_norm(hr, rm2, rv2, P[0], P[1], training=True, momentum=0.1, eps=1e-5)
+    if mode == "identity":
+        z = z + rr
+    elif mode == "downsample":
+        z = z + F.batch_norm(rr, None, None, P[2], P[3], training=True, eps=1e-5)
+    ref = F.prelu(z, P[4])
+    assert _rel(y, ref) < _tol(dtype, 1e-5)
+    assert _rel(rmd, rm2) < 1e-5 and _rel(rvd, rv2) < 1e-5
+    dy = torch.randn(M, C, generator=g)
+    ref.backward(dy.double())
+    dh = torch.empty_like(hd); dh2 = torch.empty_like(hd) if mode == "downsample" else None
+    grads = [torch.zeros(C, device=dev) for _ in range(5)]
+    dz = ops.bn_act_bwd(dy.to(dev, dtype), hd, st, a.to(dev), dh, res=None if mode == "plain" else rd, st2=st2,
+                        dh2=dh2, dprelu=grads[4], dgamma=grads[0], dbeta=grads[1],
+                        dgamma2=grads[2] if st2 else None, dbeta2=grads[3] if st2 else None)
+    tol = _tol(dtype, 1e-4, 3e-2)
+    assert _rel(dh, hr.grad) < tol
+    if mode == "identity":
+        assert _rel(dz, rr.grad) < tol
+    if mode == "downsample":
+        assert _rel(dh2, rr.grad) < tol
+        assert _rel(grads[2], P[2].grad) < tol and _rel(grads[3], P[3].grad) < tol
+    assert _rel(grads[0], P[0].grad) < tol and _rel(grads[1], P[1].grad) < tol
+    assert _rel(grads[4], P[4].grad) < tol
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_stem_pool(dev, dtype):
+    g = torch.Generator().manual_seed(5)
+    n, H, W, C = 6, 44, 44, 64
+    h = torch.randn(n, H, W, C, generator=g)
+    gam = 1 + 0.1 * torch.randn(C, generator=g); bet = 0.1 * torch.randn(C, generator=g)
+    a = 0.25 + 0.05 * torch.randn(C, generator=g)
+    hd = h.to(dev, dtype)
+    st = ops.BnState(C, dev)
+    ops.bn_finalize(st, gam.to(dev), bet.to(dev), None, None, partials=_partials(hd.float().cpu().view(-1, C)).to(dev))
+    y = torch.empty(n, 22, 22, C, device=dev, dtype=dtype)
+    am = torch.empty(n, 22, 22, C, device=dev, dtype=torch.uint8)
+    ops.stem_pool_fwd(hd, n, H, W, st, a.to(dev), y, am)
+    hr = hd.double().cpu().permute(0, 3, 1, 2).requires_grad_()
+    P = [t.double().requires_grad_() for t in (gam, bet, a)]
+    z = F.prelu(F.batch_norm(hr, None, None, P[0], P[1], training=True, eps=1e-5), P[2])
+    ref = F.max_pool2d(z, 3, 2, 1)
+    assert _rel(y.permute(0, 3, 1, 2), ref) < _tol(dtype, 1e-5)
+    dy = torch.randn(n, C, 22, 22, generator=g)
+    ref.backward(dy.double())
+    dh = torch.empty_like(hd)
+    grads = [torch.zeros(C, device=dev) for _ in range(3)]
+    ops.stem_pool_bwd(dy.permute(0, 2, 3, 1).contiguous().to(dev, dtype), am, hd, n, H, W, st, a.to(dev), dh,
+                      dgamma=grads[0], dbeta=grads[1], dprelu=grads[2])
+    tol = _tol(dtype, 1e-4, 3e-2)
+    assert _rel(dh.permute(0, 3, 1, 2), hr.grad) < tol
+    for gg, pp in zip(grads, P):
+        assert _rel(gg, pp.grad) < tol
+
+
+def test_avgpool(dev):
+    x = torch.randn(50, 9, 512, device=dev)
+    y = torch.empty(50, 512, device=dev)
+    ops.avgpool_fwd(x, 50, 9, 512, y)
+    assert _rel(y, x.mean(1)) < 1e-6
+    dx = torch.empty_like(x)
+    ops.avgpool_bwd(y, 50, 9, 512, dx)
+    assert _rel(dx, y[:, None, :].expand_as(x) / 9) < 1e-6
