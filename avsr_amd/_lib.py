@@ -94,6 +94,17 @@ class StemPoolParams(ctypes.Structure):
     ]
 
 
+class AttnParams(ctypes.Structure):
+    _fields_ = [
+        ("dtype", _i), ("B", _i), ("H", _i), ("Lq", _i), ("Lk", _i), ("scale", _f),
+        ("q", _c_p), ("ldq", _i64), ("k", _c_p), ("ldk", _i64), ("v", _c_p), ("ldv", _i64),
+        ("o", _c_p), ("ldo", _i64), ("lse", _c_p), ("klen", _c_p), ("causal", _i),
+        ("drop_p", _f), ("seed", ctypes.c_uint64),
+        ("dout", _c_p), ("lddo", _i64), ("delta", _c_p), ("dq", _c_p), ("lddq", _i64),
+        ("dk", _c_p), ("lddk", _i64), ("dv", _c_p), ("lddv", _i64),
+    ]
+
+
 def fill(struct_cls, **kw):
     """Build a params struct; torch tensors become raw device pointers, None -> NULL."""
     p = struct_cls()
@@ -124,6 +135,9 @@ SYMBOLS = {
     "avsr_stem_pool_bwd_reduce": ([ctypes.POINTER(StemPoolParams), _c_p], _i),
     "avsr_avgpool_fwd": ([_i, _i, _i, _i, _c_p, _c_p, _c_p], _i),
     "avsr_avgpool_bwd": ([_i, _i, _i, _i, _c_p, _c_p, _c_p], _i),
+    "avsr_attn_fwd": ([ctypes.POINTER(AttnParams), _c_p], _i),
+    "avsr_attn_bwd_prep": ([ctypes.POINTER(AttnParams), _c_p], _i),
+    "avsr_attn_bwd": ([ctypes.POINTER(AttnParams), _c_p], _i),
 }
 
 _lib = None

@@ -1,0 +1,412 @@
+// Fused multi-head attention (head dim 64) forward / backward on bf16 MFMA 32x32x16 tiles.
+// C-ABI: avsr_attn_fwd / avsr_attn_bwd_prep / avsr_attn_bwd (include/avsr_hip.h).
+//
+// Forward (one workgroup = 4 waves = 128 queries of one (batch, head); K/V tiles of 32 keys
+// staged in LDS and shared by the 4 waves):
+//   S^T = K Q^T with the query on the MFMA lane, so each lane owns one query row of the
+//   online softmax (16 of the 32 keys in registers, the other 16 on lane^32); P^T is then
+//   already the B operand of O^T += V^T P^T (accumulator-as-operand, no LDS round trip);
+//   V is staged transposed so its A fragments are two 8-byte LDS reads.
+// Backward (one workgroup = 4 waves = 128 keys; each wave owns 32 keys and keeps dK^T,
+//   dV^T in accumulators while sweeping all query tiles): S and dP are computed with the
+//   key on the lane so they feed dV^T += dO^T P' and dK^T += Q^T dS directly; dS crosses
+//   LDS once for dQ = dS K, which is summed over the 4 waves in LDS and added to an fp32
+//   accumulator with one atomic per element per workgroup.
+// fp32 storage ("parity mode") runs the same tiles on bf16 hi/lo splits (3 products).
+#include "common.h"
+
+namespace {
+
+constexpr int DH = 64;
+constexpr float LOG2E = 1.4426950408889634f;
+constexpr float LN2 = 0.6931471805599453f;
+
+struct Frag { bf16x8 hi, lo; };
+
+template <typename T> AVSR_DEV Frag mkfrag(const float* x) {
+  Frag f;
+  if constexpr (sizeof(T) == 2) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { f.hi[j] = (bf16)x[j]; f.lo[j] = (bf16)0.f; }
+  } else {
+    split8(x, f.hi, f.lo);
+  }
+  return f;
+}
+template <typename T> AVSR_DEV Frag zfrag() {
+  float z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  return mkfrag<T>(z);
+}
+// 8 contiguous elements
+template <typename T> AVSR_DEV Frag ld8(const T* p) {
+  if constexpr (sizeof(T) == 2) {
+    Frag f; f.hi = *(const bf16x8*)p; return f;
+  } else {
+    f32x4 a = *(const f32x4*)p, b = *(const f32x4*)(p + 4);
+    float x[8] = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+    return mkfrag<T>(x);
+  }
+}
+// two groups of 4 contiguous elements
+template <typename T> AVSR_DEV Frag ld4x2(const T* p0, const T* p1) {
+  if constexpr (sizeof(T) == 2) {
+    bf16x4 a = *(const bf16x4*)p0, b = *(const bf16x4*)p1;
+    Frag f;
+    f.hi = bf16x8{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+    return f;
+  } else {
+    f32x4 a = *(const f32x4*)p0, b = *(const f32x4*)p1;
+    float x[8] = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+    return mkfrag<T>(x);
+  }
+}
+// registers 8s..8s+7 of an accumulator as an operand fragment
+template <typename T, int S> AVSR_DEV Frag accfrag(const f32x16& x) {
+  float v[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = x[8 * S + j];
+  return mkfrag<T>(v);
+}
+template <typename T> AVSR_DEV void mm(f32x16& acc, const Frag& a, const Frag& b) {
+  acc = mfma32(a.hi, b.hi, acc);
+  if constexpr (sizeof(T) == 4) {
+    acc = mfma32(a.hi, b.lo, acc);
+    acc = mfma32(a.lo, b.hi, acc);
+  }
+}
+AVSR_DEV int qrow(int r, int hh) { return (r & 3) + 8 * (r >> 2) + 4 * hh; }
+AVSR_DEV void zacc(f32x16& x) {
+#pragma unroll
+  for (int r = 0; r < 16; ++r) x[r] = 0.f;
+}
+
+struct AttnArgs {
+  int B, H, Lq, Lk; float scale;
+  const void* q; int64_t ldq; const void* k; int64_t ldk; const void* v; int64_t ldv;
+  void* o; int64_t ldo; float* lse; const int* klen; int causal; float drop_p; uint64_t seed;
+  const void* dout; int64_t lddo; float* delta; float* dq; int64_t lddq;
+  void* dk; int64_t lddk; void* dv; int64_t lddv;
+};
+
+template <typename T> struct L {
+  static constexpr int VE = 16 / (int)sizeof(T);
+  static constexpr int KROW = DH + VE;                       // [rows][64] tiles, b128-aligned rows
+  static constexpr int VROW = 32 + (sizeof(T) == 2 ? 8 : 4); // [64][32] transposed tiles
+};
+
+// write a pair of accumulator tiles X[dt] (rows d = dt*32 + qrow, column = lane&31) transposed
+// (out row = column index) through the wave's LDS slab st[32][65]; rows r0.. of out
+template <typename T>
+AVSR_DEV void store_t(const f32x16& x0, const f32x16& x1, float mul, float* st, T* out, int64_t ld, int nvalid) {
+  const int l = threadIdx.x & 63, c = l & 31, hh = l >> 5;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    st[c * 65 + qrow(r, hh)] = x0[r] * mul;
+    st[c * 65 + 32 + qrow(r, hh)] = x1[r] * mul;
+  }
+  __syncthreads();
+  const int i = l >> 1, cb = (l & 1) * 32;
+  constexpr int VE = 16 / (int)sizeof(T);
+  if (i < nvalid) {
+#pragma unroll
+    for (int e = 0; e < 32; e += VE) {
+      float v[VE];
+#pragma unroll
+      for (int j = 0; j < VE; ++j) v[j] = st[i * 65 + cb + e + j];
+      stv(out + (int64_t)i * ld + cb + e, v);
+    }
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
+  constexpr int VE = L<T>::VE, KROW = L<T>::KROW, VROW = L<T>::VROW;
+  __shared__ __attribute__((aligned(16))) T Ks[32 * KROW];
+  __shared__ __attribute__((aligned(16))) T Vt[DH * VROW];
+  __shared__ __attribute__((aligned(16))) float Os[4 * 32 * 65];
+  const int b = blockIdx.y / a.H, h = blockIdx.y % a.H;
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, c = l & 31, hh = l >> 5;
+  const int q0 = blockIdx.x * 128 + w * 32, qi = q0 + c;
+  const T* Q = (const T*)a.q + (int64_t)b * a.Lq * a.ldq + h * DH;
+  const T* K = (const T*)a.k + (int64_t)b * a.Lk * a.ldk + h * DH;
+  const T* V = (const T*)a.v + (int64_t)b * a.Lk * a.ldv + h * DH;
+  Frag qf[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) qf[s] = qi < a.Lq ? ld8<T>(Q + (int64_t)qi * a.ldq + s * 16 + 8 * hh) : zfrag<T>();
+  f32x16 o0, o1;
+  zacc(o0); zacc(o1);
+  float m = -INFINITY, lsum = 0.f;
+  const int klen = a.klen ? min(a.klen[b], a.Lk) : a.Lk;
+  int kend = klen;
+  if (a.causal) kend = min(kend, (int)blockIdx.x * 128 + 128);
+  const float sl2 = a.scale * LOG2E;
+  const uint64_t dbase = ((uint64_t)(b * a.H + h) * a.Lq + qi) * (uint64_t)a.Lk;
+  for (int kt0 = 0; kt0 < kend; kt0 += 32) {
+    __syncthreads();
+    for (int v = tid; v < 32 * DH / VE; v += 256) {
+      const int key = v / (DH / VE), dv = (v % (DH / VE)) * VE;
+      v16 kv, vv;
+      if (kt0 + key < a.Lk) {
+        kv = *(const v16*)(K + (int64_t)(kt0 + key) * a.ldk + dv);
+        vv = *(const v16*)(V + (int64_t)(kt0 + key) * a.ldv + dv);
+      } else {
+        kv.w[0] = kv.w[1] = kv.w[2] = kv.w[3] = 0u; vv = kv;
+      }
+      *(v16*)&Ks[key * KROW + dv] = kv;
+      const T* ve = (const T*)&vv;
+#pragma unroll
+      for (int e = 0; e < VE; ++e) Vt[(dv + e) * VROW + key] = ve[e];
+    }
+    __syncthreads();
+    f32x16 st;
+    zacc(st);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) mm<T>(st, ld8<T>(&Ks[c * KROW + s * 16 + 8 * hh]), qf[s]);
+    float mt = -INFINITY;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int key = kt0 + qrow(r, hh);
+      const bool ok = key < klen && (!a.causal || key <= qi);
+      st[r] = ok ? st[r] * sl2 : -INFINITY;
+      mt = fmaxf(mt, st[r]);
+    }
+    mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+    const float mn = fmaxf(m, mt);
+    const float alpha = mn == -INFINITY ? 1.f : exp2f(m - mn);
+    float ps = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float p = st[r] == -INFINITY ? 0.f : exp2f(st[r] - mn);
+      ps += p;
+      st[r] = p;
+    }
+    ps += __shfl_xor(ps, 32, 64);
+    lsum = lsum * alpha + ps;
+    m = mn;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) { o0[r] *= alpha; o1[r] *= alpha; }
+    if (a.drop_p > 0.f) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) st[r] *= drop_scale(a.drop_p, a.seed, dbase + kt0 + qrow(r, hh));
+    }
+    const Frag pf0 = accfrag<T, 0>(st), pf1 = accfrag<T, 1>(st);
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt) {
+      const T* row = &Vt[(dt * 32 + c) * VROW + 4 * hh];
+      const Frag v0 = ld4x2<T>(row, row + 8), v1 = ld4x2<T>(row + 16, row + 24);
+      if (dt == 0) { mm<T>(o0, v0, pf0); mm<T>(o0, v1, pf1); }
+      else { mm<T>(o1, v0, pf0); mm<T>(o1, v1, pf1); }
+    }
+  }
+  const float inv = lsum > 0.f ? 1.f / lsum : 0.f;
+  if (hh == 0 && qi < a.Lq) a.lse[(int64_t)(b * a.H + h) * a.Lq + qi] = lsum > 0.f ? (m + log2f(lsum)) * LN2 : -INFINITY;
+  T* O = (T*)a.o + ((int64_t)b * a.Lq + q0) * a.ldo + h * DH;
+  store_t<T>(o0, o1, inv, Os + w * 32 * 65, O, a.ldo, a.Lq - q0);
+}
+
+// delta[b][h][i] = sum_d dO * O
+template <typename T>
+__global__ __launch_bounds__(256) void attn_prep_kernel(AttnArgs a) {
+  constexpr int VE = L<T>::VE;
+  const int64_t n = (int64_t)a.B * a.Lq * a.H;
+  for (int64_t t = blockIdx.x * 256 + threadIdx.x; t < n; t += (int64_t)gridDim.x * 256) {
+    const int h = (int)(t % a.H);
+    const int64_t row = t / a.H;                 // b*Lq + i
+    const T* o = (const T*)a.o + row * a.ldo + h * DH;
+    const T* d = (const T*)a.dout + row * a.lddo + h * DH;
+    float s = 0.f;
+#pragma unroll
+    for (int e = 0; e < DH; e += VE) {
+      float x[VE], y[VE];
+      ldv(o + e, x); ldv(d + e, y);
+#pragma unroll
+      for (int j = 0; j < VE; ++j) s += x[j] * y[j];
+    }
+    const int64_t b = row / a.Lq, i = row % a.Lq;
+    a.delta[(b * a.H + h) * a.Lq + i] = s;
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void attn_bwd_kernel(AttnArgs a) {
+  constexpr int VE = L<T>::VE, KROW = L<T>::KROW, VROW = L<T>::VROW, SROW = 32 + VE;
+  __shared__ __attribute__((aligned(16))) T Qs[32 * KROW];
+  __shared__ __attribute__((aligned(16))) T QsT[DH * VROW];
+  __shared__ __attribute__((aligned(16))) T dOs[32 * KROW];
+  __shared__ __attribute__((aligned(16))) T dOsT[DH * VROW];
+  __shared__ __attribute__((aligned(16))) T dSs[4 * 32 * SROW];
+  __shared__ __attribute__((aligned(16))) float red[4 * 32 * 65];
+  __shared__ float lse_s[32], dl_s[32];
+  const int b = blockIdx.y / a.H, h = blockIdx.y % a.H;
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, c = l & 31, hh = l >> 5;
+  const int kb0 = blockIdx.x * 128 + w * 32, key = kb0 + c;
+  const T* Q = (const T*)a.q + (int64_t)b * a.Lq * a.ldq + h * DH;
+  const T* K = (const T*)a.k + (int64_t)b * a.Lk * a.ldk + h * DH;
+  const T* V = (const T*)a.v + (int64_t)b * a.Lk * a.ldv + h * DH;
+  const T* dO = (const T*)a.dout + (int64_t)b * a.Lq * a.lddo + h * DH;
+  const float* LSE = a.lse + (int64_t)(b * a.H + h) * a.Lq;
+  const float* DL = a.delta + (int64_t)(b * a.H + h) * a.Lq;
+  Frag kf[4], vf[4], ktf[2][2];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    kf[s] = key < a.Lk ? ld8<T>(K + (int64_t)key * a.ldk + s * 16 + 8 * hh) : zfrag<T>();
+    vf[s] = key < a.Lk ? ld8<T>(V + (int64_t)key * a.ldv + s * 16 + 8 * hh) : zfrag<T>();
+  }
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      float x[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int kk = kb0 + s * 16 + 8 * hh + j;
+        x[j] = kk < a.Lk ? to_f(K[(int64_t)kk * a.ldk + dt * 32 + c]) : 0.f;
+      }
+      ktf[dt][s] = mkfrag<T>(x);
+    }
+  f32x16 dv0, dv1, dk0, dk1;
+  zacc(dv0); zacc(dv1); zacc(dk0); zacc(dk1);
+  const int klen = a.klen ? min(a.klen[b], a.Lk) : a.Lk;
+  const float sl2 = a.scale * LOG2E;
+  const int qstart = a.causal ? (int)blockIdx.x * 128 : 0;
+  T* dsw = dSs + w * 32 * SROW;
+  float* rw = red + w * 32 * 65;
+  for (int qt0 = qstart; qt0 < a.Lq; qt0 += 32) {
+    __syncthreads();
+    for (int v = tid; v < 32 * DH / VE; v += 256) {
+      const int qq = v / (DH / VE), dv = (v % (DH / VE)) * VE;
+      v16 qv, ov;
+      if (qt0 + qq < a.Lq) {
+        qv = *(const v16*)(Q + (int64_t)(qt0 + qq) * a.ldq + dv);
+        ov = *(const v16*)(dO + (int64_t)(qt0 + qq) * a.lddo + dv);
+      } else {
+        qv.w[0] = qv.w[1] = qv.w[2] = qv.w[3] = 0u; ov = qv;
+      }
+      *(v16*)&Qs[qq * KROW + dv] = qv;
+      *(v16*)&dOs[qq * KROW + dv] = ov;
+      const T* qe = (const T*)&qv;
+      const T* oe = (const T*)&ov;
+#pragma unroll
+      for (int e = 0; e < VE; ++e) {
+        QsT[(dv + e) * VROW + qq] = qe[e];
+        dOsT[(dv + e) * VROW + qq] = oe[e];
+      }
+    }
+    if (tid < 32) lse_s[tid] = qt0 + tid < a.Lq ? LSE[qt0 + tid] : 0.f;
+    else if (tid < 64) dl_s[tid - 32] = qt0 + tid - 32 < a.Lq ? DL[qt0 + tid - 32] : 0.f;
+    __syncthreads();
+    f32x16 sc, dp;
+    zacc(sc); zacc(dp);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      mm<T>(sc, ld8<T>(&Qs[c * KROW + s * 16 + 8 * hh]), kf[s]);
+      mm<T>(dp, ld8<T>(&dOs[c * KROW + s * 16 + 8 * hh]), vf[s]);
+    }
+    f32x16 pp, ds;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int ql = qrow(r, hh), q = qt0 + ql;
+      const bool ok = q < a.Lq && key < klen && (!a.causal || key <= q);
+      const float p = ok ? exp2f(sc[r] * sl2 - lse_s[ql] * LOG2E) : 0.f;
+      const float keep = (a.drop_p > 0.f && ok)
+          ? drop_scale(a.drop_p, a.seed, ((uint64_t)(b * a.H + h) * a.Lq + q) * (uint64_t)a.Lk + key) : 1.f;
+      ds[r] = p * (dp[r] * keep - dl_s[ql]) * a.scale;
+      pp[r] = p * keep;
+    }
+    const Frag pf0 = accfrag<T, 0>(pp), pf1 = accfrag<T, 1>(pp);
+    const Frag sf0 = accfrag<T, 0>(ds), sf1 = accfrag<T, 1>(ds);
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt) {
+      const T* ro = &dOsT[(dt * 32 + c) * VROW + 4 * hh];
+      const T* rq = &QsT[(dt * 32 + c) * VROW + 4 * hh];
+      const Frag a0 = ld4x2<T>(ro, ro + 8), a1 = ld4x2<T>(ro + 16, ro + 24);
+      const Frag b0 = ld4x2<T>(rq, rq + 8), b1 = ld4x2<T>(rq + 16, rq + 24);
+      if (dt == 0) { mm<T>(dv0, a0, pf0); mm<T>(dv0, a1, pf1); mm<T>(dk0, b0, sf0); mm<T>(dk0, b1, sf1); }
+      else { mm<T>(dv1, a0, pf0); mm<T>(dv1, a1, pf1); mm<T>(dk1, b0, sf0); mm<T>(dk1, b1, sf1); }
+    }
+    // dQ = dS K : dS through LDS (row q, column key)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dsw[qrow(r, hh) * SROW + c] = from_f<T>(ds[r]);
+    __syncthreads();
+    f32x16 dq0, dq1;
+    zacc(dq0); zacc(dq1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const Frag sa = ld8<T>(&dsw[c * SROW + s * 16 + 8 * hh]);
+      mm<T>(dq0, sa, ktf[0][s]);
+      mm<T>(dq1, sa, ktf[1][s]);
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      rw[qrow(r, hh) * 64 + c] = dq0[r];
+      rw[qrow(r, hh) * 64 + 32 + c] = dq1[r];
+    }
+    __syncthreads();
+    for (int e = tid; e < 32 * 64; e += 256) {
+      const int qq = e >> 6, d = e & 63;
+      const float v = red[e] + red[32 * 65 + e] + red[2 * 32 * 65 + e] + red[3 * 32 * 65 + e];
+      if (qt0 + qq < a.Lq && v != 0.f) atomicAdd(a.dq + ((int64_t)b * a.Lq + qt0 + qq) * a.lddq + h * DH + d, v);
+    }
+  }
+  __syncthreads();
+  T* DK = (T*)a.dk + ((int64_t)b * a.Lk + kb0) * a.lddk + h * DH;
+  store_t<T>(dk0, dk1, 1.f, rw, DK, a.lddk, a.Lk - kb0);
+  __syncthreads();
+  T* DV = (T*)a.dv + ((int64_t)b * a.Lk + kb0) * a.lddv + h * DH;
+  store_t<T>(dv0, dv1, 1.f, rw, DV, a.lddv, a.Lk - kb0);
+}
+
+AttnArgs args(const avsr_attn_params* p) {
+  AttnArgs a;
+  a.B = p->B; a.H = p->H; a.Lq = p->Lq; a.Lk = p->Lk; a.scale = p->scale;
+  a.q = p->q; a.ldq = p->ldq; a.k = p->k; a.ldk = p->ldk; a.v = p->v; a.ldv = p->ldv;
+  a.o = p->o; a.ldo = p->ldo; a.lse = p->lse; a.klen = p->klen; a.causal = p->causal;
+  a.drop_p = p->drop_p; a.seed = p->seed; a.dout = p->dout; a.lddo = p->lddo; a.delta = p->delta;
+  a.dq = p->dq; a.lddq = p->lddq; a.dk = p->dk; a.lddk = p->lddk; a.dv = p->dv; a.lddv = p->lddv;
+  return a;
+}
+
+int check(const avsr_attn_params* p) {
+  if (!p) return AVSR_E_ARG;
+  const int ve = p->dtype == AVSR_BF16 ? 8 : 4;
+  if (p->ldq % ve || p->ldk % ve || p->ldv % ve || p->ldo % ve) return AVSR_E_ALIGN;
+  if (p->dtype != AVSR_BF16 && p->dtype != AVSR_F32) return AVSR_E_DTYPE;
+  return 0;
+}
+
+}  // namespace
+
+extern "C" int avsr_attn_fwd(const avsr_attn_params* p, void* stream) {
+  int rc = check(p);
+  if (rc) return rc;
+  if (p->B * p->H == 0 || p->Lq == 0) return 0;
+  AttnArgs a = args(p);
+  dim3 grid((p->Lq + 127) / 128, p->B * p->H);
+  if (p->dtype == AVSR_BF16) hipLaunchKernelGGL(attn_fwd_kernel<bf16>, grid, dim3(256), 0, (hipStream_t)stream, a);
+  else hipLaunchKernelGGL(attn_fwd_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, a);
+  AVSR_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int avsr_attn_bwd_prep(const avsr_attn_params* p, void* stream) {
+  int rc = check(p);
+  if (rc) return rc;
+  AttnArgs a = args(p);
+  const int g = avsr_grid((int64_t)p->B * p->Lq * p->H);
+  if (p->dtype == AVSR_BF16) hipLaunchKernelGGL(attn_prep_kernel<bf16>, dim3(g), dim3(256), 0, (hipStream_t)stream, a);
+  else hipLaunchKernelGGL(attn_prep_kernel<float>, dim3(g), dim3(256), 0, (hipStream_t)stream, a);
+  AVSR_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int avsr_attn_bwd(const avsr_attn_params* p, void* stream) {
+  int rc = check(p);
+  if (rc) return rc;
+  if (p->B * p->H == 0 || p->Lk == 0) return 0;
+  AttnArgs a = args(p);
+  dim3 grid((p->Lk + 127) / 128, p->B * p->H);
+  if (p->dtype == AVSR_BF16) hipLaunchKernelGGL(attn_bwd_kernel<bf16>, grid, dim3(256), 0, (hipStream_t)stream, a);
+  else hipLaunchKernelGGL(attn_bwd_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, a);
+  AVSR_CHECK_LAUNCH();
+  return 0;
+}

@@ -284,3 +284,33 @@ def avgpool_bwd(dy, nimg, P, C, dx):
     L.check(L.load().avsr_avgpool_bwd(dtype_code(dy), nimg, P, C, dy.data_ptr(), dx.data_ptr(), L.stream_ptr()),
             "avsr_avgpool_bwd")
     return dx
+
+
+# ---------------------------------------------------------------------------------------
+# Fused attention (head dim 64). q/k/v/o are 2-D row views (rows = batch*len, head h at
+# columns h*64..h*64+63); they may be column slices of a fused QKV buffer.
+# ---------------------------------------------------------------------------------------
+
+def _attn_params(q, k, v, o, B, H, Lq, Lk, lse, klen, causal, scale, drop_p, seed):
+    return L.fill(L.AttnParams, dtype=dtype_code(q), B=B, H=H, Lq=Lq, Lk=Lk, scale=scale,
+                  q=q, ldq=q.stride(0), k=k, ldk=k.stride(0), v=v, ldv=v.stride(0), o=o, ldo=o.stride(0),
+                  lse=lse, klen=klen, causal=int(causal), drop_p=float(drop_p), seed=int(seed) & (2 ** 64 - 1))
+
+
+def attn_fwd(q, k, v, o, lse, *, B, H, Lq, Lk, klen=None, causal=False, scale=0.125, drop_p=0.0, seed=0):
+    p = _attn_params(q, k, v, o, B, H, Lq, Lk, lse, klen, causal, scale, drop_p, seed)
+    _call("avsr_attn_fwd", p)
+    return o
+
+
+def attn_bwd(dout, q, k, v, o, lse, dq32, dk, dv, delta, *, B, H, Lq, Lk, klen=None, causal=False,
+             scale=0.125, drop_p=0.0, seed=0):
+    """dq32: fp32 accumulator (zeroed by the caller), dk/dv in the activation dtype."""
+    p = _attn_params(q, k, v, o, B, H, Lq, Lk, lse, klen, causal, scale, drop_p, seed)
+    p.dout, p.lddo = dout.data_ptr(), dout.stride(0)
+    p.delta = delta.data_ptr()
+    p.dq, p.lddq = dq32.data_ptr(), dq32.stride(0)
+    p.dk, p.lddk = dk.data_ptr(), dk.stride(0)
+    p.dv, p.lddv = dv.data_ptr(), dv.stride(0)
+    _call("avsr_attn_bwd_prep", p)
+    _call("avsr_attn_bwd", p)

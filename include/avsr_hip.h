@@ -198,6 +198,42 @@ int avsr_stem_pool_bwd_reduce(const avsr_stem_pool_params* p, void* stream);
 int avsr_avgpool_fwd(int dtype, int nimg, int P, int C, const void* x, void* y, void* stream);
 int avsr_avgpool_bwd(int dtype, int nimg, int P, int C, const void* dy, void* dx, void* stream);
 
+/* ------------------------------------------------------------------------------------
+ * Fused multi-head attention, head dim 64, fp32 online softmax (flash-style; the Lq x Lk
+ * score matrix is never stored).  o = softmax(scale * q k^T + mask) v  per (batch, head).
+ *   q row (b, i), head h: q[(b*Lq + i)*ldq + h*64 .. +63]; likewise k, v (Lk rows), o.
+ *   mask: key j of batch b valid iff j < klen[b] (klen NULL: all Lk valid) and, if causal,
+ *   j <= i.  Optional dropout on the probabilities (counter-based; bwd recomputes it).
+ * fwd stores lse[b][h][i] (natural log) for the backward.
+ * bwd: dq (fp32 accumulator [B*Lq][ldq_f32], atomics, caller zeroes), dk, dv (dtype);
+ *   needs delta[b][h][i] = sum_d dO*O from avsr_attn_bwd_prep.
+ * Replaces: HF:eager_attention_forward + Wav2Vec2Attention core (:438-548; encoder, key
+ *   padding mask from avhubert.py:688-696) and MultiHeadedAttention.forward_attention
+ *   (src/nets/backend/transformer/attention.py:56-106; decoder causal self-attention and
+ *   memory-masked source attention).
+ * ------------------------------------------------------------------------------------ */
+typedef struct {
+  int dtype, B, H, Lq, Lk;
+  float scale;
+  const void* q; int64_t ldq;
+  const void* k; int64_t ldk;
+  const void* v; int64_t ldv;
+  void* o; int64_t ldo;
+  float* lse;                 /* [B][H][Lq] */
+  const int* klen;            /* [B] or NULL */
+  int causal;
+  float drop_p; uint64_t seed;
+  /* backward */
+  const void* dout; int64_t lddo;
+  float* delta;               /* [B][H][Lq] */
+  float* dq; int64_t lddq;    /* fp32 */
+  void* dk; int64_t lddk;
+  void* dv; int64_t lddv;
+} avsr_attn_params;
+int avsr_attn_fwd(const avsr_attn_params* p, void* stream);
+int avsr_attn_bwd_prep(const avsr_attn_params* p, void* stream);   /* delta = rowsum(dO * O) */
+int avsr_attn_bwd(const avsr_attn_params* p, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

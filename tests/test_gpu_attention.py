@@ -1,0 +1,127 @@
+"""Fused attention fwd/bwd vs a torch fp64 reference (encoder key-padding mask, decoder
+causal self-attention, decoder source attention, probability dropout)."""
+import math
+
+import pytest
+import torch
+
+from avsr_amd import ops
+
+pytestmark = pytest.mark.gpu
+
+
+def _rel(a, b):
+    a = a.detach().double().cpu(); b = b.detach().double().cpu()
+    return ((a - b).abs().max() / b.abs().max().clamp_min(1e-30)).item()
+
+
+def _ref(q, k, v, B, H, Lq, Lk, klen, causal, scale, mask_mult=None):
+    qh = q.view(B, Lq, H, 64).transpose(1, 2)
+    kh = k.view(B, Lk, H, 64).transpose(1, 2)
+    vh = v.view(B, Lk, H, 64).transpose(1, 2)
+    s = qh @ kh.transpose(-1, -2) * scale
+    m = torch.ones(B, 1, Lq, Lk, dtype=torch.bool)
+    if klen is not None:
+        m &= (torch.arange(Lk)[None, :] < torch.tensor(klen)[:, None])[:, None, None, :]
+    if causal:
+        m &= torch.tril(torch.ones(Lq, Lk, dtype=torch.bool))[None, None]
+    s = s.masked_fill(~m, float("-inf"))
+    p = torch.softmax(s, -1)
+    if mask_mult is not None:
+        p = p * mask_mult
+    return (p @ vh).transpose(1, 2).reshape(B * Lq, H * 64)
+
+
+CASES = [
+    # B, H, Lq, Lk, klen, causal
+    (3, 4, 75, 75, [75, 60, 33], False),
+    (2, 2, 41, 41, None, True),
+    (3, 2, 41, 150, [150, 77, 129], False),
+    (2, 16, 375, 375, [375, 301], False),
+]
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("case", CASES)
+def test_attention(dev, dtype, case):
+    B, H, Lq, Lk, klen, causal = case
+    D = H * 64
+    g = torch.Generator().manual_seed(B * 1000 + Lq)
+    qkv = torch.randn(B * Lq, 3 * D, generator=g)          # fused layout [q | k | v]
+    kv = torch.randn(B * Lk, 2 * D, generator=g)
+    q = qkv[:, :D]
+    if Lq == Lk:
+        k, v = qkv[:, D:2 * D], qkv[:, 2 * D:]
+    else:
+        k, v = kv[:, :D], kv[:, D:]
+    scale = 1 / math.sqrt(64)
+    qr, kr, vr = (t.double().clone().requires_grad_() for t in (q, k, v))
+    ref = _ref(qr, kr, vr, B, H, Lq, Lk, klen, causal, scale)
+    dout = torch.randn(B * Lq, D, generator=g)
+    ref.backward(dout.double())
+    # device copies (q/k/v as column slices of one buffer where the layout is fused)
+    if Lq == Lk:
+        buf = qkv.to(dev, dtype)
+        qd, kd, vd = buf[:, :D], buf[:, D:2 * D], buf[:, 2 * D:]
+    else:
+        qd = q.contiguous().to(dev, dtype)
+        kvd = kv.to(dev, dtype)
+        kd, vd = kvd[:, :D], kvd[:, D:]
+    o = torch.empty(B * Lq, D, device=dev, dtype=dtype)
+    lse = torch.empty(B, H, Lq, device=dev)
+    kl = None if klen is None else torch.tensor(klen, dtype=torch.int32, device=dev)
+    ops.attn_fwd(qd, kd, vd, o, lse, B=B, H=H, Lq=Lq, Lk=Lk, klen=kl, causal=causal, scale=scale)
+    tol = 3e-5 if dtype == torch.float32 else 2e-2
+    assert _rel(o, ref) < tol
+    dq = torch.zeros(B * Lq, D, device=dev)
+    dk = torch.empty(B * Lk, D, device=dev, dtype=dtype)
+    dv = torch.empty(B * Lk, D, device=dev, dtype=dtype)
+    delta = torch.empty(B, H, Lq, device=dev)
+    ops.attn_bwd(dout.to(dev, dtype), qd, kd, vd, o, lse, dq, dk, dv, delta, B=B, H=H, Lq=Lq, Lk=Lk,
+                 klen=kl, causal=causal, scale=scale)
+    gt = 1e-4 if dtype == torch.float32 else 3e-2
+    assert _rel(dq, qr.grad) < gt
+    assert _rel(dk, kr.grad) < gt
+    assert _rel(dv, vr.grad) < gt
+
+
+def test_attention_dropout(dev):
+    """Recover the dropout mask through V = one-hot rows (Lk <= 64), then check fwd/bwd
+    against the reference with that mask applied."""
+    B, H, L, p, seed = 2, 2, 48, 0.1, 77
+    D = H * 64
+    g = torch.Generator().manual_seed(1)
+    q = torch.randn(B * L, D, generator=g); k = torch.randn(B * L, D, generator=g)
+    eye = torch.zeros(B * L, D)
+    for b in range(B):
+        for j in range(L):
+            for h in range(H):
+                eye[b * L + j, h * 64 + j] = 1.0
+    qd, kd = q.to(dev), k.to(dev)
+    o = torch.empty(B * L, D, device=dev)
+    lse = torch.empty(B, H, L, device=dev)
+    ops.attn_fwd(qd, kd, eye.to(dev), o, lse, B=B, H=H, Lq=L, Lk=L, scale=0.125, drop_p=p, seed=seed)
+    pm = o.cpu().double().view(B, L, H, 64)[..., :L].permute(0, 2, 1, 3)       # P' (B, H, L, L)
+    qh = q.double().view(B, L, H, 64).transpose(1, 2); kh = k.double().view(B, L, H, 64).transpose(1, 2)
+    pr = torch.softmax(qh @ kh.transpose(-1, -2) * 0.125, -1)
+    mult = (pm / pr).round(decimals=3)
+    kept = (mult > 0.5)
+    assert 0.85 < kept.double().mean().item() < 0.95
+    assert torch.allclose(mult[kept], torch.full_like(mult[kept], 1 / (1 - p)), atol=1e-3)
+    mask_mult = kept.double() / (1 - p)
+    v = torch.randn(B * L, D, generator=g)
+    qr, kr, vr = (t.double().clone().requires_grad_() for t in (q, k, v))
+    ref = _ref(qr, kr, vr, B, H, L, L, None, False, 0.125, mask_mult)
+    dout = torch.randn(B * L, D, generator=g)
+    ref.backward(dout.double())
+    vd = v.to(dev)
+    ops.attn_fwd(qd, kd, vd, o, lse, B=B, H=H, Lq=L, Lk=L, scale=0.125, drop_p=p, seed=seed)
+    assert _rel(o, ref) < 3e-5
+    dq = torch.zeros(B * L, D, device=dev)
+    dk = torch.empty(B * L, D, device=dev); dv = torch.empty(B * L, D, device=dev)
+    delta = torch.empty(B, H, L, device=dev)
+    ops.attn_bwd(dout.to(dev), qd, kd, vd, o, lse, dq, dk, dv, delta, B=B, H=H, Lq=L, Lk=L, scale=0.125,
+                 drop_p=p, seed=seed)
+    assert _rel(dq, qr.grad) < 1e-4
+    assert _rel(dk, kr.grad) < 1e-4
+    assert _rel(dv, vr.grad) < 1e-4
