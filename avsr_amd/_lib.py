@@ -105,15 +105,59 @@ class AttnParams(ctypes.Structure):
     ]
 
 
+class XentParams(ctypes.Structure):
+    _fields_ = [
+        ("dtype", _i), ("rows", _i), ("V", _i), ("x", _c_p), ("ldx", _i64), ("target", _c_p),
+        ("smoothing", _f), ("lse", _c_p), ("row_loss", _c_p), ("row_correct", _c_p),
+        ("dloss", _c_p), ("coef", _f), ("dx", _c_p), ("lddx", _i64),
+    ]
+
+
+class CtcParams(ctypes.Structure):
+    _fields_ = [
+        ("dtype", _i), ("B", _i), ("T", _i), ("V", _i), ("Lmax", _i), ("x", _c_p), ("ldx", _i64),
+        ("lse", _c_p), ("labels", _c_p), ("label_len", _c_p), ("in_len", _c_p),
+        ("alpha", _c_p), ("gamma", _c_p), ("nll", _c_p), ("dloss", _c_p), ("coef", _f),
+        ("dx", _c_p), ("lddx", _i64),
+    ]
+
+
+class EwParams(ctypes.Structure):
+    _fields_ = [
+        ("dtype", _i), ("rows", _i), ("N", _i), ("dy", _c_p), ("lddy", _i64), ("out", _c_p), ("ldout", _i64),
+        ("gate", _c_p), ("ldgate", _i64), ("act", _i), ("drop_p", _f), ("seed", ctypes.c_uint64),
+        ("alpha", _f), ("db", _c_p),
+    ]
+
+
+class EmbedParams(ctypes.Structure):
+    _fields_ = [
+        ("dtype", _i), ("rows", _i), ("L", _i), ("D", _i), ("tok", _c_p), ("table", _c_p), ("pe", _c_p),
+        ("scale", _f), ("y", _c_p), ("drop_p", _f), ("seed", ctypes.c_uint64), ("dy", _c_p), ("dtable", _c_p),
+    ]
+
+
+class AdamWParams(ctypes.Structure):
+    _fields_ = [
+        ("n", _i64), ("param", _c_p), ("grad", _c_p), ("exp_avg", _c_p), ("exp_avg_sq", _c_p),
+        ("shadow", _c_p), ("shadow_dtype", _i), ("lr", _f), ("beta1", _f), ("beta2", _f), ("eps", _f),
+        ("weight_decay", _f), ("bias_corr1", _f), ("bias_corr2", _f), ("sumsq", _c_p), ("max_norm", _f),
+        ("grad_scale", _f),
+    ]
+
+
 def fill(struct_cls, **kw):
     """Build a params struct; torch tensors become raw device pointers, None -> NULL."""
     p = struct_cls()
+    keep = []
     for k, v in kw.items():
         if v is None:
             continue
         if isinstance(v, torch.Tensor):
+            keep.append(v)          # the struct owns a reference: no use-after-free of temporaries
             v = v.data_ptr()
         setattr(p, k, v)
+    p._keep = keep
     return p
 
 
@@ -138,6 +182,26 @@ SYMBOLS = {
     "avsr_attn_fwd": ([ctypes.POINTER(AttnParams), _c_p], _i),
     "avsr_attn_bwd_prep": ([ctypes.POINTER(AttnParams), _c_p], _i),
     "avsr_attn_bwd": ([ctypes.POINTER(AttnParams), _c_p], _i),
+    "avsr_row_lse": ([ctypes.POINTER(XentParams), _c_p], _i),
+    "avsr_lsm_fwd": ([ctypes.POINTER(XentParams), _c_p], _i),
+    "avsr_lsm_bwd": ([ctypes.POINTER(XentParams), _c_p], _i),
+    "avsr_ctc_fwd": ([ctypes.POINTER(CtcParams), _c_p], _i),
+    "avsr_ctc_bwd": ([ctypes.POINTER(CtcParams), _c_p], _i),
+    "avsr_loss_finalize": ([_i, _c_p, _i, _c_p, _c_p, _f, _c_p, _c_p], _i),
+    "avsr_ew_bwd": ([ctypes.POINTER(EwParams), _c_p], _i),
+    "avsr_dropout_fwd": ([ctypes.POINTER(EwParams), _c_p], _i),
+    "avsr_mask_rows": ([_i, _i, _i, _i, _c_p, _i64, _c_p, _c_p], _i),
+    "avsr_embed_fwd": ([ctypes.POINTER(EmbedParams), _c_p], _i),
+    "avsr_embed_bwd": ([ctypes.POINTER(EmbedParams), _c_p], _i),
+    "avsr_cast": ([_i, _i, _i, _i, _c_p, _i64, _c_p, _i64, _f, _f, _c_p], _i),
+    "avsr_stem_pack": ([_i, _i, _i, _c_p, _c_p, _c_p], _i),
+    "avsr_stem_wpack": ([_i, _c_p, _c_p, _c_p], _i),
+    "avsr_stem_wgrad_unpack": ([_c_p, _c_p, _c_p], _i),
+    "avsr_audio_pack": ([_i, _i, _i, _i, _c_p, _c_p, _c_p], _i),
+    "avsr_weightnorm_fwd": ([_i, _i, _i, _i, _c_p, _c_p, _c_p, _c_p, _c_p], _i),
+    "avsr_weightnorm_bwd": ([_i, _i, _i, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p], _i),
+    "avsr_sumsq": ([_c_p, _i64, _c_p, _c_p], _i),
+    "avsr_adamw": ([ctypes.POINTER(AdamWParams), _c_p], _i),
 }
 
 _lib = None

@@ -1,0 +1,380 @@
+// Elementwise / data-movement kernels around the GEMMs (declarations, reference call sites:
+// include/avsr_hip.h): bias-gradient column sums with dropout/activation masks, dropout,
+// padded-frame masking, decoder embedding + positional encoding, casts, stem/audio input
+// packing, pos-conv weight norm, and the fused clip-grad-norm + AdamW step.
+// All HBM-bound: 16-byte vectors where the layout allows, grid-stride loops.
+#include "common.h"
+
+namespace {
+
+struct EwArgs {
+  int rows, N;
+  const void* dy; int64_t lddy; void* out; int64_t ldout;
+  const void* gate; int64_t ldgate; int act;
+  float drop_p; uint64_t seed; float alpha; float* db;
+};
+
+template <typename T>
+__global__ __launch_bounds__(256) void ew_bwd_kernel(EwArgs a) {
+  constexpr int VE = VecW<T>::VE;
+  const int nv = a.N / VE;
+  const int cv = blockIdx.x * 256 + threadIdx.x;
+  if (cv >= nv) return;
+  float acc[VE];
+#pragma unroll
+  for (int j = 0; j < VE; ++j) acc[j] = 0.f;
+  for (int r = blockIdx.y; r < a.rows; r += gridDim.y) {
+    float d[VE], g[VE];
+    ldv((const T*)a.dy + (int64_t)r * a.lddy + cv * VE, d);
+    if (a.gate) ldv((const T*)a.gate + (int64_t)r * a.ldgate + cv * VE, g);
+#pragma unroll
+    for (int j = 0; j < VE; ++j) {
+      float v = d[j] * a.alpha;
+      if (a.drop_p > 0.f) v *= drop_scale(a.drop_p, a.seed, (uint64_t)r * a.N + cv * VE + j);
+      if (a.gate) v *= act_bwd(a.act, g[j]);
+      acc[j] += v;
+      d[j] = v;
+    }
+    if (a.out) stv((T*)a.out + (int64_t)r * a.ldout + cv * VE, d);
+  }
+  if (a.db)
+#pragma unroll
+    for (int j = 0; j < VE; ++j) atomicAdd(a.db + cv * VE + j, acc[j]);
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void mask_rows_kernel(int B, int T_, int N, T* x, int64_t ldx, const int* len) {
+  constexpr int VE = VecW<T>::VE;
+  const int nv = N / VE;
+  const int64_t total = (int64_t)B * T_ * nv;
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int64_t row = i / nv;
+    const int b = (int)(row / T_), t = (int)(row % T_);
+    if (t >= len[b]) {
+      float z[VE];
+#pragma unroll
+      for (int j = 0; j < VE; ++j) z[j] = 0.f;
+      stv(x + row * ldx + (i % nv) * VE, z);
+    }
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void embed_kernel(avsr_embed_params p, int bwd) {
+  constexpr int VE = VecW<T>::VE;
+  const int nv = p.D / VE;
+  const int64_t total = (int64_t)p.rows * nv;
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int r = (int)(i / nv), d0 = (int)(i % nv) * VE;
+    const int tok = p.tok[r];
+    const int pos = r % p.L;
+    if (!bwd) {
+      float e[VE], o[VE];
+      ldv((const T*)p.table + (int64_t)tok * p.D + d0, e);
+#pragma unroll
+      for (int j = 0; j < VE; ++j) {
+        float v = e[j] * p.scale + p.pe[(int64_t)pos * p.D + d0 + j];
+        if (p.drop_p > 0.f) v *= drop_scale(p.drop_p, p.seed, (uint64_t)r * p.D + d0 + j);
+        o[j] = v;
+      }
+      stv((T*)p.y + (int64_t)r * p.D + d0, o);
+    } else {
+      float g[VE];
+      ldv((const T*)p.dy + (int64_t)r * p.D + d0, g);
+#pragma unroll
+      for (int j = 0; j < VE; ++j) {
+        float v = g[j] * p.scale;
+        if (p.drop_p > 0.f) v *= drop_scale(p.drop_p, p.seed, (uint64_t)r * p.D + d0 + j);
+        atomicAdd(p.dtable + (int64_t)tok * p.D + d0 + j, v);
+      }
+    }
+  }
+}
+
+template <typename S, typename D>
+__global__ __launch_bounds__(256) void cast_kernel(int rows, int cols, const S* src, int64_t lds, D* dst,
+                                                   int64_t ldd, float alpha, float beta) {
+  const int64_t total = (int64_t)rows * cols;
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int64_t r = i / cols, c = i % cols;
+    float v = alpha * to_f(src[r * lds + c]);
+    if (beta != 0.f) v += beta * to_f(dst[r * ldd + c]);
+    dst[r * ldd + c] = from_f<D>(v);
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void stem_pack_kernel(int B, int T_, const float* video, T* out) {
+  constexpr int HW = 88 * 88;
+  const int64_t total = (int64_t)B * T_ * HW;
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int64_t frame = i / HW;
+    const int pix = (int)(i % HW);
+    const int b = (int)(frame / T_), t = (int)(frame % T_);
+    float o[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const int tt = t + c - 2;
+      o[c] = (c < 5 && tt >= 0 && tt < T_) ? video[((int64_t)b * T_ + tt) * HW + pix] : 0.f;
+    }
+    if constexpr (sizeof(T) == 2) {
+      stv(out + i * 8, o);
+    } else {
+      stv(out + i * 8, o);
+      stv(out + i * 8 + 4, o + 4);
+    }
+  }
+}
+
+template <typename T>
+__global__ void stem_wpack_kernel(const float* w, T* wp) {
+  const int i = blockIdx.x * 256 + threadIdx.x;   // [64][7][7][8]
+  if (i >= 64 * 49 * 8) return;
+  const int c = i % 8, khw = (i / 8) % 49, o = i / (49 * 8);
+  wp[i] = from_f<T>(c < 5 ? w[(o * 5 + c) * 49 + khw] : 0.f);
+}
+
+__global__ void stem_wgrad_unpack_kernel(const float* gp, float* gw) {
+  const int i = blockIdx.x * 256 + threadIdx.x;   // [64][5][7][7]
+  if (i >= 64 * 5 * 49) return;
+  const int khw = i % 49, c = (i / 49) % 5, o = i / (5 * 49);
+  gw[i] += gp[(o * 49 + khw) * 8 + c];
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void audio_pack_kernel(int B, int F, int T_, const float* a, T* out) {
+  const int64_t total = (int64_t)B * T_ * F;
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int f = (int)(i % F);
+    const int64_t bt = i / F;
+    const int b = (int)(bt / T_), t = (int)(bt % T_);
+    out[i] = from_f<T>(a[((int64_t)b * F + f) * T_ + t]);
+  }
+}
+
+// norm[k] = ||v[:, k, :]||  (v stored [O][K][C]); one block per k
+__global__ __launch_bounds__(256) void wn_norm_kernel(int O, int K, int C, const float* v, const float* dw,
+                                                      float* out) {
+  const int k = blockIdx.x;
+  float s = 0.f;
+  for (int i = threadIdx.x; i < O * C; i += 256) {
+    const int o = i / C, c = i % C;
+    const int64_t idx = ((int64_t)o * K + k) * C + c;
+    s += dw ? dw[idx] * v[idx] : v[idx] * v[idx];
+  }
+  s = wave_sum(s);
+  __shared__ float sh[4];
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float t = sh[0] + sh[1] + sh[2] + sh[3];
+    out[k] = dw ? t : sqrtf(t);
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void wn_apply_kernel(int O, int K, int C, const float* v, const float* g,
+                                                       const float* norm, T* w) {
+  const int64_t total = (int64_t)O * K * C;
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int k = (int)((i / C) % K);
+    w[i] = from_f<T>(g[k] * v[i] / norm[k]);
+  }
+}
+
+__global__ __launch_bounds__(256) void wn_bwd_kernel(int O, int K, int C, const float* v, const float* g,
+                                                     const float* norm, const float* dw, const float* s,
+                                                     float* dv) {
+  const int64_t total = (int64_t)O * K * C;
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int k = (int)((i / C) % K);
+    const float n = norm[k];
+    dv[i] += g[k] / n * dw[i] - g[k] * s[k] / (n * n * n) * v[i];
+  }
+}
+
+__global__ void wn_dg_kernel(int K, const float* s, const float* norm, float* dg) {
+  const int k = blockIdx.x * 256 + threadIdx.x;
+  if (k < K) dg[k] += s[k] / norm[k];
+}
+
+__global__ __launch_bounds__(256) void sumsq_kernel(const float* x, int64_t n, float* out) {
+  float s = 0.f;
+  const int64_t n4 = n / 4;
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+    const f32x4 v = ((const f32x4*)x)[i];
+    s += v[0] * v[0] + v[1] * v[1] + v[2] * v[2] + v[3] * v[3];
+  }
+  if (blockIdx.x == 0)
+    for (int64_t i = n4 * 4 + threadIdx.x; i < n; i += 256) s += x[i] * x[i];
+  s = wave_sum(s);
+  __shared__ float sh[4];
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) atomicAdd(out, sh[0] + sh[1] + sh[2] + sh[3]);
+}
+
+template <typename S>
+__global__ __launch_bounds__(256) void adamw_kernel(avsr_adamw_params p) {
+  float coef = p.grad_scale;
+  if (p.sumsq) {
+    const float tn = sqrtf(*p.sumsq) * p.grad_scale;
+    coef *= fminf(1.f, p.max_norm / (tn + 1e-6f));
+  }
+  const float step = p.lr / p.bias_corr1;
+  const float rbc2 = 1.f / sqrtf(p.bias_corr2);
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < p.n; i += (int64_t)gridDim.x * 256) {
+    const float g = p.grad[i] * coef;
+    float w = p.param[i];
+    w -= p.lr * p.weight_decay * w;
+    const float m = p.beta1 * p.exp_avg[i] + (1.f - p.beta1) * g;
+    const float v = p.beta2 * p.exp_avg_sq[i] + (1.f - p.beta2) * g * g;
+    p.exp_avg[i] = m;
+    p.exp_avg_sq[i] = v;
+    w -= step * m / (sqrtf(v) * rbc2 + p.eps);
+    p.param[i] = w;
+    if (p.shadow) ((S*)p.shadow)[i] = from_f<S>(w);
+  }
+}
+
+EwArgs ew_args(const avsr_ew_params* p) {
+  EwArgs a;
+  a.rows = p->rows; a.N = p->N; a.dy = p->dy; a.lddy = p->lddy; a.out = p->out; a.ldout = p->ldout;
+  a.gate = p->gate; a.ldgate = p->ldgate; a.act = p->act; a.drop_p = p->drop_p; a.seed = p->seed;
+  a.alpha = p->alpha; a.db = p->db;
+  return a;
+}
+
+int ew_launch(const avsr_ew_params* p, hipStream_t st) {
+  const int ve = p->dtype == AVSR_BF16 ? 8 : 4;
+  if (p->N % ve) return AVSR_E_SHAPE;
+  if (p->rows == 0) return 0;
+  const int nv = p->N / ve;
+  dim3 grid((nv + 255) / 256, 1);
+  int gy = 1024 / (int)grid.x;
+  gy = gy < 1 ? 1 : (gy > p->rows ? p->rows : gy);
+  grid.y = gy;
+  EwArgs a = ew_args(p);
+  if (p->dtype == AVSR_BF16) hipLaunchKernelGGL(ew_bwd_kernel<bf16>, grid, dim3(256), 0, st, a);
+  else hipLaunchKernelGGL(ew_bwd_kernel<float>, grid, dim3(256), 0, st, a);
+  AVSR_CHECK_LAUNCH();
+  return 0;
+}
+
+}  // namespace
+
+extern "C" int avsr_ew_bwd(const avsr_ew_params* p, void* stream) {
+  if (!p) return AVSR_E_ARG;
+  return ew_launch(p, (hipStream_t)stream);
+}
+
+extern "C" int avsr_dropout_fwd(const avsr_ew_params* p, void* stream) {
+  if (!p || !p->out) return AVSR_E_ARG;
+  avsr_ew_params q = *p;
+  q.gate = nullptr; q.db = nullptr;
+  return ew_launch(&q, (hipStream_t)stream);
+}
+
+extern "C" int avsr_mask_rows(int dtype, int B, int T, int N, void* x, int64_t ldx, const int* len, void* stream) {
+  const int ve = dtype == AVSR_BF16 ? 8 : 4;
+  if (N % ve || ldx % ve) return AVSR_E_ALIGN;
+  const int g = avsr_grid((int64_t)B * T * N / ve);
+  if (dtype == AVSR_BF16) hipLaunchKernelGGL(mask_rows_kernel<bf16>, dim3(g), dim3(256), 0, (hipStream_t)stream, B, T, N, (bf16*)x, ldx, len);
+  else hipLaunchKernelGGL(mask_rows_kernel<float>, dim3(g), dim3(256), 0, (hipStream_t)stream, B, T, N, (float*)x, ldx, len);
+  AVSR_CHECK_LAUNCH();
+  return 0;
+}
+
+static int embed_launch(const avsr_embed_params* p, int bwd, hipStream_t st) {
+  const int ve = p->dtype == AVSR_BF16 ? 8 : 4;
+  if (p->D % ve) return AVSR_E_SHAPE;
+  const int g = avsr_grid((int64_t)p->rows * p->D / ve);
+  if (p->dtype == AVSR_BF16) hipLaunchKernelGGL(embed_kernel<bf16>, dim3(g), dim3(256), 0, st, *p, bwd);
+  else hipLaunchKernelGGL(embed_kernel<float>, dim3(g), dim3(256), 0, st, *p, bwd);
+  AVSR_CHECK_LAUNCH();
+  return 0;
+}
+extern "C" int avsr_embed_fwd(const avsr_embed_params* p, void* stream) { return p ? embed_launch(p, 0, (hipStream_t)stream) : AVSR_E_ARG; }
+extern "C" int avsr_embed_bwd(const avsr_embed_params* p, void* stream) { return p ? embed_launch(p, 1, (hipStream_t)stream) : AVSR_E_ARG; }
+
+extern "C" int avsr_cast(int sd, int dd, int rows, int cols, const void* src, int64_t lds, void* dst, int64_t ldd,
+                         float alpha, float beta, void* stream) {
+  const int g = avsr_grid((int64_t)rows * cols);
+  hipStream_t st = (hipStream_t)stream;
+  if (sd == AVSR_F32 && dd == AVSR_BF16) hipLaunchKernelGGL((cast_kernel<float, bf16>), dim3(g), dim3(256), 0, st, rows, cols, (const float*)src, lds, (bf16*)dst, ldd, alpha, beta);
+  else if (sd == AVSR_F32 && dd == AVSR_F32) hipLaunchKernelGGL((cast_kernel<float, float>), dim3(g), dim3(256), 0, st, rows, cols, (const float*)src, lds, (float*)dst, ldd, alpha, beta);
+  else if (sd == AVSR_BF16 && dd == AVSR_F32) hipLaunchKernelGGL((cast_kernel<bf16, float>), dim3(g), dim3(256), 0, st, rows, cols, (const bf16*)src, lds, (float*)dst, ldd, alpha, beta);
+  else if (sd == AVSR_BF16 && dd == AVSR_BF16) hipLaunchKernelGGL((cast_kernel<bf16, bf16>), dim3(g), dim3(256), 0, st, rows, cols, (const bf16*)src, lds, (bf16*)dst, ldd, alpha, beta);
+  else return AVSR_E_DTYPE;
+  AVSR_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int avsr_stem_pack(int dtype, int B, int T, const float* video, void* out, void* stream) {
+  const int g = avsr_grid((int64_t)B * T * 88 * 88);
+  if (dtype == AVSR_BF16) hipLaunchKernelGGL(stem_pack_kernel<bf16>, dim3(g), dim3(256), 0, (hipStream_t)stream, B, T, video, (bf16*)out);
+  else hipLaunchKernelGGL(stem_pack_kernel<float>, dim3(g), dim3(256), 0, (hipStream_t)stream, B, T, video, (float*)out);
+  AVSR_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int avsr_stem_wpack(int dtype, const float* w, void* wp, void* stream) {
+  const int g = (64 * 49 * 8 + 255) / 256;
+  if (dtype == AVSR_BF16) hipLaunchKernelGGL(stem_wpack_kernel<bf16>, dim3(g), dim3(256), 0, (hipStream_t)stream, w, (bf16*)wp);
+  else hipLaunchKernelGGL(stem_wpack_kernel<float>, dim3(g), dim3(256), 0, (hipStream_t)stream, w, (float*)wp);
+  AVSR_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int avsr_stem_wgrad_unpack(const float* gp, float* gw, void* stream) {
+  hipLaunchKernelGGL(stem_wgrad_unpack_kernel, dim3((64 * 5 * 49 + 255) / 256), dim3(256), 0, (hipStream_t)stream, gp, gw);
+  AVSR_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int avsr_audio_pack(int dtype, int B, int F, int T, const float* audio, void* out, void* stream) {
+  const int g = avsr_grid((int64_t)B * T * F);
+  if (dtype == AVSR_BF16) hipLaunchKernelGGL(audio_pack_kernel<bf16>, dim3(g), dim3(256), 0, (hipStream_t)stream, B, F, T, audio, (bf16*)out);
+  else hipLaunchKernelGGL(audio_pack_kernel<float>, dim3(g), dim3(256), 0, (hipStream_t)stream, B, F, T, audio, (float*)out);
+  AVSR_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int avsr_weightnorm_fwd(int dtype, int O, int K, int C, const float* v, const float* g, float* norm,
+                                   void* w, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(wn_norm_kernel, dim3(K), dim3(256), 0, st, O, K, C, v, (const float*)nullptr, norm);
+  const int gr = avsr_grid((int64_t)O * K * C);
+  if (dtype == AVSR_BF16) hipLaunchKernelGGL(wn_apply_kernel<bf16>, dim3(gr), dim3(256), 0, st, O, K, C, v, g, norm, (bf16*)w);
+  else hipLaunchKernelGGL(wn_apply_kernel<float>, dim3(gr), dim3(256), 0, st, O, K, C, v, g, norm, (float*)w);
+  AVSR_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int avsr_weightnorm_bwd(int O, int K, int C, const float* v, const float* g, const float* norm,
+                                   const float* dw, float* dv, float* dg, float* scratch, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(wn_norm_kernel, dim3(K), dim3(256), 0, st, O, K, C, v, dw, scratch);
+  hipLaunchKernelGGL(wn_dg_kernel, dim3((K + 255) / 256), dim3(256), 0, st, K, (const float*)scratch, norm, dg);
+  hipLaunchKernelGGL(wn_bwd_kernel, dim3(avsr_grid((int64_t)O * K * C)), dim3(256), 0, st, O, K, C, v, g, norm, dw,
+                     (const float*)scratch, dv);
+  AVSR_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int avsr_sumsq(const float* x, int64_t n, float* out, void* stream) {
+  if (!avsr_aligned16(x)) return AVSR_E_ALIGN;
+  hipLaunchKernelGGL(sumsq_kernel, dim3(avsr_grid(n / 4 + 1, 256, 1024)), dim3(256), 0, (hipStream_t)stream, x, n, out);
+  AVSR_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int avsr_adamw(const avsr_adamw_params* p, void* stream) {
+  if (!p) return AVSR_E_ARG;
+  if (p->n == 0) return 0;
+  const int g = avsr_grid(p->n, 256, 4096);
+  if (p->shadow_dtype == AVSR_F32) hipLaunchKernelGGL(adamw_kernel<float>, dim3(g), dim3(256), 0, (hipStream_t)stream, *p);
+  else hipLaunchKernelGGL(adamw_kernel<bf16>, dim3(g), dim3(256), 0, (hipStream_t)stream, *p);
+  AVSR_CHECK_LAUNCH();
+  return 0;
+}

@@ -314,3 +314,153 @@ def attn_bwd(dout, q, k, v, o, lse, dq32, dk, dv, delta, *, B, H, Lq, Lk, klen=N
     p.dv, p.lddv = dv.data_ptr(), dv.stride(0)
     _call("avsr_attn_bwd_prep", p)
     _call("avsr_attn_bwd", p)
+
+
+# ---------------------------------------------------------------------------------------
+# Losses
+# ---------------------------------------------------------------------------------------
+
+def _p(t):
+    return None if t is None else t.data_ptr()
+
+
+def row_lse(x, V, lse):
+    _call("avsr_row_lse", L.fill(L.XentParams, dtype=dtype_code(x), rows=x.shape[0], V=V, x=x,
+                                  ldx=x.stride(0), lse=lse))
+    return lse
+
+
+def lsm_fwd(x, V, target, smoothing, lse, row_loss, row_correct):
+    _call("avsr_lsm_fwd", L.fill(L.XentParams, dtype=dtype_code(x), rows=x.shape[0], V=V, x=x, ldx=x.stride(0),
+                                  target=target, smoothing=smoothing, lse=lse, row_loss=row_loss,
+                                  row_correct=row_correct))
+
+
+def lsm_bwd(x, V, target, smoothing, lse, dloss, coef, dx):
+    _call("avsr_lsm_bwd", L.fill(L.XentParams, dtype=dtype_code(x), rows=x.shape[0], V=V, x=x, ldx=x.stride(0),
+                                  target=target, smoothing=smoothing, lse=lse, dloss=dloss, coef=coef,
+                                  dx=dx, lddx=dx.stride(0)))
+    return dx
+
+
+def ctc_params(x, B, T, V, labels, label_len, in_len, lse, alpha, gamma, nll):
+    return L.fill(L.CtcParams, dtype=dtype_code(x), B=B, T=T, V=V, Lmax=labels.shape[1], x=x, ldx=x.stride(0),
+                  lse=lse, labels=labels, label_len=label_len, in_len=in_len, alpha=alpha, gamma=gamma, nll=nll)
+
+
+def ctc_fwd(p):
+    _call("avsr_ctc_fwd", p)
+
+
+def ctc_bwd(p, dloss, coef, dx):
+    p.dloss, p.coef, p.dx, p.lddx = dloss.data_ptr(), coef, dx.data_ptr(), dx.stride(0)
+    _call("avsr_ctc_bwd", p)
+    return dx
+
+
+def loss_finalize(B, nll, row_loss, row_correct, mtlalpha, out):
+    L.check(L.load().avsr_loss_finalize(B, nll.data_ptr(), row_loss.shape[0], row_loss.data_ptr(),
+                                        _p(row_correct), mtlalpha, out.data_ptr(), L.stream_ptr()),
+            "avsr_loss_finalize")
+    return out
+
+
+# ---------------------------------------------------------------------------------------
+# Elementwise / data movement
+# ---------------------------------------------------------------------------------------
+
+def ew_bwd(dy, *, out=None, gate=None, act=L.ACT_NONE, drop_p=0.0, seed=0, alpha=1.0, db=None):
+    rows, N = dy.shape
+    _call("avsr_ew_bwd", L.fill(L.EwParams, dtype=dtype_code(dy), rows=rows, N=N, dy=dy, lddy=dy.stride(0),
+                                 out=out, ldout=0 if out is None else out.stride(0), gate=gate,
+                                 ldgate=0 if gate is None else gate.stride(0), act=act, drop_p=float(drop_p),
+                                 seed=int(seed) & (2 ** 64 - 1), alpha=alpha, db=db))
+    return out
+
+
+def dropout_fwd(x, out, p, seed):
+    rows, N = x.shape
+    _call("avsr_dropout_fwd", L.fill(L.EwParams, dtype=dtype_code(x), rows=rows, N=N, dy=x, lddy=x.stride(0),
+                                      out=out, ldout=out.stride(0), drop_p=float(p),
+                                      seed=int(seed) & (2 ** 64 - 1), alpha=1.0))
+    return out
+
+
+def mask_rows(x, B, T, lengths):
+    L.check(L.load().avsr_mask_rows(dtype_code(x), B, T, x.shape[1], x.data_ptr(), x.stride(0),
+                                    lengths.data_ptr(), L.stream_ptr()), "avsr_mask_rows")
+    return x
+
+
+def embed_fwd(tok, table, pe, scale, y, L_, drop_p=0.0, seed=0):
+    _call("avsr_embed_fwd", L.fill(L.EmbedParams, dtype=dtype_code(table), rows=tok.shape[0], L=L_,
+                                    D=table.shape[1], tok=tok, table=table, pe=pe, scale=scale, y=y,
+                                    drop_p=float(drop_p), seed=int(seed) & (2 ** 64 - 1)))
+    return y
+
+
+def embed_bwd(tok, dy, scale, dtable, L_, drop_p=0.0, seed=0):
+    _call("avsr_embed_bwd", L.fill(L.EmbedParams, dtype=dtype_code(dy), rows=tok.shape[0], L=L_,
+                                    D=dy.shape[1], tok=tok, scale=scale, dy=dy, dtable=dtable,
+                                    drop_p=float(drop_p), seed=int(seed) & (2 ** 64 - 1)))
+
+
+def cast(src, dst, alpha=1.0, beta=0.0):
+    rows, cols = src.shape
+    assert dst.shape == src.shape
+    L.check(L.load().avsr_cast(dtype_code(src), dtype_code(dst), rows, cols, src.data_ptr(), src.stride(0),
+                               dst.data_ptr(), dst.stride(0), alpha, beta, L.stream_ptr()), "avsr_cast")
+    return dst
+
+
+def stem_pack(videos, out):
+    B, _, T = videos.shape[:3]
+    assert videos.dtype == torch.float32 and videos.is_contiguous()
+    L.check(L.load().avsr_stem_pack(dtype_code(out), B, T, videos.data_ptr(), out.data_ptr(), L.stream_ptr()),
+            "avsr_stem_pack")
+    return out
+
+
+def stem_wpack(w, wp):
+    L.check(L.load().avsr_stem_wpack(dtype_code(wp), w.data_ptr(), wp.data_ptr(), L.stream_ptr()), "avsr_stem_wpack")
+    return wp
+
+
+def stem_wgrad_unpack(gp, gw):
+    L.check(L.load().avsr_stem_wgrad_unpack(gp.data_ptr(), gw.data_ptr(), L.stream_ptr()), "avsr_stem_wgrad_unpack")
+
+
+def audio_pack(audios, out):
+    B, F, T = audios.shape
+    assert audios.dtype == torch.float32 and audios.is_contiguous()
+    L.check(L.load().avsr_audio_pack(dtype_code(out), B, F, T, audios.data_ptr(), out.data_ptr(), L.stream_ptr()),
+            "avsr_audio_pack")
+    return out
+
+
+def weightnorm_fwd(v, g, norm, w):
+    O, K, C = v.shape
+    L.check(L.load().avsr_weightnorm_fwd(dtype_code(w), O, K, C, v.data_ptr(), g.data_ptr(), norm.data_ptr(),
+                                         w.data_ptr(), L.stream_ptr()), "avsr_weightnorm_fwd")
+
+
+def weightnorm_bwd(v, g, norm, dw, dv, dg, scratch):
+    O, K, C = v.shape
+    L.check(L.load().avsr_weightnorm_bwd(O, K, C, v.data_ptr(), g.data_ptr(), norm.data_ptr(), dw.data_ptr(),
+                                         dv.data_ptr(), dg.data_ptr(), scratch.data_ptr(), L.stream_ptr()),
+            "avsr_weightnorm_bwd")
+
+
+def sumsq(x, out):
+    L.check(L.load().avsr_sumsq(x.data_ptr(), x.numel(), out.data_ptr(), L.stream_ptr()), "avsr_sumsq")
+    return out
+
+
+def adamw(param, grad, exp_avg, exp_avg_sq, *, lr, beta1, beta2, eps, weight_decay, step, shadow=None,
+          sumsq_buf=None, max_norm=1.0, grad_scale=1.0):
+    _call("avsr_adamw", L.fill(L.AdamWParams, n=param.numel(), param=param, grad=grad, exp_avg=exp_avg,
+                                exp_avg_sq=exp_avg_sq, shadow=shadow,
+                                shadow_dtype=L.AVSR_BF16 if shadow is None else dtype_code(shadow),
+                                lr=lr, beta1=beta1, beta2=beta2, eps=eps, weight_decay=weight_decay,
+                                bias_corr1=1 - beta1 ** step, bias_corr2=1 - beta2 ** step,
+                                sumsq=sumsq_buf, max_norm=max_norm, grad_scale=grad_scale))

@@ -234,6 +234,119 @@ int avsr_attn_fwd(const avsr_attn_params* p, void* stream);
 int avsr_attn_bwd_prep(const avsr_attn_params* p, void* stream);   /* delta = rowsum(dO * O) */
 int avsr_attn_bwd(const avsr_attn_params* p, void* stream);
 
+/* ------------------------------------------------------------------------------------
+ * Losses on logits [rows][ldx] (V valid columns; columns V..ldx-1 of every gradient row are
+ * written as 0 so padded GEMM operands stay finite).
+ * avsr_row_lse:   lse[row] = log sum_k exp(x[row][k])
+ * avsr_lsm_fwd:   LabelSmoothingLoss rows (src/nets/backend/transformer/label_smoothing_loss.py
+ *   :41-63, KL(q || softmax) with q = smoothing/(V-1) off-target, 1-smoothing on target,
+ *   target -1 ignored) -> row_loss, and th_accuracy's argmax match (nets_utils.py:303-323)
+ * avsr_lsm_bwd:   dx = (*dloss * coef) * (softmax - q), 0 on ignored rows
+ * avsr_ctc_fwd:   torch.nn.CTCLoss(blank=0, reduction none, zero_infinity=True) per utterance
+ *   (ctc.py:64-81): log-space alpha and beta over the extended label sequence; nll[b] and the
+ *   state occupancies gamma[b][t][s] = P(path at state s at t | x) (0 if infeasible)
+ * avsr_ctc_bwd:   dx[b,t,k] = (*dloss * coef) * (softmax_t(k) - sum_{s: ext_s = k} gamma_t(s))
+ *   for t < in_len[b] (0 otherwise and for infeasible utterances)
+ * avsr_loss_finalize: loss_ctc = sum nll / B, loss_att = sum row_loss / B,
+ *   loss = mtl*ctc + (1-mtl)*att, acc = correct / valid  (e2e_asr_avhubert.py:150-159)
+ *   out[4] = {loss, loss_ctc, loss_att, acc}, all on device (no host sync)
+ * ------------------------------------------------------------------------------------ */
+typedef struct {
+  int dtype, rows, V;
+  const void* x; int64_t ldx;
+  const int* target;        /* [rows], -1 = ignore */
+  float smoothing;
+  float* lse; float* row_loss; int* row_correct;   /* [rows]; row_correct: 1/0, -1 ignored */
+  const float* dloss; float coef;
+  void* dx; int64_t lddx;
+} avsr_xent_params;
+int avsr_row_lse(const avsr_xent_params* p, void* stream);
+int avsr_lsm_fwd(const avsr_xent_params* p, void* stream);
+int avsr_lsm_bwd(const avsr_xent_params* p, void* stream);
+
+typedef struct {
+  int dtype, B, T, V, Lmax;
+  const void* x; int64_t ldx;          /* rows b*T + t */
+  const float* lse;                    /* [B*T] */
+  const int* labels;                   /* [B][Lmax] */
+  const int* label_len; const int* in_len;   /* [B] */
+  float* alpha; float* gamma;          /* workspaces [B][T][2*Lmax+1] */
+  float* nll;                          /* [B] */
+  const float* dloss; float coef;
+  void* dx; int64_t lddx;
+} avsr_ctc_params;
+int avsr_ctc_fwd(const avsr_ctc_params* p, void* stream);
+int avsr_ctc_bwd(const avsr_ctc_params* p, void* stream);
+
+int avsr_loss_finalize(int B, const float* nll, int rows, const float* row_loss, const int* row_correct,
+                       float mtlalpha, float* out, void* stream);
+
+/* ------------------------------------------------------------------------------------
+ * Elementwise / data-movement kernels around the GEMMs.
+ * avsr_ew_bwd:     out = alpha * dy * dropmask(drop_p, seed; idx = row*N + col) * act'(gate),
+ *                  db[n] += sum_rows out  (bias gradients of the Linear layers; out optional)
+ * avsr_dropout_fwd: out = dy * dropmask (nn.Dropout on a [rows][N] view: CTC input dropout
+ *                  ctc.py:27,98, encoder dropout after pos-conv avhubert.py:704)
+ * avsr_mask_rows:  x[b*T + t][:] = 0 for t >= len[b]   (avhubert.py:683-686)
+ * avsr_embed_fwd:  y[r] = dropout(table[tok[r]] * scale + pe[r % L])  (decoder embed +
+ *                  PositionalEncoding, decoder.py:89-93, embedding.py:80-87); bwd: fp32
+ *                  atomics into dtable
+ * avsr_cast:       dst = alpha * src + beta * dst over a [rows][cols] strided view
+ * avsr_stem_pack:  videos (B,1,T,88,88) fp32 -> (B*T, 88, 88, 8): channel c = frame t+c-2
+ *                  (c < 5, zero outside [0,T)), the Conv3d(k=5x7x7, pad 2x3x3) stem as a 2-D conv
+ * avsr_stem_wpack / avsr_stem_wgrad_unpack: Conv3d weight (64,1,5,7,7) <-> [64][7][7][8]
+ * avsr_audio_pack: audios (B, F, T) fp32 -> (B*T, F)  (SubModel.proj input, avhubert.py:194-196)
+ * avsr_weightnorm_fwd/bwd: w = g * v / ||v|| per tap k, v stored [o][k][c] (HF weight_norm
+ *                  dim=2 of the pos-conv, modeling_wav2vec2.py:336-356)
+ * avsr_sumsq / avsr_adamw: fused clip_grad_norm_(max_norm) + torch.optim.AdamW step over a
+ *                  flat fp32 parameter range; optionally refreshes the bf16 shadow copy
+ * ------------------------------------------------------------------------------------ */
+typedef struct {
+  int dtype, rows, N;
+  const void* dy; int64_t lddy;
+  void* out; int64_t ldout;
+  const void* gate; int64_t ldgate; int act;
+  float drop_p; uint64_t seed;
+  float alpha;
+  float* db;
+} avsr_ew_params;
+int avsr_ew_bwd(const avsr_ew_params* p, void* stream);
+int avsr_dropout_fwd(const avsr_ew_params* p, void* stream);
+int avsr_mask_rows(int dtype, int B, int T, int N, void* x, int64_t ldx, const int* len, void* stream);
+
+typedef struct {
+  int dtype, rows, L, D;
+  const int* tok; const void* table; const float* pe; float scale;
+  void* y; float drop_p; uint64_t seed;
+  const void* dy; float* dtable;
+} avsr_embed_params;
+int avsr_embed_fwd(const avsr_embed_params* p, void* stream);
+int avsr_embed_bwd(const avsr_embed_params* p, void* stream);
+
+int avsr_cast(int src_dtype, int dst_dtype, int rows, int cols, const void* src, int64_t lds,
+              void* dst, int64_t ldd, float alpha, float beta, void* stream);
+int avsr_stem_pack(int dtype, int B, int T, const float* video, void* out, void* stream);
+int avsr_stem_wpack(int dtype, const float* w, void* wp, void* stream);
+int avsr_stem_wgrad_unpack(const float* gp, float* gw, void* stream);
+int avsr_audio_pack(int dtype, int B, int F, int T, const float* audio, void* out, void* stream);
+
+int avsr_weightnorm_fwd(int dtype, int O, int K, int C, const float* v, const float* g, float* norm,
+                        void* w, void* stream);
+int avsr_weightnorm_bwd(int O, int K, int C, const float* v, const float* g, const float* norm,
+                        const float* dw, float* dv, float* dg, float* scratch, void* stream);
+
+int avsr_sumsq(const float* x, int64_t n, float* out, void* stream);
+typedef struct {
+  int64_t n;
+  float* param; const float* grad; float* exp_avg; float* exp_avg_sq;
+  void* shadow; int shadow_dtype;        /* bf16 copy of the updated params, or NULL */
+  float lr, beta1, beta2, eps, weight_decay;
+  float bias_corr1, bias_corr2;          /* 1 - beta^t */
+  const float* sumsq; float max_norm;    /* clip: coef = min(1, max_norm / (sqrt(*sumsq) + 1e-6)); sumsq NULL = no clip */
+  float grad_scale;                      /* extra multiplier on the gradient (1/accumulation etc.) */
+} avsr_adamw_params;
+int avsr_adamw(const avsr_adamw_params* p, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
