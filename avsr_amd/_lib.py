@@ -53,6 +53,7 @@ class ConvParams(ctypes.Structure):
         ("stats", _c_p),
         ("alpha", _f), ("beta", _f),
         ("splitk", _i),
+        ("bias", _c_p), ("act", _i), ("preact", _c_p), ("res", _c_p),
     ]
 
 

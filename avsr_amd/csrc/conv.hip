@@ -66,6 +66,9 @@ __global__ __launch_bounds__(NT) void conv_kernel(ConvArgs a) {
   }
   Epi e = a.e;
   e.C = (OutT*)e.C + (int64_t)grp * a.c_gstride;
+  if (e.res) e.res = (const T*)e.res + (int64_t)grp * a.c_gstride;
+  if (e.preact) e.preact = (T*)e.preact + (int64_t)grp * a.c_gstride;
+  if (e.bias) e.bias += (int64_t)grp * a.c_gstride;
   epilogue<T, OutT, WM, WN>(e, m0, n0, acc, smem);
 }
 
@@ -117,6 +120,8 @@ extern "C" int avsr_conv_fwd(const avsr_conv_params* p, void* stream) {
   base_epi(a.e);
   a.e.M = a.M; a.e.N = a.N; a.e.C = p->y; a.e.ldc = p->ldy; a.e.stats = p->stats;
   a.e.stats_tiles = avsr_conv_stat_tiles(p);
+  a.e.bias = p->bias; a.e.act = p->act; a.e.preact = p->preact; a.e.res = p->res; a.e.ldr = p->ldy;
+  if (p->stats && (p->bias || p->act || p->res)) return AVSR_E_ARG;
   if (a.M == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
   if (p->dtype == AVSR_F32) return by_tile<float, float, K_FWD>(a, p->groups, st);

@@ -1,0 +1,701 @@
+"""The AVSR hot path on MI355X: explicit forward and backward of E2E (encoder + CTC +
+attention decoder + joint loss) as a sequence of libavsr_hip.so launches.
+
+Reference semantics (quanpn90/avsr @ 2025-08-29):
+  E2E.forward                  src/nets/backend/e2e_asr_avhubert.py:119-159
+  AVHubertModel.forward_gen    src/nets/backend/backbones/avhubert.py:448-544
+  ResEncoder                   src/nets/backend/backbones/resnet.py:126-164
+  AVHubertEncoder(+Layer)      avhubert.py:668-768 (+ HF Wav2Vec2 modules)
+  CTC                          src/nets/backend/ctc.py:64-151
+  Decoder / DecoderLayer       src/nets/backend/transformer/decoder.py:122-151, decoder_layer.py:58-121
+  LabelSmoothingLoss           src/nets/backend/transformer/label_smoothing_loss.py:41-63
+
+Design (MI355X-first):
+  * one process per GPU; all math in hand-written HIP kernels (ops.*); activations NHWC /
+    row-major [tokens][features] in the compute dtype (bf16, or fp32 "parity mode");
+  * no autograd graph inside the model: the forward saves exactly what the backward
+    needs, the backward is written out layer by layer and accumulates fp32 weight
+    gradients straight into the flat Arena buffer (fused bias/activation/dropout/residual
+    epilogues, fused BatchNorm statistics, flash attention, fused loss gradients);
+  * dropout masks are counter-based (seed, element index): recomputed in the backward,
+    never stored; the loss and its gradient never leave the device (no host sync).
+"""
+import math
+import random
+
+import torch
+
+from . import ops
+from . import _lib as L
+from .arena import Arena
+
+GELU, RELU, NONE = L.ACT_GELU, L.ACT_RELU, L.ACT_NONE
+
+
+def _pad8(n):
+    return (n + 7) // 8 * 8
+
+
+class _Seeds:
+    """deterministic per-site dropout stream ids for one step"""
+
+    def __init__(self, base):
+        self.base = base & 0xFFFFFFFFFFFF
+        self.i = 0
+
+    def next(self):
+        self.i += 1
+        return (self.base * 0x9E3779B97F4A7C15 + self.i * 0xBF58476D1CE4E5B9) & 0xFFFFFFFFFFFFFFFF
+
+
+def positional_encoding(L_, d, device):
+    """embedding.py:59-78 sinusoidal table (fp32)."""
+    pe = torch.zeros(L_, d)
+    pos = torch.arange(0, L_, dtype=torch.float32).unsqueeze(1)
+    div = torch.exp(torch.arange(0, d, 2, dtype=torch.float32) * -(math.log(10000.0) / d))
+    pe[:, 0::2] = torch.sin(pos * div)
+    pe[:, 1::2] = torch.cos(pos * div)
+    return pe.to(device)
+
+
+class Engine:
+    RES_BLOCKS = [(1, 0, 64, 64, 1), (1, 1, 64, 64, 1), (2, 0, 64, 128, 2), (2, 1, 128, 128, 1),
+                  (3, 0, 128, 256, 2), (3, 1, 256, 256, 1), (4, 0, 256, 512, 2), (4, 1, 512, 512, 1)]
+
+    def __init__(self, shell, cfg, device, dtype=torch.bfloat16):
+        self.cfg = cfg
+        self.device = torch.device(device)
+        self.dtype = dtype
+        self.D = cfg.hidden_size
+        self.H = cfg.num_attention_heads
+        self.F = cfg.intermediate_size
+        self.nl = cfg.num_hidden_layers
+        self.dD = cfg.ddim
+        self.dH = cfg.dheads
+        self.dF = cfg.dunits
+        self.dl = cfg.dlayers
+        self.V = cfg.odim
+        self.Vp = _pad8(cfg.odim)
+        self.G = cfg.num_conv_pos_embedding_groups
+        self.PK = cfg.num_conv_pos_embeddings
+        assert self.D // self.H == 64 and self.dD // self.dH == 64, "kernels use head dim 64"
+        assert cfg.adim == self.D == self.dD, "proj_decoder (adim != ddim) not on the hot path"
+        E = "encoder.encoder.layers"
+        groups = []
+        for i in range(self.nl):
+            a = f"{E}.{i}.attention."
+            groups.append([a + "q_proj.weight", a + "k_proj.weight", a + "v_proj.weight"])
+            groups.append([a + "q_proj.bias", a + "k_proj.bias", a + "v_proj.bias"])
+        for i in range(self.dl):
+            s = f"decoder.decoders.{i}.self_attn."
+            groups.append([s + "linear_q.weight", s + "linear_k.weight", s + "linear_v.weight"])
+            groups.append([s + "linear_q.bias", s + "linear_k.bias", s + "linear_v.bias"])
+            c = f"decoder.decoders.{i}.src_attn."
+            groups.append([c + "linear_k.weight", c + "linear_v.weight"])
+            groups.append([c + "linear_k.bias", c + "linear_v.bias"])
+        perms = {}
+        for n, p in shell.named_parameters():
+            if p.dim() == 4:
+                perms[n] = (0, 2, 3, 1)
+        self.pc = "encoder.encoder.pos_conv_embed.conv."
+        perms[self.pc + "parametrizations.weight.original1"] = (0, 2, 1)
+        pad_rows = {"decoder.output_layer.weight": self.Vp, "ctc.ctc_lo.weight": self.Vp,
+                    "decoder.output_layer.bias": self.Vp, "ctc.ctc_lo.bias": self.Vp}
+        frozen = ["encoder.mask_emb", "encoder.label_embs_concat"]
+        # buffers (BN running statistics) to the device
+        for m in shell.modules():
+            for k, b in list(m._buffers.items()):
+                if b is not None:
+                    m._buffers[k] = b.to(self.device)
+        self.arena = Arena(shell, self.device, dtype, fuse_groups=groups, pad_rows=pad_rows, perms=perms, frozen=frozen)
+        self.shell = shell
+        self.step_count = 0
+        self._pe = positional_encoding(max(512, 64), self.dD, self.device)
+        self._stem_wp = None
+
+    # ------------------------------------------------------------------------------ utils
+    def _e(self, *shape, dtype=None):
+        return torch.empty(*shape, device=self.device, dtype=dtype or self.dtype)
+
+    def _z(self, *shape, dtype=None):
+        return torch.zeros(*shape, device=self.device, dtype=dtype or self.dtype)
+
+    def w(self, n):
+        return self.arena.w(n)
+
+    def g(self, n):
+        return self.arena.g(n)
+
+    def _bn(self, prefix):
+        """(module, gamma, beta master fp32 views) of a BatchNorm with the given key prefix."""
+        mod = self.shell.get_submodule(prefix)
+        return mod, self.arena.master(prefix + ".weight"), self.arena.master(prefix + ".bias")
+
+    def _wgrad(self, dy, x, dW, alpha=1.0):
+        """dW (fp32) += alpha * dy^T x, split-K over the token dimension when the tile grid is small."""
+        M, N = dy.shape
+        K = x.shape[1]
+        tiles = ((N + 127) // 128) * ((K + 127) // 128)
+        splitk = max(1, min(16, 1024 // max(tiles, 1), M // 512))
+        ops.gemm(dy, x, dW, M=N, N=K, K=M, a_kmajor=False, b_kmajor=False, lda=dy.stride(0), ldb=x.stride(0),
+                 ldc=dW.stride(0), alpha=alpha, beta=1.0, splitk=splitk)
+
+    def _bias_grad(self, g, db, alpha=1.0):
+        ops.ew_bwd(g, db=db, alpha=alpha)
+
+    # ------------------------------------------------------------------------ batch prep
+    def prepare(self, videos, audios, video_lengths, labels=None):
+        """host-side index tensors (labels / lengths are host data in the collator layout)."""
+        B, _, T = videos.shape[:3]
+        lens = video_lengths.detach().cpu().to(torch.int64)
+        b = {"B": B, "T": T, "lens_host": lens,
+             "lens": lens.to(torch.int32).to(self.device, non_blocking=True),
+             "full": bool((lens == T).all())}
+        if labels is not None:
+            lab = labels.detach().cpu()
+            ys = [r[r != -1] for r in lab]
+            L1 = max(len(y) for y in ys) + 1
+            ys_in = torch.full((B, L1), self.V - 1, dtype=torch.int32)
+            ys_out = torch.full((B, L1), -1, dtype=torch.int32)
+            Lmax = max(1, max(len(y) for y in ys))
+            ctc_lab = torch.full((B, Lmax), -1, dtype=torch.int32)
+            for i, y in enumerate(ys):
+                ys_in[i, 0] = self.V - 1
+                ys_in[i, 1:len(y) + 1] = y
+                ys_out[i, :len(y)] = y
+                ys_out[i, len(y)] = self.V - 1
+                ctc_lab[i, :len(y)] = y
+            b.update(L1=L1, ys_in=ys_in.flatten().to(self.device), ys_out=ys_out.flatten().to(self.device),
+                     ctc_lab=ctc_lab.to(self.device),
+                     ctc_len=torch.tensor([len(y) for y in ys], dtype=torch.int32).to(self.device))
+        return b
+
+    # ===================================================================== video frontend
+    def _geom(self, nimg, hin, cin, cout, k, s):
+        return ops.ConvGeom(nimg, hin, hin, cin, cout, k, k, (s, s), (k // 2, k // 2))
+
+    def _conv_bn(self, g, x, wname, bnprefix, train):
+        """conv (implicit GEMM) + BN statistics (fused in the conv epilogue) + BN finalize."""
+        h = self._e(g.out_pixels, g.cout)
+        bn, gam, bet = self._bn(bnprefix)
+        st = ops.BnState(g.cout, self.device)
+        if train:
+            part = self._e(g.cout, ops.conv_stat_tiles(g), 3, dtype=torch.float32)
+            ops.conv_fwd(g, x, self.w(wname), h, part)
+            ops.bn_finalize(st, gam, bet, bn.running_mean, bn.running_var, partials=part, training=True,
+                            momentum=bn.momentum, eps=bn.eps)
+            bn.num_batches_tracked.add_(1)
+        else:
+            ops.conv_fwd(g, x, self.w(wname), h)
+            ops.bn_finalize(st, gam, bet, bn.running_mean, bn.running_var, training=False, eps=bn.eps)
+        return h, st
+
+    def video_fwd(self, videos, train, save):
+        B, _, T = videos.shape[:3]
+        N = B * T
+        R = "encoder.feature_extractor_video.resnet."
+        ctx = {"N": N}
+        xp = self._e(N, 88, 88, 8)
+        ops.stem_pack(videos.contiguous(), xp)
+        wp = self._e(64, 7, 7, 8)
+        ops.stem_wpack(self.arena.master(R + "frontend3D.0.weight"), wp)
+        gs = ops.ConvGeom(N, 88, 88, 8, 64, 7, 7, (2, 2), (3, 3))
+        # stem conv uses the packed weight (not an arena view)
+        h0 = self._e(N * 44 * 44, 64)
+        bn, gam, bet = self._bn(R + "frontend3D.1")
+        st0 = ops.BnState(64, self.device)
+        if train:
+            part = self._e(64, ops.conv_stat_tiles(gs), 3, dtype=torch.float32)
+            ops.conv_fwd(gs, xp, wp, h0, part)
+            ops.bn_finalize(st0, gam, bet, bn.running_mean, bn.running_var, partials=part, training=True,
+                            momentum=bn.momentum, eps=bn.eps)
+            bn.num_batches_tracked.add_(1)
+        else:
+            ops.conv_fwd(gs, xp, wp, h0)
+            ops.bn_finalize(st0, gam, bet, bn.running_mean, bn.running_var, training=False, eps=bn.eps)
+        x = self._e(N * 22 * 22, 64)
+        am = self._e(N * 22 * 22, 64, dtype=torch.uint8)
+        ops.stem_pool_fwd(h0, N, 44, 44, st0, self.arena.master(R + "frontend3D.2.weight"), x, am)
+        if save:
+            ctx.update(xp=xp, gs=gs, h0=h0, st0=st0, am=am)
+        blocks = []
+        hw = 22
+        for li, bi, cin, cout, s in self.RES_BLOCKS:
+            p = f"{R}trunk.layer{li}.{bi}."
+            g1 = self._geom(N, hw, cin, cout, 3, s)
+            ho = g1.hout
+            g2 = self._geom(N, ho, cout, cout, 3, 1)
+            h1, st1 = self._conv_bn(g1, x, p + "conv1.weight", p + "bn1", train)
+            a1 = self._e(N * ho * ho, cout)
+            ops.bn_act_fwd(h1, st1, self.arena.master(p + "relu1.weight"), a1)
+            h2, st2 = self._conv_bn(g2, a1, p + "conv2.weight", p + "bn2", train)
+            out = self._e(N * ho * ho, cout)
+            if cin != cout or s != 1:
+                gd = ops.ConvGeom(N, hw, hw, cin, cout, 1, 1, (s, s), (0, 0))
+                hd, std = self._conv_bn(gd, x, p + "downsample.0.weight", p + "downsample.1", train)
+                ops.bn_act_fwd(h2, st2, self.arena.master(p + "relu2.weight"), out, res=hd, st2=std)
+            else:
+                gd, hd, std = None, None, None
+                ops.bn_act_fwd(h2, st2, self.arena.master(p + "relu2.weight"), out, res=x)
+            if save:
+                blocks.append(dict(p=p, g1=g1, g2=g2, gd=gd, x=x, h1=h1, st1=st1, a1=a1, h2=h2, st2=st2, hd=hd,
+                                   std=std, cin=cin, cout=cout, hw=hw))
+            x = out
+            hw = ho
+        feat = self._e(N, 512)
+        ops.avgpool_fwd(x, N, hw * hw, 512, feat)
+        if save:
+            ctx.update(blocks=blocks, hw_last=hw, feat=feat)
+        return feat, ctx
+
+    def video_bwd(self, ctx, dfeat):
+        N = ctx["N"]
+        R = "encoder.feature_extractor_video.resnet."
+        hw = ctx["hw_last"]
+        dout = self._e(N * hw * hw, 512)
+        ops.avgpool_bwd(dfeat, N, hw * hw, 512, dout)
+        for blk in reversed(ctx["blocks"]):
+            p, cout, cin = blk["p"], blk["cout"], blk["cin"]
+            M2 = blk["h2"].shape[0]
+            dh2 = self._e(M2, cout)
+            if blk["gd"] is not None:
+                dhd = self._e(M2, cout)
+                ops.bn_act_bwd(dout, blk["h2"], blk["st2"], self.arena.master(p + "relu2.weight"), dh2,
+                               res=blk["hd"], st2=blk["std"], dh2=dhd, dprelu=self.g(p + "relu2.weight"),
+                               dgamma=self.g(p + "bn2.weight"), dbeta=self.g(p + "bn2.bias"),
+                               dgamma2=self.g(p + "downsample.1.weight"), dbeta2=self.g(p + "downsample.1.bias"))
+                dz = None
+            else:
+                dz = ops.bn_act_bwd(dout, blk["h2"], blk["st2"], self.arena.master(p + "relu2.weight"), dh2,
+                                    res=blk["x"], dprelu=self.g(p + "relu2.weight"),
+                                    dgamma=self.g(p + "bn2.weight"), dbeta=self.g(p + "bn2.bias"))
+                dhd = None
+            # conv2
+            ops.conv_bwd_weight(blk["g2"], blk["a1"], dh2, self.g(p + "conv2.weight"))
+            da1 = self._e(M2, cout)
+            ops.conv_bwd_data(blk["g2"], dh2, self.w(p + "conv2.weight"), da1)
+            # bn1 + prelu1
+            dh1 = self._e(M2, cout)
+            ops.bn_act_bwd(da1, blk["h1"], blk["st1"], self.arena.master(p + "relu1.weight"), dh1,
+                           dprelu=self.g(p + "relu1.weight"), dgamma=self.g(p + "bn1.weight"),
+                           dbeta=self.g(p + "bn1.bias"))
+            ops.conv_bwd_weight(blk["g1"], blk["x"], dh1, self.g(p + "conv1.weight"))
+            Mi = blk["x"].shape[0]
+            if dz is not None:
+                dx = dz                      # identity shortcut: d(block input) starts as dz
+                ops.conv_bwd_data(blk["g1"], dh1, self.w(p + "conv1.weight"), dx, beta=1.0)
+            else:
+                dx = self._e(Mi, cin)
+                ops.conv_bwd_data(blk["g1"], dh1, self.w(p + "conv1.weight"), dx)
+                ops.conv_bwd_weight(blk["gd"], blk["x"], dhd, self.g(p + "downsample.0.weight"))
+                ops.conv_bwd_data(blk["gd"], dhd, self.w(p + "downsample.0.weight"), dx, beta=1.0)
+            dout = dx
+        # stem
+        dh0 = self._e(N * 44 * 44, 64)
+        ops.stem_pool_bwd(dout, ctx["am"], ctx["h0"], N, 44, 44, ctx["st0"], self.arena.master(R + "frontend3D.2.weight"),
+                          dh0, dprelu=self.g(R + "frontend3D.2.weight"), dgamma=self.g(R + "frontend3D.1.weight"),
+                          dbeta=self.g(R + "frontend3D.1.bias"))
+        gp = self._z(64, 7, 7, 8, dtype=torch.float32)
+        ops.conv_bwd_weight(ctx["gs"], ctx["xp"], dh0, gp)
+        ops.stem_wgrad_unpack(gp, self.g(R + "frontend3D.0.weight"))
+
+    # ============================================================================ encoder
+    def _ln(self, x, name, eps, save=None):
+        y, mean, rstd = ops.layernorm_fwd(x, self.arena.master(name + ".weight"), self.arena.master(name + ".bias"), eps)
+        return y, mean, rstd
+
+    def _ln_bwd(self, dy, x, name, mean, rstd, dres=None, dx=None):
+        return ops.layernorm_bwd(dy, x, self.arena.master(name + ".weight"), mean, rstd, dx=dx, dres=dres,
+                                 dgamma=self.g(name + ".weight"), dbeta=self.g(name + ".bias"))
+
+    def encoder_fwd(self, audios, videos, bt, train, save, seeds, modality=None):
+        """AVHubertModel.forward_gen(features_only=True) — returns (x (M, D), ctx)."""
+        cfg = self.cfg
+        B, T = bt["B"], bt["T"]
+        M, D = B * T, self.D
+        EN = "encoder."
+        ctx = {"B": B, "T": T, "modality": modality}
+        # audio / video frontends -> concat buffer [M][2D] (audio | video)
+        fcat = self._e(M, 2 * D)
+        ain = self._e(M, cfg.audio_feat_dim)
+        ops.audio_pack(audios.contiguous(), ain)
+        if modality == "audio_off":
+            fcat[:, :D].zero_()
+        else:
+            ops.linear_fwd(ain, self.w(EN + "feature_extractor_audio.proj.weight"),
+                           self.arena.master(EN + "feature_extractor_audio.proj.bias"), out=fcat[:, :D])
+        feat, vctx = self.video_fwd(videos, train, save)
+        if modality == "video_off":
+            fcat[:, D:].zero_()
+        else:
+            ops.linear_fwd(feat, self.w(EN + "feature_extractor_video.proj.weight"),
+                           self.arena.master(EN + "feature_extractor_video.proj.bias"), out=fcat[:, D:])
+        ln0, m0, r0 = self._ln(fcat, EN + "layer_norm", 1e-5)
+        sd_in = seeds.next()
+        p_in = cfg.dropout_input if train else 0.0
+        x = ops.linear_fwd(ln0, self.w(EN + "post_extract_proj.weight"), self.arena.master(EN + "post_extract_proj.bias"),
+                           drop_p=p_in, seed=sd_in)
+        if not bt["full"]:
+            ops.mask_rows(x, B, T, bt["lens"])
+        klen = None if bt["full"] else bt["lens"]
+        # positional conv: y = x + gelu(conv(x) + b); x0 = dropout(y)
+        pc = self.pc
+        v = self.arena.master(pc + "parametrizations.weight.original1")     # [D][K][D/G]
+        gpc = self.arena.master(pc + "parametrizations.weight.original0").reshape(-1)
+        norm = self._e(self.PK, dtype=torch.float32)
+        wpc = self._e(D, self.PK, D // self.G)
+        ops.weightnorm_fwd(v, gpc, norm, wpc)
+        geo = ops.ConvGeom(B, T, 1, D // self.G, D // self.G, self.PK, 1, (1, 1), (self.PK // 2, 0), groups=self.G,
+                           hout=T, wout=1)
+        pre = self._e(M, D)
+        y = self._e(M, D)
+        ops.conv_fwd(geo, x, wpc, y, bias=self.arena.master(pc + "bias"), act=GELU, preact=pre, res=x)
+        sd_pc = seeds.next()
+        p_h = cfg.hidden_dropout if train else 0.0
+        if p_h > 0:
+            ops.dropout_fwd(y, y, p_h, sd_pc)
+        if save:
+            ctx.update(ain=ain, fcat=fcat, ln0=ln0, m0=m0, r0=r0, sd_in=sd_in, p_in=p_in, x_pre=x, geo=geo, wpc=wpc,
+                       norm=norm, pre=pre, sd_pc=sd_pc, p_h=p_h, vctx=vctx, feat=feat, klen=klen)
+        x = y
+        layers = []
+        for i in range(self.nl):
+            x, lc = self._enc_layer_fwd(i, x, B, T, klen, train, save, seeds)
+            if save:
+                layers.append(lc)
+        E = "encoder.encoder."
+        out, mf, rf = self._ln(x, E + "layer_norm", 1e-5)
+        if save:
+            ctx.update(layers=layers, x_last=x, mf=mf, rf=rf)
+        return out, ctx
+
+    def _enc_layer_fwd(self, i, x, B, T, klen, train, save, seeds):
+        cfg = self.cfg
+        D, H = self.D, self.H
+        M = B * T
+        p = f"encoder.encoder.layers.{i}."
+        a = p + "attention."
+        ln1, m1, r1 = self._ln(x, p + "layer_norm", 1e-5)
+        wqkv = self.arena.span([a + "q_proj.weight", a + "k_proj.weight", a + "v_proj.weight"])
+        bqkv = self.arena.span([a + "q_proj.bias", a + "k_proj.bias", a + "v_proj.bias"], buf="master")
+        qkv = ops.linear_fwd(ln1, wqkv, bqkv)
+        o = self._e(M, D)
+        lse = self._e(B, H, T, dtype=torch.float32)
+        sd_att = seeds.next()
+        p_att = cfg.attention_dropout if train else 0.0
+        ops.attn_fwd(qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:], o, lse, B=B, H=H, Lq=T, Lk=T, klen=klen,
+                     scale=0.125, drop_p=p_att, seed=sd_att)
+        sd_o = seeds.next()
+        p_h = cfg.hidden_dropout if train else 0.0
+        x1 = ops.linear_fwd(o, self.w(a + "out_proj.weight"), self.arena.master(a + "out_proj.bias"), res=x,
+                            drop_p=p_h, seed=sd_o)
+        ln2, m2, r2 = self._ln(x1, p + "final_layer_norm", 1e-5)
+        ff = p + "feed_forward."
+        h = self._e(M, self.F)
+        sd_a = seeds.next()
+        p_a = cfg.activation_dropout if train else 0.0
+        act = ops.linear_fwd(ln2, self.w(ff + "intermediate_dense.weight"), self.arena.master(ff + "intermediate_dense.bias"),
+                             act=GELU, preact=h, drop_p=p_a, seed=sd_a)
+        sd_f = seeds.next()
+        x2 = ops.linear_fwd(act, self.w(ff + "output_dense.weight"), self.arena.master(ff + "output_dense.bias"), res=x1,
+                            drop_p=p_h, seed=sd_f)
+        lc = None
+        if save:
+            lc = dict(x=x, ln1=ln1, m1=m1, r1=r1, qkv=qkv, o=o, lse=lse, sd_att=sd_att, p_att=p_att, sd_o=sd_o, p_h=p_h,
+                      x1=x1, ln2=ln2, m2=m2, r2=r2, h=h, act=act, sd_a=sd_a, p_a=p_a, sd_f=sd_f)
+        return x2, lc
+
+    def _enc_layer_bwd(self, i, lc, dx2, B, T, klen):
+        """returns d(layer input); dx2 is consumed (may be reused)."""
+        D, H = self.D, self.H
+        M = B * T
+        p = f"encoder.encoder.layers.{i}."
+        a = p + "attention."
+        ff = p + "feed_forward."
+        # x2 = x1 + drop(act W2^T + b2)
+        g2 = self._e(M, D)
+        ops.ew_bwd(dx2, out=g2, drop_p=lc["p_h"], seed=lc["sd_f"], db=self.g(ff + "output_dense.bias"))
+        self._wgrad(g2, lc["act"], self.g(ff + "output_dense.weight"))
+        dh = ops.linear_dgrad(g2, self.w(ff + "output_dense.weight"), gate=lc["h"], act=GELU, drop_p=lc["p_a"], seed=lc["sd_a"])
+        self._bias_grad(dh, self.g(ff + "intermediate_dense.bias"))
+        self._wgrad(dh, lc["ln2"], self.g(ff + "intermediate_dense.weight"))
+        dln2 = ops.linear_dgrad(dh, self.w(ff + "intermediate_dense.weight"))
+        dx1 = self._ln_bwd(dln2, lc["x1"], p + "final_layer_norm", lc["m2"], lc["r2"], dres=dx2, dx=dx2)
+        # x1 = x + drop(o Wo^T + bo)
+        go = g2
+        ops.ew_bwd(dx1, out=go, drop_p=lc["p_h"], seed=lc["sd_o"], db=self.g(a + "out_proj.bias"))
+        self._wgrad(go, lc["o"], self.g(a + "out_proj.weight"))
+        do = ops.linear_dgrad(go, self.w(a + "out_proj.weight"))
+        # attention
+        qkv = lc["qkv"]
+        dqkv = self._e(M, 3 * D)
+        dq32 = self._z(M, D, dtype=torch.float32)
+        delta = self._e(B, H, T, dtype=torch.float32)
+        ops.attn_bwd(do, qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:], lc["o"], lc["lse"], dq32, dqkv[:, D:2 * D],
+                     dqkv[:, 2 * D:], delta, B=B, H=H, Lq=T, Lk=T, klen=klen, scale=0.125, drop_p=lc["p_att"],
+                     seed=lc["sd_att"])
+        ops.cast(dq32, dqkv[:, :D])
+        names_b = [a + "q_proj.bias", a + "k_proj.bias", a + "v_proj.bias"]
+        names_w = [a + "q_proj.weight", a + "k_proj.weight", a + "v_proj.weight"]
+        self._bias_grad(dqkv, self.arena.span(names_b, buf="g"))
+        self._wgrad(dqkv, lc["ln1"], self.arena.span(names_w, buf="g"))
+        dln1 = ops.linear_dgrad(dqkv, self.arena.span(names_w))
+        return self._ln_bwd(dln1, lc["x"], p + "layer_norm", lc["m1"], lc["r1"], dres=dx1, dx=dx1)
+
+    def encoder_bwd(self, ctx, dout):
+        cfg = self.cfg
+        B, T = ctx["B"], ctx["T"]
+        M, D = B * T, self.D
+        EN = "encoder."
+        E = "encoder.encoder."
+        dx = self._ln_bwd(dout, ctx["x_last"], E + "layer_norm", ctx["mf"], ctx["rf"])
+        for i in reversed(range(self.nl)):
+            dx = self._enc_layer_bwd(i, ctx["layers"][i], dx, B, T, ctx["klen"])
+        # pos-conv block: x0 = drop(x + gelu(conv(x) + b))
+        pc = self.pc
+        if ctx["p_h"] > 0:
+            ops.ew_bwd(dx, out=dx, drop_p=ctx["p_h"], seed=ctx["sd_pc"])
+        gp = self._e(M, D)
+        ops.ew_bwd(dx, out=gp, gate=ctx["pre"], act=GELU, db=self.g(pc + "bias"))
+        dwpc = self._z(D, self.PK, D // self.G, dtype=torch.float32)
+        ops.conv_bwd_weight(ctx["geo"], ctx["x_pre"], gp, dwpc)
+        ops.weightnorm_bwd(self.arena.master(pc + "parametrizations.weight.original1"),
+                           self.arena.master(pc + "parametrizations.weight.original0").reshape(-1), ctx["norm"], dwpc,
+                           self.g(pc + "parametrizations.weight.original1"),
+                           self.g(pc + "parametrizations.weight.original0").reshape(-1),
+                           self._e(self.PK, dtype=torch.float32))
+        ops.conv_bwd_data(ctx["geo"], gp, ctx["wpc"], dx, beta=1.0)
+        if ctx["klen"] is not None:
+            ops.mask_rows(dx, B, T, ctx["klen"])
+        # post_extract_proj (+ dropout_input)
+        gi = gp
+        ops.ew_bwd(dx, out=gi, drop_p=ctx["p_in"], seed=ctx["sd_in"], db=self.g(EN + "post_extract_proj.bias"))
+        self._wgrad(gi, ctx["ln0"], self.g(EN + "post_extract_proj.weight"))
+        dln0 = ops.linear_dgrad(gi, self.w(EN + "post_extract_proj.weight"))
+        dfcat = self._ln_bwd(dln0, ctx["fcat"], EN + "layer_norm", ctx["m0"], ctx["r0"])
+        fgm = cfg.feature_grad_mult            # GradMultiply (avhubert.py:173-182) on both frontends
+        if ctx["modality"] != "audio_off":
+            da = dfcat[:, :D]
+            self._bias_grad(da, self.g(EN + "feature_extractor_audio.proj.bias"), alpha=fgm)
+            self._wgrad(da, ctx["ain"], self.g(EN + "feature_extractor_audio.proj.weight"), alpha=fgm)
+        if ctx["modality"] != "video_off":
+            dv = dfcat[:, D:]
+            self._bias_grad(dv, self.g(EN + "feature_extractor_video.proj.bias"), alpha=fgm)
+            self._wgrad(dv, ctx["feat"], self.g(EN + "feature_extractor_video.proj.weight"), alpha=fgm)
+            dfeat = self._e(M, 512)
+            ops.gemm(dv, self.w(EN + "feature_extractor_video.proj.weight"), dfeat, M=M, N=512, K=D, a_kmajor=True,
+                     b_kmajor=False, lda=dv.stride(0), ldb=512, ldc=512, alpha=fgm)
+            self.video_bwd(ctx["vctx"], dfeat)
+
+    # ============================================================================ decoder
+    def decoder_fwd(self, enc, bt, train, save, seeds):
+        cfg = self.cfg
+        B, T, L1 = bt["B"], bt["T"], bt["L1"]
+        R, D, H = B * L1, self.dD, self.dH
+        klen = None if bt["full"] else bt["lens"]
+        sd_e = seeds.next()
+        p_d = cfg.dropout_rate if train else 0.0
+        p_att = cfg.transformer_attn_dropout_rate if train else 0.0
+        y = self._e(R, D)
+        if self._pe.shape[0] < L1:
+            self._pe = positional_encoding(2 * L1, self.dD, self.device)
+        ops.embed_fwd(bt["ys_in"], self.w("decoder.embed.0.weight"), self._pe[:L1], math.sqrt(D), y, L1,
+                      drop_p=p_d, seed=sd_e)
+        ctx = {"sd_e": sd_e, "p_d": p_d, "p_att": p_att, "layers": [], "klen": klen, "L1": L1}
+        for i in range(self.dl):
+            p = f"decoder.decoders.{i}."
+            sa, ca, ff = p + "self_attn.", p + "src_attn.", p + "feed_forward."
+            n1, m1, r1 = ops.layernorm_fwd(y, self.arena.master(p + "norm1.weight"), self.arena.master(p + "norm1.bias"), 1e-12)
+            qkv = ops.linear_fwd(n1, self.arena.span([sa + "linear_q.weight", sa + "linear_k.weight", sa + "linear_v.weight"]),
+                                 self.arena.span([sa + "linear_q.bias", sa + "linear_k.bias", sa + "linear_v.bias"], buf="master"))
+            o1 = self._e(R, D)
+            lse1 = self._e(B, H, L1, dtype=torch.float32)
+            s1 = seeds.next()
+            ops.attn_fwd(qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:], o1, lse1, B=B, H=H, Lq=L1, Lk=L1, causal=True,
+                         scale=0.125, drop_p=p_att, seed=s1)
+            s2 = seeds.next()
+            y1 = ops.linear_fwd(o1, self.w(sa + "linear_out.weight"), self.arena.master(sa + "linear_out.bias"), res=y,
+                                drop_p=p_d, seed=s2)
+            n2, m2, r2 = ops.layernorm_fwd(y1, self.arena.master(p + "norm2.weight"), self.arena.master(p + "norm2.bias"), 1e-12)
+            q2 = ops.linear_fwd(n2, self.w(ca + "linear_q.weight"), self.arena.master(ca + "linear_q.bias"))
+            kv = ops.linear_fwd(enc, self.arena.span([ca + "linear_k.weight", ca + "linear_v.weight"]),
+                                self.arena.span([ca + "linear_k.bias", ca + "linear_v.bias"], buf="master"))
+            o2 = self._e(R, D)
+            lse2 = self._e(B, H, L1, dtype=torch.float32)
+            s3 = seeds.next()
+            ops.attn_fwd(q2, kv[:, :D], kv[:, D:], o2, lse2, B=B, H=H, Lq=L1, Lk=T, klen=klen, scale=0.125,
+                         drop_p=p_att, seed=s3)
+            s4 = seeds.next()
+            y2 = ops.linear_fwd(o2, self.w(ca + "linear_out.weight"), self.arena.master(ca + "linear_out.bias"), res=y1,
+                                drop_p=p_d, seed=s4)
+            n3, m3, r3 = ops.layernorm_fwd(y2, self.arena.master(p + "norm3.weight"), self.arena.master(p + "norm3.bias"), 1e-12)
+            h = self._e(R, self.dF)
+            s5 = seeds.next()
+            a = ops.linear_fwd(n3, self.w(ff + "w_1.weight"), self.arena.master(ff + "w_1.bias"), act=RELU, preact=h,
+                               drop_p=p_d, seed=s5)
+            s6 = seeds.next()
+            y3 = ops.linear_fwd(a, self.w(ff + "w_2.weight"), self.arena.master(ff + "w_2.bias"), res=y2, drop_p=p_d, seed=s6)
+            if save:
+                ctx["layers"].append(dict(y=y, n1=n1, m1=m1, r1=r1, qkv=qkv, o1=o1, lse1=lse1, s1=s1, s2=s2, y1=y1, n2=n2,
+                                          m2=m2, r2=r2, q2=q2, kv=kv, o2=o2, lse2=lse2, s3=s3, s4=s4, y2=y2, n3=n3, m3=m3,
+                                          r3=r3, h=h, a=a, s5=s5, s6=s6))
+            y = y3
+        yn, mf, rf = ops.layernorm_fwd(y, self.arena.master("decoder.after_norm.weight"),
+                                       self.arena.master("decoder.after_norm.bias"), 1e-12)
+        logits = self._e(R, self.Vp)
+        ops.linear_fwd(yn, self.w("decoder.output_layer.weight"), self.arena.master("decoder.output_layer.bias"),
+                       out=logits[:, :self.V])
+        if save:
+            ctx.update(y_last=y, yn=yn, mf=mf, rf=rf)
+        return logits, ctx
+
+    def decoder_bwd(self, ctx, dlogits, enc, denc, bt):
+        B, T, L1 = bt["B"], bt["T"], ctx["L1"]
+        R, D, H = B * L1, self.dD, self.dH
+        klen = ctx["klen"]
+        p_d, p_att = ctx["p_d"], ctx["p_att"]
+        self._bias_grad(dlogits, self.arena.g_padded("decoder.output_layer.bias"))
+        self._wgrad(dlogits[:, :self.V], ctx["yn"], self.g("decoder.output_layer.weight"))
+        dyn = self._e(R, D)
+        ops.gemm(dlogits, self.arena.w_padded("decoder.output_layer.weight"), dyn, M=R, N=D, K=self.Vp, a_kmajor=True,
+                 b_kmajor=False, lda=dlogits.stride(0), ldb=D, ldc=D)
+        dy = ops.layernorm_bwd(dyn, ctx["y_last"], self.arena.master("decoder.after_norm.weight"), ctx["mf"], ctx["rf"],
+                               dgamma=self.g("decoder.after_norm.weight"), dbeta=self.g("decoder.after_norm.bias"))
+        g = self._e(R, D)
+        for i in reversed(range(self.dl)):
+            lc = ctx["layers"][i]
+            p = f"decoder.decoders.{i}."
+            sa, ca, ff = p + "self_attn.", p + "src_attn.", p + "feed_forward."
+            # FFN
+            ops.ew_bwd(dy, out=g, drop_p=p_d, seed=lc["s6"], db=self.g(ff + "w_2.bias"))
+            self._wgrad(g, lc["a"], self.g(ff + "w_2.weight"))
+            dh = ops.linear_dgrad(g, self.w(ff + "w_2.weight"), gate=lc["h"], act=RELU, drop_p=p_d, seed=lc["s5"])
+            self._bias_grad(dh, self.g(ff + "w_1.bias"))
+            self._wgrad(dh, lc["n3"], self.g(ff + "w_1.weight"))
+            dn3 = ops.linear_dgrad(dh, self.w(ff + "w_1.weight"))
+            dy = ops.layernorm_bwd(dn3, lc["y2"], self.arena.master(p + "norm3.weight"), lc["m3"], lc["r3"], dx=dy, dres=dy,
+                                   dgamma=self.g(p + "norm3.weight"), dbeta=self.g(p + "norm3.bias"))
+            # source attention
+            ops.ew_bwd(dy, out=g, drop_p=p_d, seed=lc["s4"], db=self.g(ca + "linear_out.bias"))
+            self._wgrad(g, lc["o2"], self.g(ca + "linear_out.weight"))
+            do2 = ops.linear_dgrad(g, self.w(ca + "linear_out.weight"))
+            dkv = self._e(B * T, 2 * D)
+            dq32 = self._z(R, D, dtype=torch.float32)
+            delta = self._e(B, H, L1, dtype=torch.float32)
+            ops.attn_bwd(do2, lc["q2"], lc["kv"][:, :D], lc["kv"][:, D:], lc["o2"], lc["lse2"], dq32, dkv[:, :D], dkv[:, D:],
+                         delta, B=B, H=H, Lq=L1, Lk=T, klen=klen, scale=0.125, drop_p=p_att, seed=lc["s3"])
+            dq2 = self._e(R, D)
+            ops.cast(dq32, dq2)
+            self._bias_grad(dq2, self.g(ca + "linear_q.bias"))
+            self._wgrad(dq2, lc["n2"], self.g(ca + "linear_q.weight"))
+            dn2 = ops.linear_dgrad(dq2, self.w(ca + "linear_q.weight"))
+            kvw = [ca + "linear_k.weight", ca + "linear_v.weight"]
+            self._bias_grad(dkv, self.arena.span([ca + "linear_k.bias", ca + "linear_v.bias"], buf="g"))
+            self._wgrad(dkv, enc, self.arena.span(kvw, buf="g"))
+            ops.linear_dgrad(dkv, self.arena.span(kvw), out=denc, beta=1.0)
+            dy = ops.layernorm_bwd(dn2, lc["y1"], self.arena.master(p + "norm2.weight"), lc["m2"], lc["r2"], dx=dy, dres=dy,
+                                   dgamma=self.g(p + "norm2.weight"), dbeta=self.g(p + "norm2.bias"))
+            # causal self attention
+            ops.ew_bwd(dy, out=g, drop_p=p_d, seed=lc["s2"], db=self.g(sa + "linear_out.bias"))
+            self._wgrad(g, lc["o1"], self.g(sa + "linear_out.weight"))
+            do1 = ops.linear_dgrad(g, self.w(sa + "linear_out.weight"))
+            dqkv = self._e(R, 3 * D)
+            dq32 = self._z(R, D, dtype=torch.float32)
+            delta = self._e(B, H, L1, dtype=torch.float32)
+            qkv = lc["qkv"]
+            ops.attn_bwd(do1, qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:], lc["o1"], lc["lse1"], dq32, dqkv[:, D:2 * D],
+                         dqkv[:, 2 * D:], delta, B=B, H=H, Lq=L1, Lk=L1, causal=True, scale=0.125, drop_p=p_att, seed=lc["s1"])
+            ops.cast(dq32, dqkv[:, :D])
+            nb = [sa + "linear_q.bias", sa + "linear_k.bias", sa + "linear_v.bias"]
+            nw = [sa + "linear_q.weight", sa + "linear_k.weight", sa + "linear_v.weight"]
+            self._bias_grad(dqkv, self.arena.span(nb, buf="g"))
+            self._wgrad(dqkv, lc["n1"], self.arena.span(nw, buf="g"))
+            dn1 = ops.linear_dgrad(dqkv, self.arena.span(nw))
+            dy = ops.layernorm_bwd(dn1, lc["y"], self.arena.master(p + "norm1.weight"), lc["m1"], lc["r1"], dx=dy, dres=dy,
+                                   dgamma=self.g(p + "norm1.weight"), dbeta=self.g(p + "norm1.bias"))
+        ops.embed_bwd(bt["ys_in"], dy, math.sqrt(D), self.g("decoder.embed.0.weight"), L1, drop_p=p_d, seed=ctx["sd_e"])
+
+    # ======================================================================== full model
+    def forward(self, videos, audios, video_lengths, labels, train=True, need_grad=True, seed=None):
+        """E2E.forward: returns (out4 = [loss, loss_ctc, loss_att, acc] on device, ctx)."""
+        cfg = self.cfg
+        if seed is None:
+            seed = random.getrandbits(48)
+        seeds = _Seeds(seed)
+        bt = self.prepare(videos, audios, video_lengths, labels)
+        B, T = bt["B"], bt["T"]
+        M = B * T
+        modality = None
+        if train and cfg.modality == "av" and cfg.modality_dropout > 0:
+            # avhubert.py:476-482: np.random draws; here a host RNG (no bit-parity possible)
+            if random.random() < cfg.modality_dropout:
+                modality = "audio_off" if random.random() < cfg.audio_dropout else "video_off"
+        enc, ectx = self.encoder_fwd(audios.to(self.device), videos.to(self.device), bt, train, need_grad, seeds, modality)
+        # CTC branch: ctc_lo(dropout(enc))
+        sd_c = seeds.next()
+        p_c = cfg.dropout_rate if train else 0.0
+        xin = enc
+        if p_c > 0:
+            xin = self._e(M, self.D)
+            ops.dropout_fwd(enc, xin, p_c, sd_c)
+        clog = self._e(M, self.Vp)
+        ops.linear_fwd(xin, self.w("ctc.ctc_lo.weight"), self.arena.master("ctc.ctc_lo.bias"), out=clog[:, :self.V])
+        clse = self._e(M, dtype=torch.float32)
+        ops.row_lse(clog, self.V, clse)
+        Lmax = bt["ctc_lab"].shape[1]
+        S = 2 * Lmax + 1
+        alpha = self._e(B, T, S, dtype=torch.float32)
+        gamma = self._e(B, T, S, dtype=torch.float32)
+        nll = self._e(B, dtype=torch.float32)
+        cp = ops.ctc_params(clog, B, T, self.V, bt["ctc_lab"], bt["ctc_len"], bt["lens"], clse, alpha, gamma, nll)
+        ops.ctc_fwd(cp)
+        # attention branch
+        dlog, dctx = self.decoder_fwd(enc, bt, train, need_grad, seeds)
+        R = dlog.shape[0]
+        dlse = self._e(R, dtype=torch.float32)
+        rloss = self._e(R, dtype=torch.float32)
+        rcorr = self._e(R, dtype=torch.int32)
+        ops.lsm_fwd(dlog, self.V, bt["ys_out"], cfg.lsm_weight, dlse, rloss, rcorr)
+        out4 = self._e(4, dtype=torch.float32)
+        ops.loss_finalize(B, nll, rloss, rcorr, cfg.mtlalpha, out4)
+        ctx = None
+        if need_grad:
+            ctx = dict(bt=bt, enc=enc, ectx=ectx, xin=xin, p_c=p_c, sd_c=sd_c, clog=clog, cp=cp, dlog=dlog, dctx=dctx,
+                       dlse=dlse)
+        return out4, ctx
+
+    def backward(self, ctx, d_ctc, d_att):
+        """d_ctc / d_att: device fp32 scalars = d(total)/d(loss_ctc), d(total)/d(loss_att)
+        (for total = loss: mtlalpha * dloss and (1 - mtlalpha) * dloss). Accumulates into
+        arena.grad; nothing is synchronised with the host."""
+        cfg = self.cfg
+        bt = ctx["bt"]
+        B, T = bt["B"], bt["T"]
+        M = B * T
+        d_ctc = d_ctc.reshape(1).to(torch.float32)
+        d_att = d_att.reshape(1).to(torch.float32)
+        # attention loss -> decoder
+        dl = ctx["dlog"]
+        ddl = self._e(dl.shape[0], self.Vp)
+        ops.lsm_bwd(dl, self.V, bt["ys_out"], cfg.lsm_weight, ctx["dlse"], d_att, 1.0 / B, ddl)
+        denc = self._e(M, self.D)
+        # CTC -> denc (first write), then decoder adds
+        dcl = self._e(M, self.Vp)
+        ops.ctc_bwd(ctx["cp"], d_ctc, 1.0 / B, dcl)
+        self._bias_grad(dcl, self.arena.g_padded("ctc.ctc_lo.bias"))
+        self._wgrad(dcl[:, :self.V], ctx["xin"], self.g("ctc.ctc_lo.weight"))
+        ops.gemm(dcl, self.arena.w_padded("ctc.ctc_lo.weight"), denc, M=M, N=self.D, K=self.Vp, a_kmajor=True,
+                 b_kmajor=False, lda=dcl.stride(0), ldb=self.D, ldc=self.D, epi_bwd=True, drop_p=ctx["p_c"],
+                 seed=ctx["sd_c"])
+        self.decoder_bwd(ctx["dctx"], ddl, ctx["enc"], denc, bt)
+        self.encoder_bwd(ctx["ectx"], denc)
+
+    # ========================================================================= inference
+    def encode(self, audios, videos, video_lengths=None):
+        """eval-mode encoder (script/evaluation.py:96-101 call form: no attention mask)."""
+        B, _, T = videos.shape[:3]
+        if video_lengths is None:
+            video_lengths = torch.full((B,), T, dtype=torch.int64)
+        bt = self.prepare(videos, audios, video_lengths)
+        x, _ = self.encoder_fwd(audios.to(self.device), videos.to(self.device), bt, False, False, _Seeds(0))
+        return x.view(B, T, self.D)

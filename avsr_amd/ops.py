@@ -141,12 +141,17 @@ def conv_stat_tiles(g, dtype=L.AVSR_BF16):
     return L.load().avsr_conv_stat_tiles(ctypes.byref(p))
 
 
-def conv_fwd(g, x, w, y, stats=None):
-    """y[pix, co] = conv(x, w); stats: fp32 [tiles, cout, 3] BN partials (groups == 1)."""
+def conv_fwd(g, x, w, y, stats=None, bias=None, act=L.ACT_NONE, preact=None, res=None):
+    """y[pix, co] = act(conv(x, w) + bias) + res; stats: fp32 [cout, tiles, 3] BN partials."""
     p = g.params(dtype_code(x))
     assert x.dtype == w.dtype == y.dtype and x.is_cuda
     p.x, p.w, p.y = x.data_ptr(), w.data_ptr(), y.data_ptr()
     p.stats = None if stats is None else stats.data_ptr()
+    p.bias = None if bias is None else bias.data_ptr()
+    p.act = act
+    p.preact = None if preact is None else preact.data_ptr()
+    p.res = None if res is None else res.data_ptr()
+    p._keep = [t for t in (x, w, y, stats, bias, preact, res) if t is not None]
     L.check(L.load().avsr_conv_fwd(ctypes.byref(p), L.stream_ptr()), "avsr_conv_fwd")
     return y
 

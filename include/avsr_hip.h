@@ -100,6 +100,9 @@ typedef struct {
   float* stats;   /* fwd only: [cout][avsr_conv_stat_tiles()][3] (count, mean, M2) or NULL */
   float alpha, beta;                       /* bwd_data scaling */
   int splitk;     /* bwd_weight: 0 = auto */
+  /* fwd epilogue (optional): h = conv + bias[c]; preact = h; y = act(h) + res  (res/preact
+   * laid out like y; used by the pos-conv: x + GELU(conv(x) + b)) */
+  const float* bias; int act; void* preact; const void* res;
 } avsr_conv_params;
 
 int avsr_conv_fwd(const avsr_conv_params* p, void* stream);
