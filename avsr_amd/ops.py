@@ -11,6 +11,10 @@ from . import _lib as L
 
 _DT = {torch.float32: L.AVSR_F32, torch.bfloat16: L.AVSR_BF16}
 
+# optional launch probes (bench.py): {"gemm": {"match": fn(M, N, K, ak, bk, dtype) -> bool,
+# "events": [(start, end), ...]}} — HIP events recorded on the launching (current) stream
+PROBE = {}
+
 
 def dtype_code(t):
     try:
@@ -56,6 +60,14 @@ def gemm(A, B, C, *, M, N, K, a_kmajor, b_kmajor, lda, ldb, ldc, batch=1,
     p.gate = None if gate is None else gate.data_ptr()
     p.drop_p, p.seed = float(drop_p), int(seed) & 0xFFFFFFFFFFFFFFFF
     p.splitk = int(splitk)
+    probe = PROBE.get("gemm")
+    if probe is not None and probe["match"](M, N, K, a_kmajor, b_kmajor, dt):
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        L.check(lib.avsr_gemm(ctypes.byref(p), L.stream_ptr()), "avsr_gemm")
+        e.record()
+        probe["events"].append((s, e))
+        return C
     L.check(lib.avsr_gemm(ctypes.byref(p), L.stream_ptr()), "avsr_gemm")
     return C
 

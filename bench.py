@@ -1,0 +1,209 @@
+"""Throughput benchmark of the AVSR hot path (BASELINE.json metric / config C2, C3).
+
+One step = forward + backward + (RCCL gradient all-reduce) + fused clip/AdamW of the full
+AVHubertAVSR model (24-layer AV-HuBERT-Large encoder, ResNet-18 lip frontend, 6-layer
+decoder, joint CTC/attention loss) on 16 synthetic 15 s clips per GPU (T = 375 AV-frames,
+L = 40 labels), train mode (dropouts on), bf16 compute / fp32 master weights.
+Inputs are resident in HBM before the timed region (SURVEY.md §8(d) d1 recipe).
+
+  python bench.py [--gpus N --steps K --warmup W]
+  (N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N)
+
+Prints ONE JSON line (rank 0). `roofline` is measured live on the probe kernel (the encoder
+FFN up-projection GEMM, 6000x4096x1024 bf16, 24 launches per step) with HIP events on the
+stream it is launched on; `cpu_baseline` times the repo's CPU restatement of the same model
+(oracle/, "port") on the host cores on a bounded sample.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "AV-frames/sec/GPU (fwd+bwd) on 15s clips; WER parity on LRS2 test"
+BF16_PEAK_TFLOPS = 2500.0     # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+HBM_PEAK_GBS = 8000.0
+
+
+def synthetic_batch(B, T, L, seed=1234):
+    """uint8 96x96 lip frames -> crop 88 -> /255 -> (x-0.421)/0.165;
+    standard-normal 104-dim 'mel' frames with per-frame LayerNorm; labels U[1, 5047]."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    frames = rng.integers(0, 256, size=(B, T, 96, 96), dtype=np.uint8)
+    v = (frames[:, :, 4:92, 4:92].astype(np.float32) / 255.0 - 0.421) / 0.165
+    rng2 = np.random.Generator(np.random.PCG64(seed + 1))
+    a = rng2.standard_normal((B, T, 104)).astype(np.float32)
+    a = (a - a.mean(-1, keepdims=True)) / np.sqrt(a.var(-1, keepdims=True) + 1e-5)
+    rng3 = np.random.Generator(np.random.PCG64(seed + 2))
+    lab = rng3.integers(1, 5048, size=(B, L)).astype(np.int64)
+    return (torch.from_numpy(v[:, None]), torch.from_numpy(np.ascontiguousarray(a.transpose(0, 2, 1))),
+            torch.full((B,), T, dtype=torch.int64), torch.from_numpy(lab))
+
+
+def model_flops_per_frame(cfg, T, L):
+    """algorithmic fwd+bwd FLOPs per AV-frame: 3x the forward MACs*2."""
+    D, F, nl = cfg.hidden_size, cfg.intermediate_size, cfg.num_hidden_layers
+    enc = nl * (2 * (4 * D * D + 2 * D * F) + 4 * T * D)            # per frame, forward
+    # ResNet-18 frontend forward per frame (conv MACs * 2), stem + 4 stages + 512->D proj
+    stem = 2 * 44 * 44 * 64 * 5 * 49
+    res = 0
+    for (hw, cin, cout, s) in [(22, 64, 64, 1), (22, 64, 64, 1), (22, 64, 128, 2), (11, 128, 128, 1),
+                               (11, 128, 256, 2), (6, 256, 256, 1), (6, 256, 512, 2), (3, 512, 512, 1)]:
+        ho = (hw + 2 - 3) // s + 1
+        res += 2 * ho * ho * cout * cin * 9 + 2 * ho * ho * cout * cout * 9
+        if s != 1 or cin != cout:
+            res += 2 * ho * ho * cout * cin
+    front = stem + res + 2 * 512 * D + 2 * 104 * D + 2 * 2 * D * D
+    posconv = 2 * D * (D // cfg.num_conv_pos_embedding_groups) * cfg.num_conv_pos_embeddings
+    ctc = 2 * D * cfg.odim
+    dD, dF, dl = cfg.ddim, cfg.dunits, cfg.dlayers
+    L1 = L + 1
+    dec_tok = dl * (2 * (4 * dD * dD + 2 * dD * dF) + 4 * L1 * dD + 4 * T * dD) + 2 * dD * cfg.odim
+    dec = (dec_tok * L1 + dl * 2 * 2 * T * dD * dD) / T               # memory K/V projections per frame
+    fwd = enc + front + posconv + ctc + dec
+    # backward = 2x forward except the stem (no data-grad): stem counted fwd + wgrad only
+    return 3 * fwd - stem
+
+
+def cpu_baseline(model_cfg, state, T, threads):
+    """Time the repo's CPU restatement (oracle/avsr_oracle.py) fwd+bwd on 1 x 15 s clip."""
+    from oracle import avsr_oracle as O
+    torch.set_num_threads(threads)
+    cfg = O.OracleConfig.from_dict(dict(odim=model_cfg.odim, hidden_size=model_cfg.hidden_size,
+                                        num_attention_heads=model_cfg.num_attention_heads,
+                                        intermediate_size=model_cfg.intermediate_size,
+                                        num_hidden_layers=model_cfg.num_hidden_layers, ddim=model_cfg.ddim,
+                                        dheads=model_cfg.dheads, dunits=model_cfg.dunits, dlayers=model_cfg.dlayers))
+    sd = {k: v.detach().float().cpu().clone() for k, v in state.items()}
+    for k, v in sd.items():
+        if v.is_floating_point() and not (k.endswith("running_mean") or k.endswith("running_var")):
+            v.requires_grad_(True)
+    v, a, lens, lab = synthetic_batch(1, T, 40, seed=99)
+    t0 = time.perf_counter()
+    loss, *_ = O.e2e_forward(sd, cfg, v, a, lens, lab, train=True)
+    loss.backward()
+    dt = time.perf_counter() - t0
+    return T / dt, dt
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=16, help="clips per GPU")
+    ap.add_argument("--seq", type=int, default=375, help="AV-frames per clip (15 s at 25 fps)")
+    ap.add_argument("--labels", type=int, default=40)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--layers", type=int, default=None, help="debug only: fewer encoder layers (INVALID for the metric)")
+    args = ap.parse_args()
+
+    from avsr_amd import parallel
+    rank, world, local = parallel.init_from_env()
+    assert world == args.gpus, f"--gpus {args.gpus} but WORLD_SIZE {world}"
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    from avsr_amd import ops
+    from avsr_amd.avhubert_avsr_model import AVHubertAVSR
+    from avsr_amd.configuration_avhubert_avsr import AVHubertAVSRConfig
+    from avsr_amd.optim import FusedAdamW
+
+    torch.manual_seed(0)
+    kw = {} if args.layers is None else {"num_hidden_layers": args.layers}
+    cfg = AVHubertAVSRConfig(odim=5049, **kw)
+    model = AVHubertAVSR(cfg).train()
+    state_cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        state_cpu = {k: v.clone() for k, v in model.state_dict().items()}
+    model.setup_engine(dev, torch.bfloat16)
+    eng = model.avsr.engine()
+    arena = eng.arena
+    buffers = [b for b in model.buffers()]
+    parallel.broadcast_state(arena.data, buffers)
+    arena.sync_shadow()
+    reducer = parallel.GradReducer(arena.grad)
+    opt = FusedAdamW(arena, lr=1e-4, weight_decay=0.005, max_grad_norm=1.0)
+
+    B, T, L = args.batch, args.seq, args.labels
+    v, a, lens, lab = synthetic_batch(B, T, L, seed=1234 + rank)
+    v, a = v.to(dev), a.to(dev)
+    mtl = cfg.mtlalpha
+    d_ctc = torch.full((1,), mtl, device=dev)
+    d_att = torch.full((1,), 1.0 - mtl, device=dev)
+
+    def step():
+        arena.zero_grad()
+        out4, ctx = eng.forward(v, a, lens, lab, train=True, need_grad=True)
+        eng.backward(ctx, d_ctc, d_att)
+        reducer.allreduce(average=False)
+        opt.step(grad_scale=1.0 / world)
+        return out4
+
+    for _ in range(args.warmup):
+        out4 = step()
+    torch.cuda.synchronize()
+    # probe: encoder FFN up-projection (M = B*T, N = F, K = D), forward, bf16
+    M, N_, K_ = B * T, cfg.intermediate_size, cfg.hidden_size
+    ops.PROBE["gemm"] = {"match": lambda m, n, k, ak, bk, dt: (m, n, k, ak, bk) == (M, N_, K_, True, True),
+                         "events": []}
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out4 = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    probe_ev = ops.PROBE.pop("gemm")["events"]
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    losses = out4.cpu().tolist()
+    frames = args.steps * B * T * world
+    value = frames / elapsed
+    kern_ms = [s.elapsed_time(e) for s, e in probe_ev]
+    avg_ms = sum(kern_ms) / max(1, len(kern_ms))
+    flops = 2.0 * M * N_ * K_
+    achieved = flops / (avg_ms * 1e-3) / 1e12 if avg_ms > 0 else 0.0
+    fpf = model_flops_per_frame(cfg, T, L)
+    result = {
+        "metric": METRIC, "value": round(value, 2), "unit": "AV-frames/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+        "data": "synthetic (SURVEY d1 recipe: uint8 lip frames, normal+LN 104-d audio, U[1,5047] labels)",
+        "config": {"workload": f"C2/C3: AVHubertAVSR fwd+bwd+AdamW, {B}x{T / 25:.0f}s clips per GPU "
+                               f"(T={T}, L={L}), train mode, dropouts on",
+                   "global_batch": B * world, "seq_len": T, "parallelism": f"dp{world}",
+                   "encoder_layers": cfg.num_hidden_layers},
+        "roofline": {"bound": "mfma", "kernel": f"dense_kernel bf16 (encoder FFN1 {M}x{N_}x{K_})",
+                     "achieved": round(achieved, 1), "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": round(achieved / BF16_PEAK_TFLOPS, 4), "traffic": None,
+                     "launches": len(kern_ms), "avg_launch_ms": round(avg_ms, 4)},
+        "model_tflops_per_s": round(value * fpf / world / 1e12, 1),
+        "model_mfu": round(value * fpf / world / 1e12 / BF16_PEAK_TFLOPS, 4),
+        "loss": [round(x, 4) for x in losses],
+    }
+    if state_cpu is not None:
+        threads = min(16, os.cpu_count() or 1)
+        fps, dt = cpu_baseline(cfg, state_cpu, T, threads)
+        result["cpu_baseline"] = {"value": round(fps, 2), "unit": "AV-frames/s", "cores": threads, "kind": "port",
+                                  "sample": f"1x15s clip (T={T}, L=40) fwd+bwd, oracle/avsr_oracle.py fp32, "
+                                            f"{dt:.1f} s"}
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
