@@ -63,7 +63,7 @@ class LayerNormParams(ctypes.Structure):
         ("x", _c_p), ("ldx", _i64), ("y", _c_p), ("ldy", _i64),
         ("gamma", _c_p), ("beta", _c_p), ("mean", _c_p), ("rstd", _c_p),
         ("dy", _c_p), ("lddy", _i64), ("dx", _c_p), ("lddx", _i64),
-        ("dres", _c_p), ("lddres", _i64), ("dgamma", _c_p), ("dbeta", _c_p),
+        ("dres", _c_p), ("lddres", _i64), ("dgamma", _c_p), ("dbeta", _c_p), ("ws", _c_p),
     ]
 
 
@@ -82,7 +82,7 @@ class BnActParams(ctypes.Structure):
         ("prelu", _c_p), ("y", _c_p), ("dy", _c_p), ("dz", _c_p),
         ("mean", _c_p), ("invstd", _c_p), ("mean2", _c_p), ("invstd2", _c_p),
         ("sums", _c_p), ("dprelu", _c_p), ("dgamma", _c_p), ("dbeta", _c_p), ("dgamma2", _c_p), ("dbeta2", _c_p),
-        ("dh", _c_p), ("dh2", _c_p), ("beta_acc", _f),
+        ("dh", _c_p), ("dh2", _c_p), ("beta_acc", _f), ("ws", _c_p),
     ]
 
 
@@ -91,7 +91,7 @@ class StemPoolParams(ctypes.Structure):
         ("dtype", _i), ("nimg", _i), ("H", _i), ("W", _i), ("C", _i), ("Ho", _i), ("Wo", _i),
         ("h", _c_p), ("scale", _c_p), ("shift", _c_p), ("prelu", _c_p), ("y", _c_p), ("argmax", _c_p),
         ("dy", _c_p), ("dz", _c_p), ("mean", _c_p), ("invstd", _c_p),
-        ("sums", _c_p), ("dprelu", _c_p), ("dgamma", _c_p), ("dbeta", _c_p),
+        ("sums", _c_p), ("dprelu", _c_p), ("dgamma", _c_p), ("dbeta", _c_p), ("ws", _c_p),
     ]
 
 
@@ -127,7 +127,7 @@ class EwParams(ctypes.Structure):
     _fields_ = [
         ("dtype", _i), ("rows", _i), ("N", _i), ("dy", _c_p), ("lddy", _i64), ("out", _c_p), ("ldout", _i64),
         ("gate", _c_p), ("ldgate", _i64), ("act", _i), ("drop_p", _f), ("seed", ctypes.c_uint64),
-        ("alpha", _f), ("db", _c_p),
+        ("alpha", _f), ("db", _c_p), ("ws", _c_p),
     ]
 
 

@@ -44,7 +44,7 @@ enum { K_FWD = 0, K_DGRAD = 1, K_WGRAD = 2 };
 template <typename T, typename OutT, int WM, int WN, int KIND>
 __global__ __launch_bounds__(NT) void conv_kernel(ConvArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  using TL = Tile<T, WM, WN>;
+  using TL = Tile<T, WM, WN>;   // BM/BN only (LDS sizing: conv_lds below)
   const int z = blockIdx.z, grp = z / a.splits, sp = z % a.splits;
   const int m0 = blockIdx.y * TL::BM, n0 = blockIdx.x * TL::BN;
   const T* pa = (const T*)a.a + (int64_t)grp * a.a_gstride;
@@ -74,7 +74,8 @@ __global__ __launch_bounds__(NT) void conv_kernel(ConvArgs a) {
 
 template <typename T, typename OutT, int WM, int WN, int KIND>
 int launch(const ConvArgs& a, int groups, hipStream_t st) {
-  using TL = Tile<T, WM, WN>;
+  // operand kinds per convolution direction (fwd: K/K, dgrad: K/R, wgrad: R/R)
+  using TL = Tile<T, WM, WN, KIND != K_WGRAD, KIND == K_FWD>;
   dim3 grid((a.N + TL::BN - 1) / TL::BN, (a.M + TL::BM - 1) / TL::BM, groups * a.splits);
   if (grid.y > 65535) return AVSR_E_SHAPE;
   hipLaunchKernelGGL((conv_kernel<T, OutT, WM, WN, KIND>), grid, dim3(NT), TL::LDS_BYTES, st, a);

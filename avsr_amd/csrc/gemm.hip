@@ -18,7 +18,7 @@ struct DenseArgs {
 template <typename T, typename OutT, int WM, int WN, bool AK, bool BK>
 __global__ __launch_bounds__(NT) void dense_kernel(DenseArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  using TL = Tile<T, WM, WN>;
+  using TL = Tile<T, WM, WN, AK, BK>;
   const int z = blockIdx.z, bz = z / a.splits, sp = z % a.splits;
   const int m0 = blockIdx.y * TL::BM, n0 = blockIdx.x * TL::BN;
   using LA = typename std::conditional<AK, LdDenseK<T, TL::BM>, LdDenseR<T, TL::BM>>::type;
@@ -39,7 +39,7 @@ __global__ __launch_bounds__(NT) void dense_kernel(DenseArgs a) {
 
 template <typename T, typename OutT, int WM, int WN, bool AK, bool BK>
 int launch(const DenseArgs& a, int batch, hipStream_t st) {
-  using TL = Tile<T, WM, WN>;
+  using TL = Tile<T, WM, WN, AK, BK>;
   dim3 grid((a.N + TL::BN - 1) / TL::BN, (a.M + TL::BM - 1) / TL::BM, batch * a.splits);
   hipLaunchKernelGGL((dense_kernel<T, OutT, WM, WN, AK, BK>), grid, dim3(NT), TL::LDS_BYTES, st, a);
   AVSR_CHECK_LAUNCH();

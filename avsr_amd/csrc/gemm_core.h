@@ -185,40 +185,76 @@ template <typename T, int R> struct LdWgtR {
 };
 
 // ---------------------------------------------------------------- LDS staging
+// k-major operands: LDS image [R][BKE + VE] (row = r), fragments by ds_read_b128.
+// r-contiguous operands: LDS image [BKE][R + PAD] (row = k) filled by plain 16-byte stores
+// (no transpose on the write side); bf16 fragments come out of ds_read_b64_tr_b16 (the
+// hardware transposing read, T10), fp32 (parity mode) by scalar reads. PAD makes the row
+// stride 16 dwords mod 64, so a 32-lane half's four 4x16 transposed blocks hit 64 distinct
+// banks.
+template <typename T, int R, bool KMAJ> struct Img {
+  static constexpr int VE = V<T>::VE;
+  static constexpr int PADR = sizeof(T) == 2 ? 2 * ((16 - (R / 2) % 64 + 64) % 64) : 4;
+  static constexpr int RROW = KMAJ ? (BKE + VE) : (R + PADR);     // row stride (elements)
+  static constexpr int ELEMS = KMAJ ? R * RROW : BKE * RROW;     // one buffer
+};
+
 template <typename T, int R, bool KMAJ, int VPT>
 AVSR_DEV void lstore(T* lds, const v16 (&reg)[VPT], int tid) {
-  constexpr int VE = V<T>::VE, ROW = V<T>::ROW;
+  constexpr int VE = V<T>::VE, RROW = Img<T, R, KMAJ>::RROW;
 #pragma unroll
   for (int i = 0; i < VPT; ++i) {
     int v = tid + i * NT;
     if constexpr (KMAJ) {
       int r = v / (BKE / VE), kv = v % (BKE / VE);
-      *(v16*)(lds + r * ROW + kv * VE) = reg[i];
+      *(v16*)(lds + r * RROW + kv * VE) = reg[i];
     } else {
       int kk = v / (R / VE), rv = v % (R / VE);
-      const T* vals = (const T*)&reg[i];
-#pragma unroll
-      for (int e = 0; e < VE; ++e) lds[(rv * VE + e) * ROW + kk] = vals[e];
+      *(v16*)(lds + kk * RROW + rv * VE) = reg[i];
     }
   }
 }
 
-template <typename T>
+typedef short v4i16 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
+
+// MFMA operand fragment: rows rb..rb+31 (row = lane&31), k = s*16 + 8*(lane>>5) + 0..7
+template <typename T, int R, bool KMAJ>
 AVSR_DEV void frag(const T* lds, int rb, int s, int lane, bf16x8& hi, bf16x8& lo) {
-  constexpr int ROW = V<T>::ROW;
-  const T* p = lds + (rb + (lane & 31)) * ROW + s * 16 + 8 * (lane >> 5);
-  if constexpr (sizeof(T) == 2) {
-    hi = *(const bf16x8*)p;
+  constexpr int RROW = Img<T, R, KMAJ>::RROW;
+  if constexpr (KMAJ) {
+    const T* p = lds + (rb + (lane & 31)) * RROW + s * 16 + 8 * (lane >> 5);
+    if constexpr (sizeof(T) == 2) {
+      hi = *(const bf16x8*)p;
+    } else {
+      f32x4 x0 = *(const f32x4*)p, x1 = *(const f32x4*)(p + 4);
+      float x[8] = {x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
+      split8(x, hi, lo);
+    }
   } else {
-    f32x4 x0 = *(const f32x4*)p, x1 = *(const f32x4*)(p + 4);
-    float x[8] = {x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
-    split8(x, hi, lo);
+    const int k0 = s * 16 + 8 * (lane >> 5);
+    if constexpr (sizeof(T) == 2) {
+      // 16-lane group g supplies rows k0+q (q = (lane&15)>>2), columns 4p..4p+3 of the
+      // 16-column block starting at rb + 16*(g&1); lane receives its column (= lane&31).
+      const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+      const T* base = lds + rb + 16 * (g & 1) + 4 * p;
+      const v4i16 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(base + (k0 + q) * RROW));
+      const v4i16 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(base + (k0 + 4 + q) * RROW));
+      union { v4i16 s4[2]; bf16x8 h; } u;
+      u.s4[0] = a; u.s4[1] = b;
+      hi = u.h;
+    } else {
+      float x[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) x[j] = lds[(k0 + j) * RROW + rb + (lane & 31)];
+      split8(x, hi, lo);
+    }
   }
 }
 
-template <typename T, int WM, int WN> struct Tile {
+template <typename T, int WM, int WN, bool AK = true, bool BK = true> struct Tile {
   static constexpr int BM = 64 * WM, BN = 64 * WN;
-  static constexpr int ML_BYTES = 2 * (BM + BN) * V<T>::ROW * (int)sizeof(T);
+  static constexpr int SA = Img<T, BM, AK>::ELEMS, SB = Img<T, BN, BK>::ELEMS;
+  static constexpr int ML_BYTES = 2 * (SA + SB) * (int)sizeof(T);
   static constexpr int EP_BYTES = (BM / 2) * (BN + 4) * 4;
   static constexpr int LDS_BYTES = ML_BYTES > EP_BYTES ? ML_BYTES : EP_BYTES;
 };
@@ -226,10 +262,9 @@ template <typename T, int WM, int WN> struct Tile {
 // Main loop over K-tiles [kbeg, kend): acc[i][j] is the wave's 2x2 block of 32x32 tiles.
 template <typename T, int WM, int WN, class LA, class LB>
 AVSR_DEV void mainloop(LA& la, LB& lb, int m0, int n0, int kbeg, int kend, f32x16 (&acc)[2][2], char* smem) {
-  using TL = Tile<T, WM, WN>;
-  constexpr int ROW = V<T>::ROW;
+  using TL = Tile<T, WM, WN, LA::KMAJ, LB::KMAJ>;
   T* lA = (T*)smem;
-  T* lB = lA + 2 * TL::BM * ROW;
+  T* lB = lA + 2 * TL::SA;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;
 #pragma unroll
@@ -255,15 +290,15 @@ AVSR_DEV void mainloop(LA& la, LB& lb, int m0, int n0, int kbeg, int kend, f32x1
       la.load(m0, kbeg + (kt + 1) * BKE, ra, tid);
       lb.load(n0, kbeg + (kt + 1) * BKE, rb, tid);
     }
-    const T* cA = lA + cur * TL::BM * ROW;
-    const T* cB = lB + cur * TL::BN * ROW;
+    const T* cA = lA + cur * TL::SA;
+    const T* cB = lB + cur * TL::SB;
 #pragma unroll
     for (int s = 0; s < BKE / 16; ++s) {
       bf16x8 ah[2], al[2], bh[2], bl[2];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) frag<T>(cA, wm * 64 + i * 32, s, lane, ah[i], al[i]);
+      for (int i = 0; i < 2; ++i) frag<T, TL::BM, LA::KMAJ>(cA, wm * 64 + i * 32, s, lane, ah[i], al[i]);
 #pragma unroll
-      for (int j = 0; j < 2; ++j) frag<T>(cB, wn * 64 + j * 32, s, lane, bh[j], bl[j]);
+      for (int j = 0; j < 2; ++j) frag<T, TL::BN, LB::KMAJ>(cB, wn * 64 + j * 32, s, lane, bh[j], bl[j]);
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -276,8 +311,8 @@ AVSR_DEV void mainloop(LA& la, LB& lb, int m0, int n0, int kbeg, int kend, f32x1
         }
     }
     if (more) {
-      lstore<T, TL::BM, LA::KMAJ>(lA + (cur ^ 1) * TL::BM * ROW, ra, tid);
-      lstore<T, TL::BN, LB::KMAJ>(lB + (cur ^ 1) * TL::BN * ROW, rb, tid);
+      lstore<T, TL::BM, LA::KMAJ>(lA + (cur ^ 1) * TL::SA, ra, tid);
+      lstore<T, TL::BN, LB::KMAJ>(lB + (cur ^ 1) * TL::SB, rb, tid);
     }
     __syncthreads();
   }

@@ -11,35 +11,61 @@ struct EwArgs {
   int rows, N;
   const void* dy; int64_t lddy; void* out; int64_t ldout;
   const void* gate; int64_t ldgate; int act;
-  float drop_p; uint64_t seed; float alpha; float* db;
+  float drop_p; uint64_t seed; float alpha; float* db; float* ws;
 };
 
+// block = 64 column vectors x 4 row lanes over a chunk of rows; column partial sums are
+// reduced in LDS and written (plain stores) to ws[row_block][N], then colsum_finalize adds
+// the row-block partials into db: no atomic contention, deterministic order.
 template <typename T>
 __global__ __launch_bounds__(256) void ew_bwd_kernel(EwArgs a) {
   constexpr int VE = VecW<T>::VE;
+  __shared__ float red[4 * 64 * 8];
   const int nv = a.N / VE;
-  const int cv = blockIdx.x * 256 + threadIdx.x;
-  if (cv >= nv) return;
+  const int cvl = threadIdx.x & 63, rl = threadIdx.x >> 6;
+  const int cv = blockIdx.x * 64 + cvl;
+  const int chunk = (a.rows + gridDim.y - 1) / gridDim.y;
+  const int r0 = blockIdx.y * chunk, r1 = min(a.rows, r0 + chunk);
   float acc[VE];
 #pragma unroll
   for (int j = 0; j < VE; ++j) acc[j] = 0.f;
-  for (int r = blockIdx.y; r < a.rows; r += gridDim.y) {
-    float d[VE], g[VE];
-    ldv((const T*)a.dy + (int64_t)r * a.lddy + cv * VE, d);
-    if (a.gate) ldv((const T*)a.gate + (int64_t)r * a.ldgate + cv * VE, g);
+  if (cv < nv) {
+    for (int r = r0 + rl; r < r1; r += 4) {
+      float d[VE], g[VE];
+      ldv((const T*)a.dy + (int64_t)r * a.lddy + cv * VE, d);
+      if (a.gate) ldv((const T*)a.gate + (int64_t)r * a.ldgate + cv * VE, g);
+#pragma unroll
+      for (int j = 0; j < VE; ++j) {
+        float v = d[j] * a.alpha;
+        if (a.drop_p > 0.f) v *= drop_scale(a.drop_p, a.seed, (uint64_t)r * a.N + cv * VE + j);
+        if (a.gate) v *= act_bwd(a.act, g[j]);
+        acc[j] += v;
+        d[j] = v;
+      }
+      if (a.out) stv((T*)a.out + (int64_t)r * a.ldout + cv * VE, d);
+    }
+  }
+  if (!a.db) return;
+#pragma unroll
+  for (int j = 0; j < VE; ++j) red[(rl * 64 + cvl) * VE + j] = acc[j];
+  __syncthreads();
+  if (rl == 0 && cv < nv) {
 #pragma unroll
     for (int j = 0; j < VE; ++j) {
-      float v = d[j] * a.alpha;
-      if (a.drop_p > 0.f) v *= drop_scale(a.drop_p, a.seed, (uint64_t)r * a.N + cv * VE + j);
-      if (a.gate) v *= act_bwd(a.act, g[j]);
-      acc[j] += v;
-      d[j] = v;
+      const float t = red[(0 * 64 + cvl) * VE + j] + red[(1 * 64 + cvl) * VE + j] + red[(2 * 64 + cvl) * VE + j] +
+                      red[(3 * 64 + cvl) * VE + j];
+      a.ws[(int64_t)blockIdx.y * a.N + cv * VE + j] = t;
     }
-    if (a.out) stv((T*)a.out + (int64_t)r * a.ldout + cv * VE, d);
   }
-  if (a.db)
-#pragma unroll
-    for (int j = 0; j < VE; ++j) atomicAdd(a.db + cv * VE + j, acc[j]);
+}
+
+// out[c] += sum_b ws[b*ld + c]   (c < N)
+__global__ __launch_bounds__(256) void colsum_finalize_kernel(const float* ws, int nb, int64_t ld, int N, float* out) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= N) return;
+  float s = 0.f;
+  for (int b = 0; b < nb; ++b) s += ws[b * ld + c];
+  out[c] += s;
 }
 
 template <typename T>
@@ -94,12 +120,19 @@ __global__ __launch_bounds__(256) void embed_kernel(avsr_embed_params p, int bwd
 template <typename S, typename D>
 __global__ __launch_bounds__(256) void cast_kernel(int rows, int cols, const S* src, int64_t lds, D* dst,
                                                    int64_t ldd, float alpha, float beta) {
-  const int64_t total = (int64_t)rows * cols;
-  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
-    const int64_t r = i / cols, c = i % cols;
-    float v = alpha * to_f(src[r * lds + c]);
-    if (beta != 0.f) v += beta * to_f(dst[r * ldd + c]);
-    dst[r * ldd + c] = from_f<D>(v);
+  const int64_t c0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+  if (c0 >= cols) return;
+  for (int r = blockIdx.y; r < rows; r += gridDim.y) {
+    const S* s = src + (int64_t)r * lds + c0;
+    D* d = dst + (int64_t)r * ldd + c0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (c0 + q < cols) {
+        float v = alpha * to_f(s[q]);
+        if (beta != 0.f) v += beta * to_f(d[q]);
+        d[q] = from_f<D>(v);
+      }
+    }
   }
 }
 
@@ -241,7 +274,7 @@ EwArgs ew_args(const avsr_ew_params* p) {
   EwArgs a;
   a.rows = p->rows; a.N = p->N; a.dy = p->dy; a.lddy = p->lddy; a.out = p->out; a.ldout = p->ldout;
   a.gate = p->gate; a.ldgate = p->ldgate; a.act = p->act; a.drop_p = p->drop_p; a.seed = p->seed;
-  a.alpha = p->alpha; a.db = p->db;
+  a.alpha = p->alpha; a.db = p->db; a.ws = p->ws;
   return a;
 }
 
@@ -249,14 +282,19 @@ int ew_launch(const avsr_ew_params* p, hipStream_t st) {
   const int ve = p->dtype == AVSR_BF16 ? 8 : 4;
   if (p->N % ve) return AVSR_E_SHAPE;
   if (p->rows == 0) return 0;
+  if (p->db && !p->ws) return AVSR_E_ARG;
   const int nv = p->N / ve;
-  dim3 grid((nv + 255) / 256, 1);
-  int gy = 1024 / (int)grid.x;
-  gy = gy < 1 ? 1 : (gy > p->rows ? p->rows : gy);
+  dim3 grid((nv + 63) / 64, 1);
+  int gy = 2048 / (int)grid.x;
+  gy = gy < 16 ? 16 : (gy > 256 ? 256 : gy);
+  gy = gy > p->rows ? p->rows : gy;
   grid.y = gy;
   EwArgs a = ew_args(p);
   if (p->dtype == AVSR_BF16) hipLaunchKernelGGL(ew_bwd_kernel<bf16>, grid, dim3(256), 0, st, a);
   else hipLaunchKernelGGL(ew_bwd_kernel<float>, grid, dim3(256), 0, st, a);
+  if (p->db)
+    hipLaunchKernelGGL(colsum_finalize_kernel, dim3((p->N + 255) / 256), dim3(256), 0, st, (const float*)p->ws,
+                       (int)grid.y, (int64_t)p->N, p->N, p->db);
   AVSR_CHECK_LAUNCH();
   return 0;
 }
@@ -299,7 +337,12 @@ extern "C" int avsr_embed_bwd(const avsr_embed_params* p, void* stream) { return
 
 extern "C" int avsr_cast(int sd, int dd, int rows, int cols, const void* src, int64_t lds, void* dst, int64_t ldd,
                          float alpha, float beta, void* stream) {
-  const int g = avsr_grid((int64_t)rows * cols);
+  if (rows <= 0 || cols <= 0) return 0;
+  const int64_t gx = ((int64_t)cols + 1023) / 1024;
+  int64_t gy = 4096 / gx;
+  gy = gy < 1 ? 1 : (gy > rows ? rows : gy);
+  gy = gy > 65535 ? 65535 : gy;
+  const dim3 g((unsigned)gx, (unsigned)gy);
   hipStream_t st = (hipStream_t)stream;
   if (sd == AVSR_F32 && dd == AVSR_BF16) hipLaunchKernelGGL((cast_kernel<float, bf16>), dim3(g), dim3(256), 0, st, rows, cols, (const float*)src, lds, (bf16*)dst, ldd, alpha, beta);
   else if (sd == AVSR_F32 && dd == AVSR_F32) hipLaunchKernelGGL((cast_kernel<float, float>), dim3(g), dim3(256), 0, st, rows, cols, (const float*)src, lds, (float*)dst, ldd, alpha, beta);

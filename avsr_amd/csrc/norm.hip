@@ -12,8 +12,17 @@ struct LnArgs {
   const void* x; int64_t ldx; void* y; int64_t ldy;
   const float* gamma; const float* beta; float* mean; float* rstd;
   const void* dy; int64_t lddy; void* dx; int64_t lddx; const void* dres; int64_t lddres;
-  float* dgamma; float* dbeta;
+  float* dgamma; float* dbeta; float* ws;
 };
+
+// out[c] += sum_b ws[b*ld + c]   (c < N)
+__global__ __launch_bounds__(256) void colsum_finalize_kernel(const float* ws, int nb, int64_t ld, int N, float* out) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= N) return;
+  float s = 0.f;
+  for (int b = 0; b < nb; ++b) s += ws[b * ld + c];
+  out[c] += s;
+}
 
 // one wave per row; lane owns vectors lane, lane+64, ... (VPL of them)
 template <typename T, int VPL>
@@ -116,14 +125,23 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(LnArgs a) {
       }
     }
   }
-  if (a.dgamma) {
+  if (!a.dgamma) return;
+  // per-block column partials (4 waves summed in LDS) -> ws[block][2][N]
+  __shared__ float red[4 * 2048];
+  const int w = threadIdx.x >> 6;
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    __syncthreads();
 #pragma unroll
     for (int i = 0; i < VPL; ++i) {
       const int c = (lane + i * 64) * VE;
       if (c < a.N)
 #pragma unroll
-        for (int j = 0; j < VE; ++j) { atomicAdd(a.dgamma + c + j, dg[i][j]); atomicAdd(a.dbeta + c + j, db[i][j]); }
+        for (int j = 0; j < VE; ++j) red[w * a.N + c + j] = q == 0 ? dg[i][j] : db[i][j];
     }
+    __syncthreads();
+    for (int c = threadIdx.x; c < a.N; c += 256)
+      a.ws[((int64_t)blockIdx.x * 2 + q) * a.N + c] = red[c] + red[a.N + c] + red[2 * a.N + c] + red[3 * a.N + c];
   }
 }
 
@@ -134,14 +152,24 @@ int ln_launch(const avsr_layernorm_params* p, bool bwd, hipStream_t st) {
   a.rows = p->rows; a.N = p->N; a.eps = p->eps;
   a.x = p->x; a.ldx = p->ldx; a.y = p->y; a.ldy = p->ldy; a.gamma = p->gamma; a.beta = p->beta;
   a.mean = p->mean; a.rstd = p->rstd; a.dy = p->dy; a.lddy = p->lddy; a.dx = p->dx; a.lddx = p->lddx;
-  a.dres = p->dres; a.lddres = p->lddres; a.dgamma = p->dgamma; a.dbeta = p->dbeta;
+  a.dres = p->dres; a.lddres = p->lddres; a.dgamma = p->dgamma; a.dbeta = p->dbeta; a.ws = p->ws;
   const int vpl = (p->N / VE + 63) / 64;
   int blocks = (p->rows + 3) / 4;
   if (bwd) blocks = blocks < 256 ? blocks : 256;
+  if (bwd && p->dgamma && (!p->ws || p->N > 2048)) return AVSR_E_ARG;
 #define LNL(V)                                                                                   \
   if (vpl <= V) {                                                                                \
-    if (bwd) hipLaunchKernelGGL((ln_bwd_kernel<T, V>), dim3(blocks), dim3(256), 0, st, a);       \
-    else hipLaunchKernelGGL((ln_fwd_kernel<T, V>), dim3(blocks), dim3(256), 0, st, a);           \
+    if (bwd) {                                                                                   \
+      hipLaunchKernelGGL((ln_bwd_kernel<T, V>), dim3(blocks), dim3(256), 0, st, a);              \
+      if (p->dgamma) {                                                                           \
+        hipLaunchKernelGGL(colsum_finalize_kernel, dim3((p->N + 255) / 256), dim3(256), 0, st,  \
+                           (const float*)p->ws, blocks, (int64_t)2 * p->N, p->N, p->dgamma);     \
+        hipLaunchKernelGGL(colsum_finalize_kernel, dim3((p->N + 255) / 256), dim3(256), 0, st,  \
+                           (const float*)(p->ws + p->N), blocks, (int64_t)2 * p->N, p->N, p->dbeta); \
+      }                                                                                          \
+    } else {                                                                                     \
+      hipLaunchKernelGGL((ln_fwd_kernel<T, V>), dim3(blocks), dim3(256), 0, st, a);              \
+    }                                                                                            \
     AVSR_CHECK_LAUNCH();                                                                         \
     return 0;                                                                                    \
   }
@@ -215,7 +243,7 @@ struct BnArgs {
   const void* dy; void* dz;
   const float* mean; const float* invstd; const float* mean2; const float* invstd2;
   float* sums; float* dprelu; float* dgamma; float* dbeta; float* dgamma2; float* dbeta2;
-  void* dh; void* dh2; float beta_acc;
+  void* dh; void* dh2; float beta_acc; float* ws;
 };
 
 template <typename T>
@@ -237,11 +265,10 @@ __global__ __launch_bounds__(256) void bn_act_fwd_kernel(BnArgs a) {
   }
 }
 
-// block-level reduction of per-thread channel partials (thread's channel group is fixed:
-// the grid stride is a multiple of C/VE) followed by one fp32 atomic per channel per block
+// block-level reduction of per-thread channel partials (a thread's channel group is fixed:
+// the grid stride is a multiple of C/VE) -> ws[block][q][C] (plain stores)
 template <int VE>
-__device__ void block_chan_reduce(float (&q)[VE], float* lds, int cpv, float* out, int stride) {
-  // lds: [256][VE]
+__device__ void block_chan_partial(const float (&q)[VE], float* lds, int cpv, float* ws_row) {
 #pragma unroll
   for (int j = 0; j < VE; ++j) lds[threadIdx.x * VE + j] = q[j];
   __syncthreads();
@@ -252,13 +279,39 @@ __device__ void block_chan_reduce(float (&q)[VE], float* lds, int cpv, float* ou
     for (int t = threadIdx.x; t < 256; t += cpv)
 #pragma unroll
       for (int j = 0; j < VE; ++j) acc[j] += lds[t * VE + j];
-    if (out) {
-      const int c0 = threadIdx.x * VE;
 #pragma unroll
-      for (int j = 0; j < VE; ++j) atomicAdd(out + (int64_t)(c0 + j) * stride, acc[j]);
-    }
+    for (int j = 0; j < VE; ++j) ws_row[threadIdx.x * VE + j] = acc[j];
   }
   __syncthreads();
+}
+
+// per channel: S_q = sum over blocks; sums[c][0..2] = S0..S2 (set); grads accumulate
+__global__ __launch_bounds__(256) void bn_grad_finalize_kernel(const float* ws, int nb, int C, float* sums,
+                                                               float* dbeta, float* dgamma, float* dbeta2,
+                                                               float* dgamma2, float* dprelu) {
+  const int c = blockIdx.x;
+  __shared__ float sh[4][4];
+  float s[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int b = threadIdx.x; b < nb; b += 256)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) s[q] += ws[((int64_t)b * 4 + q) * C + c];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const float v = wave_sum(s[q]);
+    if ((threadIdx.x & 63) == 0) sh[q][threadIdx.x >> 6] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) t[q] = sh[q][0] + sh[q][1] + sh[q][2] + sh[q][3];
+    if (sums) { sums[c * 3 + 0] = t[0]; sums[c * 3 + 1] = t[1]; sums[c * 3 + 2] = t[2]; }
+    if (dbeta) dbeta[c] += t[0];
+    if (dgamma) dgamma[c] += t[1];
+    if (dbeta2) dbeta2[c] += t[0];
+    if (dgamma2) dgamma2[c] += t[2];
+    if (dprelu) dprelu[c] += t[3];
+  }
 }
 
 // MODE 0: dy given per element; MODE 1: stem max-pool — dy gathered through the argmax
@@ -317,17 +370,12 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(BnArgs a, avsr_stem_
     }
     stv((T*)a.dz + v * VE, dzo);
   }
-  // channel sums: sums[c][0..2] (scratch for bwd_apply) + gradient accumulators
-  block_chan_reduce<VE>(s0, lds, cpv, a.sums ? a.sums + 0 : nullptr, 3);
-  if (a.dbeta) { block_chan_reduce<VE>(s0, lds, cpv, a.dbeta, 1); }
-  if (a.dbeta2) { block_chan_reduce<VE>(s0, lds, cpv, a.dbeta2, 1); }
-  block_chan_reduce<VE>(s1, lds, cpv, a.sums ? a.sums + 1 : nullptr, 3);
-  if (a.dgamma) block_chan_reduce<VE>(s1, lds, cpv, a.dgamma, 1);
-  if (a.scale2) {
-    block_chan_reduce<VE>(s2, lds, cpv, a.sums ? a.sums + 2 : nullptr, 3);
-    if (a.dgamma2) block_chan_reduce<VE>(s2, lds, cpv, a.dgamma2, 1);
-  }
-  if (a.dprelu) block_chan_reduce<VE>(s3, lds, cpv, a.dprelu, 1);
+  // channel partials of this block -> ws[block][q][C]; bn_grad_finalize sums the blocks
+  float* wsb = a.ws + (int64_t)blockIdx.x * 4 * a.C;
+  block_chan_partial<VE>(s0, lds, cpv, wsb + 0 * a.C);
+  block_chan_partial<VE>(s1, lds, cpv, wsb + 1 * a.C);
+  block_chan_partial<VE>(s2, lds, cpv, wsb + 2 * a.C);
+  block_chan_partial<VE>(s3, lds, cpv, wsb + 3 * a.C);
 }
 
 template <typename T>
@@ -369,7 +417,7 @@ BnArgs bn_args(const avsr_bn_act_params* p) {
   a.scale2 = p->scale2; a.shift2 = p->shift2; a.prelu = p->prelu; a.y = p->y; a.dy = p->dy; a.dz = p->dz;
   a.mean = p->mean; a.invstd = p->invstd; a.mean2 = p->mean2; a.invstd2 = p->invstd2; a.sums = p->sums;
   a.dprelu = p->dprelu; a.dgamma = p->dgamma; a.dbeta = p->dbeta; a.dgamma2 = p->dgamma2; a.dbeta2 = p->dbeta2;
-  a.dh = p->dh; a.dh2 = p->dh2; a.beta_acc = p->beta_acc;
+  a.dh = p->dh; a.dh2 = p->dh2; a.beta_acc = p->beta_acc; a.ws = p->ws;
   return a;
 }
 
@@ -506,12 +554,15 @@ extern "C" int avsr_bn_act_fwd(const avsr_bn_act_params* p, void* stream) {
 extern "C" int avsr_bn_act_bwd_reduce(const avsr_bn_act_params* p, void* stream) {
   int rc = bn_check(p);
   if (rc) return rc;
+  if (!p->ws) return AVSR_E_ARG;
   BnArgs a = bn_args(p);
   avsr_stem_pool_params sp = {};
   const int ve = p->dtype == AVSR_BF16 ? 8 : 4;
   const int g = bn_grid((int64_t)p->M * p->C / ve, p->C / ve);
   if (p->dtype == AVSR_BF16) hipLaunchKernelGGL((bn_bwd_reduce_kernel<bf16, 0>), dim3(g), dim3(256), 0, (hipStream_t)stream, a, sp);
   else hipLaunchKernelGGL((bn_bwd_reduce_kernel<float, 0>), dim3(g), dim3(256), 0, (hipStream_t)stream, a, sp);
+  hipLaunchKernelGGL(bn_grad_finalize_kernel, dim3(p->C), dim3(256), 0, (hipStream_t)stream, (const float*)p->ws, g,
+                     p->C, p->sums, p->dbeta, p->dgamma, p->dbeta2, p->scale2 ? p->dgamma2 : nullptr, p->dprelu);
   AVSR_CHECK_LAUNCH();
   return 0;
 }
@@ -547,10 +598,13 @@ extern "C" int avsr_stem_pool_bwd_reduce(const avsr_stem_pool_params* p, void* s
   BnArgs a = {};
   a.M = p->nimg * p->H * p->W; a.C = p->C; a.h = p->h; a.scale = p->scale; a.shift = p->shift;
   a.prelu = p->prelu; a.dz = p->dz; a.mean = p->mean; a.invstd = p->invstd; a.sums = p->sums;
-  a.dprelu = p->dprelu; a.dgamma = p->dgamma; a.dbeta = p->dbeta;
+  a.dprelu = p->dprelu; a.dgamma = p->dgamma; a.dbeta = p->dbeta; a.ws = p->ws;
+  if (!p->ws) return AVSR_E_ARG;
   const int g = bn_grid((int64_t)a.M * p->C / ve, p->C / ve);
   if (p->dtype == AVSR_BF16) hipLaunchKernelGGL((bn_bwd_reduce_kernel<bf16, 1>), dim3(g), dim3(256), 0, (hipStream_t)stream, a, *p);
   else hipLaunchKernelGGL((bn_bwd_reduce_kernel<float, 1>), dim3(g), dim3(256), 0, (hipStream_t)stream, a, *p);
+  hipLaunchKernelGGL(bn_grad_finalize_kernel, dim3(p->C), dim3(256), 0, (hipStream_t)stream, (const float*)p->ws, g,
+                     p->C, p->sums, p->dbeta, p->dgamma, (float*)nullptr, (float*)nullptr, p->dprelu);
   AVSR_CHECK_LAUNCH();
   return 0;
 }

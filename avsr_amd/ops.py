@@ -210,11 +210,12 @@ def layernorm_bwd(dy, x, gamma, mean, rstd, dx=None, dres=None, dgamma=None, dbe
     """dx = dres + LN-backward(dy); dgamma/dbeta (fp32) accumulate."""
     rows, N = x.shape
     dx = torch.empty_like(x) if dx is None else dx
+    ws = None if dgamma is None else torch.empty(256 * 2 * N, device=x.device)
     _call("avsr_layernorm_bwd", L.fill(L.LayerNormParams, dtype=dtype_code(x), rows=rows, N=N, eps=0.0,
                                         x=x, ldx=x.stride(0), ldy=N, gamma=gamma, mean=mean, rstd=rstd,
                                         dy=dy, lddy=dy.stride(0), dx=dx, lddx=dx.stride(0),
                                         dres=dres, lddres=0 if dres is None else dres.stride(0),
-                                        dgamma=dgamma, dbeta=dbeta))
+                                        dgamma=dgamma, dbeta=dbeta, ws=ws))
     return dx
 
 
@@ -255,8 +256,9 @@ def bn_act_bwd(dy, h, st, prelu, dh, *, res=None, st2=None, dh2=None, dz=None, s
     input when identity) and writes dh (and dh2 for the downsample BN)."""
     M, C = h.shape
     dz = torch.empty_like(h) if dz is None else dz
-    sums = torch.zeros(C, 3, device=h.device) if sums is None else sums.zero_()
-    p = L.fill(L.BnActParams, dtype=dtype_code(h), M=M, C=C, h=h, scale=st.scale, shift=st.shift, res=res,
+    sums = torch.empty(C, 3, device=h.device) if sums is None else sums
+    ws = torch.empty(2048 * 4 * C, device=h.device)
+    p = L.fill(L.BnActParams, ws=ws, dtype=dtype_code(h), M=M, C=C, h=h, scale=st.scale, shift=st.shift, res=res,
                scale2=None if st2 is None else st2.scale, shift2=None if st2 is None else st2.shift,
                prelu=prelu, dy=dy, dz=dz, mean=st.mean, invstd=st.invstd,
                mean2=None if st2 is None else st2.mean, invstd2=None if st2 is None else st2.invstd,
@@ -280,8 +282,9 @@ def stem_pool_bwd(dy, argmax, h, nimg, H, W, st, prelu, dh, *, dz=None, sums=Non
     """Backward through max-pool, PReLU and BN of the stem: writes dh (grad of the conv output)."""
     C = h.shape[-1]
     dz = torch.empty_like(h) if dz is None else dz
-    sums = torch.zeros(C, 3, device=h.device) if sums is None else sums.zero_()
-    sp = L.fill(L.StemPoolParams, dtype=dtype_code(h), nimg=nimg, H=H, W=W, C=C, Ho=(H + 1) // 2,
+    sums = torch.empty(C, 3, device=h.device) if sums is None else sums
+    ws = torch.empty(2048 * 4 * C, device=h.device)
+    sp = L.fill(L.StemPoolParams, ws=ws, dtype=dtype_code(h), nimg=nimg, H=H, W=W, C=C, Ho=(H + 1) // 2,
                 Wo=(W + 1) // 2, h=h, scale=st.scale, shift=st.shift, prelu=prelu, argmax=argmax, dy=dy, dz=dz,
                 mean=st.mean, invstd=st.invstd, sums=sums, dprelu=dprelu, dgamma=dgamma, dbeta=dbeta)
     _call("avsr_stem_pool_bwd_reduce", sp)
@@ -388,7 +391,8 @@ def loss_finalize(B, nll, row_loss, row_correct, mtlalpha, out):
 
 def ew_bwd(dy, *, out=None, gate=None, act=L.ACT_NONE, drop_p=0.0, seed=0, alpha=1.0, db=None):
     rows, N = dy.shape
-    _call("avsr_ew_bwd", L.fill(L.EwParams, dtype=dtype_code(dy), rows=rows, N=N, dy=dy, lddy=dy.stride(0),
+    ws = None if db is None else torch.empty(256 * N, device=dy.device)
+    _call("avsr_ew_bwd", L.fill(L.EwParams, dtype=dtype_code(dy), rows=rows, N=N, dy=dy, lddy=dy.stride(0), ws=ws,
                                  out=out, ldout=0 if out is None else out.stride(0), gate=gate,
                                  ldgate=0 if gate is None else gate.stride(0), act=act, drop_p=float(drop_p),
                                  seed=int(seed) & (2 ** 64 - 1), alpha=alpha, db=db))

@@ -131,7 +131,9 @@ typedef struct {
   void* dx; int64_t lddx;                   /* bwd output */
   const void* dres; int64_t lddres;         /* bwd: residual gradient added to dx (may alias dx) */
   float* dgamma; float* dbeta;              /* bwd: fp32 accumulators [N] or NULL */
+  float* ws;                                /* bwd with dgamma: workspace >= AVSR_LN_WS(N) floats */
 } avsr_layernorm_params;
+#define AVSR_LN_WS(N) (256 * 2 * (N))
 int avsr_layernorm_fwd(const avsr_layernorm_params* p, void* stream);
 int avsr_layernorm_bwd(const avsr_layernorm_params* p, void* stream);
 
@@ -172,11 +174,13 @@ typedef struct {
   const void* dy; void* dz;
   const float* mean; const float* invstd;          /* BN of h (for xhat) */
   const float* mean2; const float* invstd2;        /* BN of res when scale2 */
-  float* sums;    /* [C][5]: sum dz, sum dz*xhat, sum dz*xhat2, prelu grad (fp32, zeroed by caller) */
+  float* sums;    /* [C][3] out: sum dz, sum dz*xhat, sum dz*xhat2 (fp32; written, not accumulated) */
   float* dprelu;  /* [C] fp32 grad accumulator */
   float* dgamma; float* dbeta; float* dgamma2; float* dbeta2;   /* fp32 grad accumulators or NULL */
   void* dh; void* dh2; float beta_acc;             /* bwd_apply outputs (dh2 for the downsample BN) */
+  float* ws;                                       /* bwd_reduce workspace >= AVSR_BN_WS(C) floats */
 } avsr_bn_act_params;
+#define AVSR_BN_WS(C) (2048 * 4 * (C))
 int avsr_bn_act_fwd(const avsr_bn_act_params* p, void* stream);
 int avsr_bn_act_bwd_reduce(const avsr_bn_act_params* p, void* stream);
 int avsr_bn_bwd_apply(const avsr_bn_act_params* p, void* stream);
@@ -192,6 +196,7 @@ typedef struct {
   const void* dy; void* dz;
   const float* mean; const float* invstd;
   float* sums; float* dprelu; float* dgamma; float* dbeta;
+  float* ws;                                       /* >= AVSR_BN_WS(C) floats */
 } avsr_stem_pool_params;
 int avsr_stem_pool_fwd(const avsr_stem_pool_params* p, void* stream);
 int avsr_stem_pool_bwd_reduce(const avsr_stem_pool_params* p, void* stream);
@@ -312,7 +317,9 @@ typedef struct {
   float drop_p; uint64_t seed;
   float alpha;
   float* db;
+  float* ws;                                       /* with db: workspace >= AVSR_EW_WS(N) floats */
 } avsr_ew_params;
+#define AVSR_EW_WS(N) (256 * (N))
 int avsr_ew_bwd(const avsr_ew_params* p, void* stream);
 int avsr_dropout_fwd(const avsr_ew_params* p, void* stream);
 int avsr_mask_rows(int dtype, int B, int T, int N, void* x, int64_t ldx, const int* len, void* stream);

@@ -1,0 +1,35 @@
+"""Summarise a rocprofv3 kernel trace per training step.
+
+  python tools/profsum.py <run_kernel_trace.csv> [last_steps] [top]
+
+Steps are delimited by the optimizer launches (adamw_kernel closes each step); only the last
+`last_steps` steps are counted so setup work (initial shadow cast, warm-up) is excluded.
+"""
+import csv
+import sys
+from collections import defaultdict
+
+path = sys.argv[1]
+last = int(sys.argv[2]) if len(sys.argv) > 2 else 3
+top = int(sys.argv[3]) if len(sys.argv) > 3 else 30
+rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
+ends = [i for i, r in enumerate(rows) if "adamw_kernel" in r["Kernel_Name"]]
+# two adamw launches (decay / no-decay segments) per step
+ends = ends[1::2]
+if len(ends) > last:
+    rows = rows[ends[-last - 1] + 1: ends[-1] + 1]
+    steps = last
+else:
+    steps = max(1, len(ends))
+agg = defaultdict(lambda: [0.0, 0])
+for r in rows:
+    d = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+    a = agg[r["Kernel_Name"]]
+    a[0] += d
+    a[1] += 1
+tot = sum(v[0] for v in agg.values())
+wall = (int(rows[-1]["End_Timestamp"]) - int(rows[0]["Start_Timestamp"])) / 1e6 / steps
+for name, (t, n) in sorted(agg.items(), key=lambda kv: -kv[1][0])[:top]:
+    print(f"{t / 1e6 / steps:8.2f} ms/step {100 * t / tot:6.2f}% n={n / steps:6.1f}/step "
+          f"avg={t / n / 1e3:8.1f}us  {name[:110]}")
+print(f"kernel total {tot / 1e6 / steps:.2f} ms/step, span {wall:.2f} ms/step over {steps} steps")
