@@ -37,6 +37,7 @@ class GemmParams(ctypes.Structure):
         ("drop_p", _f),
         ("seed", ctypes.c_uint64),
         ("splitk", _i),
+        ("ws", _c_p),
     ]
 
 

@@ -114,9 +114,55 @@ template <typename T> AVSR_DEV void stv(T* p, const float* o) {
     *(f32x4*)p = v;
   }
 }
+// q = n / d for 0 <= n < 2^31 (Granlund-Montgomery round-up multiplier)
+struct FastDiv {
+  uint32_t d, m, s;
+};
+static inline FastDiv make_fastdiv(uint32_t d) {
+  FastDiv f; f.d = d; uint32_t s = 0;
+  while ((1ull << s) < d) ++s;
+  f.s = s;
+  f.m = (uint32_t)(((1ull << 32) * ((1ull << s) - d)) / d + 1);
+  return f;
+}
+AVSR_DEV uint32_t fdiv(uint32_t n, const FastDiv& f) { return (__umulhi(n, f.m) + n) >> f.s; }
+
 // grid-stride launch size for memory-bound kernels (<= 8 blocks of 256 per CU)
 static inline int avsr_grid(long work, int per_block = 256, int cap = 2048) {
   long g = (work + per_block - 1) / per_block;
   if (g < 1) g = 1;
   return (int)(g < cap ? g : cap);
 }
+
+// Column sums of a row-block partial workspace: out[c] += sum_b ws[b*ld + c] for c < N, or,
+// when out1 != nullptr, columns [N1, N) go to out1[c - N1] (LayerNorm dgamma/dbeta in one
+// launch). Block = 32 columns (one 128-byte line per row) x 8 row lanes, 4 independent
+// accumulators per lane, LDS reduce: the partial rows are read in parallel, not as a serial
+// dependent chain.
+static __global__ __launch_bounds__(256) void colsum_finalize_kernel(const float* ws, int nb, int64_t ld, int N,
+                                                                     float* out, int N1, float* out1) {
+  __shared__ float red[8][33];
+  const int cl = threadIdx.x & 31, rl = threadIdx.x >> 5;
+  const int c = blockIdx.x * 32 + cl;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  if (c < N) {
+    int b = rl;
+    for (; b + 24 < nb; b += 32) {
+      s0 += ws[(int64_t)b * ld + c];
+      s1 += ws[(int64_t)(b + 8) * ld + c];
+      s2 += ws[(int64_t)(b + 16) * ld + c];
+      s3 += ws[(int64_t)(b + 24) * ld + c];
+    }
+    for (; b < nb; b += 8) s0 += ws[(int64_t)b * ld + c];
+  }
+  red[rl][cl] = (s0 + s1) + (s2 + s3);
+  __syncthreads();
+  if (rl == 0 && c < N) {
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s += red[i][cl];
+    if (out1 && c >= N1) out1[c - N1] += s;
+    else out[c] += s;
+  }
+}
+static inline dim3 colsum_grid(int N) { return dim3((N + 31) / 32); }

@@ -2,6 +2,7 @@
 // Replaces every torch.nn.Linear on the AVSR hot path (forward, data-grad, weight-grad);
 // see include/avsr_hip.h for the reference call sites.
 #include "gemm_core.h"
+#include "gemm_glds.h"
 
 using namespace gemmcore;
 
@@ -9,6 +10,7 @@ namespace {
 
 struct DenseArgs {
   int M, N, K, splits, kchunk;
+  int64_t sSplit;      // slab mode: C offset between K splits (0: atomics / no split)
   const void* A; int64_t lda, sA;
   const void* B; int64_t ldb, sB;
   int64_t sC, sR;
@@ -29,12 +31,66 @@ __global__ __launch_bounds__(NT) void dense_kernel(DenseArgs a) {
   f32x16 acc[2][2];
   mainloop<T, WM, WN>(la, lb, m0, n0, kbeg, kend, acc, smem);
   Epi e = a.e;
-  e.C = (OutT*)e.C + (int64_t)bz * a.sC;
+  e.C = (OutT*)e.C + (int64_t)bz * a.sC + sp * a.sSplit;
   if (e.res) e.res = (const T*)e.res + (int64_t)bz * a.sR;
   if (e.preact) e.preact = (T*)e.preact + (int64_t)bz * a.sC;
   if (e.gate) e.gate = (const T*)e.gate + (int64_t)bz * a.sC;
   e.drop_base = (uint64_t)bz * (uint64_t)a.M * (uint64_t)a.N;
   epilogue<T, OutT, WM, WN>(e, m0, n0, acc, smem);
+}
+
+// bf16 LDS-DMA path (gemm_glds.h): 128x128x64 tiles, 1-D XCD-remapped grid
+template <typename OutT, bool AK, bool BK>
+__global__ __launch_bounds__(256, 2) void dense_glds_kernel(DenseArgs a, int tiles_m, int tiles_n) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  using TL = gemmg::GTile<2, 2>;
+  const int nwg = gridDim.x;
+  const int id = gemmg::xcd_remap(blockIdx.x, nwg);
+  const int tn = id % tiles_n, tm = (id / tiles_n) % tiles_m, z = id / (tiles_n * tiles_m);
+  const int bz = z / a.splits, sp = z % a.splits;
+  const int m0 = tm * TL::BM, n0 = tn * TL::BN;
+  const int kbeg = sp * a.kchunk, kend = min(a.K, kbeg + a.kchunk);
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  using LA = typename std::conditional<AK, gemmg::GDenseK<TL::BM, 4>, gemmg::GDenseR<TL::BM, 4>>::type;
+  using LB = typename std::conditional<BK, gemmg::GDenseK<TL::BN, 4>, gemmg::GDenseR<TL::BN, 4>>::type;
+  LA la; la.init((const bf16*)a.A + (int64_t)bz * a.sA, a.lda, m0, a.M, kend, wave, lane);
+  LB lb; lb.init((const bf16*)a.B + (int64_t)bz * a.sB, a.ldb, n0, a.N, kend, wave, lane);
+  f32x16 acc[2][2];
+  gemmg::mainloop_glds<2, 2>(la, lb, kbeg, (kend - kbeg + gemmg::GBK - 1) / gemmg::GBK, acc, smem);
+  Epi e = a.e;
+  e.C = (OutT*)e.C + (int64_t)bz * a.sC + sp * a.sSplit;
+  if (e.res) e.res = (const bf16*)e.res + (int64_t)bz * a.sR;
+  if (e.preact) e.preact = (bf16*)e.preact + (int64_t)bz * a.sC;
+  if (e.gate) e.gate = (const bf16*)e.gate + (int64_t)bz * a.sC;
+  e.drop_base = (uint64_t)bz * (uint64_t)a.M * (uint64_t)a.N;
+  epilogue<bf16, OutT, 2, 2>(e, m0, n0, acc, smem);
+}
+
+template <typename OutT, bool AK, bool BK>
+int launch_glds(const DenseArgs& a, int batch, hipStream_t st) {
+  using TL = gemmg::GTile<2, 2>;
+  const int tm = (a.M + TL::BM - 1) / TL::BM, tn = (a.N + TL::BN - 1) / TL::BN;
+  const long nwg = (long)tm * tn * batch * a.splits;
+  if (nwg > 0x7fffffffL) return AVSR_E_SHAPE;
+  hipLaunchKernelGGL((dense_glds_kernel<OutT, AK, BK>), dim3((unsigned)nwg), dim3(256), TL::LDS_BYTES, st, a, tm, tn);
+  AVSR_CHECK_LAUNCH();
+  return 0;
+}
+
+template <typename OutT>
+int glds_by_layout(const avsr_gemm_params* p, const DenseArgs& a, hipStream_t st) {
+  if (p->a_kmajor && p->b_kmajor) return launch_glds<OutT, true, true>(a, p->batch, st);
+  if (p->a_kmajor) return launch_glds<OutT, true, false>(a, p->batch, st);
+  if (p->b_kmajor) return launch_glds<OutT, false, true>(a, p->batch, st);
+  return launch_glds<OutT, false, false>(a, p->batch, st);
+}
+
+// the LDS-DMA path needs whole 16-byte vectors along every operand's contiguous dimension
+bool glds_ok(const avsr_gemm_params* p) {
+  if (p->dtype != AVSR_BF16 || p->M < 128 || p->N < 128) return false;
+  if (!p->a_kmajor && (p->M % 8)) return false;
+  if (!p->b_kmajor && (p->N % 8)) return false;
+  return true;
 }
 
 template <typename T, typename OutT, int WM, int WN, bool AK, bool BK>
@@ -61,6 +117,32 @@ int by_tile(const avsr_gemm_params* p, const DenseArgs& a, hipStream_t st) {
   return by_layout<T, OutT, 2, 2>(p, a, st);
 }
 
+// split-K slab reduce: C[b] = alpha * sum_s ws[b][s] + beta * C[b]   (fp32, 4 columns/thread)
+__global__ __launch_bounds__(256) void slab_reduce_kernel(const float* ws, int splits, int M, int N, float* C,
+                                                          int64_t ldc, int64_t sC, float alpha, float beta) {
+  const int nq = N / 4;
+  const int64_t per = (int64_t)M * nq;
+  const int b = blockIdx.y;
+  const int64_t mn = (int64_t)M * N;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < per; i += (int64_t)gridDim.x * 256) {
+    const int m = (int)(i / nq), n = (int)(i % nq) * 4;
+    const float* w = ws + (int64_t)b * splits * mn + (int64_t)m * N + n;
+    f32x4 s = *(const f32x4*)w;
+    for (int q = 1; q < splits; ++q) s += *(const f32x4*)(w + q * mn);
+    float* c = C + (int64_t)b * sC + (int64_t)m * ldc + n;
+    f32x4 o = s * alpha;
+    if (beta != 0.f) o += *(const f32x4*)c * beta;
+    *(f32x4*)c = o;
+  }
+}
+
+// AVSR_GEMM_NOGLDS=1 forces the register-staged core (A/B comparisons, debugging)
+bool getenv_flag_noglds() {
+  static int v = -1;
+  if (v < 0) { const char* e = getenv("AVSR_GEMM_NOGLDS"); v = (e && e[0] == '1') ? 1 : 0; }
+  return v == 1;
+}
+
 }  // namespace
 
 extern "C" int avsr_gemm(const avsr_gemm_params* p, void* stream) {
@@ -74,22 +156,42 @@ extern "C" int avsr_gemm(const avsr_gemm_params* p, void* stream) {
   if ((p->a_kmajor || p->b_kmajor) && (p->K % ve)) return AVSR_E_ALIGN;
   const int splits = p->splitk > 1 ? p->splitk : 1;
   if (splits > 1 && !(p->c_f32 || p->dtype == AVSR_F32)) return AVSR_E_ARG;
+  const bool slab = splits > 1 && p->ws != nullptr;
+  if (slab && (p->bias || p->act || p->preact || p->res || p->gate || p->drop_p > 0.f || p->epi_bwd || (p->N % 4) ||
+               (p->ldc % 4) || (p->strideC % 4) || !avsr_aligned16(p->C)))
+    return AVSR_E_ARG;
   DenseArgs a;
   a.M = p->M; a.N = p->N; a.K = p->K;
   a.splits = splits;
-  a.kchunk = ((p->K + splits - 1) / splits + BKE - 1) / BKE * BKE;
+  const bool glds = glds_ok(p) && !getenv_flag_noglds();
+  const int kq = glds ? gemmg::GBK : BKE;
+  a.kchunk = ((p->K + splits - 1) / splits + kq - 1) / kq * kq;
   a.A = p->A; a.lda = p->lda; a.sA = p->strideA;
   a.B = p->B; a.ldb = p->ldb; a.sB = p->strideB;
   a.sC = p->strideC; a.sR = p->strideR;
   Epi& e = a.e;
   e.M = p->M; e.N = p->N; e.C = p->C; e.ldc = p->ldc;
   e.alpha = p->alpha; e.beta = p->beta; e.bias = p->bias;
-  e.act = p->act; e.bwd = p->epi_bwd; e.atomic = splits > 1;
+  e.act = p->act; e.bwd = p->epi_bwd; e.atomic = splits > 1 && !slab;
+  a.sSplit = 0;
+  if (slab) {   // partial tiles -> ws[b][split][M][N], reduced below
+    e.C = p->ws; e.ldc = p->N; e.alpha = 1.f; e.beta = 0.f;
+    a.sC = (int64_t)splits * p->M * p->N; a.sSplit = (int64_t)p->M * p->N;
+  }
   e.preact = p->preact; e.res = p->res; e.ldr = p->ldr; e.gate = p->gate;
   e.drop_p = p->drop_p; e.seed = p->seed; e.drop_base = 0; e.stats = nullptr; e.stats_tiles = 0;
   hipStream_t st = (hipStream_t)stream;
   if (p->K == 0) return AVSR_E_SHAPE;
-  if (p->dtype == AVSR_F32) return by_tile<float, float>(p, a, st);
-  if (p->c_f32) return by_tile<bf16, float>(p, a, st);
-  return by_tile<bf16, bf16>(p, a, st);
+  int rc;
+  if (glds) rc = p->c_f32 ? glds_by_layout<float>(p, a, st) : glds_by_layout<bf16>(p, a, st);
+  else if (p->dtype == AVSR_F32) rc = by_tile<float, float>(p, a, st);
+  else if (p->c_f32) rc = by_tile<bf16, float>(p, a, st);
+  else rc = by_tile<bf16, bf16>(p, a, st);
+  if (rc || !slab) return rc;
+  const int64_t per = (int64_t)p->M * (p->N / 4);
+  const dim3 g((unsigned)avsr_grid(per, 256, 1024), p->batch);
+  hipLaunchKernelGGL(slab_reduce_kernel, g, dim3(256), 0, st, (const float*)p->ws, splits, p->M, p->N, (float*)p->C,
+                     p->ldc, p->strideC, p->alpha, p->beta);
+  AVSR_CHECK_LAUNCH();
+  return 0;
 }

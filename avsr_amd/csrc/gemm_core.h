@@ -25,19 +25,6 @@ constexpr int BKE = 32, NT = 256;
 
 template <typename T> struct V { static constexpr int VE = 16 / (int)sizeof(T); static constexpr int ROW = BKE + VE; };
 
-// q = n / d for 0 <= n < 2^31 (Granlund-Montgomery round-up multiplier)
-struct FastDiv {
-  uint32_t d, m, s;
-};
-static inline FastDiv make_fastdiv(uint32_t d) {
-  FastDiv f; f.d = d; uint32_t s = 0;
-  while ((1ull << s) < d) ++s;
-  f.s = s;
-  f.m = (uint32_t)(((1ull << 32) * ((1ull << s) - d)) / d + 1);
-  return f;
-}
-AVSR_DEV uint32_t fdiv(uint32_t n, const FastDiv& f) { return (__umulhi(n, f.m) + n) >> f.s; }
-
 AVSR_DEV void zero(v16& v) { v.w[0] = v.w[1] = v.w[2] = v.w[3] = 0u; }
 
 // ---- convolution geometry (one group) ----------------------------------------------

@@ -59,14 +59,6 @@ __global__ __launch_bounds__(256) void ew_bwd_kernel(EwArgs a) {
   }
 }
 
-// out[c] += sum_b ws[b*ld + c]   (c < N)
-__global__ __launch_bounds__(256) void colsum_finalize_kernel(const float* ws, int nb, int64_t ld, int N, float* out) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= N) return;
-  float s = 0.f;
-  for (int b = 0; b < nb; ++b) s += ws[b * ld + c];
-  out[c] += s;
-}
 
 template <typename T>
 __global__ __launch_bounds__(256) void mask_rows_kernel(int B, int T_, int N, T* x, int64_t ldx, const int* len) {
@@ -293,8 +285,8 @@ int ew_launch(const avsr_ew_params* p, hipStream_t st) {
   if (p->dtype == AVSR_BF16) hipLaunchKernelGGL(ew_bwd_kernel<bf16>, grid, dim3(256), 0, st, a);
   else hipLaunchKernelGGL(ew_bwd_kernel<float>, grid, dim3(256), 0, st, a);
   if (p->db)
-    hipLaunchKernelGGL(colsum_finalize_kernel, dim3((p->N + 255) / 256), dim3(256), 0, st, (const float*)p->ws,
-                       (int)grid.y, (int64_t)p->N, p->N, p->db);
+    hipLaunchKernelGGL(colsum_finalize_kernel, colsum_grid(p->N), dim3(256), 0, st, (const float*)p->ws,
+                       (int)grid.y, (int64_t)p->N, p->N, p->db, 0, (float*)nullptr);
   AVSR_CHECK_LAUNCH();
   return 0;
 }

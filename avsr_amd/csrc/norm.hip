@@ -15,15 +15,6 @@ struct LnArgs {
   float* dgamma; float* dbeta; float* ws;
 };
 
-// out[c] += sum_b ws[b*ld + c]   (c < N)
-__global__ __launch_bounds__(256) void colsum_finalize_kernel(const float* ws, int nb, int64_t ld, int N, float* out) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= N) return;
-  float s = 0.f;
-  for (int b = 0; b < nb; ++b) s += ws[b * ld + c];
-  out[c] += s;
-}
-
 // one wave per row; lane owns vectors lane, lane+64, ... (VPL of them)
 template <typename T, int VPL>
 __global__ __launch_bounds__(256) void ln_fwd_kernel(LnArgs a) {
@@ -162,10 +153,9 @@ int ln_launch(const avsr_layernorm_params* p, bool bwd, hipStream_t st) {
     if (bwd) {                                                                                   \
       hipLaunchKernelGGL((ln_bwd_kernel<T, V>), dim3(blocks), dim3(256), 0, st, a);              \
       if (p->dgamma) {                                                                           \
-        hipLaunchKernelGGL(colsum_finalize_kernel, dim3((p->N + 255) / 256), dim3(256), 0, st,  \
-                           (const float*)p->ws, blocks, (int64_t)2 * p->N, p->N, p->dgamma);     \
-        hipLaunchKernelGGL(colsum_finalize_kernel, dim3((p->N + 255) / 256), dim3(256), 0, st,  \
-                           (const float*)(p->ws + p->N), blocks, (int64_t)2 * p->N, p->N, p->dbeta); \
+        hipLaunchKernelGGL(colsum_finalize_kernel, colsum_grid(2 * p->N), dim3(256), 0, st,     \
+                           (const float*)p->ws, blocks, (int64_t)2 * p->N, 2 * p->N, p->dgamma, \
+                           p->N, p->dbeta);                                                      \
       }                                                                                          \
     } else {                                                                                     \
       hipLaunchKernelGGL((ln_fwd_kernel<T, V>), dim3(blocks), dim3(256), 0, st, a);              \
@@ -246,22 +236,48 @@ struct BnArgs {
   void* dh; void* dh2; float beta_acc; float* ws;
 };
 
+// Per-channel parameters of the thread's fixed channel group (the grid stride is a multiple
+// of C/VE, so every vector a thread visits has the same channels): loaded once.
+template <int VE>
+AVSR_DEV void chan_load(const float* p, int c0, float (&o)[VE]) {
+#pragma unroll
+  for (int j = 0; j < VE; ++j) o[j] = p ? p[c0 + j] : 0.f;
+}
+
+// y = PReLU(h*scale + shift [+ res*scale2 + shift2 | + res]); two vectors per iteration so
+// each wave keeps two independent 16-byte loads (x2 with the residual) in flight.
 template <typename T>
 __global__ __launch_bounds__(256) void bn_act_fwd_kernel(BnArgs a) {
   constexpr int VE = VecW<T>::VE;
-  const int64_t nv = (int64_t)a.M * a.C / VE;
-  for (int64_t v = blockIdx.x * 256 + threadIdx.x; v < nv; v += (int64_t)gridDim.x * 256) {
-    const int c0 = (int)(v % (a.C / VE)) * VE;
-    float h[VE], r[VE], o[VE];
-    ldv((const T*)a.h + v * VE, h);
-    if (a.res) ldv((const T*)a.res + v * VE, r);
-#pragma unroll
-    for (int j = 0; j < VE; ++j) {
-      float z = h[j] * a.scale[c0 + j] + a.shift[c0 + j];
-      if (a.res) z += a.scale2 ? r[j] * a.scale2[c0 + j] + a.shift2[c0 + j] : r[j];
-      o[j] = z > 0.f ? z : z * a.prelu[c0 + j];
+  const int cpv = a.C / VE;
+  const int64_t nv = (int64_t)a.M * cpv, stride = (int64_t)gridDim.x * 256;
+  const int64_t t0 = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int c0 = (int)(t0 % cpv) * VE;
+  float sc[VE], sh[VE], pw[VE], sc2[VE], sh2[VE];
+  chan_load(a.scale, c0, sc); chan_load(a.shift, c0, sh); chan_load(a.prelu, c0, pw);
+  chan_load(a.scale2, c0, sc2); chan_load(a.shift2, c0, sh2);
+  const bool res = a.res != nullptr, res_bn = a.scale2 != nullptr;
+  for (int64_t v = t0; v < nv; v += 2 * stride) {
+    const bool two = v + stride < nv;
+    float h[2][VE], r[2][VE];
+    ldv((const T*)a.h + v * VE, h[0]);
+    if (two) ldv((const T*)a.h + (v + stride) * VE, h[1]);
+    if (res) {
+      ldv((const T*)a.res + v * VE, r[0]);
+      if (two) ldv((const T*)a.res + (v + stride) * VE, r[1]);
     }
-    stv((T*)a.y + v * VE, o);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      if (u == 1 && !two) break;
+      float o[VE];
+#pragma unroll
+      for (int j = 0; j < VE; ++j) {
+        float z = h[u][j] * sc[j] + sh[j];
+        if (res) z += res_bn ? r[u][j] * sc2[j] + sh2[j] : r[u][j];
+        o[j] = z > 0.f ? z : z * pw[j];
+      }
+      stv((T*)a.y + (v + u * stride) * VE, o);
+    }
   }
 }
 
@@ -315,40 +331,53 @@ __global__ __launch_bounds__(256) void bn_grad_finalize_kernel(const float* ws, 
 }
 
 // MODE 0: dy given per element; MODE 1: stem max-pool — dy gathered through the argmax
+// (sp.fd_w / sp.fd_hw: host-built fast divisions by W and H*W).
+struct StemGeo { FastDiv fw, fhw; };
+
 template <typename T, int MODE>
-__global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(BnArgs a, avsr_stem_pool_params sp) {
+__global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(BnArgs a, avsr_stem_pool_params sp, StemGeo geo) {
   constexpr int VE = VecW<T>::VE;
   __shared__ float lds[256 * VE];
   const int cpv = a.C / VE;
-  const int64_t nv = (int64_t)a.M * cpv;
+  const int64_t nv = (int64_t)a.M * cpv, stride = (int64_t)gridDim.x * 256;
   float s0[VE], s1[VE], s2[VE], s3[VE];
 #pragma unroll
   for (int j = 0; j < VE; ++j) { s0[j] = s1[j] = s2[j] = s3[j] = 0.f; }
-  const int64_t tid0 = blockIdx.x * 256 + threadIdx.x;
-  const int c0 = (int)(tid0 % cpv) * VE;
-  for (int64_t v = tid0; v < nv; v += (int64_t)gridDim.x * 256) {
+  const int64_t t0 = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int c0 = (int)(t0 % cpv) * VE;
+  float sc[VE], sh[VE], pw[VE], mu[VE], is[VE];
+  chan_load(a.scale, c0, sc); chan_load(a.shift, c0, sh); chan_load(a.prelu, c0, pw);
+  chan_load(a.mean, c0, mu); chan_load(a.invstd, c0, is);
+  const bool res = a.res != nullptr, res_bn = a.scale2 != nullptr;
+  for (int64_t v = t0; v < nv; v += stride) {
     float h[VE], r[VE], d[VE];
     ldv((const T*)a.h + v * VE, h);
-    if (a.res) ldv((const T*)a.res + v * VE, r);
+    if (res) ldv((const T*)a.res + v * VE, r);
     if constexpr (MODE == 0) {
       ldv((const T*)a.dy + v * VE, d);
     } else {
       // input pixel (n, ih, iw) of the stem max-pool; windows (oh, ow) with 2*o-1 <= i <= 2*o+1
-      const int64_t pix = v / cpv;
-      const int iw = (int)(pix % sp.W), ih = (int)((pix / sp.W) % sp.H);
-      const int64_t n = pix / ((int64_t)sp.W * sp.H);
+      const uint32_t pix = (uint32_t)(v >> (31 - __builtin_clz(cpv)));   // cpv | 256: a power of two
+      const uint32_t n = fdiv(pix, geo.fhw), rem = pix - n * geo.fhw.d;
+      const int ih = (int)fdiv(rem, geo.fw), iw = (int)(rem - ih * geo.fw.d);
 #pragma unroll
       for (int j = 0; j < VE; ++j) d[j] = 0.f;
       const int oh0 = (ih + 1) / 2 - 1, ow0 = (iw + 1) / 2 - 1;
-      for (int oh = oh0; oh <= oh0 + 1; ++oh) {
+#pragma unroll
+      for (int dh = 0; dh < 2; ++dh) {
+        const int oh = oh0 + dh;
         if (oh < 0 || oh >= sp.Ho || ih < 2 * oh - 1 || ih > 2 * oh + 1) continue;
-        for (int ow = ow0; ow <= ow0 + 1; ++ow) {
+#pragma unroll
+        for (int dw = 0; dw < 2; ++dw) {
+          const int ow = ow0 + dw;
           if (ow < 0 || ow >= sp.Wo || iw < 2 * ow - 1 || iw > 2 * ow + 1) continue;
-          const int64_t ov = ((n * sp.Ho + oh) * sp.Wo + ow) * cpv + c0 / VE;
+          const int64_t ov = (((int64_t)n * sp.Ho + oh) * sp.Wo + ow) * cpv + c0 / VE;
           const uint8_t want = (uint8_t)((ih - 2 * oh + 1) * 3 + (iw - 2 * ow + 1));
           float g[VE];
           ldv((const T*)sp.dy + ov * VE, g);
-          const uint8_t* am = sp.argmax + ov * VE;
+          uint8_t am[VE];
+          if constexpr (VE == 8) *(uint2*)am = *(const uint2*)(sp.argmax + ov * VE);
+          else *(uint32_t*)am = *(const uint32_t*)(sp.argmax + ov * VE);
 #pragma unroll
           for (int j = 0; j < VE; ++j) d[j] += am[j] == want ? g[j] : 0.f;
         }
@@ -357,16 +386,14 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(BnArgs a, avsr_stem_
     float dzo[VE];
 #pragma unroll
     for (int j = 0; j < VE; ++j) {
-      const int c = c0 + j;
-      float z = h[j] * a.scale[c] + a.shift[c];
-      if (a.res) z += a.scale2 ? r[j] * a.scale2[c] + a.shift2[c] : r[j];
-      const float pw = a.prelu[c];
-      const float dz = z > 0.f ? d[j] : d[j] * pw;
+      float z = h[j] * sc[j] + sh[j];
+      if (res) z += res_bn ? r[j] * a.scale2[c0 + j] + a.shift2[c0 + j] : r[j];
+      const float dz = z > 0.f ? d[j] : d[j] * pw[j];
       s3[j] += z > 0.f ? 0.f : d[j] * z;
       dzo[j] = dz;
       s0[j] += dz;
-      s1[j] += dz * (h[j] - a.mean[c]) * a.invstd[c];
-      if (a.scale2) s2[j] += dz * (r[j] - a.mean2[c]) * a.invstd2[c];
+      s1[j] += dz * (h[j] - mu[j]) * is[j];
+      if (res_bn) s2[j] += dz * (r[j] - a.mean2[c0 + j]) * a.invstd2[c0 + j];
     }
     stv((T*)a.dz + v * VE, dzo);
   }
@@ -381,31 +408,46 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(BnArgs a, avsr_stem_
 template <typename T>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(BnArgs a) {
   constexpr int VE = VecW<T>::VE;
-  const int64_t nv = (int64_t)a.M * a.C / VE;
+  const int cpv = a.C / VE;
+  const int64_t nv = (int64_t)a.M * cpv, stride = (int64_t)gridDim.x * 256;
+  const int64_t t0 = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int c0 = (int)(t0 % cpv) * VE;
   const float invM = 1.f / (float)a.M;
-  for (int64_t v = blockIdx.x * 256 + threadIdx.x; v < nv; v += (int64_t)gridDim.x * 256) {
-    const int c0 = (int)(v % (a.C / VE)) * VE;
+  // dh = scale*(dz - S0/M - xh*S1/M) with xh = (h-mean)*invstd  ==  A*dz + B*(h-mean) + Cc
+  float ka[VE], kb[VE], kc[VE], km[VE], ka2[VE], kb2[VE], kc2[VE], km2[VE];
+#pragma unroll
+  for (int j = 0; j < VE; ++j) {
+    const int c = c0 + j;
+    const float s0 = a.sums[c * 3 + 0] * invM, s1 = a.sums[c * 3 + 1] * invM;
+    ka[j] = a.scale[c];
+    kb[j] = -a.scale[c] * s1 * a.invstd[c];
+    kc[j] = -a.scale[c] * s0;
+    km[j] = a.mean[c];
+    if (a.dh2) {
+      const float s2 = a.sums[c * 3 + 2] * invM;
+      ka2[j] = a.scale2[c];
+      kb2[j] = -a.scale2[c] * s2 * a.invstd2[c];
+      kc2[j] = -a.scale2[c] * s0;
+      km2[j] = a.mean2[c];
+    }
+  }
+  const bool acc = a.beta_acc != 0.f;
+  for (int64_t v = t0; v < nv; v += stride) {
     float dz[VE], h[VE], o[VE];
     ldv((const T*)a.dz + v * VE, dz);
     ldv((const T*)a.h + v * VE, h);
-    if (a.beta_acc != 0.f) ldv((const T*)a.dh + v * VE, o);
+    if (acc) ldv((const T*)a.dh + v * VE, o);
 #pragma unroll
     for (int j = 0; j < VE; ++j) {
-      const int c = c0 + j;
-      const float xh = (h[j] - a.mean[c]) * a.invstd[c];
-      const float g = a.scale[c] * (dz[j] - a.sums[c * 3 + 0] * invM - xh * a.sums[c * 3 + 1] * invM);
-      o[j] = a.beta_acc != 0.f ? a.beta_acc * o[j] + g : g;
+      const float g = ka[j] * dz[j] + kb[j] * (h[j] - km[j]) + kc[j];
+      o[j] = acc ? a.beta_acc * o[j] + g : g;
     }
     stv((T*)a.dh + v * VE, o);
     if (a.dh2) {
       float r[VE], o2[VE];
       ldv((const T*)a.res + v * VE, r);
 #pragma unroll
-      for (int j = 0; j < VE; ++j) {
-        const int c = c0 + j;
-        const float xh = (r[j] - a.mean2[c]) * a.invstd2[c];
-        o2[j] = a.scale2[c] * (dz[j] - a.sums[c * 3 + 0] * invM - xh * a.sums[c * 3 + 2] * invM);
-      }
+      for (int j = 0; j < VE; ++j) o2[j] = ka2[j] * dz[j] + kb2[j] * (r[j] - km2[j]) + kc2[j];
       stv((T*)a.dh2 + v * VE, o2);
     }
   }
@@ -422,40 +464,47 @@ BnArgs bn_args(const avsr_bn_act_params* p) {
 }
 
 // =============================================================== stem max-pool
+// grid (vector blocks of one image, image): 32-bit in-image indexing, the nine window
+// loads issued together (clamped addresses, masked values)
 template <typename T>
-__global__ __launch_bounds__(256) void stem_pool_fwd_kernel(avsr_stem_pool_params p) {
+__global__ __launch_bounds__(256) void stem_pool_fwd_kernel(avsr_stem_pool_params p, FastDiv fwo) {
   constexpr int VE = VecW<T>::VE;
   const int cpv = p.C / VE;
-  const int64_t nv = (int64_t)p.nimg * p.Ho * p.Wo * cpv;
-  for (int64_t v = blockIdx.x * 256 + threadIdx.x; v < nv; v += (int64_t)gridDim.x * 256) {
-    const int c0 = (int)(v % cpv) * VE;
-    const int64_t pix = v / cpv;
-    const int ow = (int)(pix % p.Wo), oh = (int)((pix / p.Wo) % p.Ho);
-    const int64_t n = pix / ((int64_t)p.Wo * p.Ho);
-    float best[VE];
-    uint8_t idx[VE];
+  const int per_img = p.Ho * p.Wo * cpv;
+  const int v = blockIdx.x * 256 + threadIdx.x;
+  if (v >= per_img) return;
+  const int n = blockIdx.y;
+  const int cv = v % cpv, c0 = cv * VE;
+  const uint32_t opix = (uint32_t)(v / cpv);
+  const int oh = (int)fdiv(opix, fwo), ow = (int)(opix - oh * fwo.d);
+  float sc[VE], sh[VE], pw[VE];
+  chan_load(p.scale, c0, sc); chan_load(p.shift, c0, sh); chan_load(p.prelu, c0, pw);
+  const T* base = (const T*)p.h + (int64_t)n * p.H * p.W * p.C + c0;
+  float hv[9][VE];
 #pragma unroll
-    for (int j = 0; j < VE; ++j) { best[j] = -INFINITY; idx[j] = 0; }
-    for (int dh = 0; dh < 3; ++dh) {
-      const int ih = 2 * oh - 1 + dh;
-      if (ih < 0 || ih >= p.H) continue;
-      for (int dw = 0; dw < 3; ++dw) {
-        const int iw = 2 * ow - 1 + dw;
-        if (iw < 0 || iw >= p.W) continue;
-        float h[VE];
-        ldv((const T*)p.h + (((n * p.H + ih) * p.W + iw) * p.C + c0), h);
-#pragma unroll
-        for (int j = 0; j < VE; ++j) {
-          const float z = h[j] * p.scale[c0 + j] + p.shift[c0 + j];
-          const float y = z > 0.f ? z : z * p.prelu[c0 + j];
-          if (y > best[j]) { best[j] = y; idx[j] = (uint8_t)(dh * 3 + dw); }
-        }
-      }
-    }
-    stv((T*)p.y + v * VE, best);
-#pragma unroll
-    for (int j = 0; j < VE; ++j) p.argmax[v * VE + j] = idx[j];
+  for (int q = 0; q < 9; ++q) {
+    const int ih = min(max(2 * oh - 1 + q / 3, 0), p.H - 1), iw = min(max(2 * ow - 1 + q % 3, 0), p.W - 1);
+    ldv(base + (ih * p.W + iw) * p.C, hv[q]);
   }
+  float best[VE];
+  uint8_t idx[VE];
+#pragma unroll
+  for (int j = 0; j < VE; ++j) { best[j] = -INFINITY; idx[j] = 0; }
+#pragma unroll
+  for (int q = 0; q < 9; ++q) {
+    const int ih = 2 * oh - 1 + q / 3, iw = 2 * ow - 1 + q % 3;
+    if (ih < 0 || ih >= p.H || iw < 0 || iw >= p.W) continue;
+#pragma unroll
+    for (int j = 0; j < VE; ++j) {
+      const float z = hv[q][j] * sc[j] + sh[j];
+      const float y = z > 0.f ? z : z * pw[j];
+      if (y > best[j]) { best[j] = y; idx[j] = (uint8_t)q; }
+    }
+  }
+  const int64_t ov = (int64_t)n * per_img + v;
+  stv((T*)p.y + ov * VE, best);
+  if constexpr (VE == 8) *(uint2*)(p.argmax + ov * VE) = *(const uint2*)idx;
+  else *(uint32_t*)(p.argmax + ov * VE) = *(const uint32_t*)idx;
 }
 
 // =============================================================== avg pool
@@ -559,8 +608,8 @@ extern "C" int avsr_bn_act_bwd_reduce(const avsr_bn_act_params* p, void* stream)
   avsr_stem_pool_params sp = {};
   const int ve = p->dtype == AVSR_BF16 ? 8 : 4;
   const int g = bn_grid((int64_t)p->M * p->C / ve, p->C / ve);
-  if (p->dtype == AVSR_BF16) hipLaunchKernelGGL((bn_bwd_reduce_kernel<bf16, 0>), dim3(g), dim3(256), 0, (hipStream_t)stream, a, sp);
-  else hipLaunchKernelGGL((bn_bwd_reduce_kernel<float, 0>), dim3(g), dim3(256), 0, (hipStream_t)stream, a, sp);
+  if (p->dtype == AVSR_BF16) hipLaunchKernelGGL((bn_bwd_reduce_kernel<bf16, 0>), dim3(g), dim3(256), 0, (hipStream_t)stream, a, sp, StemGeo{});
+  else hipLaunchKernelGGL((bn_bwd_reduce_kernel<float, 0>), dim3(g), dim3(256), 0, (hipStream_t)stream, a, sp, StemGeo{});
   hipLaunchKernelGGL(bn_grad_finalize_kernel, dim3(p->C), dim3(256), 0, (hipStream_t)stream, (const float*)p->ws, g,
                      p->C, p->sums, p->dbeta, p->dgamma, p->dbeta2, p->scale2 ? p->dgamma2 : nullptr, p->dprelu);
   AVSR_CHECK_LAUNCH();
@@ -584,9 +633,11 @@ extern "C" int avsr_stem_pool_fwd(const avsr_stem_pool_params* p, void* stream) 
   if (!p) return AVSR_E_ARG;
   const int ve = p->dtype == AVSR_BF16 ? 8 : 4;
   if (p->C % ve) return AVSR_E_SHAPE;
-  const int g = avsr_grid((int64_t)p->nimg * p->Ho * p->Wo * p->C / ve);
-  if (p->dtype == AVSR_BF16) hipLaunchKernelGGL(stem_pool_fwd_kernel<bf16>, dim3(g), dim3(256), 0, (hipStream_t)stream, *p);
-  else hipLaunchKernelGGL(stem_pool_fwd_kernel<float>, dim3(g), dim3(256), 0, (hipStream_t)stream, *p);
+  if (p->nimg > 65535) return AVSR_E_SHAPE;
+  const dim3 g((p->Ho * p->Wo * p->C / ve + 255) / 256, p->nimg);
+  const FastDiv fwo = make_fastdiv(p->Wo);
+  if (p->dtype == AVSR_BF16) hipLaunchKernelGGL(stem_pool_fwd_kernel<bf16>, g, dim3(256), 0, (hipStream_t)stream, *p, fwo);
+  else hipLaunchKernelGGL(stem_pool_fwd_kernel<float>, g, dim3(256), 0, (hipStream_t)stream, *p, fwo);
   AVSR_CHECK_LAUNCH();
   return 0;
 }
@@ -600,9 +651,11 @@ extern "C" int avsr_stem_pool_bwd_reduce(const avsr_stem_pool_params* p, void* s
   a.prelu = p->prelu; a.dz = p->dz; a.mean = p->mean; a.invstd = p->invstd; a.sums = p->sums;
   a.dprelu = p->dprelu; a.dgamma = p->dgamma; a.dbeta = p->dbeta; a.ws = p->ws;
   if (!p->ws) return AVSR_E_ARG;
+  if ((int64_t)p->nimg * p->H * p->W >= (1ll << 31)) return AVSR_E_SHAPE;
+  const StemGeo geo{make_fastdiv(p->W), make_fastdiv(p->H * p->W)};
   const int g = bn_grid((int64_t)a.M * p->C / ve, p->C / ve);
-  if (p->dtype == AVSR_BF16) hipLaunchKernelGGL((bn_bwd_reduce_kernel<bf16, 1>), dim3(g), dim3(256), 0, (hipStream_t)stream, a, *p);
-  else hipLaunchKernelGGL((bn_bwd_reduce_kernel<float, 1>), dim3(g), dim3(256), 0, (hipStream_t)stream, a, *p);
+  if (p->dtype == AVSR_BF16) hipLaunchKernelGGL((bn_bwd_reduce_kernel<bf16, 1>), dim3(g), dim3(256), 0, (hipStream_t)stream, a, *p, geo);
+  else hipLaunchKernelGGL((bn_bwd_reduce_kernel<float, 1>), dim3(g), dim3(256), 0, (hipStream_t)stream, a, *p, geo);
   hipLaunchKernelGGL(bn_grad_finalize_kernel, dim3(p->C), dim3(256), 0, (hipStream_t)stream, (const float*)p->ws, g,
                      p->C, p->sums, p->dbeta, p->dgamma, (float*)nullptr, (float*)nullptr, p->dprelu);
   AVSR_CHECK_LAUNCH();

@@ -132,13 +132,17 @@ class Engine:
         return mod, self.arena.master(prefix + ".weight"), self.arena.master(prefix + ".bias")
 
     def _wgrad(self, dy, x, dW, alpha=1.0):
-        """dW (fp32) += alpha * dy^T x, split-K over the token dimension when the tile grid is small."""
+        """dW (fp32) += alpha * dy^T x. When the output tile grid is below ~2 blocks per CU the
+        token dimension is split and the partial tiles go to a slab workspace (no atomics)."""
         M, N = dy.shape
         K = x.shape[1]
         tiles = ((N + 127) // 128) * ((K + 127) // 128)
-        splitk = max(1, min(16, 1024 // max(tiles, 1), M // 512))
+        splitk = 1 if tiles >= 256 else max(1, min(16, 512 // max(tiles, 1), M // 512))
+        ws = None
+        if splitk > 1:
+            ws = torch.empty(splitk * N * K, device=dy.device, dtype=torch.float32)
         ops.gemm(dy, x, dW, M=N, N=K, K=M, a_kmajor=False, b_kmajor=False, lda=dy.stride(0), ldb=x.stride(0),
-                 ldc=dW.stride(0), alpha=alpha, beta=1.0, splitk=splitk)
+                 ldc=dW.stride(0), alpha=alpha, beta=1.0, splitk=splitk, ws=ws)
 
     def _bias_grad(self, g, db, alpha=1.0):
         ops.ew_bwd(g, db=db, alpha=alpha)

@@ -30,7 +30,7 @@ def _ptr(t):
 def gemm(A, B, C, *, M, N, K, a_kmajor, b_kmajor, lda, ldb, ldc, batch=1,
          strideA=0, strideB=0, strideC=0, alpha=1.0, beta=0.0, bias=None, act=L.ACT_NONE,
          epi_bwd=False, preact=None, res=None, ldr=None, strideR=0, gate=None, drop_p=0.0, seed=0,
-         splitk=1):
+         splitk=1, ws=None):
     """Raw GEMM launch: C[b,m,n] = epi(alpha * sum_k A(b,m,k) B(b,n,k)). See avsr_hip.h."""
     lib = L.load()
     assert A.is_cuda and B.is_cuda and C.is_cuda
@@ -60,6 +60,9 @@ def gemm(A, B, C, *, M, N, K, a_kmajor, b_kmajor, lda, ldb, ldc, batch=1,
     p.gate = None if gate is None else gate.data_ptr()
     p.drop_p, p.seed = float(drop_p), int(seed) & 0xFFFFFFFFFFFFFFFF
     p.splitk = int(splitk)
+    if ws is not None:
+        assert ws.dtype == torch.float32 and ws.numel() >= batch * splitk * M * N
+        p.ws = ws.data_ptr()
     probe = PROBE.get("gemm")
     if probe is not None and probe["match"](M, N, K, a_kmajor, b_kmajor, dt):
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

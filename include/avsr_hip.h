@@ -68,7 +68,10 @@ typedef struct {
   const void* gate;          /* backward: pre-activation h (dtype, ld = ldc) or NULL */
   float drop_p;              /* dropout probability (0 = off) */
   uint64_t seed;             /* counter-based dropout stream id */
-  int splitk;                /* >1: K split over blocks, C (fp32) += alpha*acc by atomics */
+  int splitk;                /* >1: K split over blocks (C must be fp32) */
+  float* ws;                 /* split-K slab workspace, batch*splitk*M*N fp32: each split stores its
+                                partial tile, a reduce pass writes C = alpha*sum + beta*C (plain
+                                epilogue only). NULL: C += alpha*acc by fp32 atomics */
 } avsr_gemm_params;
 
 int avsr_gemm(const avsr_gemm_params* p, void* stream);

@@ -1,5 +1,6 @@
-"""Micro-benchmark of the HIP GEMM (fwd / dgrad / wgrad shapes of the encoder) vs torch.matmul."""
-import sys, os, time
+"""Micro-benchmark of the HIP GEMM (fwd / dgrad / wgrad shapes of the encoder) vs torch.matmul.
+AVSR_GEMM_NOGLDS=1 selects the register-staged core for A/B comparisons."""
+import sys, os
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
 from avsr_amd import ops
@@ -18,7 +19,9 @@ def t(fn, n=20):
 
 
 dev = torch.device("cuda")
-for (M, N, K) in [(6000, 1024, 1024), (6000, 3072, 1024), (6000, 4096, 1024), (6000, 1024, 4096), (8192, 8192, 8192)]:
+tag = "noglds" if os.environ.get("AVSR_GEMM_NOGLDS") == "1" else "glds"
+for (M, N, K) in [(6000, 1024, 1024), (6000, 3072, 1024), (6000, 4096, 1024), (6000, 1024, 4096), (6000, 5056, 1024),
+                  (8192, 8192, 8192)]:
     x = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
     W = torch.randn(N, K, device=dev, dtype=torch.bfloat16)
     dy = torch.randn(M, N, device=dev, dtype=torch.bfloat16)
@@ -28,4 +31,5 @@ for (M, N, K) in [(6000, 1024, 1024), (6000, 3072, 1024), (6000, 4096, 1024), (6
     b = t(lambda: ops.linear_dgrad(dy, W))
     c = t(lambda: ops.linear_wgrad(dy, x, dW))
     r = t(lambda: x @ W.t())
-    print(f"M{M} N{N} K{K}: fwd {fl/a/1e9:.0f} TF/s  dgrad {fl/b/1e9:.0f}  wgrad {fl/c/1e9:.0f}  torch {fl/r/1e9:.0f}", flush=True)
+    print(f"[{tag}] M{M} N{N} K{K}: fwd {fl/a/1e9:.0f} TF/s  dgrad {fl/b/1e9:.0f}  wgrad {fl/c/1e9:.0f}  "
+          f"torch {fl/r/1e9:.0f}", flush=True)

@@ -12,7 +12,20 @@ from collections import defaultdict
 path = sys.argv[1]
 last = int(sys.argv[2]) if len(sys.argv) > 2 else 3
 top = int(sys.argv[3]) if len(sys.argv) > 3 else 30
-rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
+
+
+def load_rows(path):
+    if path.endswith(".db"):   # rocprofv3 default (rocpd sqlite) output
+        import sqlite3
+        c = sqlite3.connect(path)
+        q = ("select s.kernel_name, d.start, d.end, d.grid_size_x, d.grid_size_y, d.grid_size_z "
+             "from rocpd_kernel_dispatch d join rocpd_info_kernel_symbol s on d.kernel_id = s.id")
+        return [{"Kernel_Name": n, "Start_Timestamp": a, "End_Timestamp": b, "Grid_Size_X": x, "Grid_Size_Y": y,
+                 "Grid_Size_Z": z} for n, a, b, x, y, z in c.execute(q)]
+    return list(csv.DictReader(open(path)))
+
+
+rows = sorted(load_rows(path), key=lambda r: int(r["Start_Timestamp"]))
 ends = [i for i, r in enumerate(rows) if "adamw_kernel" in r["Kernel_Name"]]
 # two adamw launches (decay / no-decay segments) per step
 ends = ends[1::2]
@@ -21,10 +34,14 @@ if len(ends) > last:
     steps = last
 else:
     steps = max(1, len(ends))
+by_grid = "--grid" in sys.argv
 agg = defaultdict(lambda: [0.0, 0])
 for r in rows:
     d = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
-    a = agg[r["Kernel_Name"]]
+    key = r["Kernel_Name"]
+    if by_grid:
+        key = f'{r["Grid_Size_X"]}x{r["Grid_Size_Y"]}x{r["Grid_Size_Z"]} ' + key
+    a = agg[key]
     a[0] += d
     a[1] += 1
 tot = sum(v[0] for v in agg.values())
