@@ -3,6 +3,7 @@
 // see include/avsr_hip.h for the reference call sites.
 #include "gemm_core.h"
 #include "gemm_glds.h"
+#include <cstring>
 
 using namespace gemmcore;
 
@@ -39,50 +40,79 @@ __global__ __launch_bounds__(NT) void dense_kernel(DenseArgs a) {
   epilogue<T, OutT, WM, WN>(e, m0, n0, acc, smem);
 }
 
-// bf16 LDS-DMA path (gemm_glds.h): 128x128x64 tiles, 1-D XCD-remapped grid
-template <typename OutT, bool AK, bool BK>
-__global__ __launch_bounds__(256, 2) void dense_glds_kernel(DenseArgs a, int tiles_m, int tiles_n) {
+// bf16 LDS-DMA path (gemm_glds.h): GCfg tiles, 1-D XCD-remapped grid
+template <typename OutT, bool AK, bool BK, class CF>
+__global__ __launch_bounds__(CF::NTH, CF::MINB) void dense_glds_kernel(DenseArgs a, int tiles_m, int tiles_n) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  using TL = gemmg::GTile<2, 2>;
   const int nwg = gridDim.x;
   const int id = gemmg::xcd_remap(blockIdx.x, nwg);
   const int tn = id % tiles_n, tm = (id / tiles_n) % tiles_m, z = id / (tiles_n * tiles_m);
   const int bz = z / a.splits, sp = z % a.splits;
-  const int m0 = tm * TL::BM, n0 = tn * TL::BN;
+  const int m0 = tm * CF::BM, n0 = tn * CF::BN;
   const int kbeg = sp * a.kchunk, kend = min(a.K, kbeg + a.kchunk);
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  using LA = typename std::conditional<AK, gemmg::GDenseK<TL::BM, 4>, gemmg::GDenseR<TL::BM, 4>>::type;
-  using LB = typename std::conditional<BK, gemmg::GDenseK<TL::BN, 4>, gemmg::GDenseR<TL::BN, 4>>::type;
+  using LA = typename std::conditional<AK, gemmg::GDenseK<CF::BM, CF::NW>, gemmg::GDenseR<CF::BM, CF::NW>>::type;
+  using LB = typename std::conditional<BK, gemmg::GDenseK<CF::BN, CF::NW>, gemmg::GDenseR<CF::BN, CF::NW>>::type;
   LA la; la.init((const bf16*)a.A + (int64_t)bz * a.sA, a.lda, m0, a.M, kend, wave, lane);
   LB lb; lb.init((const bf16*)a.B + (int64_t)bz * a.sB, a.ldb, n0, a.N, kend, wave, lane);
-  f32x16 acc[2][2];
-  gemmg::mainloop_glds<2, 2>(la, lb, kbeg, (kend - kbeg + gemmg::GBK - 1) / gemmg::GBK, acc, smem);
+  f32x16 acc[CF::FM][CF::FN];
+  gemmg::mainloop_glds<CF>(la, lb, kbeg, (kend - kbeg + gemmg::GBK - 1) / gemmg::GBK, acc, smem);
   Epi e = a.e;
   e.C = (OutT*)e.C + (int64_t)bz * a.sC + sp * a.sSplit;
   if (e.res) e.res = (const bf16*)e.res + (int64_t)bz * a.sR;
   if (e.preact) e.preact = (bf16*)e.preact + (int64_t)bz * a.sC;
   if (e.gate) e.gate = (const bf16*)e.gate + (int64_t)bz * a.sC;
   e.drop_base = (uint64_t)bz * (uint64_t)a.M * (uint64_t)a.N;
-  epilogue<bf16, OutT, 2, 2>(e, m0, n0, acc, smem);
+  gemmg::epilogue_g<bf16, OutT, CF>(e, m0, n0, acc, smem);
 }
 
-template <typename OutT, bool AK, bool BK>
+template <typename OutT, bool AK, bool BK, class CF>
 int launch_glds(const DenseArgs& a, int batch, hipStream_t st) {
-  using TL = gemmg::GTile<2, 2>;
-  const int tm = (a.M + TL::BM - 1) / TL::BM, tn = (a.N + TL::BN - 1) / TL::BN;
+  const int tm = (a.M + CF::BM - 1) / CF::BM, tn = (a.N + CF::BN - 1) / CF::BN;
   const long nwg = (long)tm * tn * batch * a.splits;
   if (nwg > 0x7fffffffL) return AVSR_E_SHAPE;
-  hipLaunchKernelGGL((dense_glds_kernel<OutT, AK, BK>), dim3((unsigned)nwg), dim3(256), TL::LDS_BYTES, st, a, tm, tn);
+  hipLaunchKernelGGL((dense_glds_kernel<OutT, AK, BK, CF>), dim3((unsigned)nwg), dim3(CF::NTH), CF::LDS_BYTES, st, a,
+                     tm, tn);
   AVSR_CHECK_LAUNCH();
   return 0;
 }
 
+using Cfg128 = gemmg::GCfg<2, 2, 2, 2, 2>;       // 128x128, 4 waves, 2 stages, 2 blocks/CU
+using Cfg256 = gemmg::GCfg<2, 4, 4, 2, 2>;       // 256x256, 8 waves, 2 stages (128 KiB)
+using Cfg256x128 = gemmg::GCfg<4, 2, 2, 2, 3>;   // 256x128, 8 waves, 3 stages (144 KiB)
+using Cfg128x256 = gemmg::GCfg<2, 4, 2, 2, 3>;   // 128x256, 8 waves, 3 stages
+using Cfg128s3 = gemmg::GCfg<2, 2, 2, 2, 3>;     // 128x128, 4 waves, 3 stages (96 KiB)
+using Cfg128s4 = gemmg::GCfg<2, 2, 2, 2, 4>;     // 128x128, 4 waves, 4 stages (128 KiB)
+
+// tile choice: AVSR_GEMM_TILE=128|256|256x128|128x256 forces one (benchmarks); otherwise the
+// configuration with the fewest block rounds x per-tile work (wave quantisation over 256 CUs)
+int tile_cfg(const avsr_gemm_params* p, int splits) {
+  const char* e = getenv("AVSR_GEMM_TILE");
+  const int forced = !e ? -1 : !strcmp(e, "128") ? 0 : !strcmp(e, "256") ? 1 : !strcmp(e, "256x128") ? 2
+                   : !strcmp(e, "128x256") ? 3 : !strcmp(e, "128s3") ? 4 : !strcmp(e, "128s4") ? 5 : -1;
+  if (forced >= 0) return forced;
+  return 0;
+}
+
+template <typename OutT, bool AK, bool BK>
+int launch_cfg(int cfg, const DenseArgs& a, int batch, hipStream_t st) {
+  switch (cfg) {
+    case 1: return launch_glds<OutT, AK, BK, Cfg256>(a, batch, st);
+    case 2: return launch_glds<OutT, AK, BK, Cfg256x128>(a, batch, st);
+    case 3: return launch_glds<OutT, AK, BK, Cfg128x256>(a, batch, st);
+    case 4: return launch_glds<OutT, AK, BK, Cfg128s3>(a, batch, st);
+    case 5: return launch_glds<OutT, AK, BK, Cfg128s4>(a, batch, st);
+    default: return launch_glds<OutT, AK, BK, Cfg128>(a, batch, st);
+  }
+}
+
 template <typename OutT>
 int glds_by_layout(const avsr_gemm_params* p, const DenseArgs& a, hipStream_t st) {
-  if (p->a_kmajor && p->b_kmajor) return launch_glds<OutT, true, true>(a, p->batch, st);
-  if (p->a_kmajor) return launch_glds<OutT, true, false>(a, p->batch, st);
-  if (p->b_kmajor) return launch_glds<OutT, false, true>(a, p->batch, st);
-  return launch_glds<OutT, false, false>(a, p->batch, st);
+  const int cfg = tile_cfg(p, a.splits);
+  if (p->a_kmajor && p->b_kmajor) return launch_cfg<OutT, true, true>(cfg, a, p->batch, st);
+  if (p->a_kmajor) return launch_cfg<OutT, true, false>(cfg, a, p->batch, st);
+  if (p->b_kmajor) return launch_cfg<OutT, false, true>(cfg, a, p->batch, st);
+  return launch_cfg<OutT, false, false>(cfg, a, p->batch, st);
 }
 
 // the LDS-DMA path needs whole 16-byte vectors along every operand's contiguous dimension

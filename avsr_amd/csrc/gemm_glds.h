@@ -106,53 +106,187 @@ AVSR_DEV bf16x8 gfrag(const char* img, int rb, int s, int lane) {
   }
 }
 
-template <int WM, int WN> struct GTile {
-  static constexpr int BM = 64 * WM, BN = 64 * WN, NW = WM * WN, NTH = 64 * NW;
+// Block tile BM x BN = (WM*32*FM) x (WN*32*FN): WM x WN waves, each owning FM x FN
+// accumulators of 32x32 (fp32, 16 registers each).
+// S LDS stages: S-1 K-tiles in flight (the DMA of tile t+S-1 is issued at the top of t).
+template <int WM_, int WN_, int FM_, int FN_, int S_ = 2> struct GCfg {
+  static constexpr int WM = WM_, WN = WN_, FM = FM_, FN = FN_, S = S_;
+  static constexpr int BM = WM * 32 * FM, BN = WN * 32 * FN, NW = WM * WN, NTH = 64 * NW;
   static constexpr int SA = BM * GBK * 2, SB = BN * GBK * 2, STAGE = SA + SB;
-  static constexpr int EP_BYTES = (BM / 2) * (BN + 4) * 4;
-  static constexpr int LDS_BYTES = 2 * STAGE > EP_BYTES ? 2 * STAGE : EP_BYTES;
+  static constexpr int GL = (BM + BN) * GBK * 2 / 1024 / NW;    // DMA instructions per wave per K-tile
+  static constexpr int EP_BYTES = WM * 32 * (BN + 4) * 4;       // one 32-row strip per wave row
+  static constexpr int LDS_BYTES = S * STAGE > EP_BYTES ? S * STAGE : EP_BYTES;
+  static constexpr int MINB = LDS_BYTES <= 80 * 1024 ? 2 : 1;    // blocks per CU the LDS allows
 };
 
-// K-tiles [0, nk) with k0 = kbeg + t*64; acc = the wave's 2x2 block of 32x32 tiles
-template <int WM, int WN, class LA, class LB>
-AVSR_DEV void mainloop_glds(const LA& la, const LB& lb, int kbeg, int nk, f32x16 (&acc)[2][2], char* smem) {
-  using TL = GTile<WM, WN>;
+template <int N> AVSR_DEV void wait_vmcnt() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+
+// K-tiles [0, nk) with k0 = kbeg + t*64; acc = the wave's FM x FN block of 32x32 tiles.
+// Ring of S stages. Fragments are double-buffered in registers: the reads for k-step s+1
+// are issued before the MFMAs of step s, and at the last k-step of tile t the ring
+// advances first (counted vmcnt for tile t+1's DMAs, raw s_barrier that also retires every
+// wave's reads of tile t, DMA of tile t+S into tile t's stage) so that tile t+1's first
+// fragments are in flight behind tile t's last MFMAs.
+template <class CF, bool AK, bool BK>
+struct Frags {
+  bf16x8 a[CF::FM], b[CF::FN];
+  AVSR_DEV void load(const char* stage, int s, int wm, int wn, int lane) {
+#pragma unroll
+    for (int i = 0; i < CF::FM; ++i) a[i] = gfrag<CF::BM, AK>(stage, (wm * CF::FM + i) * 32, s, lane);
+#pragma unroll
+    for (int j = 0; j < CF::FN; ++j) b[j] = gfrag<CF::BN, BK>(stage + CF::SA, (wn * CF::FN + j) * 32, s, lane);
+  }
+  AVSR_DEV void mma(f32x16 (&acc)[CF::FM][CF::FN]) const {
+#pragma unroll
+    for (int i = 0; i < CF::FM; ++i)
+#pragma unroll
+      for (int j = 0; j < CF::FN; ++j) acc[i][j] = mfma32(a[i], b[j], acc[i][j]);
+  }
+};
+
+template <class CF>
+AVSR_DEV void wait_tiles_ahead(bool full) {   // all but the newest S-2 tiles' DMAs retired
+  if (full) wait_vmcnt<CF::GL * (CF::S - 2)>();
+  else wait_vmcnt<0>();
+}
+
+template <class CF, class LA, class LB>
+AVSR_DEV void mainloop_glds(const LA& la, const LB& lb, int kbeg, int nk, f32x16 (&acc)[CF::FM][CF::FN], char* smem) {
+  constexpr int S = CF::S, KS = GBK / 16;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wm = wave / WN, wn = wave % WN;
+  const int wm = wave / CF::WN, wn = wave % CF::WN;
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < CF::FM; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < CF::FN; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
   if (nk <= 0) return;
-  la.issue(smem, kbeg, wave);
-  lb.issue(smem + TL::SA, kbeg, wave);
+#pragma unroll
+  for (int p = 0; p < S - 1; ++p)
+    if (p < nk) {
+      la.issue(smem + p * CF::STAGE, kbeg + p * GBK, wave);
+      lb.issue(smem + p * CF::STAGE + CF::SA, kbeg + p * GBK, wave);
+    }
+  wait_tiles_ahead<CF>(S - 2 <= nk - 1);
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  Frags<CF, LA::KMAJ, LB::KMAJ> cur, nxt;
+  cur.load(smem, 0, wm, wn, lane);
+  int cs = 0;                       // stage of tile kt
   for (int kt = 0; kt < nk; ++kt) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (kt + 1 < nk) {
-      char* nx = smem + ((kt + 1) & 1) * TL::STAGE;
-      la.issue(nx, kbeg + (kt + 1) * GBK, wave);
-      lb.issue(nx + TL::SA, kbeg + (kt + 1) * GBK, wave);
+    const char* stage = smem + cs * CF::STAGE;
+    const int ns = cs + 1 == S ? 0 : cs + 1;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      if (s + 1 < KS) {
+        nxt.load(stage, s + 1, wm, wn, lane);
+      } else if (kt + 1 < nk) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        wait_tiles_ahead<CF>(kt + S - 1 < nk);
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (kt + S < nk) {
+          char* st = smem + cs * CF::STAGE;
+          la.issue(st, kbeg + (kt + S) * GBK, wave);
+          lb.issue(st + CF::SA, kbeg + (kt + S) * GBK, wave);
+        }
+        nxt.load(smem + ns * CF::STAGE, 0, wm, wn, lane);
+      }
+      cur.mma(acc);
+      cur = nxt;
     }
-    const char* cA = smem + (kt & 1) * TL::STAGE;
-    const char* cB = cA + TL::SA;
-#pragma unroll
-    for (int s = 0; s < GBK / 16; ++s) {
-      bf16x8 a[2], b[2];
-#pragma unroll
-      for (int i = 0; i < 2; ++i) a[i] = gfrag<TL::BM, LA::KMAJ>(cA, wm * 64 + i * 32, s, lane);
-#pragma unroll
-      for (int j = 0; j < 2; ++j) b[j] = gfrag<TL::BN, LB::KMAJ>(cB, wn * 64 + j * 32, s, lane);
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = mfma32(a[i], b[j], acc[i][j]);
-    }
+    cs = ns;
   }
   __syncthreads();
+}
+
+// Epilogue for a GCfg tile: (1) optional BN column statistics from the accumulators;
+// (2) FM passes, each staging one 32-row strip per wave row through LDS and writing it
+// row-major, 4 consecutive columns per thread (coalesced stores, vector residual reads).
+template <typename T, typename OutT, class CF>
+AVSR_DEV void epilogue_g(const Epi& e, int m0, int n0, f32x16 (&acc)[CF::FM][CF::FN], char* smem) {
+  constexpr int BN = CF::BN, LDR = BN + 4, SR = CF::WM * 32;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / CF::WN, wn = wave % CF::WN;
+  float* st = (float*)smem;
+  if (e.stats) {
+    __syncthreads();
+    float* red = st;  // [WM][BN][3]
+#pragma unroll
+    for (int j = 0; j < CF::FN; ++j) {
+      float s = 0.f, c = 0.f;
+#pragma unroll
+      for (int i = 0; i < CF::FM; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = (wm * CF::FM + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+          const bool ok = m0 + row < e.M;
+          s += ok ? e.alpha * acc[i][j][r] : 0.f;
+          c += ok ? 1.f : 0.f;
+        }
+      s += __shfl_xor(s, 32, 64);
+      c += __shfl_xor(c, 32, 64);
+      const float mean = c > 0.f ? s / c : 0.f;
+      float m2 = 0.f;
+#pragma unroll
+      for (int i = 0; i < CF::FM; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = (wm * CF::FM + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+          const float d = e.alpha * acc[i][j][r] - mean;
+          m2 += m0 + row < e.M ? d * d : 0.f;
+        }
+      m2 += __shfl_xor(m2, 32, 64);
+      if (lane < 32) {
+        const int lc = (wn * CF::FN + j) * 32 + lane;
+        red[(wm * BN + lc) * 3 + 0] = c;
+        red[(wm * BN + lc) * 3 + 1] = mean;
+        red[(wm * BN + lc) * 3 + 2] = m2;
+      }
+    }
+    __syncthreads();
+    for (int lc = tid; lc < BN; lc += CF::NTH) {
+      const int col = n0 + lc;
+      if (col < e.N) {
+        float n = 0.f, mean = 0.f, m2 = 0.f;
+        for (int w = 0; w < CF::WM; ++w) {
+          const float nb = red[(w * BN + lc) * 3 + 0], mb = red[(w * BN + lc) * 3 + 1], qb = red[(w * BN + lc) * 3 + 2];
+          if (nb > 0.f) {
+            const float nn = n + nb, d = mb - mean;
+            mean += d * nb / nn;
+            m2 += qb + d * d * n * nb / nn;
+            n = nn;
+          }
+        }
+        float* o = e.stats + ((int64_t)col * e.stats_tiles + m0 / CF::BM) * 3;
+        o[0] = n; o[1] = mean; o[2] = m2;
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < CF::FM; ++i) {
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < CF::FN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int lr = wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        st[lr * LDR + (wn * CF::FN + j) * 32 + (lane & 31)] = acc[i][j][r];
+      }
+    __syncthreads();
+    for (int c = tid; c < SR * BN / 4; c += CF::NTH) {
+      const int lr = c / (BN / 4), lc = (c % (BN / 4)) * 4;
+      const int row = m0 + ((lr >> 5) * CF::FM + i) * 32 + (lr & 31);
+      const int col = n0 + lc;
+      if (row < e.M && col < e.N) {
+        const f32x4 v4 = *(const f32x4*)(st + lr * LDR + lc);
+        const float v[4] = {v4[0], v4[1], v4[2], v4[3]};
+        epi_elems<T, OutT, 4>(e, row, col, v);
+      }
+    }
+  }
 }
 
 // XCD-aware block order: consecutive remapped ids run on one XCD (shared L2), bijective for

@@ -93,10 +93,18 @@ def _ref_gemm(A, B, a_kmajor, b_kmajor):
     return Af @ Bf.t()
 
 
+@pytest.fixture(params=["auto", "128", "256", "256x128", "128x256", "128s3", "128s4"])
+def gemm_tile(request, monkeypatch):
+    """forces each LDS-DMA tile configuration (AVSR_GEMM_TILE, read per launch by avsr_gemm)"""
+    if request.param != "auto":
+        monkeypatch.setenv("AVSR_GEMM_TILE", request.param)
+    return request.param
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("a_kmajor,b_kmajor", [(True, True), (True, False), (False, True), (False, False)])
 @pytest.mark.parametrize("M,N,K,splitk", [(296, 200, 200, 1), (128, 136, 64, 1), (1000, 384, 1000, 3), (6000, 1024, 512, 2)])
-def test_gemm_layouts_bf16(dev, a_kmajor, b_kmajor, M, N, K, splitk):
+def test_gemm_layouts_bf16(dev, gemm_tile, a_kmajor, b_kmajor, M, N, K, splitk):
     """Every operand layout through the bf16 LDS-DMA path (M, N >= 128) and the register-staged
     path, ragged M/N/K edges, split-K into an fp32 C; tolerance: fp32 accumulation of bf16
     products vs torch fp32 on the same bf16 inputs (2e-3 relative to the output scale)."""
@@ -126,7 +134,7 @@ def test_gemm_layouts_bf16(dev, a_kmajor, b_kmajor, M, N, K, splitk):
 
 
 @pytest.mark.gpu
-def test_gemm_batched_strided_bf16(dev):
+def test_gemm_batched_strided_bf16(dev, gemm_tile):
     """batch > 1 with operand / output strides (attention-style batched products)."""
     g = torch.Generator().manual_seed(5)
     Bt, M, N, K = 3, 256, 192, 96

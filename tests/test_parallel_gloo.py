@@ -1,0 +1,59 @@
+"""Data-parallel plumbing on CPU with the gloo backend, world_size 2:
+the bucketed gradient all-reduce of the flat arena buffer (sum and average, buckets that
+split the buffer unevenly) and the rank-0 parameter / buffer broadcast."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from avsr_amd import parallel
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    try:
+        r, w, _ = parallel.init_from_env(backend="gloo")
+        assert (r, w) == (rank, world)
+        n = 1000003                                   # odd size: last bucket is short
+        g = torch.arange(n, dtype=torch.float32) * (rank + 1)
+        red = parallel.GradReducer(g, bucket_bytes=4 * 65536)
+        assert len(red.buckets) == (n + 65535) // 65536
+        red.allreduce(average=False)
+        want = torch.arange(n, dtype=torch.float32) * sum(range(1, world + 1))
+        ok_sum = torch.equal(g, want)
+        red.allreduce(average=True)                   # sum over ranks of identical buffers / world
+        ok_avg = torch.allclose(g, want, rtol=1e-6)
+        params = torch.full((17,), float(rank))
+        bufs = [torch.full((3,), 10.0 + rank), torch.tensor([rank], dtype=torch.int64)]
+        parallel.broadcast_state(params, bufs)
+        ok_bc = bool((params == 0).all()) and bool((bufs[0] == 10).all()) and int(bufs[1]) == 0
+        q.put((rank, ok_sum, ok_avg, ok_bc))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def test_grad_reducer_and_broadcast_world2():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, ok_sum, ok_avg, ok_bc in res:
+        assert ok_sum and ok_avg and ok_bc, (rank, ok_sum, ok_avg, ok_bc)
