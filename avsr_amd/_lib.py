@@ -164,6 +164,34 @@ def fill(struct_cls, **kw):
 
 
 # (symbol name, params struct or None for custom signature)
+class DecAttnParams(ctypes.Structure):
+    _fields_ = [
+        ("dtype", _i), ("n", _i), ("H", _i), ("klen_max", _i), ("scale", _f),
+        ("q", _c_p), ("ldq", _i64), ("k", _c_p), ("ldk", _i64), ("k_bstride", _i64),
+        ("v", _c_p), ("ldv", _i64), ("v_bstride", _i64), ("klen", _c_p), ("o", _c_p), ("ldo", _i64),
+    ]
+
+
+class TopkParams(ctypes.Structure):
+    _fields_ = [("rows", _i), ("V", _i), ("K", _i), ("x", _c_p), ("ldx", _i64), ("ids", _c_p)]
+
+
+class CtcPrefixParams(ctypes.Structure):
+    _fields_ = [
+        ("n", _i), ("T", _i), ("V", _i), ("P", _i), ("blank", _i), ("eos", _i), ("out_len", _i),
+        ("logp", _c_p), ("r_prev", _c_p), ("last", _c_p), ("ids", _c_p), ("r_new", _c_p), ("psi", _c_p),
+    ]
+
+
+class BeamSelectParams(ctypes.Structure):
+    _fields_ = [
+        ("n", _i), ("V", _i), ("P", _i), ("beam", _i), ("blank", _i), ("eos", _i), ("w_dec", _f), ("w_ctc", _f),
+        ("dec", _c_p), ("ld", _i64), ("ids", _c_p), ("psi", _c_p), ("s_prev", _c_p), ("score", _c_p),
+        ("out_prev", _c_p), ("out_tok", _c_p), ("out_col", _c_p), ("out_score", _c_p), ("out_dec", _c_p),
+        ("out_ctc", _c_p), ("out_s", _c_p),
+    ]
+
+
 SYMBOLS = {
     "avsr_version": ([], ctypes.c_char_p),
     "avsr_gemm": ([ctypes.POINTER(GemmParams), _c_p], _i),
@@ -204,6 +232,12 @@ SYMBOLS = {
     "avsr_weightnorm_bwd": ([_i, _i, _i, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p], _i),
     "avsr_sumsq": ([_c_p, _i64, _c_p, _c_p], _i),
     "avsr_adamw": ([ctypes.POINTER(AdamWParams), _c_p], _i),
+    "avsr_log_softmax_rows": ([_i, _i, _i, _c_p, _i64, _c_p, _i64, _c_p], _i),
+    "avsr_dec_attn": ([ctypes.POINTER(DecAttnParams), _c_p], _i),
+    "avsr_row_topk": ([ctypes.POINTER(TopkParams), _c_p], _i),
+    "avsr_ctc_prefix": ([ctypes.POINTER(CtcPrefixParams), _c_p], _i),
+    "avsr_beam_select": ([ctypes.POINTER(BeamSelectParams), _c_p], _i),
+    "avsr_gather_rows": ([_i, _i, _i64, _c_p, _i64, _i64, _c_p, _i64, _i64, _c_p, _c_p], _i),
 }
 
 _lib = None

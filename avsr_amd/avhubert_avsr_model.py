@@ -15,6 +15,7 @@ from transformers.modeling_outputs import BaseModelOutput
 from transformers.utils import ModelOutput
 
 from .configuration_avhubert_avsr import AVHubertAVSRConfig
+from .decode import BatchBeamSearch, Hypothesis, get_beam_search_decoder  # noqa: F401  (reference surface)
 from .nets.modules import E2EShell
 
 

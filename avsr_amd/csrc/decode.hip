@@ -1,0 +1,360 @@
+// Joint CTC / attention beam-search kernels (declarations and the
+// reference call sites in include/avsr_hip.h):
+//   avsr_log_softmax_rows  log_softmax over V (decoder output layer, CTC log-probs)
+//   avsr_dec_attn          one-query multi-head attention per hypothesis over a K/V cache
+//   avsr_row_topk          pre-beam: top-P decoder tokens per hypothesis
+//   avsr_ctc_prefix        CTC prefix scores of the pre-beam tokens (T recursion)
+//   avsr_beam_select       weighted scores + flat top-beam over (hyps x V)
+//   avsr_gather_rows       reorder per-hypothesis state (K/V caches, CTC variables)
+// All fp32 math; decode runs at batch 1 utterance x beam hypotheses, so these kernels are
+// latency-bound: one block per row / hypothesis, no host round trip inside a step.
+#include "common.h"
+
+namespace {
+
+constexpr float LOGZERO = -10000000000.0f;   // CTCPrefixScoreTH.logzero (ctc_prefix_score.py:29)
+
+// torch.logsumexp of two finite values: m + log(exp(a-m) + exp(b-m))
+AVSR_DEV float lse2(float a, float b) {
+  const float m = fmaxf(a, b);
+  return m + logf(expf(a - m) + expf(b - m));
+}
+
+AVSR_DEV float block_max256(float v, float* sh) {
+  v = wave_max(v);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
+  __syncthreads();
+  v = fmaxf(fmaxf(sh[0], sh[1]), fmaxf(sh[2], sh[3]));
+  __syncthreads();
+  return v;
+}
+AVSR_DEV float block_sum256(float v, float* sh) {
+  v = wave_sum(v);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
+  __syncthreads();
+  v = sh[0] + sh[1] + sh[2] + sh[3];
+  __syncthreads();
+  return v;
+}
+
+// (value, index) arg-max across the 256-thread block; ties -> smaller index
+AVSR_DEV void block_argmax256(float& v, int& i, float* shv, int* shi) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ov = __shfl_xor(v, o, 64);
+    const int oi = __shfl_xor(i, o, 64);
+    if (ov > v || (ov == v && oi < i)) { v = ov; i = oi; }
+  }
+  if ((threadIdx.x & 63) == 0) { shv[threadIdx.x >> 6] = v; shi[threadIdx.x >> 6] = i; }
+  __syncthreads();
+  v = shv[0]; i = shi[0];
+#pragma unroll
+  for (int w = 1; w < 4; ++w)
+    if (shv[w] > v || (shv[w] == v && shi[w] < i)) { v = shv[w]; i = shi[w]; }
+  __syncthreads();
+}
+
+// ---------------------------------------------------------------- log_softmax rows
+template <typename T>
+__global__ __launch_bounds__(256) void log_softmax_kernel(int V, const T* x, int64_t ldx, float* out, int64_t ldo) {
+  __shared__ float sh[4];
+  const T* r = x + (int64_t)blockIdx.x * ldx;
+  float m = -INFINITY;
+  for (int c = threadIdx.x; c < V; c += 256) m = fmaxf(m, to_f(r[c]));
+  m = block_max256(m, sh);
+  float s = 0.f;
+  for (int c = threadIdx.x; c < V; c += 256) s += expf(to_f(r[c]) - m);
+  s = block_sum256(s, sh);
+  const float ls = logf(s);
+  float* o = out + (int64_t)blockIdx.x * ldo;
+  for (int c = threadIdx.x; c < V; c += 256) o[c] = to_f(r[c]) - m - ls;
+}
+
+// ---------------------------------------------------------------- one-query attention
+// block (hyp i, head h): scores of all valid keys in LDS, softmax, then o = sum_j p_j v_j
+// with 64 dims x 4 key groups per block and an LDS reduce of the groups.
+template <typename T>
+__global__ __launch_bounds__(256) void dec_attn_kernel(avsr_dec_attn_params p) {
+  extern __shared__ float sc[];           // [klen_max] scores, then [4][64] partials
+  __shared__ float sh[4];
+  const int h = blockIdx.x, i = blockIdx.y;
+  const int klen = p.klen ? min(p.klen[i], p.klen_max) : p.klen_max;
+  const T* q = (const T*)p.q + (int64_t)i * p.ldq + h * 64;
+  const T* K = (const T*)p.k + (int64_t)i * p.k_bstride + h * 64;
+  const T* Vv = (const T*)p.v + (int64_t)i * p.v_bstride + h * 64;
+  float qr[64];
+#pragma unroll
+  for (int d = 0; d < 64; ++d) qr[d] = to_f(q[d]);
+  float m = -INFINITY;
+  for (int j = threadIdx.x; j < klen; j += 256) {
+    const T* kr = K + (int64_t)j * p.ldk;
+    float s = 0.f;
+#pragma unroll
+    for (int d = 0; d < 64; ++d) s += qr[d] * to_f(kr[d]);
+    s *= p.scale;
+    sc[j] = s;
+    m = fmaxf(m, s);
+  }
+  m = block_max256(m, sh);
+  float l = 0.f;
+  for (int j = threadIdx.x; j < klen; j += 256) {
+    const float e = expf(sc[j] - m);
+    sc[j] = e;
+    l += e;
+  }
+  l = block_sum256(l, sh);     // includes a barrier: every sc[j] is final
+  const int d = threadIdx.x & 63, g = threadIdx.x >> 6;
+  float acc = 0.f;
+  for (int j = g; j < klen; j += 4) acc += sc[j] * to_f(Vv[(int64_t)j * p.ldv + d]);
+  float* part = sc + p.klen_max;
+  part[g * 64 + d] = acc;
+  __syncthreads();
+  if (g == 0) {
+    const float o = (part[d] + part[64 + d] + part[128 + d] + part[192 + d]) / l;
+    ((T*)p.o)[(int64_t)i * p.ldo + h * 64 + d] = from_f<T>(o);
+  }
+}
+
+// ---------------------------------------------------------------- pre-beam top-P
+// one block per hypothesis row; P rounds of block arg-max over per-thread sorted candidate
+// lists (each thread keeps its own top-P of a strided slice)
+constexpr int KMAX = 16;
+
+__global__ __launch_bounds__(256) void row_topk_kernel(avsr_topk_params p) {
+  __shared__ float shv[4];
+  __shared__ int shi[4];
+  const float* x = p.x + (int64_t)blockIdx.x * p.ldx;   // one row per block
+  float tv[KMAX];
+  int ti[KMAX];
+#pragma unroll
+  for (int k = 0; k < KMAX; ++k) { tv[k] = -INFINITY; ti[k] = 0x7fffffff; }
+  for (int c = threadIdx.x; c < p.V; c += 256) {
+    float v = x[c];
+    int id = c;
+    // insertion into the descending list (ties keep the smaller index first)
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) {
+      if (k < p.K && (v > tv[k] || (v == tv[k] && id < ti[k]))) {
+        const float t = tv[k]; const int u = ti[k];
+        tv[k] = v; ti[k] = id; v = t; id = u;
+      }
+    }
+  }
+  int head = 0;
+  for (int r = 0; r < p.K; ++r) {
+    float v = -INFINITY; int id = 0x7fffffff;
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) if (k == head) { v = tv[k]; id = ti[k]; }
+    const int mine = id;
+    block_argmax256(v, id, shv, shi);
+    if (threadIdx.x == 0) p.ids[(int64_t)blockIdx.x * p.K + r] = id;
+    if (mine == id && id != 0x7fffffff) ++head;
+  }
+}
+
+// ---------------------------------------------------------------- CTC prefix scores
+// CTCPrefixScoreTH.__call__ (ctc_prefix_score.py:65-187) for one utterance: block = one
+// hypothesis, lane j = its j-th scored token; the T recursion is sequential per lane.
+__global__ __launch_bounds__(64) void ctc_prefix_kernel(avsr_ctc_prefix_params p) {
+  const int h = blockIdx.x, j = threadIdx.x;
+  const int T = p.T, V = p.V;
+  const bool act = j < p.P;
+  const int id = act ? p.ids[h * p.P + j] : 0;
+  const bool same = act && id == p.last[h];
+  const float* rp = p.r_prev ? p.r_prev + (int64_t)h * T * 2 : nullptr;
+  float* rn = act ? p.r_new + ((int64_t)h * p.P + j) * T * 2 : nullptr;
+  // r_prev at the first step: (logzero, cumsum of blank log-probs)
+  auto rprev = [&](int t, int q, float cum) -> float { return rp ? rp[t * 2 + q] : (q == 0 ? LOGZERO : cum); };
+  const int start = max(p.out_len, 1);
+  // values of r for t < start
+  float r0 = LOGZERO, r1 = LOGZERO;
+  float cum = 0.f;          // running cumsum of logp[t][blank] (first step only)
+  for (int t = 0; t < start; ++t) {
+    const float xb = p.logp[(int64_t)t * V + p.blank];
+    cum += xb;
+    float a0 = LOGZERO;
+    if (t == 0 && p.out_len == 0) a0 = act ? p.logp[id] : LOGZERO;
+    if (act) { rn[t * 2 + 0] = a0; rn[t * 2 + 1] = LOGZERO; }
+    if (t == start - 1) { r0 = a0; r1 = LOGZERO; }
+  }
+  // psi accumulates logsumexp over { phi(t-1) + x0(t) : t in [start, T) } U { r0(start-1) }
+  float pm = r0;            // running max
+  float ps = 1.f;           // sum of exp(. - pm)
+  // phi(t-1) needs r_prev at t-1: carry the previous frame's values
+  float prev_r0 = rprev(start - 1, 0, 0.f);
+  float prev_r1 = rprev(start - 1, 1, cum);   // cum = cumsum of blank log-probs through start-1
+  float cur_cum = cum;
+  for (int t = start; t < T; ++t) {
+    const float rsum_prev = lse2(prev_r0, prev_r1);
+    const float phi = same ? prev_r1 : rsum_prev;
+    const float x0 = act ? p.logp[(int64_t)t * V + id] : LOGZERO;
+    const float xb = p.logp[(int64_t)t * V + p.blank];
+    const float n0 = lse2(r0, phi) + x0;
+    const float n1 = lse2(r0, r1) + xb;
+    r0 = n0; r1 = n1;
+    if (act) { rn[t * 2 + 0] = r0; rn[t * 2 + 1] = r1; }
+    const float term = phi + x0;
+    if (term > pm) { ps = ps * expf(pm - term) + 1.f; pm = term; }
+    else ps += expf(term - pm);
+    cur_cum += xb;
+    prev_r0 = rprev(t, 0, 0.f);
+    prev_r1 = rprev(t, 1, cur_cum);
+  }
+  // r_sum at the last frame (for eos): logsumexp of r_prev[T-1]
+  const float rsum_last = lse2(prev_r0, prev_r1);
+  float psi = pm + logf(ps);
+  if (act) {
+    if (id == p.blank) psi = LOGZERO;
+    if (id == p.eos) psi = rsum_last;
+    p.psi[h * (p.P + 1) + j] = psi;
+  }
+  if (j == 0) p.psi[h * (p.P + 1) + p.P] = rsum_last;
+}
+
+// ---------------------------------------------------------------- beam selection
+// weighted[h][v] = w_dec * dec[h][v] + w_ctc * (psi[h][v] - s_prev[h]) + score[h]
+// (psi = LOGZERO for tokens outside the pre-beam, r_sum[T-1] for eos; batch_beam_search.py
+// :228-260), flat top-`beam` over h*V + v; ties -> smaller flat index.
+__global__ __launch_bounds__(256) void beam_select_kernel(avsr_beam_select_params p) {
+  __shared__ float shv[4];
+  __shared__ int shi[4];
+  float tv[KMAX];
+  int ti[KMAX];
+#pragma unroll
+  for (int k = 0; k < KMAX; ++k) { tv[k] = -INFINITY; ti[k] = 0x7fffffff; }
+  const int total = p.n * p.V;
+  for (int f = threadIdx.x; f < total; f += 256) {
+    const int h = f / p.V, v = f - h * p.V;
+    float psi = LOGZERO;
+    if (v == p.eos) psi = p.psi[h * (p.P + 1) + p.P];
+    else if (v != p.blank)
+      for (int c = 0; c < p.P; ++c)
+        if (p.ids[h * p.P + c] == v) { psi = p.psi[h * (p.P + 1) + c]; break; }
+    float w = 0.f;
+    w += p.w_dec * (p.dec[(int64_t)h * p.ld + v]);
+    w += p.w_ctc * (psi - p.s_prev[h]);
+    w += p.score[h];
+    float val = w;
+    int id = f;
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) {
+      if (k < p.beam && (val > tv[k] || (val == tv[k] && id < ti[k]))) {
+        const float t = tv[k]; const int u = ti[k];
+        tv[k] = val; ti[k] = id; val = t; id = u;
+      }
+    }
+  }
+  int head = 0;
+  for (int r = 0; r < p.beam; ++r) {
+    float v = -INFINITY; int id = 0x7fffffff;
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) if (k == head) { v = tv[k]; id = ti[k]; }
+    const int mine = id;
+    block_argmax256(v, id, shv, shi);
+    if (mine == id && id != 0x7fffffff) ++head;
+    if (threadIdx.x == 0) {
+      const int h = id / p.V, tok = id - h * p.V;
+      int col = p.P - 1;                       // scoring_idmap == -1 -> python index -1
+      for (int c = 0; c < p.P; ++c)
+        if (p.ids[h * p.P + c] == tok) { col = c; break; }
+      float psi = LOGZERO;
+      if (tok == p.eos) psi = p.psi[h * (p.P + 1) + p.P];
+      else if (tok != p.blank && p.ids[h * p.P + col] == tok) psi = p.psi[h * (p.P + 1) + col];
+      p.out_prev[r] = h;
+      p.out_tok[r] = tok;
+      p.out_col[r] = col;
+      p.out_score[r] = v;
+      p.out_dec[r] = p.dec[(int64_t)h * p.ld + tok];
+      p.out_ctc[r] = psi - p.s_prev[h];
+      p.out_s[r] = psi;
+    }
+  }
+}
+
+// ---------------------------------------------------------------- state gather
+template <typename W>
+__global__ __launch_bounds__(256) void gather_rows_kernel(int groups, int n, int64_t vecs, const W* src,
+                                                          int64_t sg, int64_t sr, W* dst, int64_t dg, int64_t dr,
+                                                          const int* idx) {
+  const int64_t total = (int64_t)groups * n * vecs;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+    const int64_t v = e % vecs, gi = e / vecs;
+    const int i = (int)(gi % n), g = (int)(gi / n);
+    dst[g * dg + i * dr + v] = src[g * sg + (int64_t)idx[i] * sr + v];
+  }
+}
+
+}  // namespace
+
+extern "C" int avsr_log_softmax_rows(int dtype, int rows, int V, const void* x, int64_t ldx, float* out, int64_t ldo,
+                                     void* stream) {
+  if (rows <= 0) return 0;
+  if (V <= 0 || !x || !out) return AVSR_E_ARG;
+  if (dtype == AVSR_BF16)
+    hipLaunchKernelGGL(log_softmax_kernel<bf16>, dim3(rows), dim3(256), 0, (hipStream_t)stream, V, (const bf16*)x, ldx, out, ldo);
+  else if (dtype == AVSR_F32)
+    hipLaunchKernelGGL(log_softmax_kernel<float>, dim3(rows), dim3(256), 0, (hipStream_t)stream, V, (const float*)x, ldx, out, ldo);
+  else return AVSR_E_DTYPE;
+  AVSR_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int avsr_dec_attn(const avsr_dec_attn_params* p, void* stream) {
+  if (!p || p->n <= 0 || p->H <= 0) return AVSR_E_ARG;
+  if (p->klen_max <= 0 || p->klen_max > 16384) return AVSR_E_SHAPE;
+  const size_t lds = (size_t)(p->klen_max + 256) * sizeof(float);
+  const dim3 g(p->H, p->n);
+  if (p->dtype == AVSR_BF16) hipLaunchKernelGGL(dec_attn_kernel<bf16>, g, dim3(256), lds, (hipStream_t)stream, *p);
+  else if (p->dtype == AVSR_F32) hipLaunchKernelGGL(dec_attn_kernel<float>, g, dim3(256), lds, (hipStream_t)stream, *p);
+  else return AVSR_E_DTYPE;
+  AVSR_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int avsr_row_topk(const avsr_topk_params* p, void* stream) {
+  if (!p || p->rows <= 0) return p ? 0 : AVSR_E_ARG;
+  if (p->K < 1 || p->K > KMAX || p->K > p->V) return AVSR_E_SHAPE;
+  hipLaunchKernelGGL(row_topk_kernel, dim3(p->rows), dim3(256), 0, (hipStream_t)stream, *p);
+  AVSR_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int avsr_ctc_prefix(const avsr_ctc_prefix_params* p, void* stream) {
+  if (!p || p->n <= 0) return AVSR_E_ARG;
+  if (p->P < 1 || p->P > 64 || p->T < 1) return AVSR_E_SHAPE;
+  hipLaunchKernelGGL(ctc_prefix_kernel, dim3(p->n), dim3(64), 0, (hipStream_t)stream, *p);
+  AVSR_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int avsr_beam_select(const avsr_beam_select_params* p, void* stream) {
+  if (!p || p->n <= 0) return AVSR_E_ARG;
+  if (p->beam < 1 || p->beam > KMAX || p->beam > p->n * p->V || p->P < 1) return AVSR_E_SHAPE;
+  hipLaunchKernelGGL(beam_select_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, *p);
+  AVSR_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int avsr_gather_rows(int groups, int n, int64_t row_bytes, const void* src, int64_t src_gstride,
+                                int64_t src_rstride, void* dst, int64_t dst_gstride, int64_t dst_rstride,
+                                const int* idx, void* stream) {
+  if (groups <= 0 || n <= 0 || row_bytes <= 0) return 0;
+  const int64_t all = row_bytes | src_gstride | src_rstride | dst_gstride | dst_rstride;
+  if (all % 16 == 0 && avsr_aligned16(src) && avsr_aligned16(dst)) {   // 16-byte words
+    const int64_t vecs = row_bytes / 16;
+    const int g = avsr_grid((int64_t)groups * n * vecs, 256, 2048);
+    hipLaunchKernelGGL(gather_rows_kernel<uint4>, dim3(g), dim3(256), 0, (hipStream_t)stream, groups, n, vecs,
+                       (const uint4*)src, src_gstride / 16, src_rstride / 16, (uint4*)dst, dst_gstride / 16,
+                       dst_rstride / 16, idx);
+  } else if (all % 4 == 0 && ((uintptr_t)src & 3) == 0 && ((uintptr_t)dst & 3) == 0) {   // 4-byte words
+    const int64_t vecs = row_bytes / 4;
+    const int g = avsr_grid((int64_t)groups * n * vecs, 256, 2048);
+    hipLaunchKernelGGL(gather_rows_kernel<uint32_t>, dim3(g), dim3(256), 0, (hipStream_t)stream, groups, n, vecs,
+                       (const uint32_t*)src, src_gstride / 4, src_rstride / 4, (uint32_t*)dst, dst_gstride / 4,
+                       dst_rstride / 4, idx);
+  } else {
+    return AVSR_E_ALIGN;
+  }
+  AVSR_CHECK_LAUNCH();
+  return 0;
+}

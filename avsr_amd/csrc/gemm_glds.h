@@ -145,7 +145,7 @@ struct Frags {
 };
 
 template <class CF>
-AVSR_DEV void wait_tiles_ahead(bool full) {   // all but the newest S-2 tiles' DMAs retired
+AVSR_DEV void wait_tiles_ahead(bool full) {   // tile t+1 retired: at most tiles t+2..t+S-1 in flight
   if (full) wait_vmcnt<CF::GL * (CF::S - 2)>();
   else wait_vmcnt<0>();
 }
@@ -164,12 +164,13 @@ AVSR_DEV void mainloop_glds(const LA& la, const LB& lb, int kbeg, int nk, f32x16
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
   if (nk <= 0) return;
 #pragma unroll
-  for (int p = 0; p < S - 1; ++p)
+  for (int p = 0; p < S; ++p)        // fill every stage: tiles 0..S-1
     if (p < nk) {
       la.issue(smem + p * CF::STAGE, kbeg + p * GBK, wave);
       lb.issue(smem + p * CF::STAGE + CF::SA, kbeg + p * GBK, wave);
     }
-  wait_tiles_ahead<CF>(S - 2 <= nk - 1);
+  if (nk >= S) wait_vmcnt<CF::GL * (S - 1)>();   // tile 0 retired, tiles 1..S-1 may be in flight
+  else wait_vmcnt<0>();
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
   Frags<CF, LA::KMAJ, LB::KMAJ> cur, nxt;

@@ -488,3 +488,49 @@ def adamw(param, grad, exp_avg, exp_avg_sq, *, lr, beta1, beta2, eps, weight_dec
                                 lr=lr, beta1=beta1, beta2=beta2, eps=eps, weight_decay=weight_decay,
                                 bias_corr1=1 - beta1 ** step, bias_corr2=1 - beta2 ** step,
                                 sumsq=sumsq_buf, max_norm=max_norm, grad_scale=grad_scale))
+
+
+# ---------------------------------------------------------------------------------------
+# Beam-search decode (decode.hip)
+# ---------------------------------------------------------------------------------------
+
+def log_softmax_rows(x, V, out):
+    L.check(L.load().avsr_log_softmax_rows(dtype_code(x), x.shape[0], V, x.data_ptr(), x.stride(0), out.data_ptr(),
+                                           out.stride(0), L.stream_ptr()), "avsr_log_softmax_rows")
+    return out
+
+
+def dec_attn(q, k, v, o, *, n, H, klen_max, k_bstride, v_bstride, klen=None, scale=0.125):
+    """one query per hypothesis: q/o rows i (ld = stride(0)), keys j of hypothesis i at
+    k[i*k_bstride + j*k.stride(-2)] (bstride 0: shared keys)."""
+    _call("avsr_dec_attn", L.fill(L.DecAttnParams, dtype=dtype_code(q), n=n, H=H, klen_max=klen_max, scale=scale,
+                                   q=q, ldq=q.stride(0), k=k, ldk=k.stride(-2), k_bstride=k_bstride, v=v,
+                                   ldv=v.stride(-2), v_bstride=v_bstride, klen=klen, o=o, ldo=o.stride(0)))
+    return o
+
+
+def row_topk(x, V, K, ids):
+    _call("avsr_row_topk", L.fill(L.TopkParams, rows=x.shape[0], V=V, K=K, x=x, ldx=x.stride(0), ids=ids))
+    return ids
+
+
+def ctc_prefix(logp, r_prev, last, ids, r_new, psi, *, n, out_len, blank, eos):
+    T, V = logp.shape
+    _call("avsr_ctc_prefix", L.fill(L.CtcPrefixParams, n=n, T=T, V=V, P=ids.shape[1], blank=blank, eos=eos,
+                                     out_len=out_len, logp=logp, r_prev=r_prev, last=last, ids=ids, r_new=r_new,
+                                     psi=psi))
+
+
+def beam_select(dec, V, ids, psi, s_prev, score, out, *, n, beam, blank, eos, w_dec, w_ctc):
+    """out: dict of device tensors prev/tok/col (int32) and score/dec/ctc/s (fp32), [beam]"""
+    _call("avsr_beam_select", L.fill(L.BeamSelectParams, n=n, V=V, P=ids.shape[1], beam=beam, blank=blank, eos=eos,
+                                      w_dec=w_dec, w_ctc=w_ctc, dec=dec, ld=dec.stride(0), ids=ids, psi=psi,
+                                      s_prev=s_prev, score=score, out_prev=out["prev"], out_tok=out["tok"],
+                                      out_col=out["col"], out_score=out["score"], out_dec=out["dec"],
+                                      out_ctc=out["ctc"], out_s=out["s"]))
+
+
+def gather_rows(src, dst, idx, *, groups, n, row_bytes, src_gstride, src_rstride, dst_gstride, dst_rstride):
+    """dst[g][i] = src[g][idx[i]] (strides in bytes)"""
+    L.check(L.load().avsr_gather_rows(groups, n, row_bytes, src.data_ptr(), src_gstride, src_rstride, dst.data_ptr(),
+                                      dst_gstride, dst_rstride, idx.data_ptr(), L.stream_ptr()), "avsr_gather_rows")

@@ -360,6 +360,83 @@ typedef struct {
 } avsr_adamw_params;
 int avsr_adamw(const avsr_adamw_params* p, void* stream);
 
+/* ------------------------------------------------------------------------------------
+ * Joint CTC / attention beam search. Replaces, for the decoder
+ * that get_beam_search_decoder builds (src/avhubert_avsr/avhubert_avsr_model.py:12-36):
+ *   Decoder.batch_score / forward_one_step    src/nets/backend/transformer/decoder.py:153-227
+ *     (one query per hypothesis; the reference recomputes the cross-attention K/V of the
+ *      memory every step, here they are computed once per utterance)
+ *   CTCPrefixScoreTH.__call__                 src/nets/ctc_prefix_score.py:65-187
+ *   BatchBeamSearch.search / batch_beam       src/nets/batch_beam_search.py:102-260
+ *   index_select of the hypothesis states     src/nets/batch_beam_search.py:53-66
+ * avsr_log_softmax_rows: out[r][c] = x[r][c] - max - log(sum exp(x - max)), c < V (fp32 out)
+ * avsr_dec_attn: o[i][h*64..] = softmax(scale * q_i k_j^T, j < klen[i]) v  per hypothesis i
+ *   and head h; key j of hypothesis i at k[i*k_bstride + j*ldk + h*64] (bstride 0: the keys
+ *   are shared, e.g. the encoder memory). dynamic LDS: (klen_max + 256) * 4 bytes.
+ * avsr_row_topk: ids[r][0..K) = indices of the K largest x[r][c], c < V, descending
+ *   (ties: smaller index first); K <= 16.
+ * avsr_ctc_prefix: for hypothesis h (prefix length out_len + 1 incl. sos, last token
+ *   last[h], CTC forward variables r_prev[h][T][2] or NULL at the first step) and its P
+ *   scored tokens ids[h][:]: r_new[h][j][T][2] and psi[h][j] = log prefix probability
+ *   (LOGZERO for blank, r_sum[T-1] for eos), psi[h][P] = r_sum[T-1] (the eos score).
+ * avsr_beam_select: weighted[h][v] = w_dec*dec[h][v] + w_ctc*(psi(h,v) - s_prev[h]) +
+ *   score[h]; the beam best (h, v) in descending order -> out_prev/out_tok/out_score,
+ *   out_dec = dec[h][v], out_ctc = psi - s_prev, out_s = psi, out_col = column of v in
+ *   ids[h] (P-1 when v was not scored, the reference's scoring_idmap -1 index).
+ * avsr_gather_rows: dst[g][i] = src[g][idx[i]] for i < n, rows of row_bytes; sizes, strides and
+ *   pointers multiples of 4 bytes (16-byte words when everything is 16-byte aligned).
+ * ------------------------------------------------------------------------------------ */
+int avsr_log_softmax_rows(int dtype, int rows, int V, const void* x, int64_t ldx, float* out, int64_t ldo,
+                          void* stream);
+
+typedef struct {
+  int dtype, n, H, klen_max;
+  float scale;
+  const void* q; int64_t ldq;
+  const void* k; int64_t ldk, k_bstride;
+  const void* v; int64_t ldv, v_bstride;
+  const int* klen;            /* [n] or NULL (= klen_max) */
+  void* o; int64_t ldo;
+} avsr_dec_attn_params;
+int avsr_dec_attn(const avsr_dec_attn_params* p, void* stream);
+
+typedef struct {
+  int rows, V, K;
+  const float* x; int64_t ldx;
+  int* ids;                   /* [rows][K] */
+} avsr_topk_params;
+int avsr_row_topk(const avsr_topk_params* p, void* stream);
+
+typedef struct {
+  int n, T, V, P;
+  int blank, eos, out_len;
+  const float* logp;          /* [T][V] CTC log-probs */
+  const float* r_prev;        /* [n][T][2] or NULL (first step) */
+  const int* last;            /* [n] */
+  const int* ids;             /* [n][P] */
+  float* r_new;               /* [n][P][T][2] */
+  float* psi;                 /* [n][P+1] */
+} avsr_ctc_prefix_params;
+int avsr_ctc_prefix(const avsr_ctc_prefix_params* p, void* stream);
+
+typedef struct {
+  int n, V, P, beam;
+  int blank, eos;
+  float w_dec, w_ctc;
+  const float* dec; int64_t ld;        /* decoder log-probs [n][ld] */
+  const int* ids;                      /* [n][P] */
+  const float* psi;                    /* [n][P+1] */
+  const float* s_prev;                 /* [n] */
+  const float* score;                  /* [n] */
+  int* out_prev; int* out_tok; int* out_col;
+  float* out_score; float* out_dec; float* out_ctc; float* out_s;
+} avsr_beam_select_params;
+int avsr_beam_select(const avsr_beam_select_params* p, void* stream);
+
+int avsr_gather_rows(int groups, int n, int64_t row_bytes, const void* src, int64_t src_gstride,
+                     int64_t src_rstride, void* dst, int64_t dst_gstride, int64_t dst_rstride,
+                     const int* idx, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,139 @@
+"""Beam-search decode on the HIP engine against the CPU oracle
+(oracle/decode_oracle.py, itself pinned to the reference's own yseq / scores in
+tests/golden/avsr_tiny.npz) and torch fp32 references of the individual kernels."""
+import numpy as np
+import pytest
+import torch
+
+from avsr_amd import ops
+from avsr_amd.avhubert_avsr_model import AVHubertAVSR, get_beam_search_decoder
+from avsr_amd.configuration_avhubert_avsr import AVHubertAVSRConfig
+from oracle import avsr_oracle as O
+from oracle import decode_oracle as DO
+from oracle.weights import NO_DROPOUT, TINY_CONFIG
+from tests.oracle_util import golden_batch, golden_state, load_golden, tiny_cfg
+
+pytestmark = pytest.mark.gpu
+
+TOKENS = ["<blank>"] + [f"u{i}" for i in range(1, 5048)] + ["<eos>"]
+
+
+@pytest.fixture(scope="module")
+def g():
+    return load_golden()
+
+
+@pytest.fixture(scope="module")
+def model(g):
+    m = AVHubertAVSR(AVHubertAVSRConfig(**TINY_CONFIG, **NO_DROPOUT)).eval()
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in golden_state(g).items()}, strict=True)
+    m.setup_engine("cuda", torch.float32)
+    return m
+
+
+def test_dec_attn_matches_torch(dev):
+    g = torch.Generator().manual_seed(3)
+    n, H, L, D, Lmax = 3, 4, 37, 256, 50
+    q = torch.randn(n, 3 * D, generator=g).to(dev)
+    kc = torch.randn(n, Lmax, D, generator=g).to(dev)
+    vc = torch.randn(n, Lmax, D, generator=g).to(dev)
+    o = torch.empty(n, D, device=dev)
+    ops.dec_attn(q[:, :D], kc, vc, o, n=n, H=H, klen_max=L, k_bstride=Lmax * D, v_bstride=Lmax * D)
+    qh = q[:, :D].view(n, H, 1, 64)
+    kh = kc[:, :L].view(n, L, H, 64).transpose(1, 2)
+    vh = vc[:, :L].view(n, L, H, 64).transpose(1, 2)
+    ref = torch.softmax(qh @ kh.transpose(-1, -2) * 0.125, -1) @ vh
+    torch.testing.assert_close(o, ref.reshape(n, D), rtol=1e-5, atol=1e-5)
+    # shared keys (bstride 0), bf16 storage
+    mem = torch.randn(L, 2 * D, generator=g).to(dev)
+    ops.dec_attn(q[:, :D], mem[:, :D], mem[:, D:], o, n=n, H=H, klen_max=L, k_bstride=0, v_bstride=0)
+    km = mem[:, :D].view(L, H, 64).transpose(0, 1)
+    vm = mem[:, D:].view(L, H, 64).transpose(0, 1)
+    ref = torch.softmax(qh @ km.transpose(-1, -2).unsqueeze(0) * 0.125, -1) @ vm.unsqueeze(0)
+    torch.testing.assert_close(o, ref.reshape(n, D), rtol=1e-5, atol=1e-5)
+
+
+def test_row_topk_and_log_softmax(dev):
+    g = torch.Generator().manual_seed(4)
+    x = torch.randn(5, 5056, generator=g).to(dev)
+    lp = torch.empty(5, 5049, device=dev)
+    ops.log_softmax_rows(x, 5049, lp)
+    torch.testing.assert_close(lp, torch.log_softmax(x[:, :5049], -1), rtol=1e-5, atol=1e-5)
+    ids = torch.empty(5, 7, device=dev, dtype=torch.int32)
+    ops.row_topk(lp, 5049, 7, ids)
+    assert torch.equal(ids.long().cpu(), torch.topk(lp.cpu(), 7, dim=-1)[1])
+
+
+@pytest.mark.parametrize("first", [True, False])
+def test_ctc_prefix_matches_oracle(dev, first):
+    g = torch.Generator().manual_seed(5)
+    T, V, n, P = 40, 300, 3, 4
+    logp = torch.log_softmax(torch.randn(T, V, generator=g) * 3, -1)
+    eos = V - 1
+    if first:
+        yseqs = [[eos]] * n
+        states = [None] * n
+    else:
+        yseqs = [[eos, 5, 7], [eos, 7, 7], [eos, 9, 2]]
+        states = [(torch.log_softmax(torch.randn(T, 2, generator=g), -1) - 3.0, -2.5) for _ in range(n)]
+    ids = torch.stack([torch.randperm(V - 2, generator=g)[:P] + 1 for _ in range(n)])
+    ids[1, 0] = yseqs[1][-1]          # repeated-label path
+    ids[2, 1] = eos
+    ids[0, 2] = 0                     # blank among the scored ids
+    ref_sc, ref_r, ref_psi = DO.ctc_prefix_scores(logp.double(), yseqs, [None if s is None else (s[0].double(), s[1]) for s in states],
+                                                  ids, 0, eos)
+    r_prev = None if first else torch.stack([s[0] for s in states]).to(dev).contiguous()
+    last = torch.tensor([y[-1] for y in yseqs], dtype=torch.int32, device=dev)
+    r_new = torch.empty(n, P, T, 2, device=dev)
+    psi = torch.empty(n, P + 1, device=dev)
+    ops.ctc_prefix(logp.to(dev), r_prev, last, ids.to(dev, torch.int32), r_new, psi, n=n, out_len=len(yseqs[0]) - 1,
+                   blank=0, eos=eos)
+    for h in range(n):
+        for j in range(P):
+            want = ref_psi[h, ids[h, j]].item()
+            assert abs(psi[h, j].item() - want) <= 1e-5 * abs(want) + 1e-4, (h, j, psi[h, j].item(), want)
+        assert abs(psi[h, P].item() - ref_psi[h, eos].item()) <= 1e-5 * abs(ref_psi[h, eos].item()) + 1e-4
+    rr = ref_r.permute(2, 3, 0, 1).float()     # (n, P, T, 2)
+    ok = rr > -1e9
+    torch.testing.assert_close(r_new.cpu()[ok], rr[ok], rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.parametrize("b", [0, 1])
+@pytest.mark.parametrize("beam", [1, 3])
+def test_beam_search_on_reference_encoder_output(g, model, b, beam):
+    """the HIP decode of the reference's own encoder output reproduces the reference's best
+    hypothesis exactly (token ids) and its score (1e-4 relative)."""
+    x = torch.from_numpy(g[f"dec_enc_{b}"]).cuda()
+    bs = get_beam_search_decoder(model.avsr, TOKENS, ctc_weight=0.1, beam_size=beam)
+    hyps = bs(x)
+    best = hyps[0].asdict()
+    assert best["yseq"] == g[f"yseq_b{beam}_{b}"].tolist()
+    ref = float(g[f"score_b{beam}_{b}"][0])
+    assert abs(best["score"] - ref) <= 1e-4 * abs(ref)
+
+
+@pytest.fixture(scope="module")
+def trained_model(g):
+    """make_golden.py decodes AFTER its train-mode forward, which moved the BatchNorm running
+    statistics: replay that forward (it updates the running statistics the same way)."""
+    m = AVHubertAVSR(AVHubertAVSRConfig(**TINY_CONFIG, **NO_DROPOUT)).train()
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in golden_state(g).items()}, strict=True)
+    m.setup_engine("cuda", torch.float32)
+    batch = {k: torch.from_numpy(v) for k, v in golden_batch(g).items()}
+    with torch.no_grad():
+        m(**batch)
+    return m.eval()
+
+
+@pytest.mark.parametrize("b", [0, 1])
+def test_encode_then_decode_end_to_end(g, trained_model, b):
+    """script/evaluation.py:96-107 call form on the engine: encoder (B=1, no mask) + beam 3."""
+    batch = golden_batch(g)
+    Tb = int(g["lengths"][b])
+    v = torch.from_numpy(np.ascontiguousarray(batch["videos"][b:b + 1, :, :Tb]))
+    a = torch.from_numpy(np.ascontiguousarray(batch["audios"][b:b + 1, :, :Tb]))
+    x = trained_model.avsr.engine().encode(a, v)[0]
+    ref = torch.from_numpy(g[f"dec_enc_{b}"])
+    assert float((x.cpu() - ref).abs().max() / ref.abs().max()) < 2e-4
+    hyps = get_beam_search_decoder(trained_model.avsr, TOKENS, ctc_weight=0.1, beam_size=3)(x)
+    assert hyps[0].asdict()["yseq"] == g[f"yseq_b3_{b}"].tolist()

@@ -69,3 +69,19 @@ def test_decoder_one_step(g):
         with torch.no_grad():
             logp = O.decoder_one_step(sd, cfg, torch.tensor([[5048, 5, 17, 301]]), x.unsqueeze(0))
         assert rel(logp, g[f"onestep_{b}"]) < 1e-5
+
+
+@pytest.mark.parametrize("b", [0, 1])
+@pytest.mark.parametrize("beam", [1, 3])
+def test_beam_search_oracle(g, b, beam):
+    """oracle/decode_oracle.py (BatchBeamSearch + CTCPrefixScoreTH restated) reproduces the
+    reference's best hypothesis (token sequence exactly, score to 1e-4) on the reference's
+    own encoder output and CTC log-probs."""
+    from oracle import decode_oracle as D
+    sd = O.to_torch_state(golden_state(g))
+    x = torch.from_numpy(g[f"dec_enc_{b}"])
+    ctc_logp = torch.from_numpy(g[f"ctc_logp_{b}"])[0]
+    hyps = D.beam_search(sd, tiny_cfg(), x, ctc_logp, beam, ctc_weight=0.1)
+    assert hyps[0].yseq == g[f"yseq_b{beam}_{b}"].tolist()
+    ref = float(g[f"score_b{beam}_{b}"][0])
+    assert abs(hyps[0].score - ref) <= 1e-4 * abs(ref)
