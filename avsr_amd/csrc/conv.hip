@@ -7,6 +7,7 @@
 //  bwd_weight  dw[co][(kh,kw,ci)]       += sum_{m = y pixel} dy[m][co] * x[im2col(m, (kh,kw,ci))]
 //              (K = pixels is split over blocks; fp32 atomics into the gradient)
 #include "gemm_core.h"
+#include "gemm_glds.h"
 
 using namespace gemmcore;
 
@@ -72,6 +73,198 @@ __global__ __launch_bounds__(NT) void conv_kernel(ConvArgs a) {
   epilogue<T, OutT, WM, WN>(e, m0, n0, acc, smem);
 }
 
+// ---------------------------------------------------------------- LDS-DMA (bf16) loaders
+// Same operand views as the register-staged loaders above, but every 16-byte vector is
+// DMA'd straight into the swizzled LDS image (gemm_glds.h); invalid taps -> zero line.
+using gemmg::GBK;
+using gemmg::glds16;
+using gemmg::g_zero_line;
+
+// A of forward (TRANSP=false: r = output pixel, gather x) / data-grad (TRANSP=true: r = input
+// pixel, gather dy): k-major image, k = (kh, kw, c) with c fastest.
+template <int R, int NW, bool TRANSP> struct GConvK {
+  static constexpr bool KMAJ = true;
+  static constexpr int SLOTS = R / 8 / NW;
+  const bf16* p; ConvGeom g; int kend;
+  int pn[SLOTS], ph_[SLOTS], pw_[SLOTS], kc[SLOTS];
+  AVSR_DEV void init(const bf16* base, const ConvGeom& g_, int r0, int rext, int kend_, int wave, int lane) {
+    p = base; g = g_; kend = kend_;
+#pragma unroll
+    for (int i = 0; i < SLOTS; ++i) {
+      const int pc = i * NW + wave, pr = pc * 8 + (lane >> 3);
+      kc[i] = ((lane & 7) ^ ((pr >> 1) & 7)) * 8;
+      const int r = r0 + pr;
+      if (r >= rext) { pn[i] = 0; ph_[i] = -1000000; pw_[i] = 0; continue; }
+      if (!TRANSP) {
+        uint32_t n = fdiv(r, g.f_hw_out); uint32_t rem = r - n * g.f_hw_out.d;
+        uint32_t oh = fdiv(rem, g.f_w_out); uint32_t ow = rem - oh * g.f_w_out.d;
+        pn[i] = n * g.hin * g.win; ph_[i] = oh * g.sh - g.ph; pw_[i] = ow * g.sw - g.pw;
+      } else {
+        uint32_t n = fdiv(r, g.f_hw_in); uint32_t rem = r - n * g.f_hw_in.d;
+        uint32_t h = fdiv(rem, g.f_w_in); uint32_t w = rem - h * g.f_w_in.d;
+        pn[i] = n * g.hout * g.wout; ph_[i] = h + g.ph; pw_[i] = w + g.pw;
+      }
+    }
+  }
+  AVSR_DEV void issue(char* img, int k0, int wave) const {
+    const int cs = TRANSP ? g.cout_shift : g.cin_shift;
+#pragma unroll
+    for (int i = 0; i < SLOTS; ++i) {
+      const int k = k0 + kc[i];
+      const int c = k & ((1 << cs) - 1), khw = k >> cs;
+      const int kh = fdiv(khw, g.f_kw), kw = khw - kh * g.f_kw.d;
+      bool ok = k < kend;
+      int64_t off;
+      if (!TRANSP) {
+        const int ih = ph_[i] + kh, iw = pw_[i] + kw;
+        ok = ok && ih >= 0 && ih < g.hin && iw >= 0 && iw < g.win;
+        off = (int64_t)(pn[i] + ih * g.win + iw) * g.ldx + c;
+      } else {
+        const int th = ph_[i] - kh, tw = pw_[i] - kw;
+        const int oh = th / g.sh, ow = tw / g.sw;
+        ok = ok && th >= 0 && tw >= 0 && oh * g.sh == th && ow * g.sw == tw && oh < g.hout && ow < g.wout;
+        off = (int64_t)(pn[i] + oh * g.wout + ow) * g.ldy + c;
+      }
+      glds16(ok ? (const void*)(p + off) : (const void*)g_zero_line, img + (i * NW + wave) * 1024);
+    }
+  }
+};
+
+// B of data-grad: weight [cout][kh][kw][cin] viewed as (r = cin, k = (kh, kw, cout)); r-contiguous.
+template <int R, int NW> struct GWgtR {
+  static constexpr bool KMAJ = false;
+  static constexpr int CPR = R / 8, RPP = 64 / CPR, SLOTS = GBK / RPP / NW;
+  const bf16* p; ConvGeom g; int kend;
+  int kr[SLOTS], rr[SLOTS];
+  AVSR_DEV void init(const bf16* base, const ConvGeom& g_, int r0, int rext, int kend_, int wave, int lane) {
+    p = base; g = g_; kend = kend_;
+#pragma unroll
+    for (int i = 0; i < SLOTS; ++i) {
+      const int pc = i * NW + wave, pk = pc * RPP + lane / CPR;
+      const int c = (lane % CPR) ^ gemmg::rswz<CPR>(pk);
+      kr[i] = pk;
+      rr[i] = r0 + c * 8 < rext ? r0 + c * 8 : -1;
+    }
+  }
+  AVSR_DEV void issue(char* img, int k0, int wave) const {
+    const int ktot = g.kh * g.kw * g.cin;
+#pragma unroll
+    for (int i = 0; i < SLOTS; ++i) {
+      const int k = k0 + kr[i];
+      const int co = k & ((1 << g.cout_shift) - 1), khw = k >> g.cout_shift;
+      const bool ok = k < kend && rr[i] >= 0;
+      glds16(ok ? (const void*)(p + (int64_t)co * ktot + khw * g.cin + rr[i]) : (const void*)g_zero_line,
+             img + (i * NW + wave) * 1024);
+    }
+  }
+};
+
+// B of weight-grad: r = (kh, kw, cin) (vectors along cin), k = output pixel; r-contiguous.
+template <int R, int NW> struct GConvR {
+  static constexpr bool KMAJ = false;
+  static constexpr int CPR = R / 8, RPP = 64 / CPR, SLOTS = GBK / RPP / NW;
+  const bf16* p; ConvGeom g; int kend;
+  int kr[SLOTS], rk[SLOTS], rw[SLOTS], rc[SLOTS];
+  AVSR_DEV void init(const bf16* base, const ConvGeom& g_, int r0, int rext, int kend_, int wave, int lane) {
+    p = base; g = g_; kend = kend_;
+#pragma unroll
+    for (int i = 0; i < SLOTS; ++i) {
+      const int pc = i * NW + wave, pk = pc * RPP + lane / CPR;
+      const int r = r0 + ((lane % CPR) ^ gemmg::rswz<CPR>(pk)) * 8;
+      kr[i] = pk;
+      if (r >= rext) { rk[i] = -1000000; rw[i] = 0; rc[i] = 0; continue; }
+      const int c = r & ((1 << g.cin_shift) - 1), khw = r >> g.cin_shift;
+      const int kh = fdiv(khw, g.f_kw);
+      rk[i] = kh; rw[i] = khw - kh * g.f_kw.d; rc[i] = c;
+    }
+  }
+  AVSR_DEV void issue(char* img, int k0, int wave) const {
+#pragma unroll
+    for (int i = 0; i < SLOTS; ++i) {
+      const int k = k0 + kr[i];
+      bool ok = k < kend;
+      const uint32_t kk = ok ? k : 0;
+      const uint32_t n = fdiv(kk, g.f_hw_out), rem = kk - n * g.f_hw_out.d;
+      const uint32_t oh = fdiv(rem, g.f_w_out), ow = rem - oh * g.f_w_out.d;
+      const int ih = (int)oh * g.sh - g.ph + rk[i], iw = (int)ow * g.sw - g.pw + rw[i];
+      ok = ok && ih >= 0 && ih < g.hin && iw >= 0 && iw < g.win;
+      glds16(ok ? (const void*)(p + (int64_t)(n * g.hin * g.win + ih * g.win + iw) * g.ldx + rc[i])
+                : (const void*)g_zero_line,
+             img + (i * NW + wave) * 1024);
+    }
+  }
+};
+
+// dense wrappers with the conv loaders' init signature
+template <int R, int NW> struct GDenseKc : gemmg::GDenseK<R, NW> {
+  AVSR_DEV void init(const bf16* base, int64_t ld, const ConvGeom&, int r0, int rext, int kend, int wave, int lane) {
+    gemmg::GDenseK<R, NW>::init(base, ld, r0, rext, kend, wave, lane);
+  }
+};
+
+template <typename OutT, int KIND, class CF>
+__global__ __launch_bounds__(CF::NTH, CF::MINB) void conv_glds_kernel(ConvArgs a, int tiles_m, int tiles_n) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int id = gemmg::xcd_remap(blockIdx.x, gridDim.x);
+  int tm, tn, z;
+  gemmg::tile_of(id, tiles_m, tiles_n, tm, tn, z);
+  const int grp = z / a.splits, sp = z % a.splits;
+  const int m0 = tm * CF::BM, n0 = tn * CF::BN;
+  const bf16* pa = (const bf16*)a.a + (int64_t)grp * a.a_gstride;
+  const bf16* pb = (const bf16*)a.b + (int64_t)grp * a.b_gstride;
+  const int kbeg = sp * a.kchunk, kend = min(a.K, kbeg + a.kchunk);
+  const int nk = (kend - kbeg + GBK - 1) / GBK;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  f32x16 acc[CF::FM][CF::FN];
+  if constexpr (KIND == K_FWD) {
+    GConvK<CF::BM, CF::NW, false> la; la.init(pa, a.g, m0, a.M, kend, wave, lane);
+    gemmg::GDenseK<CF::BN, CF::NW> lb; lb.init(pb, a.K, n0, a.N, kend, wave, lane);
+    gemmg::mainloop_glds<CF>(la, lb, kbeg, nk, acc, smem);
+  } else if constexpr (KIND == K_DGRAD) {
+    GConvK<CF::BM, CF::NW, true> la; la.init(pa, a.g, m0, a.M, kend, wave, lane);
+    GWgtR<CF::BN, CF::NW> lb; lb.init(pb, a.g, n0, a.N, kend, wave, lane);
+    gemmg::mainloop_glds<CF>(la, lb, kbeg, nk, acc, smem);
+  } else {
+    gemmg::GDenseR<CF::BM, CF::NW> la; la.init(pa, a.g.ldy, m0, a.M, kend, wave, lane);
+    GConvR<CF::BN, CF::NW> lb; lb.init(pb, a.g, n0, a.N, kend, wave, lane);
+    gemmg::mainloop_glds<CF>(la, lb, kbeg, nk, acc, smem);
+  }
+  Epi e = a.e;
+  e.C = (OutT*)e.C + (int64_t)grp * a.c_gstride;
+  if (e.res) e.res = (const bf16*)e.res + (int64_t)grp * a.c_gstride;
+  if (e.preact) e.preact = (bf16*)e.preact + (int64_t)grp * a.c_gstride;
+  if (e.bias) e.bias += (int64_t)grp * a.c_gstride;
+  gemmg::epilogue_g<bf16, OutT, CF>(e, m0, n0, acc, smem);
+}
+
+using CCfg128 = gemmg::GCfg<2, 2, 2, 2, 2>;    // 128x128
+using CCfg256x64 = gemmg::GCfg<4, 1, 2, 2, 2>; // 256x64  (N <= 64: cout / cin = 64)
+using CCfg64x256 = gemmg::GCfg<1, 4, 2, 2, 2>; // 64x256  (M <= 64: weight-grad with cout = 64)
+
+template <typename OutT, int KIND, class CF>
+int launch_glds(const ConvArgs& a, int groups, hipStream_t st) {
+  const int tm = (a.M + CF::BM - 1) / CF::BM, tn = (a.N + CF::BN - 1) / CF::BN;
+  const long nwg = (long)tm * tn * groups * a.splits;
+  if (nwg > 0x7fffffffL) return AVSR_E_SHAPE;
+  hipLaunchKernelGGL((conv_glds_kernel<OutT, KIND, CF>), dim3((unsigned)nwg), dim3(CF::NTH), CF::LDS_BYTES, st, a,
+                     tm, tn);
+  AVSR_CHECK_LAUNCH();
+  return 0;
+}
+
+// AVSR_CONV_NOGLDS=1 keeps the register-staged core (A/B comparisons)
+static bool conv_glds_enabled() {
+  const char* e = getenv("AVSR_CONV_NOGLDS");
+  return !(e && e[0] == '1');
+}
+
+template <typename OutT, int KIND>
+int glds_by_tile(const ConvArgs& a, int groups, hipStream_t st) {
+  if (a.N <= 64) return launch_glds<OutT, KIND, CCfg256x64>(a, groups, st);
+  if (a.M <= 64) return launch_glds<OutT, KIND, CCfg64x256>(a, groups, st);
+  return launch_glds<OutT, KIND, CCfg128>(a, groups, st);
+}
+
 template <typename T, typename OutT, int WM, int WN, int KIND>
 int launch(const ConvArgs& a, int groups, hipStream_t st) {
   // operand kinds per convolution direction (fwd: K/K, dgrad: K/R, wgrad: R/R)
@@ -126,7 +319,8 @@ extern "C" int avsr_conv_fwd(const avsr_conv_params* p, void* stream) {
   if (a.M == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
   if (p->dtype == AVSR_F32) return by_tile<float, float, K_FWD>(a, p->groups, st);
-  if (p->dtype == AVSR_BF16) return by_tile<bf16, bf16, K_FWD>(a, p->groups, st);
+  if (p->dtype == AVSR_BF16)
+    return conv_glds_enabled() ? glds_by_tile<bf16, K_FWD>(a, p->groups, st) : by_tile<bf16, bf16, K_FWD>(a, p->groups, st);
   return AVSR_E_DTYPE;
 }
 
@@ -145,7 +339,9 @@ extern "C" int avsr_conv_bwd_data(const avsr_conv_params* p, void* stream) {
   if (a.M == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
   if (p->dtype == AVSR_F32) return by_tile<float, float, K_DGRAD>(a, p->groups, st);
-  if (p->dtype == AVSR_BF16) return by_tile<bf16, bf16, K_DGRAD>(a, p->groups, st);
+  if (p->dtype == AVSR_BF16)
+    return conv_glds_enabled() ? glds_by_tile<bf16, K_DGRAD>(a, p->groups, st)
+                               : by_tile<bf16, bf16, K_DGRAD>(a, p->groups, st);
   return AVSR_E_DTYPE;
 }
 
@@ -170,12 +366,15 @@ extern "C" int avsr_conv_bwd_weight(const avsr_conv_params* p, void* stream) {
     if (splits < 1) splits = 1;
   }
   a.splits = splits;
-  a.kchunk = ((a.K + splits - 1) / splits + BKE - 1) / BKE * BKE;
+  const bool glds = p->dtype == AVSR_BF16 && conv_glds_enabled();
+  const int kq = glds ? GBK : BKE;
+  a.kchunk = ((a.K + splits - 1) / splits + kq - 1) / kq * kq;
   a.splits = (a.K + a.kchunk - 1) / a.kchunk;
   base_epi(a.e);
   a.e.M = a.M; a.e.N = a.N; a.e.C = p->dw; a.e.ldc = ktot; a.e.atomic = 1; a.e.alpha = 1.f;
   hipStream_t st = (hipStream_t)stream;
   if (p->dtype == AVSR_F32) return by_tile<float, float, K_WGRAD>(a, p->groups, st);
-  if (p->dtype == AVSR_BF16) return by_tile<bf16, float, K_WGRAD>(a, p->groups, st);
+  if (p->dtype == AVSR_BF16)
+    return glds ? glds_by_tile<float, K_WGRAD>(a, p->groups, st) : by_tile<bf16, float, K_WGRAD>(a, p->groups, st);
   return AVSR_E_DTYPE;
 }

@@ -44,9 +44,9 @@ __global__ __launch_bounds__(NT) void dense_kernel(DenseArgs a) {
 template <typename OutT, bool AK, bool BK, class CF>
 __global__ __launch_bounds__(CF::NTH, CF::MINB) void dense_glds_kernel(DenseArgs a, int tiles_m, int tiles_n) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int nwg = gridDim.x;
-  const int id = gemmg::xcd_remap(blockIdx.x, nwg);
-  const int tn = id % tiles_n, tm = (id / tiles_n) % tiles_m, z = id / (tiles_n * tiles_m);
+  const int id = gemmg::xcd_remap(blockIdx.x, gridDim.x);
+  int tm, tn, z;
+  gemmg::tile_of(id, tiles_m, tiles_n, tm, tn, z);
   const int bz = z / a.splits, sp = z % a.splits;
   const int m0 = tm * CF::BM, n0 = tn * CF::BN;
   const int kbeg = sp * a.kchunk, kend = min(a.K, kbeg + a.kchunk);

@@ -30,6 +30,12 @@ AVSR_DEV void glds16(const void* src, char* lds_wave_base) {
   __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)lds_wave_base, 16, 0, 0);
 }
 
+// r-contiguous images: 16-byte chunk swizzle of k-row k (CPR chunks per row). Rows of >= 256 B
+// (CPR >= 16): shift by (k & 3) * 64 B; rows of 128 B (CPR == 8): rows k, k+1 already sit in
+// opposite bank halves, so only k & 2 shifts by 64 B. Either way one 32-lane group of a
+// ds_read_b64_tr_b16 (4 consecutive k-rows x 64 B) covers all 64 banks.
+template <int CPR> AVSR_DEV int rswz(int k) { return CPR >= 16 ? (k & 3) << 2 : ((k >> 1) & 1) << 2; }
+
 // ---------------------------------------------------------------- dense loaders
 // k-major operand: elem(r, k) = p[r*ld + k]
 template <int R, int NW> struct GDenseK {
@@ -69,7 +75,7 @@ template <int R, int NW> struct GDenseR {
 #pragma unroll
     for (int i = 0; i < SLOTS; ++i) {
       const int pc = i * NW + wave, pk = pc * RPP + lane / CPR;
-      const int c = (lane % CPR) ^ ((pk & 3) << 2);
+      const int c = (lane % CPR) ^ rswz<CPR>(pk);
       const int r = r0 + c * 8;
       kr[i] = pk;
       p[i] = r < rext ? base + (int64_t)pk * ld + r : nullptr;
@@ -96,7 +102,7 @@ AVSR_DEV bf16x8 gfrag(const char* img, int rb, int s, int lane) {
     const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
     const int k0 = 16 * s + 8 * (lane >> 5);
     const int r = rb + 16 * (g & 1) + 4 * pp;
-    const int off = (((r >> 3) ^ (q << 2)) << 4) + (r & 7) * 2;   // (k0 + q) & 3 == q
+    const int off = (((r >> 3) ^ rswz<R / 8>(q)) << 4) + (r & 7) * 2;   // k0 % 4 == 0: swizzle of k0+q, k0+4+q = of q
     const char* base = img + off;
     const v4i16 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(base + (k0 + q) * (R * 2)));
     const v4i16 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(base + (k0 + 4 + q) * (R * 2)));
@@ -295,6 +301,22 @@ AVSR_DEV void epilogue_g(const Epi& e, int m0, int n0, f32x16 (&acc)[CF::FM][CF:
 AVSR_DEV int xcd_remap(int orig, int nwg) {
   const int xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+}
+
+// Tile of a remapped block id: batches outermost, then groups of GM tile-rows; inside a group
+// the tile-row runs fastest, so the ~64 blocks an XCD holds at once cover about 8 x 8 tiles
+// (A and B panels ~2 MiB each at K = 1024: both stay in that XCD's 4 MiB L2) instead of
+// 2 rows x all columns (the whole B operand streamed through L2 for every pair of rows).
+AVSR_DEV void tile_of(int id, int tiles_m, int tiles_n, int& tm, int& tn, int& z) {
+  constexpr int GM = 8;
+  const int per = tiles_m * tiles_n;
+  z = id / per;
+  const int t = id - z * per;
+  const int grp = t / (GM * tiles_n), first = grp * GM;
+  const int gsz = min(tiles_m - first, GM);
+  const int r = t - grp * GM * tiles_n;
+  tm = first + r % gsz;
+  tn = r / gsz;
 }
 
 }  // namespace gemmg
