@@ -3,6 +3,7 @@
 // see include/avsr_hip.h for the reference call sites.
 #include "gemm_core.h"
 #include "gemm_glds.h"
+#include "gemm_pp.h"
 #include <cstring>
 
 using namespace gemmcore;
@@ -66,6 +67,43 @@ __global__ __launch_bounds__(CF::NTH, CF::MINB) void dense_glds_kernel(DenseArgs
   gemmg::epilogue_g<bf16, OutT, CF>(e, m0, n0, acc, smem);
 }
 
+// 256x256 ping-pong core (gemm_pp.h)
+template <typename OutT, bool AK, bool BK>
+__global__ __launch_bounds__(gemmpp::NTH, 1) void dense_pp_kernel(DenseArgs a, int tiles_m, int tiles_n) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int id = gemmg::xcd_remap(blockIdx.x, gridDim.x);
+  int tm, tn, z;
+  gemmg::tile_of(id, tiles_m, tiles_n, tm, tn, z);
+  const int bz = z / a.splits, sp = z % a.splits;
+  const int m0 = tm * gemmpp::BM, n0 = tn * gemmpp::BN;
+  const int kbeg = sp * a.kchunk, kend = min(a.K, kbeg + a.kchunk);
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  using LA = typename std::conditional<AK, gemmpp::HalfK<64>, gemmpp::HalfR<64>>::type;
+  using LB = typename std::conditional<BK, gemmpp::HalfK<32>, gemmpp::HalfR<32>>::type;
+  LA la; la.init((const bf16*)a.A + (int64_t)bz * a.sA, a.lda, m0, a.M, kend, wave, lane);
+  LB lb; lb.init((const bf16*)a.B + (int64_t)bz * a.sB, a.ldb, n0, a.N, kend, wave, lane);
+  f32x16 acc[4][2];
+  gemmpp::mainloop_pp(la, lb, kbeg, (kend - kbeg + gemmg::GBK - 1) / gemmg::GBK, acc, smem);
+  Epi e = a.e;
+  e.C = (OutT*)e.C + (int64_t)bz * a.sC + sp * a.sSplit;
+  if (e.res) e.res = (const bf16*)e.res + (int64_t)bz * a.sR;
+  if (e.preact) e.preact = (bf16*)e.preact + (int64_t)bz * a.sC;
+  if (e.gate) e.gate = (const bf16*)e.gate + (int64_t)bz * a.sC;
+  e.drop_base = (uint64_t)bz * (uint64_t)a.M * (uint64_t)a.N;
+  gemmg::epilogue_g<bf16, OutT, gemmpp::CF>(e, m0, n0, acc, smem);
+}
+
+template <typename OutT, bool AK, bool BK>
+int launch_pp(const DenseArgs& a, int batch, hipStream_t st) {
+  const int tm = (a.M + 255) / 256, tn = (a.N + 255) / 256;
+  const long nwg = (long)tm * tn * batch * a.splits;
+  if (nwg > 0x7fffffffL) return AVSR_E_SHAPE;
+  hipLaunchKernelGGL((dense_pp_kernel<OutT, AK, BK>), dim3((unsigned)nwg), dim3(gemmpp::NTH), gemmpp::LDS_BYTES, st, a,
+                     tm, tn);
+  AVSR_CHECK_LAUNCH();
+  return 0;
+}
+
 template <typename OutT, bool AK, bool BK, class CF>
 int launch_glds(const DenseArgs& a, int batch, hipStream_t st) {
   const int tm = (a.M + CF::BM - 1) / CF::BM, tn = (a.N + CF::BN - 1) / CF::BN;
@@ -83,13 +121,16 @@ using Cfg256x128 = gemmg::GCfg<4, 2, 2, 2, 3>;   // 256x128, 8 waves, 3 stages (
 using Cfg128x256 = gemmg::GCfg<2, 4, 2, 2, 3>;   // 128x256, 8 waves, 3 stages
 using Cfg128s3 = gemmg::GCfg<2, 2, 2, 2, 3>;     // 128x128, 4 waves, 3 stages (96 KiB)
 using Cfg128s4 = gemmg::GCfg<2, 2, 2, 2, 4>;     // 128x128, 4 waves, 4 stages (128 KiB)
+using Cfg128w8s3 = gemmg::GCfg<2, 4, 2, 1, 3>;   // 128x128, 8 waves (64x32 each), 3 stages
+using Cfg128w8s4 = gemmg::GCfg<2, 4, 2, 1, 4>;   // 128x128, 8 waves, 4 stages
 
 // tile choice: AVSR_GEMM_TILE=128|256|256x128|128x256 forces one (benchmarks); otherwise the
 // configuration with the fewest block rounds x per-tile work (wave quantisation over 256 CUs)
 int tile_cfg(const avsr_gemm_params* p, int splits) {
   const char* e = getenv("AVSR_GEMM_TILE");
   const int forced = !e ? -1 : !strcmp(e, "128") ? 0 : !strcmp(e, "256") ? 1 : !strcmp(e, "256x128") ? 2
-                   : !strcmp(e, "128x256") ? 3 : !strcmp(e, "128s3") ? 4 : !strcmp(e, "128s4") ? 5 : -1;
+                   : !strcmp(e, "128x256") ? 3 : !strcmp(e, "128s3") ? 4 : !strcmp(e, "128s4") ? 5
+                   : !strcmp(e, "128w8s3") ? 6 : !strcmp(e, "128w8s4") ? 7 : !strcmp(e, "pp") ? 8 : -1;
   if (forced >= 0) return forced;
   return 0;
 }
@@ -102,6 +143,9 @@ int launch_cfg(int cfg, const DenseArgs& a, int batch, hipStream_t st) {
     case 3: return launch_glds<OutT, AK, BK, Cfg128x256>(a, batch, st);
     case 4: return launch_glds<OutT, AK, BK, Cfg128s3>(a, batch, st);
     case 5: return launch_glds<OutT, AK, BK, Cfg128s4>(a, batch, st);
+    case 6: return launch_glds<OutT, AK, BK, Cfg128w8s3>(a, batch, st);
+    case 7: return launch_glds<OutT, AK, BK, Cfg128w8s4>(a, batch, st);
+    case 8: return launch_pp<OutT, AK, BK>(a, batch, st);
     default: return launch_glds<OutT, AK, BK, Cfg128>(a, batch, st);
   }
 }
