@@ -108,6 +108,17 @@ class Engine:
                 if b is not None:
                     m._buffers[k] = b.to(self.device)
         self.arena = Arena(shell, self.device, dtype, fuse_groups=groups, pad_rows=pad_rows, perms=perms, frozen=frozen)
+        # gradient-readiness hook for the overlapped all-reduce (parallel.GradReducer): after
+        # encoder layer i's backward, the weight-decay segment is final from the first element of
+        # layer i on (the arena keeps module order inside a segment; decoder / CTC head come later
+        # and are done before the encoder).
+        self.on_grad_ready = None
+        d0, d1 = self.arena.segments["decay"]
+        self._layer_decay_off = []
+        for i in range(self.nl):
+            pre = f"encoder.encoder.layers.{i}."
+            offs = [m["off"] for n, m in self.arena.meta.items() if n.startswith(pre) and d0 <= m["off"] < d1]
+            self._layer_decay_off.append(min(offs) if offs else d1)
         self.shell = shell
         self.step_count = 0
         self._pe = positional_encoding(max(512, 64), self.dD, self.device)
@@ -455,6 +466,8 @@ class Engine:
         dx = self._ln_bwd(dout, ctx["x_last"], E + "layer_norm", ctx["mf"], ctx["rf"])
         for i in reversed(range(self.nl)):
             dx = self._enc_layer_bwd(i, ctx["layers"][i], dx, B, T, ctx["klen"])
+            if self.on_grad_ready is not None:      # layers >= i (and everything after them) final
+                self.on_grad_ready(self._layer_decay_off[i])
         # pos-conv block: x0 = drop(x + gelu(conv(x) + b))
         pc = self.pc
         if ctx["p_h"] > 0:

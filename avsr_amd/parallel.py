@@ -31,38 +31,91 @@ def init_from_env(backend=None):
 
 
 class GradReducer:
-    """Bucketed averaging all-reduce of a flat fp32 gradient buffer."""
+    """Bucketed all-reduce (sum) of the flat fp32 gradient arena on a dedicated stream,
+    overlapped with the backward pass.
 
-    def __init__(self, flat_grad, bucket_bytes=BUCKET_BYTES, group=None, use_stream=True):
+    Buckets tile the weight-decay segment from its END backwards (64 MiB each), then the
+    small no-decay / frozen tail. The engine reports readiness with `ready(offset)`: the
+    decay segment is final from `offset` on (encoder layer i done => layers >= i, decoder
+    and CTC head final). Every newly complete bucket is all-reduced right away on the comm
+    stream, which first waits on an event of the compute stream; `finish()` reduces the
+    rest and makes the compute stream wait for the comm stream. `allreduce()` = begin +
+    finish (no overlap)."""
+
+    def __init__(self, flat_grad, bucket_bytes=BUCKET_BYTES, group=None, use_stream=True, segment=None):
         self.flat = flat_grad
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         n = flat_grad.numel()
         step = max(1, bucket_bytes // flat_grad.element_size())
-        self.buckets = [(s, min(n, s + step)) for s in range(0, n, step)]
+        d0, d1 = segment if segment is not None else (0, n)
+        self.seg = (d0, d1)
+        self.buckets = []                       # decay segment, last bucket first
+        e = d1
+        while e > d0:
+            s = max(d0, e - step)
+            self.buckets.append((s, e))
+            e = s
+        self.tail = [(a, min(n, a + step)) for a in range(d1, n, step)]
+        if d0 > 0:
+            self.tail = [(a, min(d0, a + step)) for a in range(0, d0, step)] + self.tail
         self.stream = torch.cuda.Stream(device=flat_grad.device) if (use_stream and flat_grad.is_cuda) else None
+        self._next = 0
+        self._works = []
+
+    def _reduce(self, a, b):
+        w = dist.all_reduce(self.flat[a:b], op=dist.ReduceOp.SUM, group=self.group, async_op=self.stream is not None)
+        if w is not None:
+            self._works.append(w)
+
+    def _launch(self, ranges):
+        if not ranges:
+            return
+        if self.stream is None:
+            for a, b in ranges:
+                self._reduce(a, b)
+            return
+        cur = torch.cuda.current_stream(self.flat.device)
+        self.stream.wait_stream(cur)             # gradients of these ranges are complete
+        with torch.cuda.stream(self.stream):
+            for a, b in ranges:
+                self._reduce(a, b)
+
+    def begin(self):
+        self._next = 0
+        self._works = []
+
+    def ready(self, offset):
+        """the decay segment is final from `offset` on: reduce every bucket inside it"""
+        if self.world == 1:
+            return
+        todo = []
+        while self._next < len(self.buckets) and self.buckets[self._next][0] >= offset:
+            todo.append(self.buckets[self._next])
+            self._next += 1
+        self._launch(todo)
+
+    def finish(self, average=False):
+        if self.world == 1:
+            return
+        self._launch(self.buckets[self._next:] + self.tail)
+        self._next = len(self.buckets)
+        if self.stream is not None:
+            with torch.cuda.stream(self.stream):
+                for w in self._works:
+                    w.wait()
+                if average:
+                    self.flat.mul_(1.0 / self.world)
+            torch.cuda.current_stream(self.flat.device).wait_stream(self.stream)
+        elif average:
+            self.flat.mul_(1.0 / self.world)
+        self._works = []
 
     def allreduce(self, average=True):
         """sum over ranks; average=False leaves the 1/world scale to the optimizer
         (FusedAdamW.step(grad_scale=1/world)) and saves a pass over the buffer."""
-        if self.world == 1:
-            return
-        if self.stream is not None:
-            cur = torch.cuda.current_stream(self.flat.device)
-            self.stream.wait_stream(cur)
-            with torch.cuda.stream(self.stream):
-                works = [dist.all_reduce(self.flat[a:b], op=dist.ReduceOp.SUM, group=self.group, async_op=True)
-                         for a, b in self.buckets]
-                for w in works:
-                    w.wait()
-                if average:
-                    self.flat.mul_(1.0 / self.world)
-            cur.wait_stream(self.stream)
-        else:
-            for a, b in self.buckets:
-                dist.all_reduce(self.flat[a:b], op=dist.ReduceOp.SUM, group=self.group)
-            if average:
-                self.flat.mul_(1.0 / self.world)
+        self.begin()
+        self.finish(average=average)
 
 
 def broadcast_state(flat_params, buffers, src=0, group=None):

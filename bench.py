@@ -128,7 +128,8 @@ def main():
     buffers = [b for b in model.buffers()]
     parallel.broadcast_state(arena.data, buffers)
     arena.sync_shadow()
-    reducer = parallel.GradReducer(arena.grad)
+    reducer = parallel.GradReducer(arena.grad, segment=arena.segments["decay"])
+    eng.on_grad_ready = reducer.ready          # all-reduce buckets as soon as their layers are done
     opt = FusedAdamW(arena, lr=1e-4, weight_decay=0.005, max_grad_norm=1.0)
 
     B, T, L = args.batch, args.seq, args.labels
@@ -140,9 +141,10 @@ def main():
 
     def step():
         arena.zero_grad()
+        reducer.begin()
         out4, ctx = eng.forward(v, a, lens, lab, train=True, need_grad=True)
         eng.backward(ctx, d_ctc, d_att)
-        reducer.allreduce(average=False)
+        reducer.finish(average=False)
         opt.step(grad_scale=1.0 / world)
         return out4
 

@@ -33,6 +33,15 @@ def _worker(rank, world, port, q):
         ok_sum = torch.equal(g, want)
         red.allreduce(average=True)                   # sum over ranks of identical buffers / world
         ok_avg = torch.allclose(g, want, rtol=1e-6)
+        # overlapped protocol: readiness watermarks over the decay segment, then finish();
+        # every element must be reduced exactly once
+        g2 = torch.arange(n, dtype=torch.float32) * (rank + 1)
+        red2 = parallel.GradReducer(g2, bucket_bytes=4 * 50000, segment=(1000, 900000))
+        red2.begin()
+        for off in (850000, 850000, 600001, 400000, 1000):
+            red2.ready(off)
+        red2.finish(average=False)
+        ok_sum = ok_sum and torch.equal(g2, want)
         params = torch.full((17,), float(rank))
         bufs = [torch.full((3,), 10.0 + rank), torch.tensor([rank], dtype=torch.int64)]
         parallel.broadcast_state(params, bufs)
