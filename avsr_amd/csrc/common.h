@@ -80,6 +80,11 @@ AVSR_DEV void split8(const float* x, bf16x8& hi, bf16x8& lo) {
   }
 }
 
+// v_mfma_f32_16x16x32_bf16: lane l holds A[row l&15][k 8(l>>4)..+7], B[k 8(l>>4)..+7][col l&15];
+// C/D: 4 registers, C[row 4(l>>4) + r][col l&15]
+AVSR_DEV f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
 AVSR_DEV f32x16 mfma32(const bf16x8& a, const bf16x8& b, const f32x16& c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }

@@ -215,7 +215,7 @@ __global__ __launch_bounds__(CF::NTH, CF::MINB) void conv_glds_kernel(ConvArgs a
   const int kbeg = sp * a.kchunk, kend = min(a.K, kbeg + a.kchunk);
   const int nk = (kend - kbeg + GBK - 1) / GBK;
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  f32x16 acc[CF::FM][CF::FN];
+  f32x4 acc[CF::TM][CF::TN];
   if constexpr (KIND == K_FWD) {
     GConvK<CF::BM, CF::NW, false> la; la.init(pa, a.g, m0, a.M, kend, wave, lane);
     gemmg::GDenseK<CF::BN, CF::NW> lb; lb.init(pb, a.K, n0, a.N, kend, wave, lane);

@@ -56,7 +56,7 @@ __global__ __launch_bounds__(CF::NTH, CF::MINB) void dense_glds_kernel(DenseArgs
   using LB = typename std::conditional<BK, gemmg::GDenseK<CF::BN, CF::NW>, gemmg::GDenseR<CF::BN, CF::NW>>::type;
   LA la; la.init((const bf16*)a.A + (int64_t)bz * a.sA, a.lda, m0, a.M, kend, wave, lane);
   LB lb; lb.init((const bf16*)a.B + (int64_t)bz * a.sB, a.ldb, n0, a.N, kend, wave, lane);
-  f32x16 acc[CF::FM][CF::FN];
+  f32x4 acc[CF::TM][CF::TN];
   gemmg::mainloop_glds<CF>(la, lb, kbeg, (kend - kbeg + gemmg::GBK - 1) / gemmg::GBK, acc, smem);
   Epi e = a.e;
   e.C = (OutT*)e.C + (int64_t)bz * a.sC + sp * a.sSplit;
@@ -82,7 +82,7 @@ __global__ __launch_bounds__(gemmpp::NTH, 1) void dense_pp_kernel(DenseArgs a, i
   using LB = typename std::conditional<BK, gemmpp::HalfK<32>, gemmpp::HalfR<32>>::type;
   LA la; la.init((const bf16*)a.A + (int64_t)bz * a.sA, a.lda, m0, a.M, kend, wave, lane);
   LB lb; lb.init((const bf16*)a.B + (int64_t)bz * a.sB, a.ldb, n0, a.N, kend, wave, lane);
-  f32x16 acc[4][2];
+  f32x4 acc[8][4];
   gemmpp::mainloop_pp(la, lb, kbeg, (kend - kbeg + gemmg::GBK - 1) / gemmg::GBK, acc, smem);
   Epi e = a.e;
   e.C = (OutT*)e.C + (int64_t)bz * a.sC + sp * a.sSplit;
@@ -132,7 +132,14 @@ int tile_cfg(const avsr_gemm_params* p, int splits) {
                    : !strcmp(e, "128x256") ? 3 : !strcmp(e, "128s3") ? 4 : !strcmp(e, "128s4") ? 5
                    : !strcmp(e, "128w8s3") ? 6 : !strcmp(e, "128w8s4") ? 7 : !strcmp(e, "pp") ? 8 : -1;
   if (forced >= 0) return forced;
-  return 0;
+  // cost ~ rounds of the grid over 256 CUs x work per CU per round / efficiency: the 128x128
+  // tile runs 2 blocks per CU (512 per round), the 256x256 ping-pong tile 1 block (4x the
+  // work) at ~1.27x the per-CU rate (measured 1262 vs 990 TFLOP/s at 8192^3)
+  const long t128 = (long)((p->M + 127) / 128) * ((p->N + 127) / 128) * p->batch * splits;
+  const long tpp = (long)((p->M + 255) / 256) * ((p->N + 255) / 256) * p->batch * splits;
+  const double c128 = (double)((t128 + 511) / 512) * 2.0;
+  const double cpp = (double)((tpp + 255) / 256) * 4.0 / 1.27;
+  return cpp < c128 ? 8 : 0;
 }
 
 template <typename OutT, bool AK, bool BK>

@@ -1,17 +1,17 @@
 // bf16 MFMA GEMM core with LDS-DMA staging (global_load_lds_dwordx4) for libavsr_hip.so.
 //
-// Block tile (64*WM) x (64*WN) x 64, 64*WM*WN threads, each wave a 64x64 sub-tile (2x2
-// v_mfma_f32_32x32x16_bf16 accumulators). Operand tiles go HBM/L2 -> LDS directly by
-// global_load_lds (no register round trip, no ds_write pass), two LDS stages: the DMA of
-// K-tile t+1 is issued right after the barrier that opens K-tile t and lands while t's 16
-// MFMAs per wave run. Two blocks per CU (64 KiB LDS each) cover each other's barrier.
+// Block tile (WM*32*FM) x (WN*32*FN) x 64 (GCfg), each wave a (32FM)x(32FN) sub-tile of
+// v_mfma_f32_16x16x32_bf16 accumulators (the 16x16x32 shape holds a higher clock than
+// 32x32x16 on random data at the same cycles per FLOP: MI355X_MICROARCH.md, DVFS item 7).
+// Operand tiles go HBM/L2 -> LDS directly by global_load_lds (no register round trip, no
+// ds_write pass) into a ring of S stages.
 //
 // LDS images are lane-linear (one wave instruction fills 1 KiB contiguously), so bank
 // spreading is done by XOR-swizzling the 16-byte chunk index on the GLOBAL side:
 //   k-major operand  [R][64] (128-B rows):  chunk' = chunk ^ ((row >> 1) & 7)
 //       -> ds_read_b128 fragments, each 16-lane group hits 16 distinct 16-B bank slots;
-//   r-contiguous     [64][R] (2R-B rows):   chunk' = chunk ^ ((k & 3) << 2)
-//       -> ds_read_b64_tr_b16 fragments, each 32-lane group covers 4 rows x 64 B = 256 B.
+//   r-contiguous     [64][R] (2R-B rows):   chunk' = chunk ^ rswz(k)
+//       -> ds_read_b64_tr_b16 fragments, each 32-lane group covers 8 rows x 32 B = 256 B.
 // Out-of-range vectors are DMA'd from a zero line (a masked lane would leave stale LDS).
 #pragma once
 #include "gemm_core.h"
@@ -30,11 +30,14 @@ AVSR_DEV void glds16(const void* src, char* lds_wave_base) {
   __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)lds_wave_base, 16, 0, 0);
 }
 
-// r-contiguous images: 16-byte chunk swizzle of k-row k (CPR chunks per row). Rows of >= 256 B
-// (CPR >= 16): shift by (k & 3) * 64 B; rows of 128 B (CPR == 8): rows k, k+1 already sit in
-// opposite bank halves, so only k & 2 shifts by 64 B. Either way one 32-lane group of a
-// ds_read_b64_tr_b16 (4 consecutive k-rows x 64 B) covers all 64 banks.
-template <int CPR> AVSR_DEV int rswz(int k) { return CPR >= 16 ? (k & 3) << 2 : ((k >> 1) & 1) << 2; }
+// r-contiguous images: 16-byte chunk swizzle of k-row k (CPR chunks per row, always an even
+// XOR so 32-byte chunk pairs stay together). One 32-lane group of a 16x16x32 fragment's
+// ds_read_b64_tr_b16 reads rows {k0 + q, k0 + 8 + q : q < 4} x 32 B (k0 % 16 == 0). Rows of
+// >= 256 B (CPR >= 16): 8 distinct 32-B windows from (k & 3, k & 8); rows of 128 B
+// (CPR == 8): k & 1 picks the bank half, (k & 2, k & 8) the 32-B window in it.
+template <int CPR> AVSR_DEV int rswz(int k) {
+  return CPR >= 16 ? ((k & 3) | (((k >> 3) & 1) << 2)) << 1 : (((k >> 1) & 1) | (((k >> 3) & 1) << 1)) << 1;
+}
 
 // ---------------------------------------------------------------- dense loaders
 // k-major operand: elem(r, k) = p[r*ld + k]
@@ -91,29 +94,30 @@ template <int R, int NW> struct GDenseR {
 };
 
 // ---------------------------------------------------------------- fragments
-// rows rb..rb+31 (row = lane&31), k = 16s + 8(lane>>5) + 0..7
+// 16x16x32 operand fragment: rows rb..rb+15 (row = lane&15), k = 32kb + 8(lane>>4) + 0..7
 template <int R, bool KMAJ>
-AVSR_DEV bf16x8 gfrag(const char* img, int rb, int s, int lane) {
+AVSR_DEV bf16x8 gfrag(const char* img, int rb, int kb, int lane) {
   if constexpr (KMAJ) {
-    const int row = rb + (lane & 31);
-    const int c = (2 * s + (lane >> 5)) ^ ((row >> 1) & 7);
+    const int row = rb + (lane & 15);
+    const int c = (4 * kb + (lane >> 4)) ^ ((row >> 1) & 7);
     return *(const bf16x8*)(img + row * 128 + c * 16);
   } else {
+    // 16-lane group g reads k-rows k0+q and k0+4+q (k0 = 32kb + 8g, q = (lane&15)>>2), 4
+    // columns each from rb + 4p; the transposing read hands lane i its column rb + i.
     const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
-    const int k0 = 16 * s + 8 * (lane >> 5);
-    const int r = rb + 16 * (g & 1) + 4 * pp;
-    const int off = (((r >> 3) ^ rswz<R / 8>(q)) << 4) + (r & 7) * 2;   // k0 % 4 == 0: swizzle of k0+q, k0+4+q = of q
-    const char* base = img + off;
-    const v4i16 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(base + (k0 + q) * (R * 2)));
-    const v4i16 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(base + (k0 + 4 + q) * (R * 2)));
+    const int k0 = 32 * kb + 8 * g;
+    const int r = rb + 4 * pp;
+    const int ka = k0 + q, kb2 = k0 + 4 + q;
+    const char* pa = img + ka * (R * 2) + (((r >> 3) ^ rswz<R / 8>(ka)) << 4) + (r & 7) * 2;
+    const char* pb = img + kb2 * (R * 2) + (((r >> 3) ^ rswz<R / 8>(kb2)) << 4) + (r & 7) * 2;
+    const v4i16 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)pa);
+    const v4i16 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)pb);
     union { v4i16 s4[2]; bf16x8 h; } u;
     u.s4[0] = a; u.s4[1] = b;
     return u.h;
   }
 }
 
-// Block tile BM x BN = (WM*32*FM) x (WN*32*FN): WM x WN waves, each owning FM x FN
-// accumulators of 32x32 (fp32, 16 registers each).
 // S LDS stages: S-1 K-tiles in flight (the DMA of tile t+S-1 is issued at the top of t).
 template <int WM_, int WN_, int FM_, int FN_, int S_ = 2> struct GCfg {
   static constexpr int WM = WM_, WN = WN_, FM = FM_, FN = FN_, S = S_;
@@ -123,6 +127,7 @@ template <int WM_, int WN_, int FM_, int FN_, int S_ = 2> struct GCfg {
   static constexpr int EP_BYTES = WM * 32 * (BN + 4) * 4;       // one 32-row strip per wave row
   static constexpr int LDS_BYTES = S * STAGE > EP_BYTES ? S * STAGE : EP_BYTES;
   static constexpr int MINB = LDS_BYTES <= 80 * 1024 ? 2 : 1;    // blocks per CU the LDS allows
+  static constexpr int TM = 2 * FM, TN = 2 * FN;                 // 16x16 accumulator tiles per wave
 };
 
 template <int N> AVSR_DEV void wait_vmcnt() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
@@ -135,18 +140,18 @@ template <int N> AVSR_DEV void wait_vmcnt() { asm volatile("s_waitcnt vmcnt(%0)"
 // fragments are in flight behind tile t's last MFMAs.
 template <class CF, bool AK, bool BK>
 struct Frags {
-  bf16x8 a[CF::FM], b[CF::FN];
-  AVSR_DEV void load(const char* stage, int s, int wm, int wn, int lane) {
+  bf16x8 a[CF::TM], b[CF::TN];
+  AVSR_DEV void load(const char* stage, int kb, int wm, int wn, int lane) {
 #pragma unroll
-    for (int i = 0; i < CF::FM; ++i) a[i] = gfrag<CF::BM, AK>(stage, (wm * CF::FM + i) * 32, s, lane);
+    for (int i = 0; i < CF::TM; ++i) a[i] = gfrag<CF::BM, AK>(stage, (wm * CF::TM + i) * 16, kb, lane);
 #pragma unroll
-    for (int j = 0; j < CF::FN; ++j) b[j] = gfrag<CF::BN, BK>(stage + CF::SA, (wn * CF::FN + j) * 32, s, lane);
+    for (int j = 0; j < CF::TN; ++j) b[j] = gfrag<CF::BN, BK>(stage + CF::SA, (wn * CF::TN + j) * 16, kb, lane);
   }
-  AVSR_DEV void mma(f32x16 (&acc)[CF::FM][CF::FN]) const {
+  AVSR_DEV void mma(f32x4 (&acc)[CF::TM][CF::TN]) const {
 #pragma unroll
-    for (int i = 0; i < CF::FM; ++i)
+    for (int i = 0; i < CF::TM; ++i)
 #pragma unroll
-      for (int j = 0; j < CF::FN; ++j) acc[i][j] = mfma32(a[i], b[j], acc[i][j]);
+      for (int j = 0; j < CF::TN; ++j) acc[i][j] = mfma16(a[i], b[j], acc[i][j]);
   }
 };
 
@@ -157,17 +162,15 @@ AVSR_DEV void wait_tiles_ahead(bool full) {   // tile t+1 retired: at most tiles
 }
 
 template <class CF, class LA, class LB>
-AVSR_DEV void mainloop_glds(const LA& la, const LB& lb, int kbeg, int nk, f32x16 (&acc)[CF::FM][CF::FN], char* smem) {
-  constexpr int S = CF::S, KS = GBK / 16;
+AVSR_DEV void mainloop_glds(const LA& la, const LB& lb, int kbeg, int nk, f32x4 (&acc)[CF::TM][CF::TN], char* smem) {
+  constexpr int S = CF::S, KS = GBK / 32;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave / CF::WN, wn = wave % CF::WN;
 #pragma unroll
-  for (int i = 0; i < CF::FM; ++i)
+  for (int i = 0; i < CF::TM; ++i)
 #pragma unroll
-    for (int j = 0; j < CF::FN; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    for (int j = 0; j < CF::TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   if (nk <= 0) return;
 #pragma unroll
   for (int p = 0; p < S; ++p)        // fill every stage: tiles 0..S-1
@@ -210,10 +213,12 @@ AVSR_DEV void mainloop_glds(const LA& la, const LB& lb, int kbeg, int nk, f32x16
 }
 
 // Epilogue for a GCfg tile: (1) optional BN column statistics from the accumulators;
-// (2) FM passes, each staging one 32-row strip per wave row through LDS and writing it
-// row-major, 4 consecutive columns per thread (coalesced stores, vector residual reads).
+// (2) FM passes, each staging one 32-row strip per wave row (accumulator tiles 2i, 2i+1)
+// through LDS and writing it row-major, 4 consecutive columns per thread (coalesced stores,
+// vector residual reads). Accumulator tile (ti, tj) register r sits at wave-local row
+// 16ti + 4(lane>>4) + r, column 16tj + (lane&15).
 template <typename T, typename OutT, class CF>
-AVSR_DEV void epilogue_g(const Epi& e, int m0, int n0, f32x16 (&acc)[CF::FM][CF::FN], char* smem) {
+AVSR_DEV void epilogue_g(const Epi& e, int m0, int n0, f32x4 (&acc)[CF::TM][CF::TN], char* smem) {
   constexpr int BN = CF::BN, LDR = BN + 4, SR = CF::WM * 32;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / CF::WN, wn = wave % CF::WN;
@@ -222,32 +227,32 @@ AVSR_DEV void epilogue_g(const Epi& e, int m0, int n0, f32x16 (&acc)[CF::FM][CF:
     __syncthreads();
     float* red = st;  // [WM][BN][3]
 #pragma unroll
-    for (int j = 0; j < CF::FN; ++j) {
+    for (int j = 0; j < CF::TN; ++j) {
       float s = 0.f, c = 0.f;
 #pragma unroll
-      for (int i = 0; i < CF::FM; ++i)
+      for (int i = 0; i < CF::TM; ++i)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int row = (wm * CF::FM + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        for (int r = 0; r < 4; ++r) {
+          const int row = wm * 32 * CF::FM + i * 16 + 4 * (lane >> 4) + r;
           const bool ok = m0 + row < e.M;
           s += ok ? e.alpha * acc[i][j][r] : 0.f;
           c += ok ? 1.f : 0.f;
         }
-      s += __shfl_xor(s, 32, 64);
-      c += __shfl_xor(c, 32, 64);
+      s += __shfl_xor(s, 16, 64); s += __shfl_xor(s, 32, 64);
+      c += __shfl_xor(c, 16, 64); c += __shfl_xor(c, 32, 64);
       const float mean = c > 0.f ? s / c : 0.f;
       float m2 = 0.f;
 #pragma unroll
-      for (int i = 0; i < CF::FM; ++i)
+      for (int i = 0; i < CF::TM; ++i)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int row = (wm * CF::FM + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        for (int r = 0; r < 4; ++r) {
+          const int row = wm * 32 * CF::FM + i * 16 + 4 * (lane >> 4) + r;
           const float d = e.alpha * acc[i][j][r] - mean;
           m2 += m0 + row < e.M ? d * d : 0.f;
         }
-      m2 += __shfl_xor(m2, 32, 64);
-      if (lane < 32) {
-        const int lc = (wn * CF::FN + j) * 32 + lane;
+      m2 += __shfl_xor(m2, 16, 64); m2 += __shfl_xor(m2, 32, 64);
+      if (lane < 16) {
+        const int lc = (wn * CF::TN + j) * 16 + lane;
         red[(wm * BN + lc) * 3 + 0] = c;
         red[(wm * BN + lc) * 3 + 1] = mean;
         red[(wm * BN + lc) * 3 + 2] = m2;
@@ -276,12 +281,14 @@ AVSR_DEV void epilogue_g(const Epi& e, int m0, int n0, f32x16 (&acc)[CF::FM][CF:
   for (int i = 0; i < CF::FM; ++i) {
     __syncthreads();
 #pragma unroll
-    for (int j = 0; j < CF::FN; ++j)
+    for (int h = 0; h < 2; ++h)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int lr = wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        st[lr * LDR + (wn * CF::FN + j) * 32 + (lane & 31)] = acc[i][j][r];
-      }
+      for (int j = 0; j < CF::TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int lr = wm * 32 + h * 16 + 4 * (lane >> 4) + r;
+          st[lr * LDR + (wn * CF::TN + j) * 16 + (lane & 15)] = acc[2 * i + h][j][r];
+        }
     __syncthreads();
     for (int c = tid; c < SR * BN / 4; c += CF::NTH) {
       const int lr = c / (BN / 4), lc = (c % (BN / 4)) * 4;

@@ -1,8 +1,8 @@
 // 256x256 bf16 MFMA GEMM core with two wave groups in ping-pong (gfx950).
 //
-// Block = 8 waves as 2 (rows) x 4 (cols), each wave a 128x64 output (4x2 accumulators of
-// v_mfma_f32_32x32x16_bf16, 128 VGPRs). A K-tile (64) is processed in 4 phases, one per
-// 64x32 quadrant of the wave's output (8 MFMAs each); every phase is
+// Block = 8 waves as 2 (rows) x 4 (cols), each wave a 128x64 output (8x4 accumulators of
+// v_mfma_f32_16x16x32_bf16, 128 VGPRs). A K-tile (64) is processed in 4 phases, one per
+// 64x32 quadrant of the wave's output (16 MFMAs each); every phase is
 //     [LDS fragment reads | one half-tile DMA | counted vmcnt]  s_barrier
 //     [lgkmcnt(0), setprio 1, 8 MFMAs, setprio 0]              s_barrier
 // and wave row 1 runs one barrier behind wave row 0, so on every SIMD (one wave of each
@@ -101,16 +101,14 @@ AVSR_DEV void bar() {
 }
 
 template <class LA, class LB>
-AVSR_DEV void mainloop_pp(const LA& la, const LB& lb, int kbeg, int nk, f32x16 (&acc)[4][2], char* smem) {
+AVSR_DEV void mainloop_pp(const LA& la, const LB& lb, int kbeg, int nk, f32x4 (&acc)[8][4], char* smem) {
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wr = wave >> 2, wc = wave & 3;
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < 8; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   // part: 0 = A0, 1 = A1, 2 = B0, 3 = B1
   auto dma = [&](int t, int part) {
     char* img = smem + (t & 1) * STAGE + part * HALF;
@@ -123,7 +121,7 @@ AVSR_DEV void mainloop_pp(const LA& la, const LB& lb, int kbeg, int nk, f32x16 (
   gemmg::wait_vmcnt<4>();                  // A0(0), B0(0) retired
   bar();
   if (wr == 1) bar();                      // wave row 1 runs one barrier behind
-  bf16x8 af[2][4], bfr[4];
+  bf16x8 af[4][2], bfr[2][2];               // [row|col tile][kb]
   for (int u = 0; u < nk; ++u) {
     const char* st = smem + (u & 1) * STAGE;
 #pragma unroll
@@ -132,13 +130,17 @@ AVSR_DEV void mainloop_pp(const LA& la, const LB& lb, int kbeg, int nk, f32x16 (
       // ---- reads + DMA + counted wait
       if (p == 0 || p == 2) {
 #pragma unroll
-        for (int ii = 0; ii < 2; ++ii)
+        for (int ii = 0; ii < 4; ++ii)
 #pragma unroll
-          for (int s = 0; s < 4; ++s) af[ii][s] = gemmg::gfrag<128, LA::KMAJ>(st + mh * HALF, wr * 64 + ii * 32, s, lane);
+          for (int kb = 0; kb < 2; ++kb)
+            af[ii][kb] = gemmg::gfrag<128, LA::KMAJ>(st + mh * HALF, wr * 64 + ii * 16, kb, lane);
       }
       if (p != 2) {                        // (m1,n1) reuses the B1 fragments of (m0,n1)
 #pragma unroll
-        for (int s = 0; s < 4; ++s) bfr[s] = gemmg::gfrag<128, LB::KMAJ>(st + (2 + nh) * HALF, wc * 32, s, lane);
+        for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+          for (int kb = 0; kb < 2; ++kb)
+            bfr[jj][kb] = gemmg::gfrag<128, LB::KMAJ>(st + (2 + nh) * HALF, wc * 32 + jj * 16, kb, lane);
       }
       __builtin_amdgcn_sched_barrier(0);
       if (p == 0) dma(u + 1, 1);
@@ -152,9 +154,12 @@ AVSR_DEV void mainloop_pp(const LA& la, const LB& lb, int kbeg, int nk, f32x16 (
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-      for (int s = 0; s < 4; ++s)
+      for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-        for (int ii = 0; ii < 2; ++ii) acc[2 * mh + ii][nh] = mfma32(af[ii][s], bfr[s], acc[2 * mh + ii][nh]);
+        for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+          for (int jj = 0; jj < 2; ++jj)
+            acc[4 * mh + ii][2 * nh + jj] = mfma16(af[ii][kb], bfr[jj][kb], acc[4 * mh + ii][2 * nh + jj]);
       __builtin_amdgcn_s_setprio(0);
       bar();
     }
