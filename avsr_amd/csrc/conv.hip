@@ -34,6 +34,7 @@ static int make_geom(const avsr_conv_params* p, ConvGeom& g) {
 
 struct ConvArgs {
   ConvGeom g;
+  uint32_t a_bytes, b_bytes;      // per-group operand extents for the buffer-DMA loaders (0: pointer loaders)
   const void* a; const void* b;   // operand bases (group 0)
   int64_t a_gstride, b_gstride, c_gstride;
   int M, N, K, splits, kchunk;
@@ -195,6 +196,146 @@ template <int R, int NW> struct GConvR {
   }
 };
 
+// ---------------------------------------------------------------- buffer-DMA conv loaders
+// Tap-uniform K-tiles: with cin (forward) / cout (data-grad) a multiple of 64, one K-tile of
+// 64 lies inside one (kh, kw) tap, so the tap decomposition is wave-uniform (scalar) and a
+// lane's work per DMA piece is its bounds check and one add (see gemm_glds.h BDenseK).
+using gemmg::OOB;
+using gemmg::bglds16;
+using gemmg::make_rsrc;
+
+// forward A: r = output pixel, gather x
+template <int R, int NW> struct BConvK {
+  static constexpr bool KMAJ = true;
+  static constexpr int SLOTS = R / 8 / NW;
+  __amdgpu_buffer_rsrc_t rs; ConvGeom g;
+  int ih0[SLOTS], iw0[SLOTS], ro[SLOTS];
+  AVSR_DEV void init(const bf16* base, uint32_t bytes, const ConvGeom& g_, int r0, int rext, int wave, int lane) {
+    rs = make_rsrc(base, bytes); g = g_;
+#pragma unroll
+    for (int i = 0; i < SLOTS; ++i) {
+      const int pc = i * NW + wave, pr = pc * 8 + (lane >> 3);
+      const int kc = ((lane & 7) ^ ((pr >> 1) & 7)) * 8;
+      const int r = r0 + pr;
+      if (r >= rext) { ih0[i] = -1000000; iw0[i] = 0; ro[i] = 0; continue; }
+      const uint32_t n = fdiv(r, g.f_hw_out), rem = r - n * g.f_hw_out.d;
+      const uint32_t oh = fdiv(rem, g.f_w_out), ow = rem - oh * g.f_w_out.d;
+      ih0[i] = oh * g.sh - g.ph; iw0[i] = ow * g.sw - g.pw;
+      ro[i] = (int)((((int64_t)n * g.hin * g.win + (int64_t)ih0[i] * g.win + iw0[i]) * g.ldx + kc) * 2);
+    }
+  }
+  AVSR_DEV void issue(char* img, int k0, int wave) const {
+    const int khw = k0 >> g.cin_shift, cb = k0 & ((1 << g.cin_shift) - 1);
+    const int kh = (int)fdiv(khw, g.f_kw), kw = khw - kh * (int)g.f_kw.d;
+    const int tap = (int)(((int64_t)(kh * g.win + kw) * g.ldx + cb) * 2);
+#pragma unroll
+    for (int i = 0; i < SLOTS; ++i) {
+      const bool ok = (unsigned)(ih0[i] + kh) < (unsigned)g.hin && (unsigned)(iw0[i] + kw) < (unsigned)g.win;
+      bglds16(rs, ok ? (uint32_t)(ro[i] + tap) : OOB, 0u, img + (i * NW + wave) * 1024);
+    }
+  }
+};
+
+// data-grad A: r = input pixel, gather dy at ((h+ph-kh)/sh, (w+pw-kw)/sw); strides 1 or 2
+template <int R, int NW> struct BConvKT {
+  static constexpr bool KMAJ = true;
+  static constexpr int SLOTS = R / 8 / NW;
+  __amdgpu_buffer_rsrc_t rs; ConvGeom g;
+  int th0[SLOTS], tw0[SLOTS], ro[SLOTS];
+  AVSR_DEV void init(const bf16* base, uint32_t bytes, const ConvGeom& g_, int r0, int rext, int wave, int lane) {
+    rs = make_rsrc(base, bytes); g = g_;
+#pragma unroll
+    for (int i = 0; i < SLOTS; ++i) {
+      const int pc = i * NW + wave, pr = pc * 8 + (lane >> 3);
+      const int kc = ((lane & 7) ^ ((pr >> 1) & 7)) * 8;
+      const int r = r0 + pr;
+      if (r >= rext) { th0[i] = -1000000; tw0[i] = 0; ro[i] = 0; continue; }
+      const uint32_t n = fdiv(r, g.f_hw_in), rem = r - n * g.f_hw_in.d;
+      const uint32_t h = fdiv(rem, g.f_w_in), w = rem - h * g.f_w_in.d;
+      th0[i] = h + g.ph; tw0[i] = w + g.pw;
+      ro[i] = (int)(((int64_t)n * g.hout * g.wout * g.ldy + kc) * 2);
+    }
+  }
+  AVSR_DEV void issue(char* img, int k0, int wave) const {
+    const int khw = k0 >> g.cout_shift, cb = k0 & ((1 << g.cout_shift) - 1);
+    const int kh = (int)fdiv(khw, g.f_kw), kw = khw - kh * (int)g.f_kw.d;
+    const int ldy2 = (int)g.ldy * 2, cb2 = cb * 2;
+#pragma unroll
+    for (int i = 0; i < SLOTS; ++i) {
+      const int th = th0[i] - kh, tw = tw0[i] - kw;
+      bool ok;
+      int pix;
+      if (g.sh == 1) {
+        ok = (unsigned)th < (unsigned)g.hout && (unsigned)tw < (unsigned)g.wout;
+        pix = th * g.wout + tw;
+      } else {
+        ok = ((th | tw) & 1) == 0 && (unsigned)(th >> 1) < (unsigned)g.hout && (unsigned)(tw >> 1) < (unsigned)g.wout;
+        pix = (th >> 1) * g.wout + (tw >> 1);
+      }
+      bglds16(rs, ok ? (uint32_t)(ro[i] + pix * ldy2 + cb2) : OOB, 0u, img + (i * NW + wave) * 1024);
+    }
+  }
+};
+
+// data-grad B: weight [cout][kh][kw][cin] as (r = cin, k = (kh, kw, cout)), r-contiguous
+template <int R, int NW> struct BWgtR {
+  static constexpr bool KMAJ = false;
+  static constexpr int CPR = R / 8, RPP = 64 / CPR, SLOTS = GBK / RPP / NW;
+  __amdgpu_buffer_rsrc_t rs; ConvGeom g;
+  uint32_t vo[SLOTS];
+  AVSR_DEV void init(const bf16* base, uint32_t bytes, const ConvGeom& g_, int r0, int rext, int wave, int lane) {
+    rs = make_rsrc(base, bytes); g = g_;
+    const int ktot = g.kh * g.kw * g.cin;
+#pragma unroll
+    for (int i = 0; i < SLOTS; ++i) {
+      const int pc = i * NW + wave, pk = pc * RPP + lane / CPR;
+      const int r = r0 + ((lane % CPR) ^ gemmg::rswz<CPR>(pk)) * 8;
+      vo[i] = r < rext ? (uint32_t)(((int64_t)pk * ktot + r) * 2) : OOB;
+    }
+  }
+  AVSR_DEV void issue(char* img, int k0, int wave) const {
+    const int ktot = g.kh * g.kw * g.cin;
+    const uint32_t so = (uint32_t)((((int64_t)(k0 & ((1 << g.cout_shift) - 1))) * ktot + (int64_t)(k0 >> g.cout_shift) * g.cin) * 2);
+#pragma unroll
+    for (int i = 0; i < SLOTS; ++i) bglds16(rs, vo[i], so, img + (i * NW + wave) * 1024);
+  }
+};
+
+// weight-grad B: r = (kh, kw, cin) (vectors along cin), k = output pixel; r-contiguous
+template <int R, int NW> struct BConvR {
+  static constexpr bool KMAJ = false;
+  static constexpr int CPR = R / 8, RPP = 64 / CPR, SLOTS = GBK / RPP / NW;
+  __amdgpu_buffer_rsrc_t rs; ConvGeom g; int kend;
+  int kr[SLOTS], rk[SLOTS], rw[SLOTS], rc[SLOTS];
+  AVSR_DEV void init(const bf16* base, uint32_t bytes, const ConvGeom& g_, int r0, int rext, int kend_, int wave, int lane) {
+    rs = make_rsrc(base, bytes); g = g_; kend = kend_;
+#pragma unroll
+    for (int i = 0; i < SLOTS; ++i) {
+      const int pc = i * NW + wave, pk = pc * RPP + lane / CPR;
+      const int r = r0 + ((lane % CPR) ^ gemmg::rswz<CPR>(pk)) * 8;
+      kr[i] = pk;
+      if (r >= rext) { rk[i] = -1000000; rw[i] = 0; rc[i] = 0; continue; }
+      const int c = r & ((1 << g.cin_shift) - 1), khw = r >> g.cin_shift;
+      const int kh = fdiv(khw, g.f_kw);
+      rk[i] = kh - g.ph; rw[i] = khw - kh * g.f_kw.d - g.pw; rc[i] = c * 2;
+    }
+  }
+  AVSR_DEV void issue(char* img, int k0, int wave) const {
+    const int ldx2 = (int)g.ldx * 2;
+#pragma unroll
+    for (int i = 0; i < SLOTS; ++i) {
+      const int k = k0 + kr[i];
+      const uint32_t kk = k < kend ? k : 0;
+      const uint32_t n = fdiv(kk, g.f_hw_out), rem = kk - n * g.f_hw_out.d;
+      const uint32_t oh = fdiv(rem, g.f_w_out), ow = rem - oh * g.f_w_out.d;
+      const int ih = (int)oh * g.sh + rk[i], iw = (int)ow * g.sw + rw[i];
+      const bool ok = k < kend && (unsigned)ih < (unsigned)g.hin && (unsigned)iw < (unsigned)g.win;
+      const uint32_t v = (uint32_t)(((int)n * g.hin * g.win + ih * g.win + iw) * ldx2 + rc[i]);
+      bglds16(rs, ok ? v : OOB, 0u, img + (i * NW + wave) * 1024);
+    }
+  }
+};
+
 // dense wrappers with the conv loaders' init signature
 template <int R, int NW> struct GDenseKc : gemmg::GDenseK<R, NW> {
   AVSR_DEV void init(const bf16* base, int64_t ld, const ConvGeom&, int r0, int rext, int kend, int wave, int lane) {
@@ -216,7 +357,21 @@ __global__ __launch_bounds__(CF::NTH, CF::MINB) void conv_glds_kernel(ConvArgs a
   const int nk = (kend - kbeg + GBK - 1) / GBK;
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   f32x4 acc[CF::TM][CF::TN];
-  if constexpr (KIND == K_FWD) {
+  if (a.a_bytes) {                // buffer-DMA loaders (tap-uniform K-tiles, extents < 2 GiB)
+    if constexpr (KIND == K_FWD) {
+      BConvK<CF::BM, CF::NW> la; la.init(pa, a.a_bytes, a.g, m0, a.M, wave, lane);
+      gemmg::BDenseK<CF::BN, CF::NW> lb; lb.init(pb, a.b_bytes, a.K, n0, a.N, kend, wave, lane);
+      gemmg::mainloop_glds<CF>(la, lb, kbeg, nk, acc, smem);
+    } else if constexpr (KIND == K_DGRAD) {
+      BConvKT<CF::BM, CF::NW> la; la.init(pa, a.a_bytes, a.g, m0, a.M, wave, lane);
+      BWgtR<CF::BN, CF::NW> lb; lb.init(pb, a.b_bytes, a.g, n0, a.N, wave, lane);
+      gemmg::mainloop_glds<CF>(la, lb, kbeg, nk, acc, smem);
+    } else {
+      gemmg::BDenseR<CF::BM, CF::NW> la; la.init(pa, a.a_bytes, a.g.ldy, m0, a.M, kend, wave, lane);
+      BConvR<CF::BN, CF::NW> lb; lb.init(pb, a.b_bytes, a.g, n0, a.N, kend, wave, lane);
+      gemmg::mainloop_glds<CF>(la, lb, kbeg, nk, acc, smem);
+    }
+  } else if constexpr (KIND == K_FWD) {
     GConvK<CF::BM, CF::NW, false> la; la.init(pa, a.g, m0, a.M, kend, wave, lane);
     gemmg::GDenseK<CF::BN, CF::NW> lb; lb.init(pb, a.K, n0, a.N, kend, wave, lane);
     gemmg::mainloop_glds<CF>(la, lb, kbeg, nk, acc, smem);
@@ -286,6 +441,16 @@ int by_tile(const ConvArgs& a, int groups, hipStream_t st) {
 
 static int tile_bm(int M, int N) { return N <= 64 ? 256 : (M <= 64 ? 64 : 128); }
 
+// extents (elements, one group) of the A / B operands -> buffer-DMA loaders when allowed
+static void set_extents(ConvArgs& a, const avsr_conv_params* p, bool tap_uniform, int64_t ea, int64_t eb) {
+  const int64_t lim = ((int64_t)gemmg::OOB - (1 << 20)) / 2;
+  const char* env = getenv("AVSR_CONV_NOBUF");
+  const bool ok = p->dtype == AVSR_BF16 && tap_uniform && ea > 0 && eb > 0 && ea < lim && eb < lim &&
+                  !(env && env[0] == '1');
+  a.a_bytes = ok ? (uint32_t)(ea * 2) : 0u;
+  a.b_bytes = ok ? (uint32_t)(eb * 2) : 0u;
+}
+
 static void base_epi(Epi& e) {
   e.alpha = 1.f; e.beta = 0.f; e.bias = nullptr; e.act = 0; e.bwd = 0; e.atomic = 0;
   e.preact = nullptr; e.res = nullptr; e.ldr = 0; e.gate = nullptr; e.drop_p = 0.f; e.seed = 0;
@@ -311,6 +476,8 @@ extern "C" int avsr_conv_fwd(const avsr_conv_params* p, void* stream) {
   a.a_gstride = p->cin; a.b_gstride = (int64_t)p->cout * p->kh * p->kw * p->cin; a.c_gstride = p->cout;
   a.M = p->nimg * p->hout * p->wout; a.N = p->cout; a.K = p->kh * p->kw * p->cin;
   a.splits = 1; a.kchunk = a.K;
+  set_extents(a, p, (p->cin % 64) == 0,
+              ((int64_t)p->nimg * p->hin * p->win - 1) * p->ldx + p->cin, (int64_t)p->cout * a.K);
   base_epi(a.e);
   a.e.M = a.M; a.e.N = a.N; a.e.C = p->y; a.e.ldc = p->ldy; a.e.stats = p->stats;
   a.e.stats_tiles = avsr_conv_stat_tiles(p);
@@ -334,6 +501,8 @@ extern "C" int avsr_conv_bwd_data(const avsr_conv_params* p, void* stream) {
   a.a_gstride = p->cout; a.b_gstride = (int64_t)p->cout * p->kh * p->kw * p->cin; a.c_gstride = p->cin;
   a.M = p->nimg * p->hin * p->win; a.N = p->cin; a.K = p->kh * p->kw * p->cout;
   a.splits = 1; a.kchunk = a.K;
+  set_extents(a, p, (p->cout % 64) == 0 && (p->sh == 1 || p->sh == 2) && p->sw == p->sh,
+              ((int64_t)p->nimg * p->hout * p->wout - 1) * p->ldy + p->cout, (int64_t)p->cout * a.K);
   base_epi(a.e);
   a.e.M = a.M; a.e.N = a.N; a.e.C = p->dx; a.e.ldc = p->ldx; a.e.alpha = p->alpha; a.e.beta = p->beta;
   if (a.M == 0) return 0;
@@ -356,6 +525,8 @@ extern "C" int avsr_conv_bwd_weight(const avsr_conv_params* p, void* stream) {
   a.a_gstride = p->cout; a.b_gstride = p->cin; a.c_gstride = p->cout * ktot;
   a.M = p->cout; a.N = (int)ktot; a.K = p->nimg * p->hout * p->wout;
   if (a.K == 0) return 0;
+  set_extents(a, p, true, ((int64_t)p->nimg * p->hout * p->wout - 1) * p->ldy + p->cout,
+              ((int64_t)p->nimg * p->hin * p->win - 1) * p->ldx + p->cin);
   int splits = p->splitk;
   if (splits <= 0) {
     const int bm = tile_bm(a.M, a.N), bn = a.N <= 64 ? 64 : (a.M <= 64 ? 256 : 128);

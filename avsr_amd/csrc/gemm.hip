@@ -12,6 +12,7 @@ namespace {
 
 struct DenseArgs {
   int M, N, K, splits, kchunk;
+  uint32_t a_bytes, b_bytes;   // buffer extents of one batch's A / B (buffer-DMA loaders); 0 = pointer loaders
   int64_t sSplit;      // slab mode: C offset between K splits (0: atomics / no split)
   const void* A; int64_t lda, sA;
   const void* B; int64_t ldb, sB;
@@ -52,12 +53,21 @@ __global__ __launch_bounds__(CF::NTH, CF::MINB) void dense_glds_kernel(DenseArgs
   const int m0 = tm * CF::BM, n0 = tn * CF::BN;
   const int kbeg = sp * a.kchunk, kend = min(a.K, kbeg + a.kchunk);
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  using LA = typename std::conditional<AK, gemmg::GDenseK<CF::BM, CF::NW>, gemmg::GDenseR<CF::BM, CF::NW>>::type;
-  using LB = typename std::conditional<BK, gemmg::GDenseK<CF::BN, CF::NW>, gemmg::GDenseR<CF::BN, CF::NW>>::type;
-  LA la; la.init((const bf16*)a.A + (int64_t)bz * a.sA, a.lda, m0, a.M, kend, wave, lane);
-  LB lb; lb.init((const bf16*)a.B + (int64_t)bz * a.sB, a.ldb, n0, a.N, kend, wave, lane);
   f32x4 acc[CF::TM][CF::TN];
-  gemmg::mainloop_glds<CF>(la, lb, kbeg, (kend - kbeg + gemmg::GBK - 1) / gemmg::GBK, acc, smem);
+  const int nk = (kend - kbeg + gemmg::GBK - 1) / gemmg::GBK;
+  if (a.a_bytes) {   // buffer-DMA loaders (operands < 2 GiB)
+    using LA = typename std::conditional<AK, gemmg::BDenseK<CF::BM, CF::NW>, gemmg::BDenseR<CF::BM, CF::NW>>::type;
+    using LB = typename std::conditional<BK, gemmg::BDenseK<CF::BN, CF::NW>, gemmg::BDenseR<CF::BN, CF::NW>>::type;
+    LA la; la.init((const bf16*)a.A + (int64_t)bz * a.sA, a.a_bytes, a.lda, m0, a.M, kend, wave, lane);
+    LB lb; lb.init((const bf16*)a.B + (int64_t)bz * a.sB, a.b_bytes, a.ldb, n0, a.N, kend, wave, lane);
+    gemmg::mainloop_glds<CF>(la, lb, kbeg, nk, acc, smem);
+  } else {
+    using LA = typename std::conditional<AK, gemmg::GDenseK<CF::BM, CF::NW>, gemmg::GDenseR<CF::BM, CF::NW>>::type;
+    using LB = typename std::conditional<BK, gemmg::GDenseK<CF::BN, CF::NW>, gemmg::GDenseR<CF::BN, CF::NW>>::type;
+    LA la; la.init((const bf16*)a.A + (int64_t)bz * a.sA, a.lda, m0, a.M, kend, wave, lane);
+    LB lb; lb.init((const bf16*)a.B + (int64_t)bz * a.sB, a.ldb, n0, a.N, kend, wave, lane);
+    gemmg::mainloop_glds<CF>(la, lb, kbeg, nk, acc, smem);
+  }
   Epi e = a.e;
   e.C = (OutT*)e.C + (int64_t)bz * a.sC + sp * a.sSplit;
   if (e.res) e.res = (const bf16*)e.res + (int64_t)bz * a.sR;
@@ -217,6 +227,11 @@ __global__ __launch_bounds__(256) void slab_reduce_kernel(const float* ws, int s
   }
 }
 
+bool getenv_flag(const char* name) {
+  const char* e = getenv(name);
+  return e && e[0] == '1';
+}
+
 // AVSR_GEMM_NOGLDS=1 forces the register-staged core (A/B comparisons, debugging)
 bool getenv_flag_noglds() {
   static int v = -1;
@@ -248,6 +263,15 @@ extern "C" int avsr_gemm(const avsr_gemm_params* p, void* stream) {
   const int kq = glds ? gemmg::GBK : BKE;
   a.kchunk = ((p->K + splits - 1) / splits + kq - 1) / kq * kq;
   a.A = p->A; a.lda = p->lda; a.sA = p->strideA;
+  {   // operand extents in bytes (last element touched + 1) for the buffer-DMA loaders
+    const int esz = p->dtype == AVSR_BF16 ? 2 : 4;
+    const int64_t ea = (p->a_kmajor ? ((int64_t)(p->M - 1) * p->lda + p->K) : ((int64_t)(p->K - 1) * p->lda + p->M)) * esz;
+    const int64_t eb = (p->b_kmajor ? ((int64_t)(p->N - 1) * p->ldb + p->K) : ((int64_t)(p->K - 1) * p->ldb + p->N)) * esz;
+    const int64_t lim = (int64_t)gemmg::OOB - (1 << 20);
+    const bool ok = ea > 0 && eb > 0 && ea < lim && eb < lim && !getenv_flag("AVSR_GEMM_NOBUF");
+    a.a_bytes = ok ? (uint32_t)ea : 0u;
+    a.b_bytes = ok ? (uint32_t)eb : 0u;
+  }
   a.B = p->B; a.ldb = p->ldb; a.sB = p->strideB;
   a.sC = p->strideC; a.sR = p->strideR;
   Epi& e = a.e;

@@ -93,6 +93,80 @@ template <int R, int NW> struct GDenseR {
   }
 };
 
+// ---------------------------------------------------------------- buffer-DMA loaders
+// Same images, but the DMA is buffer_load_dwordx4 ... lds on a buffer resource (base and
+// byte extent in SGPRs): the per-lane part of the address is a 32-bit byte offset fixed at
+// init, the per-K-tile advance is a scalar offset, and a lane with nothing valid to load
+// gets offset OOB (>= the extent: the hardware returns zeros) instead of a 64-bit pointer
+// select. This keeps the DMA issue path at a few VALU per piece (the pointer loaders cost
+// ~20 VALU per piece, which made the convolutions VALU-bound). Extents must be < 2 GiB.
+constexpr uint32_t OOB = 0x80000000u;
+
+AVSR_DEV __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+AVSR_DEV void bglds16(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff, char* lds_wave_base) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void_t*)lds_wave_base, 16, voff, soff, 0, 0);
+}
+
+// k-major: elem(r, k) = base[r*ld + k]
+template <int R, int NW> struct BDenseK {
+  static constexpr bool KMAJ = true;
+  static constexpr int SLOTS = R / 8 / NW;
+  __amdgpu_buffer_rsrc_t rs;
+  uint32_t vo[SLOTS];
+  int kc[SLOTS];
+  int kend;
+  AVSR_DEV void init(const bf16* base, uint32_t bytes, int64_t ld, int r0, int rext, int kend_, int wave, int lane) {
+    rs = make_rsrc(base, bytes);
+    kend = kend_;
+#pragma unroll
+    for (int i = 0; i < SLOTS; ++i) {
+      const int pc = i * NW + wave, pr = pc * 8 + (lane >> 3);
+      const int c = (lane & 7) ^ ((pr >> 1) & 7);
+      kc[i] = c * 8;
+      vo[i] = r0 + pr < rext ? (uint32_t)(((int64_t)(r0 + pr) * ld + c * 8) * 2) : OOB;
+    }
+  }
+  AVSR_DEV void issue(char* img, int k0, int wave) const {
+    const bool full = k0 + GBK <= kend;        // wave-uniform: only a ragged last tile masks lanes
+#pragma unroll
+    for (int i = 0; i < SLOTS; ++i) {
+      const uint32_t v = (full || k0 + kc[i] < kend) ? vo[i] : OOB;
+      bglds16(rs, v, (uint32_t)k0 * 2u, img + (i * NW + wave) * 1024);
+    }
+  }
+};
+
+// r-contiguous: elem(r, k) = base[k*ld + r]   (r extent a multiple of 8)
+template <int R, int NW> struct BDenseR {
+  static constexpr bool KMAJ = false;
+  static constexpr int CPR = R / 8, RPP = 64 / CPR, SLOTS = GBK / RPP / NW;
+  __amdgpu_buffer_rsrc_t rs;
+  uint32_t vo[SLOTS];
+  int kr[SLOTS];
+  int kend; uint32_t ld2;
+  AVSR_DEV void init(const bf16* base, uint32_t bytes, int64_t ld, int r0, int rext, int kend_, int wave, int lane) {
+    rs = make_rsrc(base, bytes);
+    kend = kend_; ld2 = (uint32_t)(ld * 2);
+#pragma unroll
+    for (int i = 0; i < SLOTS; ++i) {
+      const int pc = i * NW + wave, pk = pc * RPP + lane / CPR;
+      const int r = r0 + ((lane % CPR) ^ rswz<CPR>(pk)) * 8;
+      kr[i] = pk;
+      vo[i] = r < rext ? (uint32_t)(((int64_t)pk * ld + r) * 2) : OOB;
+    }
+  }
+  AVSR_DEV void issue(char* img, int k0, int wave) const {
+    const bool full = k0 + GBK <= kend;
+#pragma unroll
+    for (int i = 0; i < SLOTS; ++i) {
+      const uint32_t v = (full || k0 + kr[i] < kend) ? vo[i] : OOB;
+      bglds16(rs, v, (uint32_t)k0 * ld2, img + (i * NW + wave) * 1024);
+    }
+  }
+};
+
 // ---------------------------------------------------------------- fragments
 // 16x16x32 operand fragment: rows rb..rb+15 (row = lane&15), k = 32kb + 8(lane>>4) + 0..7
 template <int R, bool KMAJ>
