@@ -103,7 +103,7 @@ class AttnParams(ctypes.Structure):
         ("o", _c_p), ("ldo", _i64), ("lse", _c_p), ("klen", _c_p), ("causal", _i),
         ("drop_p", _f), ("seed", ctypes.c_uint64),
         ("dout", _c_p), ("lddo", _i64), ("delta", _c_p), ("dq", _c_p), ("lddq", _i64),
-        ("dk", _c_p), ("lddk", _i64), ("dv", _c_p), ("lddv", _i64),
+        ("dk", _c_p), ("lddk", _i64), ("dv", _c_p), ("lddv", _i64), ("dq_out", _c_p), ("lddq_out", _i64),
     ]
 
 

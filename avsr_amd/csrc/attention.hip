@@ -356,6 +356,329 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(AttnArgs a) {
   store_t<T>(dv0, dv1, 1.f, rw, DV, a.lddv, a.Lk - kb0);
 }
 
+// =====================================================================================
+// bf16 streaming kernels. Each workgroup (4 waves x 32 rows of its own dimension) streams
+// 64-row tiles of the other operand pair through a double-buffered LDS ring: the next
+// tile's global loads are issued into registers before the current tile's MFMAs and
+// written to the other ring slot after them, so one barrier per tile covers both hazards.
+// Images are row-major [64][ROW]; transposed operand fragments come straight from them
+// through ds_read_b64_tr_b16 (no transposed LDS stores). The backward is split in two
+// kernels, dK/dV per key block and dQ per query block (each recomputes P): no atomics,
+// no cross-wave reduction, dQ written once in its final dtype.
+namespace v2 {
+typedef short s4v __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s4v lds_s4v;
+
+constexpr int ROW = 72;          // 144-B rows: b128 reads of 16 rows at one column hit distinct banks
+constexpr int IMG = 64 * ROW;    // elements of one [64][64] tile image
+
+struct Pref { v16 x[2]; };       // this thread's two 16-byte chunks of a tile (chunk id tid + 256 i)
+
+AVSR_DEV void pref_load(Pref& r, const bf16* base, int64_t ld, int row0, int nrows, int tid) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int id = tid + 256 * i, row = row0 + (id >> 3);
+    if (row < nrows) {
+      r.x[i] = *(const v16*)(base + (int64_t)row * ld + (id & 7) * 8);
+    } else {
+      r.x[i].w[0] = r.x[i].w[1] = r.x[i].w[2] = r.x[i].w[3] = 0u;
+    }
+  }
+}
+AVSR_DEV void pref_store(const Pref& r, bf16* img, int tid) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int id = tid + 256 * i;
+    *(v16*)&img[(id >> 3) * ROW + (id & 7) * 8] = r.x[i];
+  }
+}
+// A/B fragment of mfma32 with the operand row on the lane: X[row][col .. col+7]
+AVSR_DEV bf16x8 rd8(const bf16* img, int row, int col) { return *(const bf16x8*)&img[row * ROW + col]; }
+// Transposed A fragment of mfma32 from a row-major image: lane l gets X^T[c0 + (l&31)][r]
+// for r = r0 + 4*(l>>5) + {0..3, 8..11} — the row order of accumulator registers
+// 8S..8S+7 used as a B operand (accb), so r0 = (row block of the accumulator) + 16 S.
+AVSR_DEV bf16x8 rdT(const bf16* img, int r0, int c0, int lane) {
+  const int hh = lane >> 5, g = (lane >> 4) & 1, i = lane & 15;
+  const bf16* pa = img + (r0 + 4 * hh + (i >> 2)) * ROW + c0 + 16 * g + 4 * (i & 3);
+  union { s4v s[2]; bf16x8 h; } u;
+  u.s[0] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4v*)pa);
+  u.s[1] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4v*)(pa + 8 * ROW));
+  return u.h;
+}
+// accumulator registers 8S..8S+7 as a bf16 operand fragment
+AVSR_DEV bf16x8 accb(const f32x16& x, int S) {
+  bf16x8 h;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) h[j] = (bf16)x[8 * S + j];
+  return h;
+}
+AVSR_DEV bf16x8 ldrow(const bf16* p, bool ok) {
+  if (ok) return *(const bf16x8*)p;
+  bf16x8 z;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) z[j] = (bf16)0.f;
+  return z;
+}
+
+// forward: per wave 32 queries on the lanes; S^T = K Q^T and O^T += V^T P^T over 64-key tiles
+__global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
+  __shared__ __attribute__((aligned(16))) bf16 sm[4 * IMG];          // [slot][K | V]
+  const int b = blockIdx.y / a.H, h = blockIdx.y % a.H;
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, c = l & 31, hh = l >> 5;
+  const int q0 = blockIdx.x * 128 + w * 32, qi = q0 + c;
+  const bf16* Q = (const bf16*)a.q + (int64_t)b * a.Lq * a.ldq + h * DH;
+  const bf16* K = (const bf16*)a.k + (int64_t)b * a.Lk * a.ldk + h * DH;
+  const bf16* V = (const bf16*)a.v + (int64_t)b * a.Lk * a.ldv + h * DH;
+  bf16x8 qf[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) qf[s] = ldrow(Q + (int64_t)qi * a.ldq + s * 16 + 8 * hh, qi < a.Lq);
+  f32x16 o0, o1;
+  zacc(o0); zacc(o1);
+  float m = -INFINITY, lsum = 0.f;
+  const int klen = a.klen ? min(a.klen[b], a.Lk) : a.Lk;
+  int kend = klen;
+  if (a.causal) kend = min(kend, (int)blockIdx.x * 128 + 128);
+  const int nt = (kend + 63) / 64;
+  const float sl2 = a.scale * LOG2E;
+  const uint64_t dbase = ((uint64_t)(b * a.H + h) * a.Lq + qi) * (uint64_t)a.Lk;
+  Pref pk, pv;
+  if (nt > 0) {
+    pref_load(pk, K, a.ldk, 0, a.Lk, tid); pref_load(pv, V, a.ldv, 0, a.Lk, tid);
+    pref_store(pk, sm, tid); pref_store(pv, sm + IMG, tid);
+  }
+  __syncthreads();
+  for (int t = 0; t < nt; ++t) {
+    const int kt0 = t * 64;
+    const bf16* Ks = sm + (t & 1) * 2 * IMG;
+    const bf16* Vs = Ks + IMG;
+    if (t + 1 < nt) { pref_load(pk, K, a.ldk, kt0 + 64, a.Lk, tid); pref_load(pv, V, a.ldv, kt0 + 64, a.Lk, tid); }
+    f32x16 s0, s1;
+    zacc(s0); zacc(s1);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      s0 = mfma32(rd8(Ks, c, s * 16 + 8 * hh), qf[s], s0);
+      s1 = mfma32(rd8(Ks, 32 + c, s * 16 + 8 * hh), qf[s], s1);
+    }
+    const bool full = kt0 + 64 <= klen && !a.causal;
+    float mt = -INFINITY;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      float x0 = s0[r] * sl2, x1 = s1[r] * sl2;
+      if (!full) {
+        const int k0 = kt0 + qrow(r, hh), k1 = k0 + 32;
+        if (!(k0 < klen && (!a.causal || k0 <= qi))) x0 = -INFINITY;
+        if (!(k1 < klen && (!a.causal || k1 <= qi))) x1 = -INFINITY;
+      }
+      s0[r] = x0; s1[r] = x1;
+      mt = fmaxf(mt, fmaxf(x0, x1));
+    }
+    mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+    const float mn = fmaxf(m, mt);
+    const float mb = mn == -INFINITY ? 0.f : mn;
+    const float alpha = exp2f(m - mb);
+    float ps = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float p0 = exp2f(s0[r] - mb), p1 = exp2f(s1[r] - mb);
+      ps += p0 + p1;
+      s0[r] = p0; s1[r] = p1;
+    }
+    ps += __shfl_xor(ps, 32, 64);
+    lsum = lsum * alpha + ps;
+    m = mn;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) { o0[r] *= alpha; o1[r] *= alpha; }
+    if (a.drop_p > 0.f) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        s0[r] *= drop_scale(a.drop_p, a.seed, dbase + kt0 + qrow(r, hh));
+        s1[r] *= drop_scale(a.drop_p, a.seed, dbase + kt0 + 32 + qrow(r, hh));
+      }
+    }
+    const bf16x8 p0a = accb(s0, 0), p0b = accb(s0, 1), p1a = accb(s1, 0), p1b = accb(s1, 1);
+    o0 = mfma32(rdT(Vs, 0, 0, l), p0a, o0);
+    o0 = mfma32(rdT(Vs, 16, 0, l), p0b, o0);
+    o0 = mfma32(rdT(Vs, 32, 0, l), p1a, o0);
+    o0 = mfma32(rdT(Vs, 48, 0, l), p1b, o0);
+    o1 = mfma32(rdT(Vs, 0, 32, l), p0a, o1);
+    o1 = mfma32(rdT(Vs, 16, 32, l), p0b, o1);
+    o1 = mfma32(rdT(Vs, 32, 32, l), p1a, o1);
+    o1 = mfma32(rdT(Vs, 48, 32, l), p1b, o1);
+    if (t + 1 < nt) {
+      bf16* nx = sm + ((t + 1) & 1) * 2 * IMG;
+      pref_store(pk, nx, tid); pref_store(pv, nx + IMG, tid);
+    }
+    __syncthreads();
+  }
+  const float inv = lsum > 0.f ? 1.f / lsum : 0.f;
+  if (hh == 0 && qi < a.Lq) a.lse[(int64_t)(b * a.H + h) * a.Lq + qi] = lsum > 0.f ? (m + log2f(lsum)) * LN2 : -INFINITY;
+  bf16* O = (bf16*)a.o + ((int64_t)b * a.Lq + q0) * a.ldo + h * DH;
+  store_t<bf16>(o0, o1, inv, (float*)sm + w * 32 * 65, O, a.ldo, a.Lq - q0);
+}
+
+// dK / dV: per wave 32 keys on the lanes (K, V rows in registers); 64-query tiles of Q, dO
+// (+ lse, delta) streamed; S = Q K^T, dP = dO V^T, dV^T += dO^T P', dK^T += Q^T dS
+__global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnArgs a) {
+  __shared__ __attribute__((aligned(16))) bf16 sm[4 * IMG];          // [slot][Q | dO]
+  __shared__ float lss[2][64], dls[2][64];
+  const int b = blockIdx.y / a.H, h = blockIdx.y % a.H;
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, c = l & 31, hh = l >> 5;
+  const int kb0 = blockIdx.x * 128 + w * 32, key = kb0 + c;
+  const bf16* Q = (const bf16*)a.q + (int64_t)b * a.Lq * a.ldq + h * DH;
+  const bf16* K = (const bf16*)a.k + (int64_t)b * a.Lk * a.ldk + h * DH;
+  const bf16* V = (const bf16*)a.v + (int64_t)b * a.Lk * a.ldv + h * DH;
+  const bf16* dO = (const bf16*)a.dout + (int64_t)b * a.Lq * a.lddo + h * DH;
+  const float* LSE = a.lse + (int64_t)(b * a.H + h) * a.Lq;
+  const float* DL = a.delta + (int64_t)(b * a.H + h) * a.Lq;
+  bf16x8 kf[4], vf[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    kf[s] = ldrow(K + (int64_t)key * a.ldk + s * 16 + 8 * hh, key < a.Lk);
+    vf[s] = ldrow(V + (int64_t)key * a.ldv + s * 16 + 8 * hh, key < a.Lk);
+  }
+  f32x16 dv0, dv1, dk0, dk1;
+  zacc(dv0); zacc(dv1); zacc(dk0); zacc(dk1);
+  const int klen = a.klen ? min(a.klen[b], a.Lk) : a.Lk;
+  const float sl2 = a.scale * LOG2E;
+  const int qstart = a.causal ? (int)blockIdx.x * 128 : 0;
+  const int nt = a.Lq > qstart ? (a.Lq - qstart + 63) / 64 : 0;
+  const uint64_t bh = (uint64_t)(b * a.H + h);
+  Pref pq, po;
+  float lsr = 0.f, dlr = 0.f;
+  auto fetch = [&](int qt0) {
+    pref_load(pq, Q, a.ldq, qt0, a.Lq, tid); pref_load(po, dO, a.lddo, qt0, a.Lq, tid);
+    if (tid < 64) {
+      const int q = qt0 + tid;
+      lsr = q < a.Lq ? LSE[q] * LOG2E : 0.f;
+      dlr = q < a.Lq ? DL[q] : 0.f;
+    }
+  };
+  auto stash = [&](int slot) {
+    bf16* img = sm + slot * 2 * IMG;
+    pref_store(pq, img, tid); pref_store(po, img + IMG, tid);
+    if (tid < 64) { lss[slot][tid] = lsr; dls[slot][tid] = dlr; }
+  };
+  if (nt > 0) { fetch(qstart); stash(0); }
+  __syncthreads();
+  for (int t = 0; t < nt; ++t) {
+    const int qt0 = qstart + t * 64, slot = t & 1;
+    const bf16* Qs = sm + slot * 2 * IMG;
+    const bf16* dOs = Qs + IMG;
+    if (t + 1 < nt) fetch(qt0 + 64);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      f32x16 sc, dp;
+      zacc(sc); zacc(dp);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        sc = mfma32(rd8(Qs, 32 * u + c, s * 16 + 8 * hh), kf[s], sc);
+        dp = mfma32(rd8(dOs, 32 * u + c, s * 16 + 8 * hh), vf[s], dp);
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int ql = 32 * u + qrow(r, hh), q = qt0 + ql;
+        const bool ok = q < a.Lq && key < klen && (!a.causal || key <= q);
+        const float p = ok ? exp2f(sc[r] * sl2 - lss[slot][ql]) : 0.f;
+        const float keep = (a.drop_p > 0.f && ok) ? drop_scale(a.drop_p, a.seed, (bh * a.Lq + q) * (uint64_t)a.Lk + key) : 1.f;
+        sc[r] = p * keep;                                       // P' = dropout(P)
+        dp[r] = p * (dp[r] * keep - dls[slot][ql]) * a.scale;   // dS (scaled)
+      }
+      const bf16x8 pa = accb(sc, 0), pb = accb(sc, 1), sa = accb(dp, 0), sb = accb(dp, 1);
+      dv0 = mfma32(rdT(dOs, 32 * u, 0, l), pa, dv0);
+      dv0 = mfma32(rdT(dOs, 32 * u + 16, 0, l), pb, dv0);
+      dv1 = mfma32(rdT(dOs, 32 * u, 32, l), pa, dv1);
+      dv1 = mfma32(rdT(dOs, 32 * u + 16, 32, l), pb, dv1);
+      dk0 = mfma32(rdT(Qs, 32 * u, 0, l), sa, dk0);
+      dk0 = mfma32(rdT(Qs, 32 * u + 16, 0, l), sb, dk0);
+      dk1 = mfma32(rdT(Qs, 32 * u, 32, l), sa, dk1);
+      dk1 = mfma32(rdT(Qs, 32 * u + 16, 32, l), sb, dk1);
+    }
+    if (t + 1 < nt) stash((t + 1) & 1);
+    __syncthreads();
+  }
+  float* scr = (float*)sm + w * 32 * 65;
+  bf16* DK = (bf16*)a.dk + ((int64_t)b * a.Lk + kb0) * a.lddk + h * DH;
+  store_t<bf16>(dk0, dk1, 1.f, scr, DK, a.lddk, a.Lk - kb0);
+  __syncthreads();
+  bf16* DV = (bf16*)a.dv + ((int64_t)b * a.Lk + kb0) * a.lddv + h * DH;
+  store_t<bf16>(dv0, dv1, 1.f, scr, DV, a.lddv, a.Lk - kb0);
+}
+
+// dQ: per wave 32 queries on the lanes (Q, dO rows in registers, lse / delta per lane);
+// 64-key tiles of K, V streamed; S^T = K Q^T, dP^T = V dO^T, dQ^T += K^T dS^T
+template <typename OutT>
+__global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs a, OutT* dq, int64_t lddq) {
+  __shared__ __attribute__((aligned(16))) bf16 sm[4 * IMG];          // [slot][K | V]
+  const int b = blockIdx.y / a.H, h = blockIdx.y % a.H;
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, c = l & 31, hh = l >> 5;
+  const int q0 = blockIdx.x * 128 + w * 32, qi = q0 + c;
+  const bf16* Q = (const bf16*)a.q + (int64_t)b * a.Lq * a.ldq + h * DH;
+  const bf16* K = (const bf16*)a.k + (int64_t)b * a.Lk * a.ldk + h * DH;
+  const bf16* V = (const bf16*)a.v + (int64_t)b * a.Lk * a.ldv + h * DH;
+  const bf16* dO = (const bf16*)a.dout + (int64_t)b * a.Lq * a.lddo + h * DH;
+  const bool qok = qi < a.Lq;
+  bf16x8 qf[4], of[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    qf[s] = ldrow(Q + (int64_t)qi * a.ldq + s * 16 + 8 * hh, qok);
+    of[s] = ldrow(dO + (int64_t)qi * a.lddo + s * 16 + 8 * hh, qok);
+  }
+  const int64_t bhq = (int64_t)(b * a.H + h) * a.Lq + qi;
+  const float lq = qok ? a.lse[bhq] * LOG2E : 0.f;
+  const float dl = qok ? a.delta[bhq] : 0.f;
+  f32x16 dq0, dq1;
+  zacc(dq0); zacc(dq1);
+  const int klen = a.klen ? min(a.klen[b], a.Lk) : a.Lk;
+  int kend = klen;
+  if (a.causal) kend = min(kend, (int)blockIdx.x * 128 + 128);
+  const int nt = (kend + 63) / 64;
+  const float sl2 = a.scale * LOG2E;
+  const uint64_t dbase = (uint64_t)bhq * (uint64_t)a.Lk;
+  Pref pk, pv;
+  if (nt > 0) {
+    pref_load(pk, K, a.ldk, 0, a.Lk, tid); pref_load(pv, V, a.ldv, 0, a.Lk, tid);
+    pref_store(pk, sm, tid); pref_store(pv, sm + IMG, tid);
+  }
+  __syncthreads();
+  for (int t = 0; t < nt; ++t) {
+    const int kt0 = t * 64;
+    const bf16* Ks = sm + (t & 1) * 2 * IMG;
+    const bf16* Vs = Ks + IMG;
+    if (t + 1 < nt) { pref_load(pk, K, a.ldk, kt0 + 64, a.Lk, tid); pref_load(pv, V, a.ldv, kt0 + 64, a.Lk, tid); }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      f32x16 st, dpt;
+      zacc(st); zacc(dpt);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        st = mfma32(rd8(Ks, 32 * u + c, s * 16 + 8 * hh), qf[s], st);
+        dpt = mfma32(rd8(Vs, 32 * u + c, s * 16 + 8 * hh), of[s], dpt);
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int kk = kt0 + 32 * u + qrow(r, hh);
+        const bool ok = kk < klen && (!a.causal || kk <= qi);
+        const float p = ok ? exp2f(st[r] * sl2 - lq) : 0.f;
+        const float keep = (a.drop_p > 0.f && ok) ? drop_scale(a.drop_p, a.seed, dbase + kk) : 1.f;
+        dpt[r] = p * (dpt[r] * keep - dl) * a.scale;
+      }
+      const bf16x8 sa = accb(dpt, 0), sb = accb(dpt, 1);
+      dq0 = mfma32(rdT(Ks, 32 * u, 0, l), sa, dq0);
+      dq0 = mfma32(rdT(Ks, 32 * u + 16, 0, l), sb, dq0);
+      dq1 = mfma32(rdT(Ks, 32 * u, 32, l), sa, dq1);
+      dq1 = mfma32(rdT(Ks, 32 * u + 16, 32, l), sb, dq1);
+    }
+    if (t + 1 < nt) {
+      bf16* nx = sm + ((t + 1) & 1) * 2 * IMG;
+      pref_store(pk, nx, tid); pref_store(pv, nx + IMG, tid);
+    }
+    __syncthreads();
+  }
+  OutT* DQ = dq + ((int64_t)b * a.Lq + q0) * lddq + h * DH;
+  store_t<OutT>(dq0, dq1, 1.f, (float*)sm + w * 32 * 65, DQ, lddq, a.Lq - q0);
+}
+}  // namespace v2
+
 AttnArgs args(const avsr_attn_params* p) {
   AttnArgs a;
   a.B = p->B; a.H = p->H; a.Lq = p->Lq; a.Lk = p->Lk; a.scale = p->scale;
@@ -382,7 +705,7 @@ extern "C" int avsr_attn_fwd(const avsr_attn_params* p, void* stream) {
   if (p->B * p->H == 0 || p->Lq == 0) return 0;
   AttnArgs a = args(p);
   dim3 grid((p->Lq + 127) / 128, p->B * p->H);
-  if (p->dtype == AVSR_BF16) hipLaunchKernelGGL(attn_fwd_kernel<bf16>, grid, dim3(256), 0, (hipStream_t)stream, a);
+  if (p->dtype == AVSR_BF16) hipLaunchKernelGGL(v2::attn_fwd_kernel, grid, dim3(256), 0, (hipStream_t)stream, a);
   else hipLaunchKernelGGL(attn_fwd_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, a);
   AVSR_CHECK_LAUNCH();
   return 0;
@@ -404,9 +727,19 @@ extern "C" int avsr_attn_bwd(const avsr_attn_params* p, void* stream) {
   if (rc) return rc;
   if (p->B * p->H == 0 || p->Lk == 0) return 0;
   AttnArgs a = args(p);
+  hipStream_t st = (hipStream_t)stream;
   dim3 grid((p->Lk + 127) / 128, p->B * p->H);
-  if (p->dtype == AVSR_BF16) hipLaunchKernelGGL(attn_bwd_kernel<bf16>, grid, dim3(256), 0, (hipStream_t)stream, a);
-  else hipLaunchKernelGGL(attn_bwd_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, a);
+  if (p->dtype == AVSR_BF16) {
+    if (p->dq_out && (p->lddq_out % 8 || !avsr_aligned16(p->dq_out))) return AVSR_E_ALIGN;
+    if (!p->dq_out && (p->lddq % 4 || !avsr_aligned16(p->dq))) return AVSR_E_ALIGN;
+    hipLaunchKernelGGL(v2::attn_bwd_dkdv_kernel, grid, dim3(256), 0, st, a);
+    AVSR_CHECK_LAUNCH();
+    dim3 gq((p->Lq + 127) / 128, p->B * p->H);
+    if (p->dq_out) hipLaunchKernelGGL(v2::attn_bwd_dq_kernel<bf16>, gq, dim3(256), 0, st, a, (bf16*)p->dq_out, p->lddq_out);
+    else hipLaunchKernelGGL(v2::attn_bwd_dq_kernel<float>, gq, dim3(256), 0, st, a, p->dq, p->lddq);
+  } else {
+    hipLaunchKernelGGL(attn_bwd_kernel<float>, grid, dim3(256), 0, st, a);
+  }
   AVSR_CHECK_LAUNCH();
   return 0;
 }

@@ -35,21 +35,17 @@ AVSR_DEV float wave_max(float v) {
 }
 
 // ---- counter-based dropout stream: keep(seed, idx) with P(keep) = 1 - p ------------
-// A 2-round Philox-style mix of (seed, idx) -> 32-bit uniform. Identical in forward and
-// backward so no mask is ever stored (the backward recomputes it from the index).
+// Two murmur3 finalisers over (seed, idx) -> 32-bit uniform (~16 VALU per element; the
+// outer mix of (hi, seed_hi) is loop-invariant in every caller's inner loop). Identical
+// in forward and backward so no mask is ever stored (the backward recomputes it).
+AVSR_DEV uint32_t fmix32(uint32_t h) {
+  h ^= h >> 16; h *= 0x85EBCA6Bu;
+  h ^= h >> 13; h *= 0xC2B2AE35u;
+  return h ^ (h >> 16);
+}
 AVSR_DEV uint32_t mix32(uint64_t seed, uint64_t idx) {
-  uint32_t lo = (uint32_t)idx, hi = (uint32_t)(idx >> 32);
-  uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    uint64_t p0 = (uint64_t)lo * 0xD2511F53u;
-    uint64_t p1 = (uint64_t)hi * 0xCD9E8D57u;
-    uint32_t nlo = (uint32_t)(p1 >> 32) ^ k0 ^ (uint32_t)p0;
-    uint32_t nhi = (uint32_t)(p0 >> 32) ^ k1 ^ (uint32_t)p1;
-    lo = nlo; hi = nhi;
-    k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
-  }
-  return lo ^ hi;
+  const uint32_t lo = (uint32_t)idx, hi = (uint32_t)(idx >> 32);
+  return fmix32((lo * 0x9E3779B1u) ^ (uint32_t)seed ^ fmix32(hi ^ (uint32_t)(seed >> 32) ^ 0x68E31DA4u));
 }
 AVSR_DEV float drop_scale(float p, uint64_t seed, uint64_t idx) {
   // returns 0 for dropped, 1/(1-p) for kept

@@ -131,6 +131,11 @@ class Engine:
     def _z(self, *shape, dtype=None):
         return torch.zeros(*shape, device=self.device, dtype=dtype or self.dtype)
 
+    def _dq32(self, rows, D):
+        """fp32 dQ accumulator for the fp32 (parity) attention backward; None in bf16, where
+        the backward writes dQ straight into the activation-dtype gradient buffer."""
+        return self._z(rows, D, dtype=torch.float32) if self.dtype == torch.float32 else None
+
     def w(self, n):
         return self.arena.w(n)
 
@@ -444,12 +449,13 @@ class Engine:
         # attention
         qkv = lc["qkv"]
         dqkv = self._e(M, 3 * D)
-        dq32 = self._z(M, D, dtype=torch.float32)
+        dq32 = self._dq32(M, D)
         delta = self._e(B, H, T, dtype=torch.float32)
         ops.attn_bwd(do, qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:], lc["o"], lc["lse"], dq32, dqkv[:, D:2 * D],
                      dqkv[:, 2 * D:], delta, B=B, H=H, Lq=T, Lk=T, klen=klen, scale=0.125, drop_p=lc["p_att"],
-                     seed=lc["sd_att"])
-        ops.cast(dq32, dqkv[:, :D])
+                     seed=lc["sd_att"], dq=None if dq32 is not None else dqkv[:, :D])
+        if dq32 is not None:
+            ops.cast(dq32, dqkv[:, :D])
         names_b = [a + "q_proj.bias", a + "k_proj.bias", a + "v_proj.bias"]
         names_w = [a + "q_proj.weight", a + "k_proj.weight", a + "v_proj.weight"]
         self._bias_grad(dqkv, self.arena.span(names_b, buf="g"))
@@ -597,12 +603,14 @@ class Engine:
             self._wgrad(g, lc["o2"], self.g(ca + "linear_out.weight"))
             do2 = ops.linear_dgrad(g, self.w(ca + "linear_out.weight"))
             dkv = self._e(B * T, 2 * D)
-            dq32 = self._z(R, D, dtype=torch.float32)
+            dq32 = self._dq32(R, D)
             delta = self._e(B, H, L1, dtype=torch.float32)
-            ops.attn_bwd(do2, lc["q2"], lc["kv"][:, :D], lc["kv"][:, D:], lc["o2"], lc["lse2"], dq32, dkv[:, :D], dkv[:, D:],
-                         delta, B=B, H=H, Lq=L1, Lk=T, klen=klen, scale=0.125, drop_p=p_att, seed=lc["s3"])
             dq2 = self._e(R, D)
-            ops.cast(dq32, dq2)
+            ops.attn_bwd(do2, lc["q2"], lc["kv"][:, :D], lc["kv"][:, D:], lc["o2"], lc["lse2"], dq32, dkv[:, :D], dkv[:, D:],
+                         delta, B=B, H=H, Lq=L1, Lk=T, klen=klen, scale=0.125, drop_p=p_att, seed=lc["s3"],
+                         dq=None if dq32 is not None else dq2)
+            if dq32 is not None:
+                ops.cast(dq32, dq2)
             self._bias_grad(dq2, self.g(ca + "linear_q.bias"))
             self._wgrad(dq2, lc["n2"], self.g(ca + "linear_q.weight"))
             dn2 = ops.linear_dgrad(dq2, self.w(ca + "linear_q.weight"))
@@ -617,12 +625,14 @@ class Engine:
             self._wgrad(g, lc["o1"], self.g(sa + "linear_out.weight"))
             do1 = ops.linear_dgrad(g, self.w(sa + "linear_out.weight"))
             dqkv = self._e(R, 3 * D)
-            dq32 = self._z(R, D, dtype=torch.float32)
+            dq32 = self._dq32(R, D)
             delta = self._e(B, H, L1, dtype=torch.float32)
             qkv = lc["qkv"]
             ops.attn_bwd(do1, qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:], lc["o1"], lc["lse1"], dq32, dqkv[:, D:2 * D],
-                         dqkv[:, 2 * D:], delta, B=B, H=H, Lq=L1, Lk=L1, causal=True, scale=0.125, drop_p=p_att, seed=lc["s1"])
-            ops.cast(dq32, dqkv[:, :D])
+                         dqkv[:, 2 * D:], delta, B=B, H=H, Lq=L1, Lk=L1, causal=True, scale=0.125, drop_p=p_att, seed=lc["s1"],
+                         dq=None if dq32 is not None else dqkv[:, :D])
+            if dq32 is not None:
+                ops.cast(dq32, dqkv[:, :D])
             nb = [sa + "linear_q.bias", sa + "linear_k.bias", sa + "linear_v.bias"]
             nw = [sa + "linear_q.weight", sa + "linear_k.weight", sa + "linear_v.weight"]
             self._bias_grad(dqkv, self.arena.span(nb, buf="g"))

@@ -327,12 +327,17 @@ def attn_fwd(q, k, v, o, lse, *, B, H, Lq, Lk, klen=None, causal=False, scale=0.
 
 
 def attn_bwd(dout, q, k, v, o, lse, dq32, dk, dv, delta, *, B, H, Lq, Lk, klen=None, causal=False,
-             scale=0.125, drop_p=0.0, seed=0):
-    """dq32: fp32 accumulator (zeroed by the caller), dk/dv in the activation dtype."""
+             scale=0.125, drop_p=0.0, seed=0, dq=None):
+    """dq32: fp32 accumulator (zeroed by the caller), or None with dq (bf16 only): dQ written
+    straight into dq in the activation dtype. dk/dv in the activation dtype."""
     p = _attn_params(q, k, v, o, B, H, Lq, Lk, lse, klen, causal, scale, drop_p, seed)
     p.dout, p.lddo = dout.data_ptr(), dout.stride(0)
     p.delta = delta.data_ptr()
-    p.dq, p.lddq = dq32.data_ptr(), dq32.stride(0)
+    if dq is not None:
+        assert q.dtype == torch.bfloat16 and dq.dtype == torch.bfloat16, "dq output path is bf16 only"
+        p.dq_out, p.lddq_out = dq.data_ptr(), dq.stride(0)
+    else:
+        p.dq, p.lddq = dq32.data_ptr(), dq32.stride(0)
     p.dk, p.lddk = dk.data_ptr(), dk.stride(0)
     p.dv, p.lddv = dv.data_ptr(), dv.stride(0)
     _call("avsr_attn_bwd_prep", p)

@@ -216,8 +216,9 @@ int avsr_avgpool_bwd(int dtype, int nimg, int P, int C, const void* dy, void* dx
  *   mask: key j of batch b valid iff j < klen[b] (klen NULL: all Lk valid) and, if causal,
  *   j <= i.  Optional dropout on the probabilities (counter-based; bwd recomputes it).
  * fwd stores lse[b][h][i] (natural log) for the backward.
- * bwd: dq (fp32 accumulator [B*Lq][ldq_f32], atomics, caller zeroes), dk, dv (dtype);
- *   needs delta[b][h][i] = sum_d dO*O from avsr_attn_bwd_prep.
+ * bwd: dq (fp32 accumulator [B*Lq][ldq_f32], atomics, caller zeroes) or dq_out (dtype),
+ *   dk, dv (dtype); needs delta[b][h][i] = sum_d dO*O from avsr_attn_bwd_prep. bf16 runs
+ *   two streaming kernels (dK/dV per key block, dQ per query block), fp32 one atomic kernel.
  * Replaces: HF:eager_attention_forward + Wav2Vec2Attention core (:438-548; encoder, key
  *   padding mask from avhubert.py:688-696) and MultiHeadedAttention.forward_attention
  *   (src/nets/backend/transformer/attention.py:56-106; decoder causal self-attention and
@@ -240,6 +241,9 @@ typedef struct {
   float* dq; int64_t lddq;    /* fp32 */
   void* dk; int64_t lddk;
   void* dv; int64_t lddv;
+  /* bf16 only: if non-NULL, dQ is written here in the activation dtype (dq unused);
+   * otherwise bf16 writes dq (fp32) with plain stores (= accumulate onto a zeroed buffer) */
+  void* dq_out; int64_t lddq_out;
 } avsr_attn_params;
 int avsr_attn_fwd(const avsr_attn_params* p, void* stream);
 int avsr_attn_bwd_prep(const avsr_attn_params* p, void* stream);   /* delta = rowsum(dO * O) */

@@ -83,6 +83,11 @@ def test_attention(dev, dtype, case):
     assert _rel(dq, qr.grad) < gt
     assert _rel(dk, kr.grad) < gt
     assert _rel(dv, vr.grad) < gt
+    if dtype == torch.bfloat16:      # dQ written straight in bf16 (the engine's path)
+        dqb = torch.empty(B * Lq, D, device=dev, dtype=dtype)
+        ops.attn_bwd(dout.to(dev, dtype), qd, kd, vd, o, lse, None, dk, dv, delta, B=B, H=H, Lq=Lq, Lk=Lk,
+                     klen=kl, causal=causal, scale=scale, dq=dqb)
+        assert _rel(dqb, qr.grad) < gt
 
 
 def test_attention_dropout(dev):
@@ -125,3 +130,53 @@ def test_attention_dropout(dev):
     assert _rel(dq, qr.grad) < 1e-4
     assert _rel(dk, kr.grad) < 1e-4
     assert _rel(dv, vr.grad) < 1e-4
+
+
+def test_attention_dropout_bf16(dev):
+    """bf16 streaming kernels with probability dropout: the mask (same counter hash as the
+    fp32 kernels) is recovered through one-hot V rows in fp32, then the bf16 fwd / bwd
+    (dK, dV and both dQ outputs) are checked against the reference with that mask."""
+    B, H, L, p, seed = 2, 2, 150, 0.1, 4242
+    D = H * 64
+    g = torch.Generator().manual_seed(2)
+    q = torch.randn(B * L, D, generator=g); k = torch.randn(B * L, D, generator=g)
+    qd, kd = q.to(dev), k.to(dev)
+    lse = torch.empty(B, H, L, device=dev)
+    mult = torch.empty(B, H, L, L, dtype=torch.float64)
+    for j0 in range(0, L, 64):       # 64 one-hot key columns per pass
+        eye = torch.zeros(B * L, D)
+        for b in range(B):
+            for j in range(j0, min(L, j0 + 64)):
+                for h in range(H):
+                    eye[b * L + j, h * 64 + j - j0] = 1.0
+        o = torch.empty(B * L, D, device=dev)
+        ops.attn_fwd(qd, kd, eye.to(dev), o, lse, B=B, H=H, Lq=L, Lk=L, scale=0.125, drop_p=p, seed=seed)
+        n = min(L, j0 + 64) - j0
+        mult[..., j0:j0 + n] = o.cpu().double().view(B, L, H, 64)[..., :n].permute(0, 2, 1, 3)
+    qh = q.double().view(B, L, H, 64).transpose(1, 2); kh = k.double().view(B, L, H, 64).transpose(1, 2)
+    pr = torch.softmax(qh @ kh.transpose(-1, -2) * 0.125, -1)
+    kept = (mult / pr).round(decimals=3) > 0.5
+    assert 0.85 < kept.double().mean().item() < 0.95
+    mask_mult = kept.double() / (1 - p)
+    v = torch.randn(B * L, D, generator=g)
+    qr, kr, vr = (t.double().clone().requires_grad_() for t in (q, k, v))
+    ref = _ref(qr, kr, vr, B, H, L, L, None, False, 0.125, mask_mult)
+    dout = torch.randn(B * L, D, generator=g)
+    ref.backward(dout.double())
+    bf = torch.bfloat16
+    qb, kb, vb = q.to(dev, bf), k.to(dev, bf), v.to(dev, bf)
+    o = torch.empty(B * L, D, device=dev, dtype=bf)
+    ops.attn_fwd(qb, kb, vb, o, lse, B=B, H=H, Lq=L, Lk=L, scale=0.125, drop_p=p, seed=seed)
+    assert _rel(o, ref) < 2e-2
+    dq = torch.zeros(B * L, D, device=dev)
+    dqb = torch.empty(B * L, D, device=dev, dtype=bf)
+    dk = torch.empty(B * L, D, device=dev, dtype=bf); dv = torch.empty(B * L, D, device=dev, dtype=bf)
+    delta = torch.empty(B, H, L, device=dev)
+    db = dout.to(dev, bf)
+    ops.attn_bwd(db, qb, kb, vb, o, lse, dq, dk, dv, delta, B=B, H=H, Lq=L, Lk=L, scale=0.125, drop_p=p, seed=seed)
+    assert _rel(dq, qr.grad) < 3e-2
+    assert _rel(dk, kr.grad) < 3e-2
+    assert _rel(dv, vr.grad) < 3e-2
+    ops.attn_bwd(db, qb, kb, vb, o, lse, None, dk, dv, delta, B=B, H=H, Lq=L, Lk=L, scale=0.125, drop_p=p,
+                 seed=seed, dq=dqb)
+    assert _rel(dqb, qr.grad) < 3e-2

@@ -40,8 +40,11 @@ for (M, N, K) in shapes:
     dW = torch.zeros(N, K, device=dev)
     fl = 2 * M * N * K
     a = t(lambda: ops.linear_fwd(x, W))
+    bias = torch.zeros(N, device=dev)
+    h = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    ae = t(lambda: ops.linear_fwd(x, W, bias, act=1, preact=h, drop_p=0.1, seed=7))
     b = t(lambda: ops.linear_dgrad(dy, W))
     c = t(lambda: ops.linear_wgrad(dy, x, dW))
     r = t(lambda: x @ W.t())
-    print(f"[{tag}] M{M} N{N} K{K}: fwd {fl/a/1e9:.0f} TF/s ({a*1e3:.1f}us)  dgrad {fl/b/1e9:.0f}  "
+    print(f"[{tag}] M{M} N{N} K{K}: fwd {fl/a/1e9:.0f} TF/s ({a*1e3:.1f}us) fwd+gelu/drop/preact {fl/ae/1e9:.0f}  dgrad {fl/b/1e9:.0f}  "
           f"wgrad(splitk=1) {fl/c/1e9:.0f}  torch {fl/r/1e9:.0f}", flush=True)
