@@ -346,16 +346,95 @@ AVSR_DEV void epi_elems(const Epi& e, int row, int col, const float* v_in) {
     if (!e.bwd) {
       if (e.bias) v += e.bias[col + q];
       if (P) P[off + q] = from_f<T>(v);
-      v = act_fwd(e.act, v);
+      v = act_fwd_t<T>(e.act, v);
       if (e.drop_p > 0.f) v *= drop_scale(e.drop_p, e.seed, didx);
       if (R) v += to_f(R[(int64_t)row * e.ldr + col + q]);
     } else {
       if (e.drop_p > 0.f) v *= drop_scale(e.drop_p, e.seed, didx);
-      if (G) v *= act_bwd(e.act, to_f(G[off + q]));
+      if (G) v *= act_bwd_t<T>(e.act, to_f(G[off + q]));
     }
     if (e.beta != 0.f) v += e.beta * to_f(C[off + q]);
     C[off + q] = from_f<OutT>(v);
   }
+}
+
+// Can the tile's stores use the 8-column vector path? (non-atomic; every row-major operand
+// 16-byte aligned with a row stride that keeps 8-column groups aligned)
+template <typename T, typename OutT>
+AVSR_DEV bool epi_vec_ok(const Epi& e) {
+  const uintptr_t a = (uintptr_t)e.C | (uintptr_t)e.preact | (uintptr_t)e.res | (uintptr_t)e.gate | (uintptr_t)e.bias;
+  return !e.atomic && (a & 15u) == 0 && ((e.ldc * (int64_t)sizeof(OutT)) & 15) == 0 &&
+         ((e.ldc * (int64_t)sizeof(T)) & 15) == 0 && ((e.ldr * (int64_t)sizeof(T)) & 15) == 0;
+}
+
+template <typename T> AVSR_DEV void ld8(const T* p, float (&o)[8]) {
+  if constexpr (sizeof(T) == 2) {
+    const bf16x8 x = *(const bf16x8*)p;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = (float)x[j];
+  } else {
+    const f32x4 x0 = *(const f32x4*)p, x1 = *(const f32x4*)(p + 4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { o[j] = x0[j]; o[j + 4] = x1[j]; }
+  }
+}
+template <typename T> AVSR_DEV void st8(T* p, const float (&o)[8]) {
+  if constexpr (sizeof(T) == 2) {
+    bf16x8 x;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) x[j] = (bf16)o[j];
+    *(bf16x8*)p = x;
+  } else {
+    *(f32x4*)p = f32x4{o[0], o[1], o[2], o[3]};
+    *(f32x4*)(p + 4) = f32x4{o[4], o[5], o[6], o[7]};
+  }
+}
+
+// epi_elems for 8 full columns [col, col+8) with 16-byte loads/stores (epi_vec_ok, col+8 <= N)
+template <typename T, typename OutT>
+AVSR_DEV void epi_vec8(const Epi& e, int row, int col, float (&v)[8]) {
+  const int64_t off = (int64_t)row * e.ldc + col;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) v[q] *= e.alpha;
+  float t[8];
+  const uint64_t d0 = e.drop_base + (uint64_t)row * (uint64_t)e.N + col;
+  if (!e.bwd) {
+    if (e.bias) {
+      ld8(e.bias + col, t);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v[q] += t[q];
+    }
+    if (e.preact) st8((T*)e.preact + off, v);
+    if (e.act) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v[q] = act_fwd_t<T>(e.act, v[q]);
+    }
+    if (e.drop_p > 0.f) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v[q] *= drop_scale(e.drop_p, e.seed, d0 + q);
+    }
+    if (e.res) {
+      ld8((const T*)e.res + (int64_t)row * e.ldr + col, t);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v[q] += t[q];
+    }
+  } else {
+    if (e.drop_p > 0.f) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v[q] *= drop_scale(e.drop_p, e.seed, d0 + q);
+    }
+    if (e.gate) {
+      ld8((const T*)e.gate + off, t);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v[q] *= act_bwd_t<T>(e.act, t[q]);
+    }
+  }
+  if (e.beta != 0.f) {
+    ld8((const OutT*)e.C + off, t);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v[q] += e.beta * t[q];
+  }
+  st8((OutT*)e.C + off, v);
 }
 
 // Epilogue: (1) optional BN statistics straight from the accumulators; (2) the tile is

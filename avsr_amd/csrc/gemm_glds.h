@@ -288,8 +288,8 @@ AVSR_DEV void mainloop_glds(const LA& la, const LB& lb, int kbeg, int nk, f32x4 
 
 // Epilogue for a GCfg tile: (1) optional BN column statistics from the accumulators;
 // (2) FM passes, each staging one 32-row strip per wave row (accumulator tiles 2i, 2i+1)
-// through LDS and writing it row-major, 4 consecutive columns per thread (coalesced stores,
-// vector residual reads). Accumulator tile (ti, tj) register r sits at wave-local row
+// through LDS and writing it row-major, 8 consecutive columns per thread (one 16-byte store
+// per bf16 output row segment; 16-byte preact/residual/gate reads). Accumulator tile (ti, tj) register r sits at wave-local row
 // 16ti + 4(lane>>4) + r, column 16tj + (lane&15).
 template <typename T, typename OutT, class CF>
 AVSR_DEV void epilogue_g(const Epi& e, int m0, int n0, f32x4 (&acc)[CF::TM][CF::TN], char* smem) {
@@ -297,6 +297,7 @@ AVSR_DEV void epilogue_g(const Epi& e, int m0, int n0, f32x4 (&acc)[CF::TM][CF::
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / CF::WN, wn = wave % CF::WN;
   float* st = (float*)smem;
+  const bool vec = epi_vec_ok<T, OutT>(e);
   if (e.stats) {
     __syncthreads();
     float* red = st;  // [WM][BN][3]
@@ -364,14 +365,19 @@ AVSR_DEV void epilogue_g(const Epi& e, int m0, int n0, f32x4 (&acc)[CF::TM][CF::
           st[lr * LDR + (wn * CF::TN + j) * 16 + (lane & 15)] = acc[2 * i + h][j][r];
         }
     __syncthreads();
-    for (int c = tid; c < SR * BN / 4; c += CF::NTH) {
-      const int lr = c / (BN / 4), lc = (c % (BN / 4)) * 4;
+    for (int c = tid; c < SR * BN / 8; c += CF::NTH) {
+      const int lr = c / (BN / 8), lc = (c % (BN / 8)) * 8;
       const int row = m0 + ((lr >> 5) * CF::FM + i) * 32 + (lr & 31);
       const int col = n0 + lc;
       if (row < e.M && col < e.N) {
-        const f32x4 v4 = *(const f32x4*)(st + lr * LDR + lc);
-        const float v[4] = {v4[0], v4[1], v4[2], v4[3]};
-        epi_elems<T, OutT, 4>(e, row, col, v);
+        const f32x4 v0 = *(const f32x4*)(st + lr * LDR + lc), v1 = *(const f32x4*)(st + lr * LDR + lc + 4);
+        float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+        if (vec && col + 8 <= e.N) {
+          epi_vec8<T, OutT>(e, row, col, v);
+        } else {
+          epi_elems<T, OutT, 4>(e, row, col, v);
+          if (col + 4 < e.N) epi_elems<T, OutT, 4>(e, row, col + 4, v + 4);
+        }
       }
     }
   }

@@ -38,7 +38,7 @@ __global__ __launch_bounds__(256) void ew_bwd_kernel(EwArgs a) {
       for (int j = 0; j < VE; ++j) {
         float v = d[j] * a.alpha;
         if (a.drop_p > 0.f) v *= drop_scale(a.drop_p, a.seed, (uint64_t)r * a.N + cv * VE + j);
-        if (a.gate) v *= act_bwd(a.act, g[j]);
+        if (a.gate) v *= act_bwd_t<T>(a.act, g[j]);
         acc[j] += v;
         d[j] = v;
       }

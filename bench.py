@@ -178,6 +178,12 @@ def main():
     flops = 2.0 * M * N_ * K_
     achieved = flops / (avg_ms * 1e-3) / 1e12 if avg_ms > 0 else 0.0
     fpf = model_flops_per_frame(cfg, T, L)
+    traffic = None      # HBM bytes per launch from the committed PMC passes (tools/pmc_traffic.py)
+    tp = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "pmc_traffic.json")
+    if os.path.exists(tp):
+        rec = json.load(open(tp))
+        if rec.get("shape") == [M, N_, K_]:
+            traffic = rec["traffic_bytes"]
     result = {
         "metric": METRIC, "value": round(value, 2), "unit": "AV-frames/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
@@ -189,7 +195,8 @@ def main():
                    "encoder_layers": cfg.num_hidden_layers},
         "roofline": {"bound": "mfma", "kernel": f"dense_kernel bf16 (encoder FFN1 {M}x{N_}x{K_})",
                      "achieved": round(achieved, 1), "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": round(achieved / BF16_PEAK_TFLOPS, 4), "traffic": None,
+                     "frac": round(achieved / BF16_PEAK_TFLOPS, 4), "traffic": traffic,
+                     "traffic_unit": "bytes/launch (rocprofv3 FETCH_SIZEx2+WRITE_SIZE, profiles/pmc_traffic.json)",
                      "launches": len(kern_ms), "avg_launch_ms": round(avg_ms, 4)},
         "model_tflops_per_s": round(value * fpf / world / 1e12, 1),
         "model_mfu": round(value * fpf / world / 1e12 / BF16_PEAK_TFLOPS, 4),

@@ -1,5 +1,5 @@
 """Run one GEMM shape/layout N times (for rocprofv3 counter passes).
-usage: python tools/gemm_one.py M N K [fwd|dgrad|wgrad] [reps]"""
+usage: python tools/gemm_one.py M N K [fwd|ffn1|dgrad|wgrad] [reps]"""
 import os
 import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -14,7 +14,11 @@ x = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
 W = torch.randn(N, K, device=dev, dtype=torch.bfloat16)
 dy = torch.randn(M, N, device=dev, dtype=torch.bfloat16)
 dW = torch.zeros(N, K, device=dev)
-fn = {"fwd": lambda: ops.linear_fwd(x, W), "dgrad": lambda: ops.linear_dgrad(dy, W),
+bias = torch.zeros(N, device=dev)
+h = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+fn = {"fwd": lambda: ops.linear_fwd(x, W),
+      "ffn1": lambda: ops.linear_fwd(x, W, bias, act=1, preact=h, drop_p=0.1, seed=7),   # bench probe's epilogue
+      "dgrad": lambda: ops.linear_dgrad(dy, W),
       "wgrad": lambda: ops.linear_wgrad(dy, x, dW)}[kind]
 for _ in range(reps):
     fn()
