@@ -55,6 +55,7 @@ class ConvParams(ctypes.Structure):
         ("alpha", _f), ("beta", _f),
         ("splitk", _i),
         ("bias", _c_p), ("act", _i), ("preact", _c_p), ("res", _c_p),
+        ("ws", _c_p),
     ]
 
 
@@ -199,6 +200,7 @@ SYMBOLS = {
     "avsr_conv_bwd_data": ([ctypes.POINTER(ConvParams), _c_p], _i),
     "avsr_conv_bwd_weight": ([ctypes.POINTER(ConvParams), _c_p], _i),
     "avsr_conv_stat_tiles": ([ctypes.POINTER(ConvParams)], _i),
+    "avsr_conv_wgrad_ws": ([ctypes.POINTER(ConvParams)], _i64),
     "avsr_layernorm_fwd": ([ctypes.POINTER(LayerNormParams), _c_p], _i),
     "avsr_layernorm_bwd": ([ctypes.POINTER(LayerNormParams), _c_p], _i),
     "avsr_bn_finalize": ([ctypes.POINTER(BnFinalizeParams), _c_p], _i),

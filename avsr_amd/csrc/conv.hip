@@ -38,6 +38,7 @@ struct ConvArgs {
   const void* a; const void* b;   // operand bases (group 0)
   int64_t a_gstride, b_gstride, c_gstride;
   int M, N, K, splits, kchunk;
+  float* ws;                      // bwd_weight split-K slabs [groups][splits][M][N] (nullptr: direct / atomics)
   Epi e;
 };
 
@@ -385,7 +386,8 @@ __global__ __launch_bounds__(CF::NTH, CF::MINB) void conv_glds_kernel(ConvArgs a
     gemmg::mainloop_glds<CF>(la, lb, kbeg, nk, acc, smem);
   }
   Epi e = a.e;
-  e.C = (OutT*)e.C + (int64_t)grp * a.c_gstride;
+  if (KIND == K_WGRAD && a.ws) e.C = a.ws + ((int64_t)grp * a.splits + sp) * a.M * a.N;
+  else e.C = (OutT*)e.C + (int64_t)grp * a.c_gstride;
   if (e.res) e.res = (const bf16*)e.res + (int64_t)grp * a.c_gstride;
   if (e.preact) e.preact = (bf16*)e.preact + (int64_t)grp * a.c_gstride;
   if (e.bias) e.bias += (int64_t)grp * a.c_gstride;
@@ -457,6 +459,53 @@ static void base_epi(Epi& e) {
   e.drop_base = 0; e.stats = nullptr; e.stats_tiles = 0;
 }
 
+// weight-gradient split-K plan. The LDS-DMA path writes per-split fp32 slabs (plain stores)
+// and reduces them afterwards: device-scope fp32 atomics on the 8-XCD part are resolved beyond
+// the per-XCD L2 and sustain only ~50 G adds/s (measured: splits x M x N atomics dominated the
+// ResNet wgrad at 683 splits), while a slab costs 8 bytes/float of HBM traffic. ~512 blocks
+// (2 per CU) with >= 16 K-tiles each.
+struct WgradPlan { int splits, kchunk; bool slab; };
+
+static WgradPlan wgrad_plan(const avsr_conv_params* p, bool glds, bool with_ws) {
+  const int M = p->cout, N = p->kh * p->kw * p->cin, K = p->nimg * p->hout * p->wout;
+  const int bm = tile_bm(M, N), bn = N <= 64 ? 64 : (M <= 64 ? 256 : 128);
+  const long tiles = (long)((M + bm - 1) / bm) * ((N + bn - 1) / bn) * p->groups;
+  WgradPlan w;
+  const int kq = glds ? GBK : BKE;
+  long splits = p->splitk;
+  w.slab = glds && with_ws;
+  if (splits <= 0) {
+    const long target = w.slab ? 512 : 2048;
+    const long want = (target + tiles - 1) / tiles;
+    const long maxs = w.slab ? (K + 1023) / 1024 : (K + 2047) / 2048;
+    splits = want < maxs ? want : maxs;
+    if (splits < 1) splits = 1;
+  }
+  w.kchunk = (int)(((K + splits - 1) / splits + kq - 1) / kq * kq);
+  w.splits = (K + w.kchunk - 1) / w.kchunk;
+  if (w.splits <= 1) { w.splits = 1; w.slab = false; }
+  return w;
+}
+
+// dw[g] += sum over a chunk of splits of ws[g][s]; chunks > 1 combine with fp32 atomics
+// (chunks x M x N of them, a few hundred thousand at most)
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* ws, int splits, int chunks, int64_t mn,
+                                                           float* dw, int64_t dw_gstride) {
+  const int g = blockIdx.y, c = blockIdx.z;
+  const int s0 = (int)((int64_t)splits * c / chunks), s1 = (int)((int64_t)splits * (c + 1) / chunks);
+  const float* w = ws + (int64_t)g * splits * mn;
+  float* d = dw + (int64_t)g * dw_gstride;
+  for (int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4; i < mn; i += (int64_t)gridDim.x * 1024) {
+    f32x4 s = {0.f, 0.f, 0.f, 0.f};
+    for (int q = s0; q < s1; ++q) s += *(const f32x4*)(w + (int64_t)q * mn + i);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {       // dw is a view into the parameter arena: 4-byte aligned only
+      if (chunks == 1) d[i + r] += s[r];
+      else atomicAdd(d + i + r, s[r]);
+    }
+  }
+}
+
 }  // namespace
 
 extern "C" int avsr_conv_stat_tiles(const avsr_conv_params* p) {
@@ -475,7 +524,7 @@ extern "C" int avsr_conv_fwd(const avsr_conv_params* p, void* stream) {
   a.a = p->x; a.b = p->w;
   a.a_gstride = p->cin; a.b_gstride = (int64_t)p->cout * p->kh * p->kw * p->cin; a.c_gstride = p->cout;
   a.M = p->nimg * p->hout * p->wout; a.N = p->cout; a.K = p->kh * p->kw * p->cin;
-  a.splits = 1; a.kchunk = a.K;
+  a.splits = 1; a.kchunk = a.K; a.ws = nullptr;
   set_extents(a, p, (p->cin % 64) == 0,
               ((int64_t)p->nimg * p->hin * p->win - 1) * p->ldx + p->cin, (int64_t)p->cout * a.K);
   base_epi(a.e);
@@ -500,7 +549,7 @@ extern "C" int avsr_conv_bwd_data(const avsr_conv_params* p, void* stream) {
   a.a = p->dy; a.b = p->w;
   a.a_gstride = p->cout; a.b_gstride = (int64_t)p->cout * p->kh * p->kw * p->cin; a.c_gstride = p->cin;
   a.M = p->nimg * p->hin * p->win; a.N = p->cin; a.K = p->kh * p->kw * p->cout;
-  a.splits = 1; a.kchunk = a.K;
+  a.splits = 1; a.kchunk = a.K; a.ws = nullptr;
   set_extents(a, p, (p->cout % 64) == 0 && (p->sh == 1 || p->sh == 2) && p->sw == p->sh,
               ((int64_t)p->nimg * p->hout * p->wout - 1) * p->ldy + p->cout, (int64_t)p->cout * a.K);
   base_epi(a.e);
@@ -527,25 +576,35 @@ extern "C" int avsr_conv_bwd_weight(const avsr_conv_params* p, void* stream) {
   if (a.K == 0) return 0;
   set_extents(a, p, true, ((int64_t)p->nimg * p->hout * p->wout - 1) * p->ldy + p->cout,
               ((int64_t)p->nimg * p->hin * p->win - 1) * p->ldx + p->cin);
-  int splits = p->splitk;
-  if (splits <= 0) {
-    const int bm = tile_bm(a.M, a.N), bn = a.N <= 64 ? 64 : (a.M <= 64 ? 256 : 128);
-    const long tiles = (long)((a.M + bm - 1) / bm) * ((a.N + bn - 1) / bn) * p->groups;
-    long want = (2048 + tiles - 1) / tiles;                 // ~8 blocks per CU
-    long maxs = (a.K + 2047) / 2048;                          // keep >= 64 K-tiles per block
-    splits = (int)(want < maxs ? want : maxs);
-    if (splits < 1) splits = 1;
-  }
-  a.splits = splits;
   const bool glds = p->dtype == AVSR_BF16 && conv_glds_enabled();
-  const int kq = glds ? GBK : BKE;
-  a.kchunk = ((a.K + splits - 1) / splits + kq - 1) / kq * kq;
-  a.splits = (a.K + a.kchunk - 1) / a.kchunk;
+  const WgradPlan w = wgrad_plan(p, glds, p->ws != nullptr);
+  a.splits = w.splits; a.kchunk = w.kchunk;
+  a.ws = w.slab ? p->ws : nullptr;
   base_epi(a.e);
-  a.e.M = a.M; a.e.N = a.N; a.e.C = p->dw; a.e.ldc = ktot; a.e.atomic = 1; a.e.alpha = 1.f;
+  a.e.M = a.M; a.e.N = a.N; a.e.C = p->dw; a.e.ldc = ktot; a.e.alpha = 1.f;
+  if (w.slab) { a.e.ldc = a.N; }                       // plain stores into the slabs
+  else if (w.splits == 1) { a.e.beta = 1.f; }          // dw += wgrad, one writer per element
+  else { a.e.atomic = 1; }
   hipStream_t st = (hipStream_t)stream;
   if (p->dtype == AVSR_F32) return by_tile<float, float, K_WGRAD>(a, p->groups, st);
-  if (p->dtype == AVSR_BF16)
-    return glds ? glds_by_tile<float, K_WGRAD>(a, p->groups, st) : by_tile<bf16, float, K_WGRAD>(a, p->groups, st);
-  return AVSR_E_DTYPE;
+  if (p->dtype != AVSR_BF16) return AVSR_E_DTYPE;
+  if (!glds) return by_tile<bf16, float, K_WGRAD>(a, p->groups, st);
+  rc = glds_by_tile<float, K_WGRAD>(a, p->groups, st);
+  if (rc || !w.slab) return rc;
+  const int64_t mn = (int64_t)a.M * a.N;
+  const int xb = avsr_grid(mn / 4, 256, 1024);
+  int chunks = (int)((65536 / 256 + (int64_t)xb * p->groups - 1) / ((int64_t)xb * p->groups));
+  if (chunks > w.splits) chunks = w.splits;
+  if (chunks < 1) chunks = 1;
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)xb, (unsigned)p->groups, (unsigned)chunks), dim3(256), 0, st,
+                     (const float*)p->ws, w.splits, chunks, mn, p->dw, a.c_gstride);
+  AVSR_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int64_t avsr_conv_wgrad_ws(const avsr_conv_params* p) {
+  if (!p || p->dtype != AVSR_BF16 || !conv_glds_enabled()) return 0;
+  const WgradPlan w = wgrad_plan(p, true, true);
+  if (!w.slab) return 0;
+  return (int64_t)p->groups * w.splits * p->cout * ((int64_t)p->kh * p->kw * p->cin);
 }

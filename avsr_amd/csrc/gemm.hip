@@ -208,25 +208,6 @@ int by_tile(const avsr_gemm_params* p, const DenseArgs& a, hipStream_t st) {
   return by_layout<T, OutT, 2, 2>(p, a, st);
 }
 
-// split-K slab reduce: C[b] = alpha * sum_s ws[b][s] + beta * C[b]   (fp32, 4 columns/thread)
-__global__ __launch_bounds__(256) void slab_reduce_kernel(const float* ws, int splits, int M, int N, float* C,
-                                                          int64_t ldc, int64_t sC, float alpha, float beta) {
-  const int nq = N / 4;
-  const int64_t per = (int64_t)M * nq;
-  const int b = blockIdx.y;
-  const int64_t mn = (int64_t)M * N;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < per; i += (int64_t)gridDim.x * 256) {
-    const int m = (int)(i / nq), n = (int)(i % nq) * 4;
-    const float* w = ws + (int64_t)b * splits * mn + (int64_t)m * N + n;
-    f32x4 s = *(const f32x4*)w;
-    for (int q = 1; q < splits; ++q) s += *(const f32x4*)(w + q * mn);
-    float* c = C + (int64_t)b * sC + (int64_t)m * ldc + n;
-    f32x4 o = s * alpha;
-    if (beta != 0.f) o += *(const f32x4*)c * beta;
-    *(f32x4*)c = o;
-  }
-}
-
 bool getenv_flag(const char* name) {
   const char* e = getenv(name);
   return e && e[0] == '1';

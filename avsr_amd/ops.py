@@ -4,6 +4,7 @@ Each function validates shapes/dtypes on the host, then launches on the caller's
 stream. Nothing here computes on the CPU; a missing library raises (no fallback).
 """
 import ctypes
+import os
 
 import torch
 
@@ -180,13 +181,24 @@ def conv_bwd_data(g, dy, w, dx, alpha=1.0, beta=0.0):
     return dx
 
 
-def conv_bwd_weight(g, x, dy, dw, splitk=0):
-    """dw (fp32, [groups*cout, kh, kw, cin]) += wgrad(x, dy)."""
+_WGRAD_SLAB = os.environ.get("AVSR_WGRAD_SLAB", "1") == "1"   # 0: atomic split-K (A/B runs)
+
+
+def conv_bwd_weight(g, x, dy, dw, splitk=0, slab=None):
+    """dw (fp32, [groups*cout, kh, kw, cin]) += wgrad(x, dy). The split-K partials go to an
+    fp32 slab workspace from the caching allocator (slab=False: fp32 atomics instead)."""
     p = g.params(dtype_code(x))
     assert x.dtype == dy.dtype and dw.dtype == torch.float32
     p.x, p.dy, p.dw = x.data_ptr(), dy.data_ptr(), dw.data_ptr()
     p.splitk = splitk
-    L.check(L.load().avsr_conv_bwd_weight(ctypes.byref(p), L.stream_ptr()), "avsr_conv_bwd_weight")
+    lib = L.load()
+    ws = None
+    if _WGRAD_SLAB if slab is None else slab:
+        n = lib.avsr_conv_wgrad_ws(ctypes.byref(p))
+        if n > 0:
+            ws = torch.empty(n, device=dw.device, dtype=torch.float32)
+            p.ws = ws.data_ptr()
+    L.check(lib.avsr_conv_bwd_weight(ctypes.byref(p), L.stream_ptr()), "avsr_conv_bwd_weight")
     return dw
 
 

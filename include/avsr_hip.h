@@ -83,7 +83,8 @@ int avsr_gemm(const avsr_gemm_params* p, void* stream);
  *   w [groups*cout][kh][kw][cin]  (= torch channels_last physical order)
  * fwd:         y  = conv(x, w)                          (+ BN partial statistics if stats)
  * bwd_data:    dx = alpha * conv_transpose(dy, w) (+ beta * dx)
- * bwd_weight:  dw (fp32) += conv_wgrad(x, dy)   (split-K, fp32 atomics)
+ * bwd_weight:  dw (fp32) += conv_wgrad(x, dy)   (split-K over pixels: fp32 slabs in ws, reduced
+ *              by a second kernel; without ws, fp32 atomics)
  * Replaces: nn.Conv2d in src/nets/backend/backbones/resnet.py:10-22 (3x3 and 1x1
  *   downsample, ResNet-18 trunk), nn.Conv3d stem resnet.py:132 (as a 2-D conv over 5
  *   time-stacked channels, see avsr_stem_pack), and the grouped pos-conv Conv1d
@@ -106,6 +107,7 @@ typedef struct {
   /* fwd epilogue (optional): h = conv + bias[c]; preact = h; y = act(h) + res  (res/preact
    * laid out like y; used by the pos-conv: x + GELU(conv(x) + b)) */
   const float* bias; int act; void* preact; const void* res;
+  float* ws;      /* bwd_weight split-K workspace of avsr_conv_wgrad_ws() floats, or NULL */
 } avsr_conv_params;
 
 int avsr_conv_fwd(const avsr_conv_params* p, void* stream);
@@ -113,6 +115,8 @@ int avsr_conv_bwd_data(const avsr_conv_params* p, void* stream);
 int avsr_conv_bwd_weight(const avsr_conv_params* p, void* stream);
 /* number of row tiles the forward partial statistics are split into */
 int avsr_conv_stat_tiles(const avsr_conv_params* p);
+/* fp32 workspace (floats) bwd_weight uses when p->ws is given (0: it needs none) */
+int64_t avsr_conv_wgrad_ws(const avsr_conv_params* p);
 
 /* ------------------------------------------------------------------------------------
  * LayerNorm over the last dim (rows of N), fp32 statistics.

@@ -101,3 +101,31 @@ def test_gemm_splitk(dev):
     ops.gemm(a, b, c, M=M, N=N, K=K, a_kmajor=False, b_kmajor=False, lda=M, ldb=N, ldc=N, splitk=16)
     ref = a.double().t() @ b.double()
     assert _rel(c, ref) < 1e-2
+
+
+@pytest.mark.parametrize("splitk", [0, 1, 3, 40])
+@pytest.mark.parametrize("case", [(40, 22, 22, 64, 64, 3, 1, 1), (30, 11, 11, 128, 256, 3, 2, 1)])
+def test_wgrad_slab_accumulates(dev, case, splitk):
+    """Split-K weight gradient through the fp32 slab workspace (+ chunked reduce) matches the
+    atomic path and torch, accumulates into a non-zero dw, and tolerates a 4-byte-aligned dw view."""
+    n, h, w, cin, cout, k, s, p = case
+    g = torch.Generator().manual_seed(n + cout)
+    x = torch.randn(n, cin, h, w, generator=g)
+    geom = ops.ConvGeom(n, h, w, cin, cout, k, k, (s, s), (p, p))
+    ho, wo = geom.hout, geom.wout
+    dyt = torch.randn(n, cout, ho, wo, generator=g)
+    xr = x.double().requires_grad_()
+    wr = torch.zeros(cout, cin, k, k, dtype=torch.float64, requires_grad=True)
+    F.conv2d(xr, wr, stride=s, padding=p).backward(dyt.double())
+    xd = x.permute(0, 2, 3, 1).contiguous().to(dev, torch.bfloat16)
+    dy = dyt.permute(0, 2, 3, 1).contiguous().to(dev, torch.bfloat16)
+    init = torch.randn(cout, k, k, cin, generator=g)
+    buf = torch.zeros(1 + init.numel(), device=dev)
+    dw = buf[1:].view(cout, k, k, cin)                   # offset by one float
+    dw.copy_(init.to(dev))
+    ops.conv_bwd_weight(geom, xd, dy, dw, splitk=splitk)
+    dwa = init.to(dev).clone()
+    ops.conv_bwd_weight(geom, xd, dy, dwa, splitk=splitk, slab=False)
+    ref = wr.grad.permute(0, 2, 3, 1) + init.double()
+    assert _rel(dw, ref) < 2e-2
+    assert _rel(dw - init.to(dev), dwa - init.to(dev)) < 1e-4
