@@ -193,6 +193,20 @@ class BeamSelectParams(ctypes.Structure):
     ]
 
 
+class FbankParams(ctypes.Structure):
+    _fields_ = [
+        ("B", _i), ("T", _i), ("wav", _c_p), ("ldw", _i64), ("n_samples", _c_p),
+        ("bins", _i * 28), ("preemph", _f), ("ln_eps", _f), ("out", _c_p),
+    ]
+
+
+class VideoNormParams(ctypes.Structure):
+    _fields_ = [
+        ("B", _i), ("T", _i), ("H", _i), ("W", _i), ("crop", _i), ("oy", _i), ("ox", _i),
+        ("frames", _c_p), ("mean", _f), ("std", _f), ("out", _c_p),
+    ]
+
+
 SYMBOLS = {
     "avsr_version": ([], ctypes.c_char_p),
     "avsr_gemm": ([ctypes.POINTER(GemmParams), _c_p], _i),
@@ -240,6 +254,8 @@ SYMBOLS = {
     "avsr_ctc_prefix": ([ctypes.POINTER(CtcPrefixParams), _c_p], _i),
     "avsr_beam_select": ([ctypes.POINTER(BeamSelectParams), _c_p], _i),
     "avsr_gather_rows": ([_i, _i, _i64, _c_p, _i64, _i64, _c_p, _i64, _i64, _c_p, _c_p], _i),
+    "avsr_fbank_stack": ([ctypes.POINTER(FbankParams), _c_p], _i),
+    "avsr_video_normalize": ([ctypes.POINTER(VideoNormParams), _c_p], _i),
 }
 
 _lib = None

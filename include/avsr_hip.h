@@ -445,6 +445,41 @@ int avsr_gather_rows(int groups, int n, int64_t row_bytes, const void* src, int6
                      int64_t src_rstride, void* dst, int64_t dst_gstride, int64_t dst_rstride,
                      const int* idx, void* stream);
 
+/* ------------------------------------------------------------------------------------
+ * Input front end (the collator's per-clip CPU transforms moved on device).
+ * avsr_fbank_stack: log mel filterbank features of 16 kHz waveforms, stacked 4 frames per
+ *   video frame and layer-normalised per row, written in the model's audios layout.
+ *   Replaces FBanksAndStack.forward src/dataset/avhubert_dataset.py:108-116 (logfbank of
+ *   python_speech_features 0.6 at :111: preemphasis 0.97, 400-sample frames every 160,
+ *   rectangular window, |rfft_512|^2 / 512, 26 triangular mel filters, eps floor, log;
+ *   stacker :91-106; F.layer_norm over 104, eps 1e-5) + collate_pad's 0.0 row padding
+ *   (:280-311) + the permute to (B, 104, T) (:351).
+ *   wav [B][ldw] f32 (clip b uses n_samples[b] >= 1 samples, e.g. 640 * video frames after
+ *   cut_or_pad :22-33); out [B][104][T] f32, rows >= ceil(frames_b / 4) are zero.
+ *   bins: the 28 filter edges floor(513 * mel2hz(linspace(0, hz2mel(8000), 28)) / 16000).
+ * avsr_video_normalize: uint8 frames [B][T][H][W] -> f32 [B][1][T][crop][crop] =
+ *   ((x / 255) cropped at (oy, ox) - mean) / std.  Replaces VideoTransform
+ *   (avhubert_dataset.py:225-246: /255, CenterCrop(88) or RandomCrop(88) offsets,
+ *   Normalize(0.421, 0.165)) + the collator permute (:350).
+ * ------------------------------------------------------------------------------------ */
+typedef struct {
+  int B, T;                  /* clips, output rows (>= the longest clip's rows) */
+  const float* wav; int64_t ldw;
+  const int64_t* n_samples;  /* device [B] */
+  int bins[28];
+  float preemph, ln_eps;
+  float* out;
+} avsr_fbank_params;
+int avsr_fbank_stack(const avsr_fbank_params* p, void* stream);
+
+typedef struct {
+  int B, T, H, W, crop, oy, ox;
+  const uint8_t* frames;
+  float mean, std;
+  float* out;
+} avsr_video_norm_params;
+int avsr_video_normalize(const avsr_video_norm_params* p, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
