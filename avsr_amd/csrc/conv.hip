@@ -462,8 +462,7 @@ static void base_epi(Epi& e) {
 // weight-gradient split-K plan. The LDS-DMA path writes per-split fp32 slabs (plain stores)
 // and reduces them afterwards: device-scope fp32 atomics on the 8-XCD part are resolved beyond
 // the per-XCD L2 and sustain only ~50 G adds/s (measured: splits x M x N atomics dominated the
-// ResNet wgrad at 683 splits), while a slab costs 8 bytes/float of HBM traffic. ~512 blocks
-// (2 per CU) with >= 16 K-tiles each.
+// ResNet wgrad at 683 splits), while a slab costs 8 bytes/float of HBM traffic.
 struct WgradPlan { int splits, kchunk; bool slab; };
 
 static WgradPlan wgrad_plan(const avsr_conv_params* p, bool glds, bool with_ws) {
@@ -475,8 +474,10 @@ static WgradPlan wgrad_plan(const avsr_conv_params* p, bool glds, bool with_ws) 
   long splits = p->splitk;
   w.slab = glds && with_ws;
   if (splits <= 0) {
-    const long target = w.slab ? 512 : 2048;
-    const long want = (target + tiles - 1) / tiles;
+    // slab: ~2 full rounds of 512 block slots (2 per CU), rounded DOWN so the last round is
+    // not a 1-block tail (513 blocks cost 2 rounds: measured 812 -> ~550 us on stage 1)
+    const long target = w.slab ? 1024 : 2048;
+    const long want = w.slab ? (target / tiles > 0 ? target / tiles : 1) : (target + tiles - 1) / tiles;
     const long maxs = w.slab ? (K + 1023) / 1024 : (K + 2047) / 2048;
     splits = want < maxs ? want : maxs;
     if (splits < 1) splits = 1;
