@@ -93,6 +93,30 @@ def cpu_baseline(model_cfg, state, T, threads):
     return T / dt, dt
 
 
+def frontend_timing(B, T, dev, reps=5):
+    """Device front end on one C2 batch -- 16 x 240000-sample waveforms -> log-fbank /
+    stack / LN, 16 x T x 96 x 96 uint8 frames -> crop / normalise. Reported beside the metric,
+    not part of `value` (the reference runs these in CPU collator workers)."""
+    from avsr_amd import frontend
+    g = torch.Generator(device="cpu").manual_seed(99)
+    wav = (0.1 * torch.randn(B, 640 * T, generator=g)).to(dev)
+    ns = torch.full((B,), 640 * T, dtype=torch.int64)
+    fr = torch.randint(0, 256, (B, T, 96, 96), generator=g, dtype=torch.uint8).to(dev)
+    frontend.audio_features(wav, ns, T=T)
+    frontend.video_transform(fr)
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        frontend.audio_features(wav, ns, T=T)
+        frontend.video_transform(fr)
+    e.record()
+    torch.cuda.synchronize()
+    ms = s.elapsed_time(e) / reps
+    return {"ms_per_batch": round(ms, 3), "clips_per_s": round(B / ms * 1e3, 1),
+            "what": f"{B} clips: log-fbank+stack4+LN of {640 * T} samples and crop/normalise of {T}x96x96 u8 frames"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -202,6 +226,7 @@ def main():
         "model_mfu": round(value * fpf / world / 1e12 / BF16_PEAK_TFLOPS, 4),
         "loss": [round(x, 4) for x in losses],
     }
+    result["frontend"] = frontend_timing(B, T, dev)
     if state_cpu is not None:
         threads = min(16, os.cpu_count() or 1)
         fps, dt = cpu_baseline(cfg, state_cpu, T, threads)
