@@ -441,6 +441,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
   const int nt = (kend + 63) / 64;
   const float sl2 = a.scale * LOG2E;
   const uint64_t dbase = ((uint64_t)(b * a.H + h) * a.Lq + qi) * (uint64_t)a.Lk;
+  const DropTile dt(a.drop_p, a.seed, (uint64_t)a.B * a.H * a.Lq * a.Lk);
   Pref pk, pv;
   if (nt > 0) {
     pref_load(pk, K, a.ldk, 0, a.Lk, tid); pref_load(pv, V, a.ldv, 0, a.Lk, tid);
@@ -491,8 +492,8 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
     if (a.drop_p > 0.f) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        s0[r] *= drop_scale(a.drop_p, a.seed, dbase + kt0 + qrow(r, hh));
-        s1[r] *= drop_scale(a.drop_p, a.seed, dbase + kt0 + 32 + qrow(r, hh));
+        s0[r] *= dt.scale(a.seed, dbase + kt0 + qrow(r, hh));
+        s1[r] *= dt.scale(a.seed, dbase + kt0 + 32 + qrow(r, hh));
       }
     }
     const bf16x8 p0a = accb(s0, 0), p0b = accb(s0, 1), p1a = accb(s1, 0), p1b = accb(s1, 1);
@@ -543,6 +544,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnArgs a) {
   const int qstart = a.causal ? (int)blockIdx.x * 128 : 0;
   const int nt = a.Lq > qstart ? (a.Lq - qstart + 63) / 64 : 0;
   const uint64_t bh = (uint64_t)(b * a.H + h);
+  const DropTile dt(a.drop_p, a.seed, (uint64_t)a.B * a.H * a.Lq * a.Lk);
   Pref pq, po;
   float lsr = 0.f, dlr = 0.f;
   auto fetch = [&](int qt0) {
@@ -565,6 +567,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnArgs a) {
     const bf16* Qs = sm + slot * 2 * IMG;
     const bf16* dOs = Qs + IMG;
     if (t + 1 < nt) fetch(qt0 + 64);
+    // dropout indices of this tile: (bh*Lq + q)*Lk + key for q in [qt0, qt0+64), key < Lk
+    const uint64_t dt0 = (bh * a.Lq + qt0) * (uint64_t)a.Lk;
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       f32x16 sc, dp;
@@ -579,7 +583,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnArgs a) {
         const int ql = 32 * u + qrow(r, hh), q = qt0 + ql;
         const bool ok = q < a.Lq && key < klen && (!a.causal || key <= q);
         const float p = ok ? exp2f(sc[r] * sl2 - lss[slot][ql]) : 0.f;
-        const float keep = (a.drop_p > 0.f && ok) ? drop_scale(a.drop_p, a.seed, (bh * a.Lq + q) * (uint64_t)a.Lk + key) : 1.f;
+        const float keep = (a.drop_p > 0.f && ok) ? dt.scale(a.seed, dt0 + (uint64_t)ql * a.Lk + key) : 1.f;
         sc[r] = p * keep;                                       // P' = dropout(P)
         dp[r] = p * (dp[r] * keep - dls[slot][ql]) * a.scale;   // dS (scaled)
       }
@@ -634,6 +638,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs a, OutT* dq, 
   const int nt = (kend + 63) / 64;
   const float sl2 = a.scale * LOG2E;
   const uint64_t dbase = (uint64_t)bhq * (uint64_t)a.Lk;
+  const DropTile dt(a.drop_p, a.seed, (uint64_t)a.B * a.H * a.Lq * a.Lk);
   Pref pk, pv;
   if (nt > 0) {
     pref_load(pk, K, a.ldk, 0, a.Lk, tid); pref_load(pv, V, a.ldv, 0, a.Lk, tid);
@@ -659,7 +664,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs a, OutT* dq, 
         const int kk = kt0 + 32 * u + qrow(r, hh);
         const bool ok = kk < klen && (!a.causal || kk <= qi);
         const float p = ok ? exp2f(st[r] * sl2 - lq) : 0.f;
-        const float keep = (a.drop_p > 0.f && ok) ? drop_scale(a.drop_p, a.seed, dbase + kk) : 1.f;
+        const float keep = (a.drop_p > 0.f && ok) ? dt.scale(a.seed, dbase + kk) : 1.f;
         dpt[r] = p * (dpt[r] * keep - dl) * a.scale;
       }
       const bf16x8 sa = accb(dpt, 0), sb = accb(dpt, 1);

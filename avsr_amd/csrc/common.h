@@ -43,10 +43,32 @@ AVSR_DEV uint32_t fmix32(uint32_t h) {
   h ^= h >> 13; h *= 0xC2B2AE35u;
   return h ^ (h >> 16);
 }
-AVSR_DEV uint32_t mix32(uint64_t seed, uint64_t idx) {
-  const uint32_t lo = (uint32_t)idx, hi = (uint32_t)(idx >> 32);
-  return fmix32((lo * 0x9E3779B1u) ^ (uint32_t)seed ^ fmix32(hi ^ (uint32_t)(seed >> 32) ^ 0x68E31DA4u));
+// mix32 = mix32_lo(mix32_hi(seed, hi), lo): callers whose index range shares one high word
+// hoist mix32_hi and pay one finaliser per element (bit-identical mask)
+AVSR_DEV uint32_t mix32_hi(uint64_t seed, uint32_t hi) {
+  return (uint32_t)seed ^ fmix32(hi ^ (uint32_t)(seed >> 32) ^ 0x68E31DA4u);
 }
+AVSR_DEV uint32_t mix32_lo(uint32_t pre, uint32_t lo) { return fmix32((lo * 0x9E3779B1u) ^ pre); }
+AVSR_DEV uint32_t mix32(uint64_t seed, uint64_t idx) {
+  return mix32_lo(mix32_hi(seed, (uint32_t)(idx >> 32)), (uint32_t)idx);
+}
+// dropout over an index space of `total` elements: when every index fits in 32 bits (a
+// kernel-uniform test, e.g. B*H*Lq*Lk = 36 M for the C2 encoder attention) the high-word mix
+// is a constant and each element costs one finaliser; same mask as drop_scale
+struct DropTile {
+  uint32_t pre, thr; float keep_scale; bool small;
+  AVSR_DEV DropTile(float p, uint64_t seed, uint64_t total) {
+    thr = (uint32_t)(p * 4294967296.0f);
+    keep_scale = 1.0f / (1.0f - p);
+    small = total <= 0x100000000ull;
+    pre = mix32_hi(seed, 0u);
+  }
+  AVSR_DEV float scale(uint64_t seed, uint64_t idx) const {
+    const uint32_t h = small ? mix32_lo(pre, (uint32_t)idx) : mix32(seed, idx);
+    return h >= thr ? keep_scale : 0.0f;
+  }
+};
+
 AVSR_DEV float drop_scale(float p, uint64_t seed, uint64_t idx) {
   // returns 0 for dropped, 1/(1-p) for kept
   uint32_t thr = (uint32_t)(p * 4294967296.0f);
