@@ -124,9 +124,16 @@ __global__ __launch_bounds__(256) void lsm_bwd_kernel(avsr_xent_params p) {
 // ------------------------------------------------------------------------------- CTC
 AVSR_DEV int ext_label(const int* lab, int s) { return (s & 1) ? lab[s >> 1] : 0; }
 
+// One block per utterance; the recursions are sequential in t, so every global access is
+// taken off the per-step critical path: extended labels / skip flags live in LDS, and the
+// emissions lp(t, s) = x[t][l'(s)] - lse[t] (and, for the beta pass, alpha) are gathered
+// cooperatively into LDS in chunks of CH time steps -- one exposed memory latency per chunk
+// instead of one per step.
+constexpr int CTC_CHUNK = 6144;   // floats per LDS chunk buffer
+
 template <typename T>
 __global__ __launch_bounds__(256) void ctc_fwd_kernel(avsr_ctc_params p) {
-  const int b = blockIdx.x;
+  const int b = blockIdx.x, tid = threadIdx.x;
   const int L = p.label_len[b], Tb = min(p.in_len[b], p.T), S = 2 * L + 1;
   const int SS = 2 * p.Lmax + 1;
   const int* lab = p.labels + (int64_t)b * p.Lmax;
@@ -135,74 +142,101 @@ __global__ __launch_bounds__(256) void ctc_fwd_kernel(avsr_ctc_params p) {
   float* A = p.alpha + (int64_t)b * p.T * SS;
   float* G = p.gamma + (int64_t)b * p.T * SS;
   __shared__ float buf[2][1024];
+  __shared__ float E[CTC_CHUNK], AC[CTC_CHUNK];
+  __shared__ int kl[1024];
+  __shared__ unsigned char sk[1024];
   __shared__ float logp_s;
   if (S > 1024 || Tb <= 0) {   // unsupported label length or empty input: zero_infinity semantics
-    for (int i = threadIdx.x; i < p.T * SS; i += 256) G[i] = 0.f;
-    if (threadIdx.x == 0) p.nll[b] = 0.f;
+    for (int i = tid; i < p.T * SS; i += 256) G[i] = 0.f;
+    if (tid == 0) p.nll[b] = 0.f;
     return;
   }
-  auto lp = [&](int t, int s) -> float {
-    const int k = ext_label(lab, s);
-    return to_f(X[(int64_t)t * p.ldx + k]) - LSE[t];
+  const int CH = max(1, min(64, CTC_CHUNK / S));
+  for (int s = tid; s < S; s += 256) kl[s] = ext_label(lab, s);
+  __syncthreads();
+  for (int s = tid; s < S; s += 256) sk[s] = s >= 2 && (s & 1) && kl[s] != kl[s - 2];
+  // E[(t - t0) * S + s] = lp(t, s) for t in [t0, t0 + n); optionally AC = alpha of the same range
+  auto load = [&](int t0, int n, bool with_alpha) {
+    for (int i = tid; i < n * S; i += 256) {
+      const int dt = i / S, s = i - dt * S, t = t0 + dt;
+      E[i] = to_f(X[(int64_t)t * p.ldx + kl[s]]) - LSE[t];
+      if (with_alpha) AC[i] = A[(int64_t)t * SS + s];
+    }
   };
+  __syncthreads();
   // alpha
-  for (int s = threadIdx.x; s < S; s += 256) {
-    const float a0 = s < 2 ? lp(0, s) : NEG;
+  int t0 = 0;
+  load(0, min(CH, Tb), false);
+  __syncthreads();
+  for (int s = tid; s < S; s += 256) {
+    const float a0 = s < 2 ? E[s] : NEG;
     buf[0][s] = a0;
     A[s] = a0;
   }
   __syncthreads();
   for (int t = 1; t < Tb; ++t) {
+    if (t - t0 >= CH) {
+      t0 = t;
+      load(t0, min(CH, Tb - t0), false);
+      __syncthreads();
+    }
     const float* prev = buf[(t - 1) & 1];
     float* cur = buf[t & 1];
-    for (int s = threadIdx.x; s < S; s += 256) {
-      float v = prev[s];
+    const float* e = E + (t - t0) * S;
+    for (int s = tid; s < S; s += 256) {
       const float a1 = s >= 1 ? prev[s - 1] : NEG;
-      float a2 = NEG;
-      if (s >= 2 && (s & 1) && ext_label(lab, s) != ext_label(lab, s - 2)) a2 = prev[s - 2];
-      v = lse3(v, a1, a2);
-      const float r = v <= NEG ? NEG : v + lp(t, s);
+      const float a2 = sk[s] ? prev[s - 2] : NEG;
+      const float v = lse3(prev[s], a1, a2);
+      const float r = v <= NEG ? NEG : v + e[s];
       cur[s] = r;
       A[(int64_t)t * SS + s] = r;
     }
     __syncthreads();
   }
-  if (threadIdx.x == 0) {
+  if (tid == 0) {
     const float* last = buf[(Tb - 1) & 1];
     logp_s = S > 1 ? lse2(last[S - 1], last[S - 2]) : last[S - 1];
   }
   __syncthreads();
   const float logp = logp_s;
   const bool feasible = logp > NEG * 0.5f;
-  if (threadIdx.x == 0) p.nll[b] = feasible ? -logp : 0.f;
+  if (tid == 0) p.nll[b] = feasible ? -logp : 0.f;
   // beta (reuse buf), occupancy gamma_t(s) = exp(alpha + beta - lp - logP)
-  for (int i = threadIdx.x; i < p.T * SS; i += 256) {
+  for (int i = tid; i < p.T * SS; i += 256) {
     const int t = i / SS;
     if (t >= Tb || !feasible || (i % SS) >= S) G[i] = 0.f;
   }
   if (!feasible) return;
+  __syncthreads();                       // alpha in global memory visible to the whole block
+  t0 = max(0, Tb - CH);
+  load(t0, Tb - t0, true);
   __syncthreads();
-  for (int s = threadIdx.x; s < S; s += 256) {
-    const float l = lp(Tb - 1, s);
+  for (int s = tid; s < S; s += 256) {
+    const int i = (Tb - 1 - t0) * S + s;
+    const float l = E[i];
     const float b0 = s >= S - 2 ? l : NEG;
     buf[(Tb - 1) & 1][s] = b0;
-    const float a = A[(int64_t)(Tb - 1) * SS + s];
+    const float a = AC[i];
     G[(int64_t)(Tb - 1) * SS + s] = (a <= NEG || b0 <= NEG) ? 0.f : expf(a + b0 - l - logp);
   }
   __syncthreads();
   for (int t = Tb - 2; t >= 0; --t) {
+    if (t < t0) {
+      t0 = max(0, t - CH + 1);
+      load(t0, t + 1 - t0, true);
+      __syncthreads();
+    }
     const float* nxt = buf[(t + 1) & 1];
     float* cur = buf[t & 1];
-    for (int s = threadIdx.x; s < S; s += 256) {
-      float v = nxt[s];
+    const int base = (t - t0) * S;
+    for (int s = tid; s < S; s += 256) {
       const float b1 = s + 1 < S ? nxt[s + 1] : NEG;
-      float b2 = NEG;
-      if (s + 2 < S && (s & 1) && ext_label(lab, s) != ext_label(lab, s + 2)) b2 = nxt[s + 2];
-      v = lse3(v, b1, b2);
-      const float l = lp(t, s);
+      const float b2 = (s + 2 < S && sk[s + 2]) ? nxt[s + 2] : NEG;
+      const float v = lse3(nxt[s], b1, b2);
+      const float l = E[base + s];
       const float r = v <= NEG ? NEG : v + l;
       cur[s] = r;
-      const float a = A[(int64_t)t * SS + s];
+      const float a = AC[base + s];
       G[(int64_t)t * SS + s] = (a <= NEG || r <= NEG) ? 0.f : expf(a + r - l - logp);
     }
     __syncthreads();

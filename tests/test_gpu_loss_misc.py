@@ -16,6 +16,47 @@ def _rel(a, b):
     return ((a - b).abs().max() / b.abs().max().clamp_min(1e-30)).item()
 
 
+@pytest.mark.parametrize("T,lens,in_len", [(375, (40, 33), (375, 300)), (240, (150, 7), (240, 240))])
+def test_ctc_multi_chunk(dev, T, lens, in_len):
+    """C2-length inputs (several LDS emission chunks per recursion; S = 301 -> 20-step chunks)
+    against torch's CTC in fp64: nll and the logits gradient."""
+    B, V, Vp = 2, 5049, 5056
+    g = torch.Generator().manual_seed(T)
+    x = torch.randn(B * T, Vp, generator=g) * 2
+    x[:, V:] = 0
+    labels = [torch.randint(1, V - 1, (n,), generator=g).tolist() for n in lens]
+    labels[0][3] = labels[0][4]                       # a repeat (no skip transition)
+    Lmax = max(lens)
+    lab = torch.full((B, Lmax), -1, dtype=torch.int32)
+    for b, l in enumerate(labels):
+        lab[b, :len(l)] = torch.tensor(l)
+    xd = x.to(dev)
+    lse = torch.empty(B * T, device=dev)
+    ops.row_lse(xd, V, lse)
+    S = 2 * Lmax + 1
+    alpha = torch.empty(B, T, S, device=dev); gamma = torch.empty(B, T, S, device=dev)
+    nll = torch.empty(B, device=dev)
+    p = ops.ctc_params(xd, B, T, V, lab.to(dev), torch.tensor(list(lens), dtype=torch.int32, device=dev),
+                       torch.tensor(list(in_len), dtype=torch.int32, device=dev), lse, alpha, gamma, nll)
+    ops.ctc_fwd(p)
+    xr = x.double()[:, :V].view(B, T, V).transpose(0, 1).contiguous().requires_grad_()
+    tgt = torch.cat([torch.tensor(l) for l in labels])
+    ref = F.ctc_loss(xr.log_softmax(-1), tgt, torch.tensor(list(in_len)), torch.tensor(list(lens)), blank=0,
+                     reduction="none", zero_infinity=True)
+    assert _rel(nll, ref) < 1e-5
+    ref.sum().backward()
+    gref = xr.grad.transpose(0, 1).reshape(B * T, V)
+    dx = torch.empty(B * T, Vp, device=dev)
+    ops.ctc_bwd(p, torch.tensor([1.0], device=dev), 1.0, dx)
+    # fp32 log-space recursions over T steps: held to torch's own fp32 CTC error (as test_ctc)
+    x32 = x.float()[:, :V].view(B, T, V).transpose(0, 1).contiguous().requires_grad_()
+    F.ctc_loss(x32.log_softmax(-1), tgt, torch.tensor(list(in_len)), torch.tensor(list(lens)), blank=0,
+               reduction="none", zero_infinity=True).sum().backward()
+    e32 = _rel(x32.grad.transpose(0, 1).reshape(B * T, V), gref)
+    err = _rel(dx[:, :V], gref)
+    assert err < max(3 * e32, 1e-4), (err, e32)
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_ctc(dev, dtype):
     B, T, V, Vp = 4, 50, 5049, 5056
