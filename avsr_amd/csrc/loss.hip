@@ -18,6 +18,14 @@ AVSR_DEV float lse3(float a, float b, float c) {
   return m <= NEG ? NEG : m + logf(expf(a - m) + expf(b - m) + expf(c - m));
 }
 
+// CTC recursion step: hardware exp2 / log2 (v_exp_f32 / v_log_f32, ~1 ulp) instead of the
+// libm sequences on the recursion's dependent chain (measured 408 -> 352 us per C2 batch);
+// the max term contributes exp(0) = 1 exactly
+AVSR_DEV float lse3_fast(float a, float b, float c) {
+  const float m = fmaxf(a, fmaxf(b, c));
+  return m <= NEG ? NEG : m + __logf(__expf(a - m) + __expf(b - m) + __expf(c - m));
+}
+
 // block-wide reductions (256 threads)
 AVSR_DEV float block_max(float v, float* sh) {
   v = wave_max(v);
@@ -186,7 +194,7 @@ __global__ __launch_bounds__(256) void ctc_fwd_kernel(avsr_ctc_params p) {
     for (int s = tid; s < S; s += 256) {
       const float a1 = s >= 1 ? prev[s - 1] : NEG;
       const float a2 = sk[s] ? prev[s - 2] : NEG;
-      const float v = lse3(prev[s], a1, a2);
+      const float v = lse3_fast(prev[s], a1, a2);
       const float r = v <= NEG ? NEG : v + e[s];
       cur[s] = r;
       A[(int64_t)t * SS + s] = r;
@@ -232,7 +240,7 @@ __global__ __launch_bounds__(256) void ctc_fwd_kernel(avsr_ctc_params p) {
     for (int s = tid; s < S; s += 256) {
       const float b1 = s + 1 < S ? nxt[s + 1] : NEG;
       const float b2 = (s + 2 < S && sk[s + 2]) ? nxt[s + 2] : NEG;
-      const float v = lse3(nxt[s], b1, b2);
+      const float v = lse3_fast(nxt[s], b1, b2);
       const float l = E[base + s];
       const float r = v <= NEG ? NEG : v + l;
       cur[s] = r;
