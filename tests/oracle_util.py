@@ -28,6 +28,48 @@ def tiny_cfg():
     return O.OracleConfig.from_dict(TINY_CONFIG)
 
 
+# ---------------------------------------------------------------------------- full size
+GOLDEN_FULL = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "avsr_full.npz")
+TOKENS = ["<blank>"] + [f"u{i}" for i in range(1, 5048)] + ["<eos>"]
+
+
+def load_golden_full():
+    return dict(np.load(GOLDEN_FULL, allow_pickle=False))
+
+
+def full_state(g, seed=0):
+    return golden_state(g, seed)
+
+
+def _digest(*arrays):
+    import hashlib
+    h = hashlib.sha256()
+    for a in arrays:
+        h.update(np.ascontiguousarray(a).tobytes())
+    return h.hexdigest()
+
+
+def full_c1_batch(g):
+    """C1 inputs of tests/golden/make_golden_full.py, regenerated from their seed and
+    checked against the digest the generator stored."""
+    from tests.golden.full_inputs import C1
+    from oracle.weights import make_inputs
+    frames, feats, lengths, _ = make_inputs(B=C1["B"], T=C1["T"], lengths=C1["lengths"], seed=C1["seed"])
+    b = collate(frames, feats, lengths, [(1,)] * C1["B"])
+    assert _digest(b["videos"], b["audios"]) == str(g["c1_digest"]), "C1 input regeneration drifted"
+    return b
+
+
+def full_train_batch(g):
+    """the T=375 train-step batch of make_golden_full.py (B=2, second row padded to 300)."""
+    from tests.golden.full_inputs import TR, TR_LABELS
+    from oracle.weights import make_inputs
+    frames, feats, lengths, _ = make_inputs(B=TR["B"], T=TR["T"], lengths=TR["lengths"], seed=TR["seed"])
+    b = collate(frames, feats, lengths, TR_LABELS)
+    assert _digest(b["videos"], b["audios"], b["labels"]) == str(g["tr_digest"]), "train input regeneration drifted"
+    return b
+
+
 def rel(a, b):
     a = torch.as_tensor(np.asarray(a), dtype=torch.float64)
     b = torch.as_tensor(np.asarray(b), dtype=torch.float64)
