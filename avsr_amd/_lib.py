@@ -240,6 +240,7 @@ SYMBOLS = {
     "avsr_embed_fwd": ([ctypes.POINTER(EmbedParams), _c_p], _i),
     "avsr_embed_bwd": ([ctypes.POINTER(EmbedParams), _c_p], _i),
     "avsr_cast": ([_i, _i, _i, _i, _c_p, _i64, _c_p, _i64, _f, _f, _c_p], _i),
+    "avsr_cast_flat": ([_i, _i, _i64, _c_p, _c_p, _c_p], _i),
     "avsr_stem_pack": ([_i, _i, _i, _c_p, _c_p, _c_p], _i),
     "avsr_stem_wpack": ([_i, _c_p, _c_p, _c_p], _i),
     "avsr_stem_wgrad_unpack": ([_c_p, _c_p, _c_p], _i),

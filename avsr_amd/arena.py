@@ -96,18 +96,21 @@ class Arena:
         self.exp_avg = None
         self.exp_avg_sq = None
         self.shadow = torch.zeros(self.total, device=dev, dtype=compute_dtype) if compute_dtype != torch.float32 else None
-        # re-home parameters
+        # re-home parameters; .grad of each trainable parameter is a view of the gradient arena
+        # (the frozen ones — mask_emb, label_embs_concat — get no gradient, as in the reference)
         self.params = {}
+        self._frozen = frozen
         for n in self.order:
             m = self.meta[n]
             old = params[n]
             view = self._logical(self.data, m)
             view.copy_(old.detach().to(dev))
             newp = nn.Parameter(view, requires_grad=old.requires_grad)
-            newp.grad = self._logical(self.grad, m)
             mod, attr = owners[n]
             mod._parameters[attr] = newp
             self.params[n] = newp
+        self.grad_views = {n: self._logical(self.grad, self.meta[n]) for n in self.order if n not in frozen}
+        self.attach_grads(zero=False)
         self.sync_shadow()
 
     @staticmethod
@@ -167,15 +170,43 @@ class Arena:
 
     # ------------------------------------------------------------------ maintenance
     def sync_shadow(self):
-        """refresh the compute-dtype shadow from the fp32 master (after loading weights)."""
+        """refresh the compute-dtype shadow from the fp32 master (after loading weights or an
+        update by a per-parameter optimizer). One flat vectorised cast launch."""
         if self.shadow is not None:
             if self.device.type == "cpu":          # layout tests only (no kernels run on CPU)
                 self.shadow.copy_(self.data)
             else:
-                ops.cast(self.data.view(1, -1), self.shadow.view(1, -1))
+                ops.cast_flat(self.data, self.shadow)
+        self._synced_version = self.data._version
+
+    def ensure_shadow(self):
+        """in-place writes through the parameter views (torch.optim steps, load_state_dict,
+        param.data.copy_) bump the arena's version counter: refresh the shadow if any happened
+        since the last sync. The fused optimizer writes master + shadow in one kernel."""
+        if self.data._version != self._synced_version:
+            self.sync_shadow()
+
+    def attach_grads(self, zero=True):
+        """(re)attach the gradient-arena views as .grad. A per-parameter optimizer's
+        zero_grad(set_to_none=True) (HF Trainer, torch.optim) sets .grad to None: those
+        parameters' gradients restart from zero, so their arena slices are cleared first (one
+        memset when every parameter was reset)."""
+        missing = [n for n, v in self.grad_views.items() if self.params[n].grad is not v]
+        if not missing:
+            return
+        if zero:
+            if len(missing) == len(self.grad_views):
+                self.grad.zero_()
+            else:
+                for n in missing:
+                    if self.params[n].grad is None:
+                        self.grad_views[n].zero_()
+        for n in missing:
+            self.params[n].grad = self.grad_views[n]
 
     def zero_grad(self):
         self.grad.zero_()
+        self.attach_grads(zero=False)
 
     def init_optimizer(self):
         if self.exp_avg is None:

@@ -210,7 +210,8 @@ class BatchBeamSearch:
                     ended.append(self._make_hyp(hyp))
                 else:
                     keep.append(hyp)
-            if end_detect([h.asdict() for h in ended], i):
+            # beam_search.py:369: end detection only when the length limit is the input length
+            if maxlenratio == 0.0 and end_detect([h.asdict() for h in ended], i):
                 break
             if not keep:
                 break

@@ -23,6 +23,7 @@ Design (MI355X-first):
 import math
 import random
 
+import numpy as np
 import torch
 
 from . import ops
@@ -80,6 +81,17 @@ class Engine:
         self.PK = cfg.num_conv_pos_embeddings
         assert self.D // self.H == 64 and self.dD // self.dH == 64, "kernels use head dim 64"
         assert cfg.adim == self.D == self.dD, "proj_decoder (adim != ddim) not on the hot path"
+        # configuration the reference reads but the engine does not implement: refuse loudly
+        if getattr(cfg, "layerdrop", 0.0):
+            raise NotImplementedError("layerdrop > 0 (avhubert.py:710-712) is not implemented by the engine")
+        if getattr(cfg, "transformer_length_normalized_loss", False):
+            raise NotImplementedError("transformer_length_normalized_loss=True is not implemented by the engine")
+        if getattr(cfg, "modality_fuse", "concat") != "concat":
+            raise NotImplementedError("modality_fuse='add' is not implemented by the engine")
+        if getattr(cfg, "modality", "av") not in ("av", "audio", "video"):
+            raise ValueError(f"unknown modality {cfg.modality!r}")
+        self.last_modality = None
+        self.capture = None          # tests: a dict receives the last forward's enc / logits / batch
         E = "encoder.encoder.layers"
         groups = []
         for i in range(self.nl):
@@ -125,6 +137,34 @@ class Engine:
         self._stem_wp = None
 
     # ------------------------------------------------------------------------------ utils
+    @staticmethod
+    def new_seeds(seed=None):
+        """per-step dropout stream ids (counter-based hash masks, recomputed in the backward)"""
+        return _Seeds(random.getrandbits(48) if seed is None else seed)
+
+    def draw_modality(self, train):
+        """which frontend's features are zeroed (avhubert.py:471-482): cfg.modality 'audio' /
+        'video' always zero the other stream; in training with 'av' the reference draws two
+        numbers from numpy's global RNG per forward (np.random.random() twice, unconditionally)
+        and drops a modality with probability modality_dropout. Same RNG, same draw order, so a
+        seeded run makes the same decisions as the reference."""
+        cfg = self.cfg
+        mod = getattr(cfg, "modality", "av")
+        if mod == "audio":
+            return "video_off"
+        if mod == "video":
+            return "audio_off"
+        if not train:
+            return None
+        p_modality, p_audio = np.random.random(), np.random.random()
+        if p_modality < cfg.modality_dropout:
+            return "audio_off" if p_audio < cfg.audio_dropout else "video_off"
+        return None
+
+    def ensure_pe(self, L_):
+        if self._pe.shape[0] < L_:
+            self._pe = positional_encoding(2 * L_, self.dD, self.device)
+
     def _e(self, *shape, dtype=None):
         return torch.empty(*shape, device=self.device, dtype=dtype or self.dtype)
 
@@ -521,8 +561,7 @@ class Engine:
         p_d = cfg.dropout_rate if train else 0.0
         p_att = cfg.transformer_attn_dropout_rate if train else 0.0
         y = self._e(R, D)
-        if self._pe.shape[0] < L1:
-            self._pe = positional_encoding(2 * L1, self.dD, self.device)
+        self.ensure_pe(L1)
         ops.embed_fwd(bt["ys_in"], self.w("decoder.embed.0.weight"), self._pe[:L1], math.sqrt(D), y, L1,
                       drop_p=p_d, seed=sd_e)
         ctx = {"sd_e": sd_e, "p_d": p_d, "p_att": p_att, "layers": [], "klen": klen, "L1": L1}
@@ -647,17 +686,12 @@ class Engine:
     def forward(self, videos, audios, video_lengths, labels, train=True, need_grad=True, seed=None):
         """E2E.forward: returns (out4 = [loss, loss_ctc, loss_att, acc] on device, ctx)."""
         cfg = self.cfg
-        if seed is None:
-            seed = random.getrandbits(48)
-        seeds = _Seeds(seed)
+        seeds = self.new_seeds(seed)
         bt = self.prepare(videos, audios, video_lengths, labels)
         B, T = bt["B"], bt["T"]
         M = B * T
-        modality = None
-        if train and cfg.modality == "av" and cfg.modality_dropout > 0:
-            # avhubert.py:476-482: np.random draws; here a host RNG (no bit-parity possible)
-            if random.random() < cfg.modality_dropout:
-                modality = "audio_off" if random.random() < cfg.audio_dropout else "video_off"
+        modality = self.draw_modality(train)
+        self.last_modality = modality
         enc, ectx = self.encoder_fwd(audios.to(self.device), videos.to(self.device), bt, train, need_grad, seeds, modality)
         # CTC branch: ctc_lo(dropout(enc))
         sd_c = seeds.next()
@@ -686,6 +720,8 @@ class Engine:
         ops.lsm_fwd(dlog, self.V, bt["ys_out"], cfg.lsm_weight, dlse, rloss, rcorr)
         out4 = self._e(4, dtype=torch.float32)
         ops.loss_finalize(B, nll, rloss, rcorr, cfg.mtlalpha, out4)
+        if self.capture is not None:
+            self.capture.update(enc=enc, clog=clog, dlog=dlog, bt=bt)
         ctx = None
         if need_grad:
             ctx = dict(bt=bt, enc=enc, ectx=ectx, xin=xin, p_c=p_c, sd_c=sd_c, clog=clog, cp=cp, dlog=dlog, dctx=dctx,
@@ -719,11 +755,14 @@ class Engine:
         self.encoder_bwd(ctx["ectx"], denc)
 
     # ========================================================================= inference
-    def encode(self, audios, videos, video_lengths=None):
-        """eval-mode encoder (script/evaluation.py:96-101 call form: no attention mask)."""
+    def encode(self, audios, videos, video_lengths=None, train=False):
+        """encoder forward without graph (script/evaluation.py:96-101 call form: eval mode, no
+        attention mask); train=True: dropouts / BatchNorm batch statistics, as the reference's
+        encoder in train mode under no_grad."""
         B, _, T = videos.shape[:3]
         if video_lengths is None:
             video_lengths = torch.full((B,), T, dtype=torch.int64)
         bt = self.prepare(videos, audios, video_lengths)
-        x, _ = self.encoder_fwd(audios.to(self.device), videos.to(self.device), bt, False, False, _Seeds(0))
+        x, _ = self.encoder_fwd(audios.to(self.device), videos.to(self.device), bt, train, False,
+                                self.new_seeds(None if train else 0), self.draw_modality(train))
         return x.view(B, T, self.D)

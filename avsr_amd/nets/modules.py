@@ -1,9 +1,11 @@
 """Parameter containers of the AVSR model, with the reference's exact module tree (and so its
 exact state-dict keys, shapes and buffers — SURVEY.md §8(b) row b2).
 
-These modules only *hold* parameters and buffers; their `forward` is never used. The whole
-forward/backward runs in avsr_amd.engine.Engine on HIP kernels over a flat parameter arena
-(avsr_amd.arena.Arena), which re-homes every parameter defined here into one fp32 buffer.
+These modules hold the parameters and buffers. The whole forward/backward runs in
+avsr_amd.engine.Engine on HIP kernels over a flat parameter arena (avsr_amd.arena.Arena),
+which re-homes every parameter defined here into one fp32 buffer. The sub-modules callers of
+the reference use directly — `avsr.encoder(...)`, `avsr.decoder.batch_score(...)`,
+`avsr.ctc.log_softmax(...)` — forward to the engine (avsr_amd.surface).
 
 Reference module tree (file:line):
   E2E                        src/nets/backend/e2e_asr_avhubert.py:24-117
@@ -25,6 +27,14 @@ from torch import nn
 class _Holder(nn.Module):
     def forward(self, *a, **k):  # pragma: no cover - never called
         raise RuntimeError("parameter container: the forward runs in avsr_amd.engine.Engine")
+
+
+def _e2e(mod):
+    """the E2E that owns this sub-module (set by avsr_amd.avhubert_avsr_model.E2E)"""
+    owner = getattr(mod, "_e2e", None)
+    if not owner:
+        raise RuntimeError(f"{type(mod).__name__} is not attached to an E2E model")
+    return owner[0]
 
 
 def _conv3x3(i, o, stride=1):
@@ -162,6 +172,11 @@ class AVHubertModel(_Holder):
         final_dim = cfg.final_dim if cfg.final_dim > 0 else e
         self.label_embs_concat = nn.Parameter(torch.FloatTensor(cfg.num_classes, final_dim).uniform_())
 
+    def forward(self, input_features, attention_mask=None, video=None, **kwargs):
+        """avhubert.py:546-561 on the engine -> BaseModelOutput(last_hidden_state (B, T, D))."""
+        from ..surface import encoder_forward
+        return encoder_forward(_e2e(self), input_features, attention_mask=attention_mask, video=video, **kwargs)
+
 
 class MHA(_Holder):
     """MultiHeadedAttention (attention.py:16-35)."""
@@ -204,11 +219,57 @@ class Decoder(_Holder):
         self.after_norm = nn.LayerNorm(d, eps=1e-12)
         self.output_layer = nn.Linear(d, odim)
 
+    # decoder.py:122-227 on the engine (ESPnet BatchScorerInterface)
+    def forward(self, tgt, tgt_mask, memory, memory_mask):
+        from ..surface import decoder_forward
+        return decoder_forward(_e2e(self), tgt, tgt_mask, memory, memory_mask)
+
+    def forward_one_step(self, tgt, tgt_mask, memory, memory_mask=None, cache=None):
+        from ..surface import decoder_forward_one_step
+        return decoder_forward_one_step(_e2e(self), tgt, tgt_mask, memory, memory_mask=memory_mask, cache=cache)
+
+    def score(self, ys, state, x):
+        from ..surface import decoder_score
+        return decoder_score(_e2e(self), ys, state, x)
+
+    def batch_score(self, ys, states, xs):
+        from ..surface import decoder_batch_score
+        return decoder_batch_score(_e2e(self), ys, states, xs)
+
+    def init_state(self, x):              # scorer_interface.py (decoder state = None)
+        return None
+
+    def select_state(self, state, i, new_id=None):
+        return None if state is None else state[i]
+
+    def batch_init_state(self, x):
+        return None
+
 
 class CTCHead(_Holder):
+    """CTC (ctc.py:12-180): ctc_lo + the loss / log-softmax / argmax entry points on the engine."""
+
     def __init__(self, odim, d):
         super().__init__()
         self.ctc_lo = nn.Linear(d, odim)
+
+    def forward(self, hs_pad, hlens, ys_pad):
+        from ..surface import ctc_forward
+        return ctc_forward(_e2e(self), hs_pad, hlens, ys_pad)
+
+    def log_softmax(self, hs_pad):
+        from ..surface import ctc_log_softmax
+        return ctc_log_softmax(_e2e(self), hs_pad)
+
+    def softmax(self, hs_pad):
+        return self.log_softmax(hs_pad).exp_()
+
+    def argmax(self, hs_pad):
+        from ..surface import ctc_argmax
+        return ctc_argmax(_e2e(self), hs_pad)
+
+
+CTC = CTCHead
 
 
 class E2EShell(_Holder):

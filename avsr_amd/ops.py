@@ -454,6 +454,14 @@ def cast(src, dst, alpha=1.0, beta=0.0):
     return dst
 
 
+def cast_flat(src, dst):
+    """dst = src over two contiguous buffers of the same length (any dtype pair)."""
+    assert src.is_contiguous() and dst.is_contiguous() and src.numel() == dst.numel()
+    L.check(L.load().avsr_cast_flat(dtype_code(src), dtype_code(dst), src.numel(), src.data_ptr(), dst.data_ptr(),
+                                    L.stream_ptr()), "avsr_cast_flat")
+    return dst
+
+
 def stem_pack(videos, out):
     B, _, T = videos.shape[:3]
     assert videos.dtype == torch.float32 and videos.is_contiguous()

@@ -127,6 +127,8 @@ def main():
     ap.add_argument("--labels", type=int, default=40)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--layers", type=int, default=None, help="debug only: fewer encoder layers (INVALID for the metric)")
+    ap.add_argument("--seed", type=int, default=1234, help="seeds the inputs, dropout streams and the "
+                    "modality-dropout draws (numpy global RNG, as the reference draws them)")
     args = ap.parse_args()
 
     from avsr_amd import parallel
@@ -157,16 +159,24 @@ def main():
     opt = FusedAdamW(arena, lr=1e-4, weight_decay=0.005, max_grad_norm=1.0)
 
     B, T, L = args.batch, args.seq, args.labels
-    v, a, lens, lab = synthetic_batch(B, T, L, seed=1234 + rank)
+    v, a, lens, lab = synthetic_batch(B, T, L, seed=args.seed + rank)
     v, a = v.to(dev), a.to(dev)
     mtl = cfg.mtlalpha
     d_ctc = torch.full((1,), mtl, device=dev)
     d_att = torch.full((1,), 1.0 - mtl, device=dev)
 
+    # modality dropout (avhubert.py:476-482) draws from numpy's global RNG like the reference;
+    # seeded here so that the timed steps' decisions are reproducible and reported
+    np.random.seed(args.seed + 7919 * rank)
+    drops = []
+    step_seed = [args.seed * 1000003 + rank]
+
     def step():
         arena.zero_grad()
         reducer.begin()
-        out4, ctx = eng.forward(v, a, lens, lab, train=True, need_grad=True)
+        step_seed[0] += 1
+        out4, ctx = eng.forward(v, a, lens, lab, train=True, need_grad=True, seed=step_seed[0])
+        drops.append(eng.last_modality)
         eng.backward(ctx, d_ctc, d_att)
         reducer.finish(average=False)
         opt.step(grad_scale=1.0 / world)
@@ -182,6 +192,7 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    drops.clear()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         out4 = step()
@@ -225,6 +236,10 @@ def main():
         "model_tflops_per_s": round(value * fpf / world / 1e12, 1),
         "model_mfu": round(value * fpf / world / 1e12 / BF16_PEAK_TFLOPS, 4),
         "loss": [round(x, 4) for x in losses],
+        "modality_drops": {"seed": args.seed, "video_off": drops.count("video_off"),
+                           "audio_off": drops.count("audio_off"), "none": drops.count(None),
+                           "note": "rank 0's timed steps; video_off skips the ResNet backward "
+                                   "(its gradient is exactly zero, avhubert.py:480)"},
     }
     result["frontend"] = frontend_timing(B, T, dev)
     if state_cpu is not None:

@@ -311,6 +311,8 @@ int avsr_loss_finalize(int B, const float* nll, int rows, const float* row_loss,
  *                  PositionalEncoding, decoder.py:89-93, embedding.py:80-87); bwd: fp32
  *                  atomics into dtable
  * avsr_cast:       dst = alpha * src + beta * dst over a [rows][cols] strided view
+ * avsr_cast_flat:  dst = src over n contiguous elements (fp32 -> bf16 vectorised: the arena's
+ *                  master -> compute-shadow refresh after load_state_dict / optimizer steps)
  * avsr_stem_pack:  videos (B,1,T,88,88) fp32 -> (B*T, 88, 88, 8): channel c = frame t+c-2
  *                  (c < 5, zero outside [0,T)), the Conv3d(k=5x7x7, pad 2x3x3) stem as a 2-D conv
  * avsr_stem_wpack / avsr_stem_wgrad_unpack: Conv3d weight (64,1,5,7,7) <-> [64][7][7][8]
@@ -346,6 +348,7 @@ int avsr_embed_bwd(const avsr_embed_params* p, void* stream);
 
 int avsr_cast(int src_dtype, int dst_dtype, int rows, int cols, const void* src, int64_t lds,
               void* dst, int64_t ldd, float alpha, float beta, void* stream);
+int avsr_cast_flat(int src_dtype, int dst_dtype, int64_t n, const void* src, void* dst, void* stream);
 int avsr_stem_pack(int dtype, int B, int T, const float* video, void* out, void* stream);
 int avsr_stem_wpack(int dtype, const float* w, void* wp, void* stream);
 int avsr_stem_wgrad_unpack(const float* gp, float* gw, void* stream);

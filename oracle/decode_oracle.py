@@ -89,7 +89,7 @@ def end_detect(ended, i, M=3, D_end=np.log(1 * np.exp(-10))):
     return count == M
 
 
-def beam_search(sd, cfg, x, ctc_logp, beam_size, ctc_weight=0.1):
+def beam_search(sd, cfg, x, ctc_logp, beam_size, ctc_weight=0.1, maxlenratio=0.0):
     """BatchBeamSearch(x) for one encoded utterance x (T, D). Returns the ended hypotheses
     sorted by score (best first)."""
     V = cfg.odim
@@ -98,7 +98,8 @@ def beam_search(sd, cfg, x, ctc_logp, beam_size, ctc_weight=0.1):
     w_dec, w_ctc = 1.0 - ctc_weight, ctc_weight
     pre_beam = int(1.5 * beam_size)
     T = x.shape[0]
-    maxlen = T
+    # beam_search.py:349-354
+    maxlen = T if maxlenratio == 0 else (-int(maxlenratio) if maxlenratio < 0 else max(1, int(maxlenratio * T)))
     running = [Hyp([sos], 0.0, {"decoder": 0.0, "ctc": 0.0}, None, 0.0)]
     ended = []
     for i in range(maxlen):
@@ -128,7 +129,7 @@ def beam_search(sd, cfg, x, ctc_logp, beam_size, ctc_weight=0.1):
         running = []
         for h in best:
             (ended if h.yseq[-1] == eos else running).append(h)
-        if end_detect(ended, i):
+        if maxlenratio == 0.0 and end_detect(ended, i):      # beam_search.py:369
             break
         if not running:
             break

@@ -1,0 +1,174 @@
+"""The reference's module-level call surface on the HIP engine, tiny
+config, fp32 parity mode, against the CPU oracle (itself pinned to the reference's golden
+vectors): the differentiable encoder sub-module, the decoder's forward / forward_one_step /
+batch_score with reference-format caches, CTC.forward / log_softmax / argmax, cfg.modality,
+and per-parameter optimizers (torch.optim) driving the arena-backed parameters."""
+import numpy as np
+import pytest
+import torch
+
+from avsr_amd.avhubert_avsr_model import AVHubertAVSR
+from avsr_amd.configuration_avhubert_avsr import AVHubertAVSRConfig
+from oracle import avsr_oracle as O
+from oracle.weights import NO_DROPOUT, TINY_CONFIG
+from tests.oracle_util import golden_batch, golden_state, load_golden, rel, tiny_cfg
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def g():
+    return load_golden()
+
+
+def _model(g, dtype=torch.float32, **over):
+    cfg = AVHubertAVSRConfig(**{**TINY_CONFIG, **NO_DROPOUT, **over})
+    m = AVHubertAVSR(cfg)
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in golden_state(g).items()}, strict=True)
+    m.setup_engine("cuda", dtype)
+    return m
+
+
+def _batch(g):
+    return {k: torch.from_numpy(v) for k, v in golden_batch(g).items()}
+
+
+def test_encoder_submodule_train_backward(g):
+    """model.avsr.encoder(input_features, attention_mask, video) in train mode is
+    differentiable: output and every encoder gradient match the oracle."""
+    m = _model(g).train()
+    b = _batch(g)
+    mask = torch.arange(b["videos"].shape[2]).unsqueeze(0) < b["video_lengths"].unsqueeze(1)
+    w = torch.randn(2, b["videos"].shape[2], TINY_CONFIG["hidden_size"], generator=torch.Generator().manual_seed(7))
+    out = m.avsr.encoder(input_features=b["audios"].cuda(), attention_mask=mask.cuda(), video=b["videos"].cuda())
+    x = out.last_hidden_state
+    assert x.requires_grad and x.dtype == torch.float32
+    (x * w.cuda()).sum().backward()
+    sd = O.to_torch_state(golden_state(g), requires_grad=True)
+    ref = O.encoder_forward(sd, tiny_cfg(), b["audios"], b["videos"], mask, train=True)
+    (ref * w).sum().backward()
+    assert rel(x.detach().cpu(), ref.detach()) < 2e-4
+    params = dict(m.named_parameters())
+    n = 0
+    for k, t in sd.items():
+        if not k.startswith("avsr.encoder.") or t.grad is None:
+            continue
+        r = t.grad.double().norm().item()
+        got = params[k].grad.double().norm().item()
+        assert abs(got - r) <= 2e-3 * r + 1e-6, (k, got, r)
+        n += 1
+    assert n > 50
+    # the decoder / CTC head got no gradient from this backward
+    assert params["avsr.ctc.ctc_lo.weight"].grad.abs().max().item() == 0.0
+
+
+def test_decoder_api_matches_oracle(g):
+    m = _model(g).eval()
+    cfg = tiny_cfg()
+    sd = O.to_torch_state(golden_state(g))
+    mem = torch.from_numpy(np.stack([g["dec_enc_0"][:19], g["dec_enc_1"][:19]]))          # (2, 19, D)
+    ys = torch.tensor([[5048, 5, 17, 301, 9], [5048, 4000, 4000, 2, 77]])
+    L = ys.shape[1]
+    causal = torch.tril(torch.ones(L, L, dtype=torch.bool)).unsqueeze(0)
+    mmask = torch.ones(2, 1, 19, dtype=torch.bool)
+    mmask[1, :, 15:] = False
+    logits, _ = m.avsr.decoder(ys.cuda(), causal.cuda(), mem.cuda(), mmask.cuda())
+    with torch.no_grad():
+        ref = O.decoder_forward(sd, cfg, ys, causal, mem, mmask)
+    assert rel(logits.cpu(), ref) < 1e-4
+    # forward_one_step without cache == the oracle's one-step log-probs
+    logp, cache = m.avsr.decoder.forward_one_step(ys.cuda(), causal.cuda(), mem.cuda())
+    with torch.no_grad():
+        ref1 = O.decoder_one_step(sd, cfg, ys, mem)
+    assert rel(logp.cpu(), ref1) < 1e-4
+    assert len(cache) == cfg.dlayers and cache[0].shape == (2, L, cfg.ddim)
+    # chained batch_score with the reference's per-hypothesis states == recomputing from scratch
+    states = [None, None]
+    for step in range(1, L + 1):
+        lp, states = m.avsr.decoder.batch_score(ys[:, :step].cuda(), states, mem.cuda())
+        with torch.no_grad():
+            want = O.decoder_one_step(sd, cfg, ys[:, :step], mem)
+        assert rel(lp.cpu(), want) < 1e-4, step
+        assert states[0][0].shape == (step, cfg.ddim)
+    # score() on one hypothesis
+    lp1, st1 = m.avsr.decoder.score(ys[0, :3].cuda(), None, mem[0].cuda())
+    with torch.no_grad():
+        assert rel(lp1.cpu(), O.decoder_one_step(sd, cfg, ys[:1, :3], mem[:1])[0]) < 1e-4
+
+
+def test_ctc_api_matches_oracle(g):
+    m = _model(g).eval()
+    sd = O.to_torch_state(golden_state(g))
+    x = torch.from_numpy(np.stack([g["dec_enc_0"][:19], g["dec_enc_1"][:19]]))
+    hlens = torch.tensor([19, 15])
+    ys_pad = torch.tensor([[5, 17, 301, 9], [77, 5047, -1, -1]])
+    loss, ys_hat = m.avsr.ctc(x.cuda(), hlens, ys_pad)
+    with torch.no_grad():
+        rloss, rlogits = O.ctc_forward(sd, x, hlens, ys_pad)
+    assert abs(loss.item() - rloss.item()) <= 1e-4 * abs(rloss.item())
+    assert ys_hat.shape == rlogits.shape and rel(ys_hat.cpu(), rlogits) < 1e-4
+    lp = m.avsr.ctc.log_softmax(x.cuda())
+    assert rel(lp.cpu(), torch.log_softmax(rlogits.transpose(0, 1), -1)) < 1e-5
+    am = m.avsr.ctc.argmax(x.cuda())
+    assert torch.equal(am.cpu(), rlogits.transpose(0, 1).argmax(-1))
+
+
+@pytest.mark.parametrize("modality", ["audio", "video"])
+def test_cfg_modality(g, modality):
+    """cfg.modality 'audio' / 'video' zero the other stream's features in train AND eval
+    (avhubert.py:471-474)."""
+    m = _model(g, modality=modality).eval()
+    b = _batch(g)
+    x = m.avsr.encoder(input_features=b["audios"].cuda(), video=b["videos"].cuda()).last_hidden_state
+    sd = O.to_torch_state(golden_state(g))
+    off = "video_off" if modality == "audio" else "audio_off"
+    with torch.no_grad():
+        ref = O.encoder_forward(sd, tiny_cfg(), b["audios"], b["videos"], None, False, modality=off)
+    assert rel(x.cpu(), ref) < 2e-4
+
+
+def test_per_parameter_optimizer_and_zero_grad(g):
+    """HF Trainer / torch.optim drive model.parameters(): zero_grad(set_to_none=True) between
+    steps must restart the gradients (arena views re-attached, slices cleared), and the
+    updated weights must be what the next forward uses. SGD with momentum keeps the update
+    linear in the gradient, so parameters are compared to the oracle doing the same steps."""
+    b = _batch(g)
+    m = _model(g).train()
+    opt = torch.optim.SGD(m.parameters(), lr=0.05, momentum=0.9)
+    sd = O.to_torch_state(golden_state(g), requires_grad=True)
+    keys = [k for k, _ in m.named_parameters()]
+    ref_opt = torch.optim.SGD([sd[k] for k in keys], lr=0.05, momentum=0.9)
+    cfg = tiny_cfg()
+    for step in range(3):
+        opt.zero_grad()                      # set_to_none=True (torch default)
+        ref_opt.zero_grad()
+        out = m(**b)
+        out.loss.backward()
+        loss, *_ = O.e2e_forward(sd, cfg, b["videos"], b["audios"], b["video_lengths"], b["labels"], True)
+        loss.backward()
+        assert abs(out.loss.item() - loss.item()) <= 2e-4 * abs(loss.item()), step
+        opt.step()
+        ref_opt.step()
+    params = dict(m.named_parameters())
+    worst = 0.0
+    for k in keys:
+        r = sd[k].detach()
+        worst = max(worst, (params[k].detach().cpu() - r).abs().max().item() / max(1e-3, r.abs().max().item()))
+    assert worst < 1e-3, worst
+    # model.zero_grad() (HF Trainer) keeps the arena views attached
+    m.zero_grad()
+    p0 = params["avsr.ctc.ctc_lo.weight"]
+    assert p0.grad is not None and p0.grad.abs().max().item() == 0.0
+
+
+def test_bf16_shadow_follows_parameter_writes(g):
+    """in bf16 mode an in-place write through a parameter view (optimizer step, load) is
+    picked up by the next forward: the compute shadow is refreshed."""
+    m = _model(g, torch.bfloat16).train()
+    eng = m.avsr.engine()
+    p = dict(m.named_parameters())["avsr.decoder.output_layer.weight"]
+    with torch.no_grad():
+        p.mul_(0.5)
+    eng = m.avsr.engine()             # every entry point fetches the engine this way
+    a = eng.arena
+    assert torch.equal(a.shadow, a.data.to(torch.bfloat16))
