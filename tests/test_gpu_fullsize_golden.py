@@ -27,7 +27,8 @@ from avsr_amd.avhubert_avsr_model import AVHubertAVSR, get_beam_search_decoder
 from avsr_amd.configuration_avhubert_avsr import AVHubertAVSRConfig
 from oracle.weights import NO_DROPOUT
 from tests.golden.full_inputs import C1, DEC_ROWS, ENC_ROWS
-from tests.oracle_util import TOKENS, full_c1_batch, full_state, full_train_batch, load_golden_full, rel
+from tests.oracle_util import (TOKENS, full_c1_batch, full_state, full_train_batch, load_golden_full, rel,
+                               zero_grad_by_symmetry)
 
 pytestmark = pytest.mark.gpu
 
@@ -188,6 +189,10 @@ def test_train_step_t375(g, model, state, dtype):
     for k, n in zip(g["grad_keys"], g["grad_norm"]):
         k = str(k)
         got = params[k].grad.double().norm().item()
+        if zero_grad_by_symmetry(k):
+            if got > 1e-2:
+                bad.append((k, got, float(n)))
+            continue
         if n > 1e-3:
             worst = max(worst, abs(got - n) / n)
         if abs(got - n) > tol["grad"] * abs(n) + 1e-6:
