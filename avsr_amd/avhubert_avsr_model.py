@@ -6,6 +6,7 @@ Trainer calls `model(**inputs)`), output dataclass and state-dict keys as the re
 The computation runs in avsr_amd.engine.Engine (HIP kernels); there is no CPU / eager
 fallback: using the model on a machine without the HIP library raises.
 """
+import contextlib
 from dataclasses import dataclass
 from typing import Optional
 
@@ -93,6 +94,7 @@ class AVHubertAVSR(PreTrainedModel):
     def __init__(self, config: AVHubertAVSRConfig):
         super().__init__(config)
         self.avsr = E2E(config)
+        self._ddp = None        # parallel.ArenaDDP once attached
         self.post_init()        # HF bookkeeping (tied-weight tables) that from_pretrained relies on
 
     def _init_weights(self, module):   # weights come from the module constructors / checkpoints
@@ -146,6 +148,11 @@ class AVHubertAVSR(PreTrainedModel):
     def half(self):
         raise NotImplementedError("fp16 parameters: the HIP kernels run fp32 (parity) or bf16 (throughput)")
 
+    def no_sync(self):
+        """DistributedDataParallel.no_sync (accelerate calls it on non-final gradient-accumulation
+        micro-steps): delegated to the attached parallel.ArenaDDP."""
+        return self._ddp.no_sync() if self._ddp is not None else contextlib.nullcontext()
+
     def zero_grad(self, set_to_none: bool = True):
         """HF Trainer calls model.zero_grad() around every optimizer step: clear the gradient
         arena and keep the .grad views attached (set_to_none would detach them)."""
@@ -168,9 +175,9 @@ class AVHubertAVSR(PreTrainedModel):
         """HF save_pretrained with the reference's keys and shapes (config.json +
         model.safetensors). The arena's parameters are views of one buffer: hand HF a state
         dict of standalone contiguous host copies."""
-        if "state_dict" not in kwargs:
-            kwargs["state_dict"] = {k: v.detach().to("cpu", copy=True).contiguous()
-                                    for k, v in self.state_dict().items()}
+        sd = kwargs.pop("state_dict", None)
+        sd = self.state_dict() if sd is None else sd
+        kwargs["state_dict"] = {k: v.detach().to("cpu", copy=True).contiguous() for k, v in sd.items()}
         return super().save_pretrained(save_directory, **kwargs)
 
 

@@ -114,17 +114,36 @@ class Engine:
         pad_rows = {"decoder.output_layer.weight": self.Vp, "ctc.ctc_lo.weight": self.Vp,
                     "decoder.output_layer.bias": self.Vp, "ctc.ctc_lo.bias": self.Vp}
         frozen = ["encoder.mask_emb", "encoder.label_embs_concat"]
-        # buffers (BN running statistics) to the device
+        # buffers to the device; the BatchNorm running statistics (fp32 running_mean / var)
+        # are re-homed into ONE flat buffer so that DDP's per-forward buffer broadcast is a
+        # single collective (parallel.ArenaDDP)
+        stats = []
         for m in shell.modules():
             for k, b in list(m._buffers.items()):
                 if b is not None:
                     m._buffers[k] = b.to(self.device)
+                    if k in ("running_mean", "running_var") and b.dtype == torch.float32:
+                        stats.append((m, k))
+        self.bn_flat = torch.empty(sum(m._buffers[k].numel() for m, k in stats), device=self.device)
+        o = 0
+        for m, k in stats:
+            b = m._buffers[k]
+            view = self.bn_flat[o:o + b.numel()].view(b.shape)
+            view.copy_(b)
+            m._buffers[k] = view
+            o += b.numel()
         self.arena = Arena(shell, self.device, dtype, fuse_groups=groups, pad_rows=pad_rows, perms=perms, frozen=frozen)
         # gradient-readiness hook for the overlapped all-reduce (parallel.GradReducer): after
         # encoder layer i's backward, the weight-decay segment is final from the first element of
         # layer i on (the arena keeps module order inside a segment; decoder / CTC head come later
         # and are done before the encoder).
+        # data-parallel hooks (set by parallel.ArenaDDP / bench.py): before_forward() at the start
+        # of a training forward, before_backward() / on_grad_ready(offset) / after_backward()
+        # around the backward (offset: the decay segment is final from there on)
         self.on_grad_ready = None
+        self.before_forward = None
+        self.before_backward = None
+        self.after_backward = None
         d0, d1 = self.arena.segments["decay"]
         self._layer_decay_off = []
         for i in range(self.nl):
@@ -686,6 +705,8 @@ class Engine:
     def forward(self, videos, audios, video_lengths, labels, train=True, need_grad=True, seed=None):
         """E2E.forward: returns (out4 = [loss, loss_ctc, loss_att, acc] on device, ctx)."""
         cfg = self.cfg
+        if train and need_grad and self.before_forward is not None:
+            self.before_forward()
         seeds = self.new_seeds(seed)
         bt = self.prepare(videos, audios, video_lengths, labels)
         B, T = bt["B"], bt["T"]
@@ -738,6 +759,8 @@ class Engine:
         M = B * T
         d_ctc = d_ctc.reshape(1).to(torch.float32)
         d_att = d_att.reshape(1).to(torch.float32)
+        if self.before_backward is not None:
+            self.before_backward()
         # attention loss -> decoder
         dl = ctx["dlog"]
         ddl = self._e(dl.shape[0], self.Vp)
@@ -753,6 +776,8 @@ class Engine:
                  seed=ctx["sd_c"])
         self.decoder_bwd(ctx["dctx"], ddl, ctx["enc"], denc, bt)
         self.encoder_bwd(ctx["ectx"], denc)
+        if self.after_backward is not None:
+            self.after_backward()
 
     # ========================================================================= inference
     def encode(self, audios, videos, video_lengths=None, train=False):

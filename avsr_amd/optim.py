@@ -29,15 +29,26 @@ class FusedAdamW:
         self.step_count = 0
         self._sumsq = torch.zeros(1, device=arena.device)
 
-    def step(self, grad_scale=1.0):
+    def grad_sumsq(self):
+        """sum of squared gradients over the trainable segments (device scalar, no sync)"""
+        a = self.arena
+        d0, _ = a.segments["decay"]
+        _, n1 = a.segments["no_decay"]
+        self._sumsq.zero_()
+        ops.sumsq(a.grad[d0:n1], self._sumsq)
+        return self._sumsq
+
+    def step(self, grad_scale=1.0, sumsq_ready=False):
+        """one AdamW step; with max_grad_norm > 0 the gradients are clipped by the global norm
+        inside the kernel (coef = min(1, max_norm / (norm + 1e-6)), torch.nn.utils.
+        clip_grad_norm_); sumsq_ready: grad_sumsq() was already computed for this step."""
         a = self.arena
         self.step_count += 1
         lr = self.schedule(self.step_count) if self.schedule else self.lr
         d0, d1 = a.segments["decay"]
         n0, n1 = a.segments["no_decay"]
-        self._sumsq.zero_()
-        if self.max_norm and self.max_norm > 0:
-            ops.sumsq(a.grad[d0:n1], self._sumsq)
+        if self.max_norm and self.max_norm > 0 and not sumsq_ready:
+            self.grad_sumsq()
         for (s, e), wd in (((d0, d1), self.wd), ((n0, n1), 0.0)):
             if e <= s:
                 continue
@@ -47,3 +58,75 @@ class FusedAdamW:
                       sumsq_buf=self._sumsq if self.max_norm else None, max_norm=self.max_norm or 1.0,
                       grad_scale=grad_scale)
         return lr
+
+    # ------------------------------------------------------------------ checkpoint / resume
+    def state_dict(self):
+        """optimizer state for resume (script/train.py:280-287,310-314): step count and the
+        arena-layout moments (tensors only: loadable with torch.load(weights_only=True))."""
+        a = self.arena
+        return {"step": self.step_count, "exp_avg": a.exp_avg.detach().clone(),
+                "exp_avg_sq": a.exp_avg_sq.detach().clone(),
+                "hyper": {"lr": self.lr, "betas": list(self.betas), "eps": self.eps, "weight_decay": self.wd,
+                          "max_grad_norm": self.max_norm}}
+
+    def load_state_dict(self, sd):
+        a = self.arena
+        if sd["exp_avg"].numel() != a.exp_avg.numel():
+            raise ValueError("optimizer state was saved for a different parameter arena")
+        a.exp_avg.copy_(sd["exp_avg"])
+        a.exp_avg_sq.copy_(sd["exp_avg_sq"])
+        self.step_count = int(sd["step"])
+
+
+class ArenaAdamW(torch.optim.Optimizer):
+    """torch.optim.AdamW semantics over the parameter arena, for per-parameter training loops
+    (HF Trainer, avsr_amd.trainer.AVSRTrainer): one fused launch per weight-decay segment.
+    param_groups[0] carries lr / betas / eps / weight_decay (HF's LR scheduler writes lr);
+    the state dict has torch's layout (state[0] = step, exp_avg, exp_avg_sq), so Trainer
+    checkpoints save and resume it unchanged. `clip_grad_norm_` computes the global norm and
+    folds the clip coefficient into the next step (no extra pass over the gradients)."""
+
+    def __init__(self, arena, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.01):
+        super().__init__([arena.data], dict(lr=lr, betas=tuple(betas), eps=eps, weight_decay=weight_decay))
+        self.arena = arena
+        self.fused = FusedAdamW(arena, lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, max_grad_norm=0.0)
+        self._clip = 0.0
+        self.state[arena.data] = {"step": torch.zeros((), dtype=torch.float32),
+                                  "exp_avg": arena.exp_avg, "exp_avg_sq": arena.exp_avg_sq}
+
+    def grad_norm(self):
+        return self.fused.grad_sumsq().sqrt()
+
+    def clip_grad_norm_(self, max_norm):
+        """returns the pre-clip global gradient norm; the next step() applies the clip"""
+        norm = self.fused.grad_sumsq().sqrt()
+        self._clip = float(max_norm)
+        return norm
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        g = self.param_groups[0]
+        f = self.fused
+        f.lr, f.betas, f.eps, f.wd = g["lr"], tuple(g["betas"]), g["eps"], g["weight_decay"]
+        f.max_norm = self._clip
+        f.step(sumsq_ready=self._clip > 0)
+        self._clip = 0.0
+        st = self.state[self.arena.data]
+        st["step"] = torch.tensor(float(f.step_count))
+        return loss
+
+    def zero_grad(self, set_to_none=True):
+        self.arena.zero_grad()
+
+    def load_state_dict(self, state_dict):
+        super().load_state_dict(state_dict)
+        a = self.arena
+        st = self.state[a.data]
+        a.exp_avg.copy_(st["exp_avg"])
+        a.exp_avg_sq.copy_(st["exp_avg_sq"])
+        self.fused.step_count = int(float(st["step"]))
+        self.state[a.data] = {"step": st["step"], "exp_avg": a.exp_avg, "exp_avg_sq": a.exp_avg_sq}

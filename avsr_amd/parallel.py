@@ -4,9 +4,19 @@ Replaces the DDP reducer that HF Trainer / accelerate wrap around the reference
 (script/train.py:259-308, src/custom_trainer.py:4-41): gradients live in ONE flat fp32 arena
 buffer, so the all-reduce is a handful of large contiguous buckets (no per-parameter copy
 into bucket storage) issued on a dedicated communication stream. Gradients are averaged
-(sum / world), like DDP. Parameters and BN buffers are broadcast from rank 0 at start; BN
-running statistics follow DDP's broadcast_buffers=True semantics (rank 0's buffers win).
+(sum / world), like DDP.
+
+`ArenaDDP` reproduces the DistributedDataParallel semantics the reference trains under
+(HF Trainer -> accelerate -> DDP, broadcast_buffers=True):
+  * at construction: parameters and buffers broadcast from rank 0;
+  * before a training forward: the BatchNorm running statistics are broadcast from rank 0
+    (one collective over the engine's flat statistics buffer) when the previous forward was a
+    synchronising one — DDP's require_forward_param_sync rule;
+  * backward: buckets all-reduced as soon as their layers' gradients are final, overlapped
+    with the rest of the backward on a communication stream; under `no_sync()` (non-final
+    gradient-accumulation micro-steps) nothing is exchanged and gradients accumulate locally.
 """
+import contextlib
 import os
 
 import torch
@@ -62,6 +72,7 @@ class GradReducer:
         self.stream = torch.cuda.Stream(device=flat_grad.device) if (use_stream and flat_grad.is_cuda) else None
         self._next = 0
         self._works = []
+        self.enabled = True          # False inside ArenaDDP.no_sync(): gradients accumulate locally
 
     def _reduce(self, a, b):
         w = dist.all_reduce(self.flat[a:b], op=dist.ReduceOp.SUM, group=self.group, async_op=self.stream is not None)
@@ -87,7 +98,7 @@ class GradReducer:
 
     def ready(self, offset):
         """the decay segment is final from `offset` on: reduce every bucket inside it"""
-        if self.world == 1:
+        if self.world == 1 or not self.enabled:
             return
         todo = []
         while self._next < len(self.buckets) and self.buckets[self._next][0] >= offset:
@@ -96,7 +107,7 @@ class GradReducer:
         self._launch(todo)
 
     def finish(self, average=False):
-        if self.world == 1:
+        if self.world == 1 or not self.enabled:
             return
         self._launch(self.buckets[self._next:] + self.tail)
         self._next = len(self.buckets)
@@ -125,3 +136,67 @@ def broadcast_state(flat_params, buffers, src=0, group=None):
     dist.broadcast(flat_params, src=src, group=group)
     for b in buffers:
         dist.broadcast(b, src=src, group=group)
+
+
+class ArenaDDP:
+    """DistributedDataParallel semantics for an AVHubertAVSR on the HIP engine (see module
+    docstring). Attach once per process after the engine exists:
+
+        ddp = ArenaDDP(model)                   # broadcasts rank 0's state
+        with ddp.no_sync():                     # GA micro-steps 1..n-1
+            model(**mb).loss.backward()
+        model(**mb_last).loss.backward()        # all-reduce overlapped with this backward
+
+    average=True divides the summed gradients by the world size (DDP); average=False leaves
+    the 1/world factor to FusedAdamW.step(grad_scale=1/world) and saves one pass."""
+
+    def __init__(self, model, bucket_bytes=BUCKET_BYTES, broadcast_buffers=True, average=True, use_stream=True,
+                 group=None):
+        eng = model.avsr.engine()
+        self.model, self.eng, self.group = model, eng, group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        arena = eng.arena
+        int_buffers = [b for b in model.buffers() if not b.is_floating_point()]
+        broadcast_state(arena.data, [eng.bn_flat] + int_buffers, group=group)
+        arena.sync_shadow()
+        self.reducer = GradReducer(arena.grad, bucket_bytes=bucket_bytes, group=group, use_stream=use_stream,
+                                   segment=arena.segments["decay"])
+        self.average = average
+        self.broadcast_buffers = broadcast_buffers
+        self.require_backward_grad_sync = True
+        self.require_forward_param_sync = True
+        self.buffer_broadcasts = 0
+        eng.before_forward = self._pre_forward
+        eng.before_backward = self._pre_backward
+        eng.on_grad_ready = self.reducer.ready
+        eng.after_backward = self._post_backward
+        model._ddp = self
+
+    def _pre_forward(self):
+        if self.world > 1 and self.broadcast_buffers and self.require_forward_param_sync:
+            dist.broadcast(self.eng.bn_flat, src=0, group=self.group)
+            self.buffer_broadcasts += 1
+        # DDP _post_forward: the next forward syncs buffers iff this one synchronises grads
+        self.require_forward_param_sync = self.require_backward_grad_sync
+
+    def _pre_backward(self):
+        self.reducer.enabled = self.require_backward_grad_sync
+        self.reducer.begin()
+
+    def _post_backward(self):
+        self.reducer.finish(average=self.average)
+
+    @contextlib.contextmanager
+    def no_sync(self):
+        """DDP.no_sync: backward passes inside accumulate gradients without communication"""
+        old = self.require_backward_grad_sync
+        self.require_backward_grad_sync = False
+        try:
+            yield
+        finally:
+            self.require_backward_grad_sync = old
+
+    def detach(self):
+        e = self.eng
+        e.before_forward = e.before_backward = e.on_grad_ready = e.after_backward = None
+        self.model._ddp = None

@@ -151,11 +151,10 @@ def main():
     model.setup_engine(dev, torch.bfloat16)
     eng = model.avsr.engine()
     arena = eng.arena
-    buffers = [b for b in model.buffers()]
-    parallel.broadcast_state(arena.data, buffers)
-    arena.sync_shadow()
-    reducer = parallel.GradReducer(arena.grad, segment=arena.segments["decay"])
-    eng.on_grad_ready = reducer.ready          # all-reduce buckets as soon as their layers are done
+    # DDP semantics on the arena: rank-0 broadcast of parameters + buffers, per-forward BN
+    # statistics broadcast, bucketed RCCL all-reduce overlapped with the backward; the 1/world
+    # average is folded into the AdamW kernel (average=False, grad_scale below)
+    ddp = parallel.ArenaDDP(model, average=False)
     opt = FusedAdamW(arena, lr=1e-4, weight_decay=0.005, max_grad_norm=1.0)
 
     B, T, L = args.batch, args.seq, args.labels
@@ -173,12 +172,10 @@ def main():
 
     def step():
         arena.zero_grad()
-        reducer.begin()
         step_seed[0] += 1
         out4, ctx = eng.forward(v, a, lens, lab, train=True, need_grad=True, seed=step_seed[0])
         drops.append(eng.last_modality)
         eng.backward(ctx, d_ctc, d_att)
-        reducer.finish(average=False)
         opt.step(grad_scale=1.0 / world)
         return out4
 
