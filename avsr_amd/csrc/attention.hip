@@ -14,6 +14,8 @@
 //   accumulator with one atomic per element per workgroup.
 // fp32 storage ("parity mode") runs the same tiles on bf16 hi/lo splits (3 products).
 #include "common.h"
+#include <algorithm>
+#include <cstdlib>
 
 namespace {
 
@@ -80,6 +82,35 @@ AVSR_DEV void zacc(f32x16& x) {
   for (int r = 0; r < 16; ++r) x[r] = 0.f;
 }
 
+// ---- attention-probability dropout ------------------------------------------------------
+// One 32-bit hash per (query, key pair) supplies the 16-bit uniforms of both keys of the pair
+// (half the hash work of a per-element stream; the hash, two multiply-xorshift rounds, is the
+// VALU-dominant cost of the attention kernels). Key k of query q of head (b, h) reads pair
+//   g = ((b*H + h) * Lq + q) * ceil(Lk / 2) + k / 2,  u = (k odd ? hi : lo) 16 bits of hash(g),
+// dropped iff u < thr = round(p * 65536) (p_eff within 8e-6 of p), kept values scaled by
+// 65536 / (65536 - thr) so that E[mask] = 1 exactly. Every attention kernel (forward, dK/dV,
+// dQ; bf16 and fp32) evaluates this same function: masks are recomputed, never stored.
+struct AttnDrop {
+  uint64_t seed; uint32_t pre, thr, npair; float scale; bool small;
+  AVSR_DEV AttnDrop(float p, uint64_t seed_, int B, int H, int Lq, int Lk) {
+    seed = seed_;
+    thr = (uint32_t)(p * 65536.f + 0.5f);
+    scale = thr < 65536u ? 65536.f / (float)(65536u - thr) : 0.f;
+    npair = (uint32_t)((Lk + 1) >> 1);
+    small = (uint64_t)B * H * Lq * npair <= 0xFFFFFFFFull;
+    pre = mix32_hi(seed, 0u);
+  }
+  AVSR_DEV uint64_t index(int bh, int Lq, int q, int k) const {
+    return ((uint64_t)bh * Lq + q) * npair + (uint32_t)(k >> 1);
+  }
+  AVSR_DEV uint32_t hash(uint64_t g) const { return small ? mix32_lo(pre, (uint32_t)g) : mix32(seed, g); }
+  AVSR_DEV float keep(uint32_t h, int k) const {
+    const uint32_t u = (k & 1) ? (h >> 16) : (h & 0xFFFFu);
+    return u >= thr ? scale : 0.f;
+  }
+  AVSR_DEV float at(int bh, int Lq, int q, int k) const { return keep(hash(index(bh, Lq, q, k)), k); }
+};
+
 struct AttnArgs {
   int B, H, Lq, Lk; float scale;
   const void* q; int64_t ldq; const void* k; int64_t ldk; const void* v; int64_t ldv;
@@ -140,7 +171,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
   int kend = klen;
   if (a.causal) kend = min(kend, (int)blockIdx.x * 128 + 128);
   const float sl2 = a.scale * LOG2E;
-  const uint64_t dbase = ((uint64_t)(b * a.H + h) * a.Lq + qi) * (uint64_t)a.Lk;
+  const AttnDrop drop(a.drop_p, a.seed, a.B, a.H, a.Lq, a.Lk);
   for (int kt0 = 0; kt0 < kend; kt0 += 32) {
     __syncthreads();
     for (int v = tid; v < 32 * DH / VE; v += 256) {
@@ -187,7 +218,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
     for (int r = 0; r < 16; ++r) { o0[r] *= alpha; o1[r] *= alpha; }
     if (a.drop_p > 0.f) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) st[r] *= drop_scale(a.drop_p, a.seed, dbase + kt0 + qrow(r, hh));
+      for (int r = 0; r < 16; ++r) st[r] *= drop.at(b * a.H + h, a.Lq, qi, kt0 + qrow(r, hh));
     }
     const Frag pf0 = accfrag<T, 0>(st), pf1 = accfrag<T, 1>(st);
 #pragma unroll
@@ -269,6 +300,7 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(AttnArgs a) {
   const int klen = a.klen ? min(a.klen[b], a.Lk) : a.Lk;
   const float sl2 = a.scale * LOG2E;
   const int qstart = a.causal ? (int)blockIdx.x * 128 : 0;
+  const AttnDrop drop(a.drop_p, a.seed, a.B, a.H, a.Lq, a.Lk);
   T* dsw = dSs + w * 32 * SROW;
   float* rw = red + w * 32 * 65;
   for (int qt0 = qstart; qt0 < a.Lq; qt0 += 32) {
@@ -308,8 +340,7 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(AttnArgs a) {
       const int ql = qrow(r, hh), q = qt0 + ql;
       const bool ok = q < a.Lq && key < klen && (!a.causal || key <= q);
       const float p = ok ? exp2f(sc[r] * sl2 - lse_s[ql] * LOG2E) : 0.f;
-      const float keep = (a.drop_p > 0.f && ok)
-          ? drop_scale(a.drop_p, a.seed, ((uint64_t)(b * a.H + h) * a.Lq + q) * (uint64_t)a.Lk + key) : 1.f;
+      const float keep = (a.drop_p > 0.f && ok) ? drop.at(b * a.H + h, a.Lq, q, key) : 1.f;
       ds[r] = p * (dp[r] * keep - dl_s[ql]) * a.scale;
       pp[r] = p * keep;
     }
@@ -440,8 +471,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
   if (a.causal) kend = min(kend, (int)blockIdx.x * 128 + 128);
   const int nt = (kend + 63) / 64;
   const float sl2 = a.scale * LOG2E;
-  const uint64_t dbase = ((uint64_t)(b * a.H + h) * a.Lq + qi) * (uint64_t)a.Lk;
-  const DropTile dt(a.drop_p, a.seed, (uint64_t)a.B * a.H * a.Lq * a.Lk);
+  const AttnDrop drop(a.drop_p, a.seed, a.B, a.H, a.Lq, a.Lk);
   Pref pk, pv;
   if (nt > 0) {
     pref_load(pk, K, a.ldk, 0, a.Lk, tid); pref_load(pv, V, a.ldv, 0, a.Lk, tid);
@@ -492,8 +522,8 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
     if (a.drop_p > 0.f) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        s0[r] *= dt.scale(a.seed, dbase + kt0 + qrow(r, hh));
-        s1[r] *= dt.scale(a.seed, dbase + kt0 + 32 + qrow(r, hh));
+        s0[r] *= drop.at(b * a.H + h, a.Lq, qi, kt0 + qrow(r, hh));
+        s1[r] *= drop.at(b * a.H + h, a.Lq, qi, kt0 + 32 + qrow(r, hh));
       }
     }
     const bf16x8 p0a = accb(s0, 0), p0b = accb(s0, 1), p1a = accb(s1, 0), p1b = accb(s1, 1);
@@ -543,8 +573,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnArgs a) {
   const float sl2 = a.scale * LOG2E;
   const int qstart = a.causal ? (int)blockIdx.x * 128 : 0;
   const int nt = a.Lq > qstart ? (a.Lq - qstart + 63) / 64 : 0;
-  const uint64_t bh = (uint64_t)(b * a.H + h);
-  const DropTile dt(a.drop_p, a.seed, (uint64_t)a.B * a.H * a.Lq * a.Lk);
+  const AttnDrop drop(a.drop_p, a.seed, a.B, a.H, a.Lq, a.Lk);
   Pref pq, po;
   float lsr = 0.f, dlr = 0.f;
   auto fetch = [&](int qt0) {
@@ -567,8 +596,6 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnArgs a) {
     const bf16* Qs = sm + slot * 2 * IMG;
     const bf16* dOs = Qs + IMG;
     if (t + 1 < nt) fetch(qt0 + 64);
-    // dropout indices of this tile: (bh*Lq + q)*Lk + key for q in [qt0, qt0+64), key < Lk
-    const uint64_t dt0 = (bh * a.Lq + qt0) * (uint64_t)a.Lk;
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       f32x16 sc, dp;
@@ -583,7 +610,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnArgs a) {
         const int ql = 32 * u + qrow(r, hh), q = qt0 + ql;
         const bool ok = q < a.Lq && key < klen && (!a.causal || key <= q);
         const float p = ok ? exp2f(sc[r] * sl2 - lss[slot][ql]) : 0.f;
-        const float keep = (a.drop_p > 0.f && ok) ? dt.scale(a.seed, dt0 + (uint64_t)ql * a.Lk + key) : 1.f;
+        const float keep = (a.drop_p > 0.f && ok) ? drop.at(b * a.H + h, a.Lq, q, key) : 1.f;
         sc[r] = p * keep;                                       // P' = dropout(P)
         dp[r] = p * (dp[r] * keep - dls[slot][ql]) * a.scale;   // dS (scaled)
       }
@@ -637,8 +664,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs a, OutT* dq, 
   if (a.causal) kend = min(kend, (int)blockIdx.x * 128 + 128);
   const int nt = (kend + 63) / 64;
   const float sl2 = a.scale * LOG2E;
-  const uint64_t dbase = (uint64_t)bhq * (uint64_t)a.Lk;
-  const DropTile dt(a.drop_p, a.seed, (uint64_t)a.B * a.H * a.Lq * a.Lk);
+  const AttnDrop drop(a.drop_p, a.seed, a.B, a.H, a.Lq, a.Lk);
   Pref pk, pv;
   if (nt > 0) {
     pref_load(pk, K, a.ldk, 0, a.Lk, tid); pref_load(pv, V, a.ldv, 0, a.Lk, tid);
@@ -664,7 +690,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs a, OutT* dq, 
         const int kk = kt0 + 32 * u + qrow(r, hh);
         const bool ok = kk < klen && (!a.causal || kk <= qi);
         const float p = ok ? exp2f(st[r] * sl2 - lq) : 0.f;
-        const float keep = (a.drop_p > 0.f && ok) ? dt.scale(a.seed, dbase + kk) : 1.f;
+        const float keep = (a.drop_p > 0.f && ok) ? drop.at(b * a.H + h, a.Lq, qi, kk) : 1.f;
         dpt[r] = p * (dpt[r] * keep - dl) * a.scale;
       }
       const bf16x8 sa = accb(dpt, 0), sb = accb(dpt, 1);
@@ -683,6 +709,351 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs a, OutT* dq, 
   store_t<OutT>(dq0, dq1, 1.f, (float*)sm + w * 32 * 65, DQ, lddq, a.Lq - q0);
 }
 }  // namespace v2
+
+
+// =====================================================================================
+// Resident kernels (bf16; Lk or Lq <= 384: the encoder's 375-frame attention, the decoder's
+// self / source attention). One workgroup per (batch, head) and 32-row block range: the
+// whole streamed operand pair of that head (K and V for the forward / dQ, Q and dO for
+// dK / dV) is loaded into LDS ONCE (<= 2 x 384 x 144 B), then every wave (32 rows of its own
+// dimension on the MFMA lanes) sweeps it with no further barrier — nothing to pipeline, waves
+// drift freely, 3 waves per SIMD hide each other's MFMA / VALU / LDS latency.
+//   forward: exact two-pass softmax per 32-query block (pass 1: row max of S = Q K^T; pass 2:
+//            P = exp2(S - max), row sum, dropout, O^T += V^T P^T) — no running-max rescale of O;
+//   dK/dV:   per 32-key wave: S, dP with the key on the lane, dV^T += dO^T P', dK^T += Q^T dS;
+//            delta = rowsum(dO * O) is computed here (Q/dO already in LDS) and published for dQ;
+//   dQ:      per 32-query wave: S^T, dP^T, dQ^T += K^T dS^T.
+// Dropout: AttnDrop pairs — in the forward / dQ layout a lane holds 4 consecutive keys of one
+// query per register quad (2 hashes); in the dK/dV layout the key pair sits on lanes c, c^1,
+// which split the 16 queries' hashes and swap halves (__shfl_xor 1).
+namespace res {
+using namespace v2;
+constexpr int MAXR = 384;           // resident rows per (b, h)
+constexpr int MAXW = MAXR / 32;     // waves per workgroup (768 threads)
+constexpr uint32_t GOLD = 0x9E3779B1u;
+
+AVSR_DEV void load_img(bf16* img, const bf16* src, int64_t ld, int n, int nz, int tid, int nthr) {
+  for (int id = tid; id < nz * 8; id += nthr) {
+    const int row = id >> 3, ch = (id & 7) * 8;
+    v16 x;
+    if (row < n) x = *(const v16*)(src + (int64_t)row * ld + ch);
+    else x.w[0] = x.w[1] = x.w[2] = x.w[3] = 0u;
+    *(v16*)&img[row * ROW + ch] = x;
+  }
+}
+
+// AttnDrop's 32-bit-index form (the dispatcher guarantees B*H*Lq*ceil(Lk/2) < 2^32) with the
+// golden-ratio premultiply distributed over the index: hash(g) = fmix32(g*G ^ pre) and
+// g*G = rowG + (k/2)*G (mod 2^32), so per pair only an add, a xor and the finaliser remain
+AVSR_DEV uint32_t hashG(uint32_t gG, uint32_t pre) { return fmix32(gG ^ pre); }
+AVSR_DEV float keep16(uint32_t h, bool odd, uint32_t thr, float scale) {
+  const uint32_t u = odd ? (h >> 16) : (h & 0xFFFFu);
+  return u >= thr ? scale : 0.f;
+}
+
+// keep factors of a score tile held as (query on the lane, keys k0 + qrow(r, hh)): registers
+// r, r+1 (r even) are keys 2j, 2j+1 of one pair; tG = ((bh*Lq + q) * npair + k0/2) * G
+AVSR_DEV void drop_tile(f32x16& x, uint32_t tG, const AttnDrop& d, int hh) {
+#pragma unroll
+  for (int r = 0; r < 16; r += 2) {
+    const uint32_t kp = (uint32_t)(((r & 3) >> 1) + 4 * (r >> 2) + 2 * hh);     // (qrow(r, hh) >> 1)
+    const uint32_t h = hashG(tG + kp * GOLD, d.pre);
+    x[r] *= keep16(h, false, d.thr, d.scale);
+    x[r + 1] *= keep16(h, true, d.thr, d.scale);
+  }
+}
+
+__global__ __launch_bounds__(768) void attn_fwd_kernel(AttnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) bf16 sm[];
+  const int bh = blockIdx.x, b = bh / a.H, h = bh % a.H;
+  const int tid = threadIdx.x, nthr = blockDim.x, w = tid >> 6, l = tid & 63, c = l & 31, hh = l >> 5;
+  const int nk = (a.Lk + 31) & ~31;
+  bf16* Ks = sm;
+  bf16* Vs = sm + nk * ROW;
+  load_img(Ks, (const bf16*)a.k + (int64_t)b * a.Lk * a.ldk + h * DH, a.ldk, a.Lk, nk, tid, nthr);
+  load_img(Vs, (const bf16*)a.v + (int64_t)b * a.Lk * a.ldv + h * DH, a.ldv, a.Lk, nk, tid, nthr);
+  const int q0 = (blockIdx.y * (nthr >> 6) + w) * 32, qi = q0 + c;
+  const bf16* Q = (const bf16*)a.q + (int64_t)b * a.Lq * a.ldq + h * DH;
+  bf16x8 qf[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) qf[s] = ldrow(Q + (int64_t)qi * a.ldq + s * 16 + 8 * hh, qi < a.Lq);
+  const int klen = a.klen ? min(a.klen[b], a.Lk) : a.Lk;
+  const int kend = a.causal ? min(klen, q0 + 32) : klen;
+  const int nt = (kend + 31) >> 5;
+  const float sl2 = a.scale * LOG2E;
+  const AttnDrop drop(a.drop_p, a.seed, a.B, a.H, a.Lq, a.Lk);
+  const uint32_t rowG = ((uint32_t)bh * (uint32_t)a.Lq + (uint32_t)min(qi, a.Lq - 1)) * drop.npair * GOLD;
+  __syncthreads();
+  f32x16 o0, o1;
+  zacc(o0); zacc(o1);
+  float m = -INFINITY, lsum = 0.f;
+  if (q0 < a.Lq) {
+    // pass 1: row max of the raw scores
+    for (int t = 0; t < nt; ++t) {
+      f32x16 st;
+      zacc(st);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) st = mfma32(rd8(Ks, t * 32 + c, s * 16 + 8 * hh), qf[s], st);
+      if (t * 32 + 32 <= klen && (!a.causal || t * 32 + 31 <= q0)) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) m = fmaxf(m, st[r]);
+      } else {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int k = t * 32 + qrow(r, hh);
+          const bool ok = (k < klen) & (!a.causal | (k <= qi));
+          m = fmaxf(m, ok ? st[r] : -INFINITY);
+        }
+      }
+    }
+    m = fmaxf(m, __shfl_xor(m, 32, 64));
+    const float mb = m == -INFINITY ? 0.f : m * sl2;
+    // pass 2: probabilities, row sum, dropout, O^T += V^T P^T
+    for (int t = 0; t < nt; ++t) {
+      f32x16 st;
+      zacc(st);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) st = mfma32(rd8(Ks, t * 32 + c, s * 16 + 8 * hh), qf[s], st);
+      if (t * 32 + 32 <= klen && (!a.causal || t * 32 + 31 <= q0)) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          st[r] = fexp2(fmaf(st[r], sl2, -mb));
+          lsum += st[r];
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int k = t * 32 + qrow(r, hh);
+          const bool ok = (k < klen) & (!a.causal | (k <= qi));
+          st[r] = ok ? fexp2(fmaf(st[r], sl2, -mb)) : 0.f;
+          lsum += st[r];
+        }
+      }
+      if (a.drop_p > 0.f) drop_tile(st, rowG + (uint32_t)(t * 16) * GOLD, drop, hh);
+      const bf16x8 pa = accb(st, 0), pb = accb(st, 1);
+      o0 = mfma32(rdT(Vs, t * 32, 0, l), pa, o0);
+      o0 = mfma32(rdT(Vs, t * 32 + 16, 0, l), pb, o0);
+      o1 = mfma32(rdT(Vs, t * 32, 32, l), pa, o1);
+      o1 = mfma32(rdT(Vs, t * 32 + 16, 32, l), pb, o1);
+    }
+    lsum += __shfl_xor(lsum, 32, 64);
+    if (hh == 0 && qi < a.Lq)
+      a.lse[(int64_t)bh * a.Lq + qi] = lsum > 0.f ? (mb + log2f(lsum)) * LN2 : -INFINITY;
+  }
+  __syncthreads();                         // K/V images no longer read: reuse LDS as store slabs
+  if (q0 < a.Lq) {
+    const float inv = lsum > 0.f ? 1.f / lsum : 0.f;
+    bf16* O = (bf16*)a.o + ((int64_t)b * a.Lq + q0) * a.ldo + h * DH;
+    store_t<bf16>(o0, o1, inv, (float*)sm + w * 32 * 65, O, a.ldo, a.Lq - q0);
+  }
+}
+
+template <int NT>
+__global__ __launch_bounds__(NT) void attn_bwd_dkdv_kernel(AttnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) bf16 sm[];
+  const int bh = blockIdx.x, b = bh / a.H, h = bh % a.H;
+  const int tid = threadIdx.x, nthr = blockDim.x, w = tid >> 6, l = tid & 63, c = l & 31, hh = l >> 5;
+  const int nq = (a.Lq + 31) & ~31;
+  bf16* Qs = sm;
+  bf16* dOs = sm + nq * ROW;
+  float* lss = (float*)(sm + 2 * nq * ROW);          // lse * log2(e) (0 past Lq)
+  float* dls = lss + nq;                              // delta (0 past Lq)
+  const bf16* Q = (const bf16*)a.q + (int64_t)b * a.Lq * a.ldq + h * DH;
+  const bf16* dO = (const bf16*)a.dout + (int64_t)b * a.Lq * a.lddo + h * DH;
+  load_img(Qs, Q, a.ldq, a.Lq, nq, tid, nthr);
+  load_img(dOs, dO, a.lddo, a.Lq, nq, tid, nthr);
+  for (int q = tid; q < nq; q += nthr) lss[q] = q < a.Lq ? a.lse[(int64_t)bh * a.Lq + q] * LOG2E : 0.f;
+  __syncthreads();
+  // delta[q] = sum_d dO * O: 8 lanes per query row (one 16-byte chunk each)
+  {
+    const bf16* O = (const bf16*)a.o + (int64_t)b * a.Lq * a.ldo + h * DH;
+    for (int id = tid; id < nq * 8; id += nthr) {
+      const int q = id >> 3, ch = (id & 7) * 8;
+      float sacc = 0.f;
+      if (q < a.Lq) {
+        const bf16x8 ov = *(const bf16x8*)(O + (int64_t)q * a.ldo + ch);
+        const bf16x8 dv = *(const bf16x8*)&dOs[q * ROW + ch];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) sacc += (float)ov[j] * (float)dv[j];
+      }
+      sacc += __shfl_xor(sacc, 1, 64);
+      sacc += __shfl_xor(sacc, 2, 64);
+      sacc += __shfl_xor(sacc, 4, 64);
+      if ((id & 7) == 0) {
+        dls[q] = sacc;
+        if (blockIdx.y == 0 && q < a.Lq) a.delta[(int64_t)bh * a.Lq + q] = sacc;
+      }
+    }
+  }
+  const int kb0 = (blockIdx.y * (nthr >> 6) + w) * 32, key = kb0 + c;
+  const bf16* K = (const bf16*)a.k + (int64_t)b * a.Lk * a.ldk + h * DH;
+  const bf16* V = (const bf16*)a.v + (int64_t)b * a.Lk * a.ldv + h * DH;
+  bf16x8 kf[4], vf[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    kf[s] = ldrow(K + (int64_t)key * a.ldk + s * 16 + 8 * hh, key < a.Lk);
+    vf[s] = ldrow(V + (int64_t)key * a.ldv + s * 16 + 8 * hh, key < a.Lk);
+  }
+  const int klen = a.klen ? min(a.klen[b], a.Lk) : a.Lk;
+  const float sl2 = a.scale * LOG2E;
+  const AttnDrop drop(a.drop_p, a.seed, a.B, a.H, a.Lq, a.Lk);
+  const uint32_t nG = drop.npair * GOLD;
+  const uint32_t keyG = ((uint32_t)bh * (uint32_t)a.Lq * drop.npair + (uint32_t)(min(key, a.Lk - 1) >> 1)) * GOLD;
+  const bool odd = c & 1;
+  __syncthreads();
+  f32x16 dv0, dv1, dk0, dk1;
+  zacc(dv0); zacc(dv1); zacc(dk0); zacc(dk1);
+  if (kb0 < a.Lk && kb0 < klen) {
+    const int qstart = a.causal ? kb0 : 0;
+    const int nt = (a.Lq - qstart + 31) >> 5;
+    const bool kok = key < klen;
+    for (int t = 0; t < nt; ++t) {
+      const int qt0 = qstart + t * 32;
+      f32x16 sc, dp;
+      zacc(sc); zacc(dp);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        sc = mfma32(rd8(Qs, qt0 + c, s * 16 + 8 * hh), kf[s], sc);
+        dp = mfma32(rd8(dOs, qt0 + c, s * 16 + 8 * hh), vf[s], dp);
+      }
+      const uint32_t tG = keyG + (uint32_t)(qt0 + 4 * hh) * nG;
+      const bool full = kok && qt0 + 32 <= a.Lq && (!a.causal || key <= qt0);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {                 // registers 4i..4i+3 = queries qt0 + 8i + 4hh + 0..3
+        const f32x4 ls = *(const f32x4*)&lss[qt0 + 8 * i + 4 * hh];
+        const f32x4 ds = *(const f32x4*)&dls[qt0 + 8 * i + 4 * hh];
+        // dropout: this lane pair (keys 2j, 2j+1) splits the 4 queries' hashes: even lanes
+        // hash queries 0, 1, odd lanes 2, 3, then the two swap (static registers only)
+        float kp[4] = {1.f, 1.f, 1.f, 1.f};
+        if (a.drop_p > 0.f) {
+#pragma unroll
+          for (int u = 0; u < 2; ++u) {
+            const uint32_t mine = hashG(tG + (uint32_t)(8 * i + (odd ? 2 : 0) + u) * nG, drop.pre);
+            const uint32_t other = __shfl_xor(mine, 1, 64);
+            kp[u] = keep16(odd ? other : mine, odd, drop.thr, drop.scale);
+            kp[u + 2] = keep16(odd ? mine : other, odd, drop.thr, drop.scale);
+          }
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int r = 4 * i + e, ql = qt0 + 8 * i + 4 * hh + e;
+          const bool ok = full || (kok & (ql < a.Lq) & (!a.causal | (key <= ql)));
+          const float p = ok ? fexp2(fmaf(sc[r], sl2, -ls[e])) : 0.f;
+          sc[r] = p * kp[e];                                    // P' = dropout(P)
+          dp[r] = p * (dp[r] * kp[e] - ds[e]) * a.scale;        // dS (scaled)
+        }
+      }
+      const bf16x8 pa = accb(sc, 0), pb = accb(sc, 1), sa = accb(dp, 0), sb = accb(dp, 1);
+      dv0 = mfma32(rdT(dOs, qt0, 0, l), pa, dv0);
+      dv0 = mfma32(rdT(dOs, qt0 + 16, 0, l), pb, dv0);
+      dv1 = mfma32(rdT(dOs, qt0, 32, l), pa, dv1);
+      dv1 = mfma32(rdT(dOs, qt0 + 16, 32, l), pb, dv1);
+      dk0 = mfma32(rdT(Qs, qt0, 0, l), sa, dk0);
+      dk0 = mfma32(rdT(Qs, qt0 + 16, 0, l), sb, dk0);
+      dk1 = mfma32(rdT(Qs, qt0, 32, l), sa, dk1);
+      dk1 = mfma32(rdT(Qs, qt0 + 16, 32, l), sb, dk1);
+    }
+  }
+  __syncthreads();
+  if (kb0 < a.Lk) {
+    float* scr = (float*)sm + w * 32 * 65;
+    bf16* DK = (bf16*)a.dk + ((int64_t)b * a.Lk + kb0) * a.lddk + h * DH;
+    store_t<bf16>(dk0, dk1, 1.f, scr, DK, a.lddk, a.Lk - kb0);
+    bf16* DV = (bf16*)a.dv + ((int64_t)b * a.Lk + kb0) * a.lddv + h * DH;
+    store_t<bf16>(dv0, dv1, 1.f, scr, DV, a.lddv, a.Lk - kb0);
+  }
+}
+
+template <typename OutT>
+__global__ __launch_bounds__(768) void attn_bwd_dq_kernel(AttnArgs a, OutT* dq, int64_t lddq) {
+  extern __shared__ __attribute__((aligned(16))) bf16 sm[];
+  const int bh = blockIdx.x, b = bh / a.H, h = bh % a.H;
+  const int tid = threadIdx.x, nthr = blockDim.x, w = tid >> 6, l = tid & 63, c = l & 31, hh = l >> 5;
+  const int nk = (a.Lk + 31) & ~31;
+  bf16* Ks = sm;
+  bf16* Vs = sm + nk * ROW;
+  load_img(Ks, (const bf16*)a.k + (int64_t)b * a.Lk * a.ldk + h * DH, a.ldk, a.Lk, nk, tid, nthr);
+  load_img(Vs, (const bf16*)a.v + (int64_t)b * a.Lk * a.ldv + h * DH, a.ldv, a.Lk, nk, tid, nthr);
+  const int q0 = (blockIdx.y * (nthr >> 6) + w) * 32, qi = q0 + c;
+  const bool qok = qi < a.Lq;
+  const bf16* Q = (const bf16*)a.q + (int64_t)b * a.Lq * a.ldq + h * DH;
+  const bf16* dO = (const bf16*)a.dout + (int64_t)b * a.Lq * a.lddo + h * DH;
+  bf16x8 qf[4], of[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    qf[s] = ldrow(Q + (int64_t)qi * a.ldq + s * 16 + 8 * hh, qok);
+    of[s] = ldrow(dO + (int64_t)qi * a.lddo + s * 16 + 8 * hh, qok);
+  }
+  const int64_t bhq = (int64_t)bh * a.Lq + qi;
+  const float lq = qok ? a.lse[bhq] * LOG2E : 0.f;
+  const float dl = qok ? a.delta[bhq] : 0.f;
+  const int klen = a.klen ? min(a.klen[b], a.Lk) : a.Lk;
+  const int kend = a.causal ? min(klen, q0 + 32) : klen;
+  const int nt = (kend + 31) >> 5;
+  const float sl2 = a.scale * LOG2E;
+  const AttnDrop drop(a.drop_p, a.seed, a.B, a.H, a.Lq, a.Lk);
+  const uint32_t rowG = ((uint32_t)bh * (uint32_t)a.Lq + (uint32_t)min(qi, a.Lq - 1)) * drop.npair * GOLD;
+  __syncthreads();
+  f32x16 dq0, dq1;
+  zacc(dq0); zacc(dq1);
+  if (q0 < a.Lq) {
+    for (int t = 0; t < nt; ++t) {
+      f32x16 st, dpt;
+      zacc(st); zacc(dpt);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        st = mfma32(rd8(Ks, t * 32 + c, s * 16 + 8 * hh), qf[s], st);
+        dpt = mfma32(rd8(Vs, t * 32 + c, s * 16 + 8 * hh), of[s], dpt);
+      }
+      f32x16 keep;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) keep[r] = 1.f;
+      if (a.drop_p > 0.f) drop_tile(keep, rowG + (uint32_t)(t * 16) * GOLD, drop, hh);
+      if (t * 32 + 32 <= klen && (!a.causal || t * 32 + 31 <= q0)) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float p = fexp2(fmaf(st[r], sl2, -lq));
+          dpt[r] = p * (dpt[r] * keep[r] - dl) * a.scale;
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int k = t * 32 + qrow(r, hh);
+          const bool ok = (k < klen) & (!a.causal | (k <= qi));
+          const float p = ok ? fexp2(fmaf(st[r], sl2, -lq)) : 0.f;
+          dpt[r] = p * (dpt[r] * keep[r] - dl) * a.scale;
+        }
+      }
+      const bf16x8 sa = accb(dpt, 0), sb = accb(dpt, 1);
+      dq0 = mfma32(rdT(Ks, t * 32, 0, l), sa, dq0);
+      dq0 = mfma32(rdT(Ks, t * 32 + 16, 0, l), sb, dq0);
+      dq1 = mfma32(rdT(Ks, t * 32, 32, l), sa, dq1);
+      dq1 = mfma32(rdT(Ks, t * 32 + 16, 32, l), sb, dq1);
+    }
+  }
+  __syncthreads();
+  if (q0 < a.Lq) {
+    OutT* DQ = dq + ((int64_t)b * a.Lq + q0) * lddq + h * DH;
+    store_t<OutT>(dq0, dq1, 1.f, (float*)sm + w * 32 * 65, DQ, lddq, a.Lq - q0);
+  }
+}
+
+// launch geometry: waves per workgroup (<= 12) covering `rows` 32-row blocks, grid.y chunks
+inline int nwaves(int rows) { const int n = (rows + 31) / 32; return n < MAXW ? n : MAXW; }
+inline size_t img_lds(int rows) { return (size_t)2 * ((rows + 31) & ~31) * ROW * sizeof(bf16); }
+inline size_t slab_lds(int nw) { return (size_t)nw * 32 * 65 * sizeof(float); }
+inline bool small_index(const avsr_attn_params* p) {
+  return (uint64_t)p->B * p->H * p->Lq * (uint64_t)((p->Lk + 1) / 2) <= 0xFFFFFFFFull;
+}
+
+template <typename F> void allow_lds(F* f) {
+  static bool done = false;                     // once per kernel instantiation
+  if (!done) {
+    (void)hipFuncSetAttribute((const void*)f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    done = true;
+  }
+}
+}  // namespace res
 
 AttnArgs args(const avsr_attn_params* p) {
   AttnArgs a;
@@ -709,6 +1080,15 @@ extern "C" int avsr_attn_fwd(const avsr_attn_params* p, void* stream) {
   if (rc) return rc;
   if (p->B * p->H == 0 || p->Lq == 0) return 0;
   AttnArgs a = args(p);
+  if (p->dtype == AVSR_BF16 && p->Lk <= res::MAXR && res::small_index(p)) {
+    const int nw = res::nwaves(p->Lq);
+    const size_t lds = std::max(res::img_lds(p->Lk), res::slab_lds(nw));
+    res::allow_lds(res::attn_fwd_kernel);
+    dim3 g(p->B * p->H, (p->Lq + 32 * nw - 1) / (32 * nw));
+    hipLaunchKernelGGL(res::attn_fwd_kernel, g, dim3(64 * nw), lds, (hipStream_t)stream, a);
+    AVSR_CHECK_LAUNCH();
+    return 0;
+  }
   dim3 grid((p->Lq + 127) / 128, p->B * p->H);
   if (p->dtype == AVSR_BF16) hipLaunchKernelGGL(v2::attn_fwd_kernel, grid, dim3(256), 0, (hipStream_t)stream, a);
   else hipLaunchKernelGGL(attn_fwd_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, a);
@@ -716,9 +1096,15 @@ extern "C" int avsr_attn_fwd(const avsr_attn_params* p, void* stream) {
   return 0;
 }
 
+// the resident bf16 backward computes delta inside its dK/dV kernel (Q / dO already in LDS)
+static bool resident_bwd(const avsr_attn_params* p) {
+  return p->dtype == AVSR_BF16 && p->Lq <= res::MAXR && p->Lk <= res::MAXR && res::small_index(p);
+}
+
 extern "C" int avsr_attn_bwd_prep(const avsr_attn_params* p, void* stream) {
   int rc = check(p);
   if (rc) return rc;
+  if (resident_bwd(p)) return 0;
   AttnArgs a = args(p);
   const int g = avsr_grid((int64_t)p->B * p->Lq * p->H);
   if (p->dtype == AVSR_BF16) hipLaunchKernelGGL(attn_prep_kernel<bf16>, dim3(g), dim3(256), 0, (hipStream_t)stream, a);
@@ -737,6 +1123,34 @@ extern "C" int avsr_attn_bwd(const avsr_attn_params* p, void* stream) {
   if (p->dtype == AVSR_BF16) {
     if (p->dq_out && (p->lddq_out % 8 || !avsr_aligned16(p->dq_out))) return AVSR_E_ALIGN;
     if (!p->dq_out && (p->lddq % 4 || !avsr_aligned16(p->dq))) return AVSR_E_ALIGN;
+    if (resident_bwd(p)) {
+      // dK/dV: 12 waves (3 per SIMD; a few registers spill to scratch, measured 5 % faster than
+      // 8 spill-free waves at 2 per SIMD); AVSR_DKDV_WAVES=8 selects the other
+      static const int dkdv_max = getenv("AVSR_DKDV_WAVES") && atoi(getenv("AVSR_DKDV_WAVES")) == 8 ? 8 : 12;
+      const int nwk = std::min(res::nwaves(p->Lk), dkdv_max), nwq = res::nwaves(p->Lq);
+      const size_t ldk = std::max(res::img_lds(p->Lq) + (size_t)2 * ((p->Lq + 31) & ~31) * sizeof(float),
+                                  res::slab_lds(nwk));
+      const dim3 gk(p->B * p->H, (p->Lk + 32 * nwk - 1) / (32 * nwk));
+      if (dkdv_max == 12) {
+        res::allow_lds(res::attn_bwd_dkdv_kernel<768>);
+        hipLaunchKernelGGL(res::attn_bwd_dkdv_kernel<768>, gk, dim3(64 * nwk), ldk, st, a);
+      } else {
+        res::allow_lds(res::attn_bwd_dkdv_kernel<512>);
+        hipLaunchKernelGGL(res::attn_bwd_dkdv_kernel<512>, gk, dim3(64 * nwk), ldk, st, a);
+      }
+      AVSR_CHECK_LAUNCH();
+      const size_t ldq = std::max(res::img_lds(p->Lk), res::slab_lds(nwq));
+      dim3 gq(p->B * p->H, (p->Lq + 32 * nwq - 1) / (32 * nwq));
+      if (p->dq_out) {
+        res::allow_lds(res::attn_bwd_dq_kernel<bf16>);
+        hipLaunchKernelGGL(res::attn_bwd_dq_kernel<bf16>, gq, dim3(64 * nwq), ldq, st, a, (bf16*)p->dq_out, p->lddq_out);
+      } else {
+        res::allow_lds(res::attn_bwd_dq_kernel<float>);
+        hipLaunchKernelGGL(res::attn_bwd_dq_kernel<float>, gq, dim3(64 * nwq), ldq, st, a, p->dq, p->lddq);
+      }
+      AVSR_CHECK_LAUNCH();
+      return 0;
+    }
     hipLaunchKernelGGL(v2::attn_bwd_dkdv_kernel, grid, dim3(256), 0, st, a);
     AVSR_CHECK_LAUNCH();
     dim3 gq((p->Lq + 127) / 128, p->B * p->H);

@@ -23,6 +23,9 @@ template <> AVSR_DEV bf16 from_f<bf16>(float x) { return (bf16)x; }
 // 16-byte vector of T (8 bf16 or 4 f32)
 struct alignas(16) v16 { uint32_t w[4]; };
 
+// hardware 2^x (v_exp_f32, ~1 ulp; no denormal-result fix-up): softmax / log-sum-exp inner loops
+AVSR_DEV float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
 AVSR_DEV float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
