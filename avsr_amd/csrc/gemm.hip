@@ -133,6 +133,8 @@ using Cfg128s3 = gemmg::GCfg<2, 2, 2, 2, 3>;     // 128x128, 4 waves, 3 stages (
 using Cfg128s4 = gemmg::GCfg<2, 2, 2, 2, 4>;     // 128x128, 4 waves, 4 stages (128 KiB)
 using Cfg128w8s3 = gemmg::GCfg<2, 4, 2, 1, 3>;   // 128x128, 8 waves (64x32 each), 3 stages
 using Cfg128w8s4 = gemmg::GCfg<2, 4, 2, 1, 4>;   // 128x128, 8 waves, 4 stages
+using Cfg96 = gemmg::GCfg<3, 2, 1, 2, 2>;        // 96x128, 6 waves (32x64 each), 2 stages, 2 blocks/CU
+using Cfg128x64 = gemmg::GCfg<4, 1, 1, 2, 2>;    // 128x64, 4 waves (32x64 each), 2 stages, 3 blocks/CU
 
 // tile choice: AVSR_GEMM_TILE=128|256|256x128|128x256 forces one (benchmarks); otherwise the
 // configuration with the fewest block rounds x per-tile work (wave quantisation over 256 CUs)
@@ -140,16 +142,13 @@ int tile_cfg(const avsr_gemm_params* p, int splits) {
   const char* e = getenv("AVSR_GEMM_TILE");
   const int forced = !e ? -1 : !strcmp(e, "128") ? 0 : !strcmp(e, "256") ? 1 : !strcmp(e, "256x128") ? 2
                    : !strcmp(e, "128x256") ? 3 : !strcmp(e, "128s3") ? 4 : !strcmp(e, "128s4") ? 5
-                   : !strcmp(e, "128w8s3") ? 6 : !strcmp(e, "128w8s4") ? 7 : !strcmp(e, "pp") ? 8 : -1;
+                   : !strcmp(e, "128w8s3") ? 6 : !strcmp(e, "128w8s4") ? 7 : !strcmp(e, "pp") ? 8
+                   : !strcmp(e, "96") ? 9 : !strcmp(e, "128x64") ? 10 : -1;
   if (forced >= 0) return forced;
-  // cost ~ rounds of the grid over 256 CUs x work per CU per round / efficiency: the 128x128
-  // tile runs 2 blocks per CU (512 per round), the 256x256 ping-pong tile 1 block (4x the
-  // work) at ~1.27x the per-CU rate (measured 1262 vs 990 TFLOP/s at 8192^3)
-  const long t128 = (long)((p->M + 127) / 128) * ((p->N + 127) / 128) * p->batch * splits;
-  const long tpp = (long)((p->M + 255) / 256) * ((p->N + 255) / 256) * p->batch * splits;
-  const double c128 = (double)((t128 + 511) / 512) * 2.0;
-  const double cpp = (double)((tpp + 255) / 256) * 4.0 / 1.27;
-  return cpp < c128 ? 8 : 0;
+  // The 128x128 two-blocks-per-CU tile is the fastest configuration on every encoder shape
+  // (tools/gemm_table.py, profiles/r02_gemm_table.json: the 256x256 ping-pong core loses
+  // 8-36 % at M = 6000, the 96x128 / 128x64 / 3-stage variants are within +-4 % or slower)
+  return 0;
 }
 
 template <typename OutT, bool AK, bool BK>
@@ -163,6 +162,10 @@ int launch_cfg(int cfg, const DenseArgs& a, int batch, hipStream_t st) {
     case 6: return launch_glds<OutT, AK, BK, Cfg128w8s3>(a, batch, st);
     case 7: return launch_glds<OutT, AK, BK, Cfg128w8s4>(a, batch, st);
     case 8: return launch_pp<OutT, AK, BK>(a, batch, st);
+    case 9:
+      if constexpr (AK) return launch_glds<OutT, AK, BK, Cfg96>(a, batch, st);   // r-contiguous A needs BM % 64 == 0
+      else return launch_glds<OutT, AK, BK, Cfg128>(a, batch, st);
+    case 10: return launch_glds<OutT, AK, BK, Cfg128x64>(a, batch, st);
     default: return launch_glds<OutT, AK, BK, Cfg128>(a, batch, st);
   }
 }

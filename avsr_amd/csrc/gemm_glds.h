@@ -200,7 +200,7 @@ template <int WM_, int WN_, int FM_, int FN_, int S_ = 2> struct GCfg {
   static constexpr int GL = (BM + BN) * GBK * 2 / 1024 / NW;    // DMA instructions per wave per K-tile
   static constexpr int EP_BYTES = WM * 32 * (BN + 4) * 4;       // one 32-row strip per wave row
   static constexpr int LDS_BYTES = S * STAGE > EP_BYTES ? S * STAGE : EP_BYTES;
-  static constexpr int MINB = LDS_BYTES <= 80 * 1024 ? 2 : 1;    // blocks per CU the LDS allows
+  static constexpr int MINB = LDS_BYTES <= 53 * 1024 ? 3 : LDS_BYTES <= 80 * 1024 ? 2 : 1;   // blocks per CU the LDS allows
   static constexpr int TM = 2 * FM, TN = 2 * FN;                 // 16x16 accumulator tiles per wave
 };
 

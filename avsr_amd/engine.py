@@ -92,6 +92,11 @@ class Engine:
             raise ValueError(f"unknown modality {cfg.modality!r}")
         self.last_modality = None
         self.capture = None          # tests: a dict receives the last forward's enc / logits / batch
+        self._pinned = [(None, None)] * 4
+        self._pin_next = 0
+        import os
+        self.side = (torch.cuda.Stream(device=self.device)
+                     if self.device.type == "cuda" and os.environ.get("AVSR_SIDE_STREAM", "1") == "1" else None)
         E = "encoder.encoder.layers"
         groups = []
         for i in range(self.nl):
@@ -206,31 +211,80 @@ class Engine:
         mod = self.shell.get_submodule(prefix)
         return mod, self.arena.master(prefix + ".weight"), self.arena.master(prefix + ".bias")
 
+    # weight gradients run on a side stream: nothing on the backward's critical path (the data-
+    # gradient chain) waits for them, so they fill the CUs the chain's kernels leave idle (grid
+    # tails, one-block-per-CU attention, small LayerNorm / bias kernels). Their inputs are kept
+    # alive for the side stream (record_stream) and never overwritten afterwards; gradient
+    # consumers (all-reduce buckets, the optimizer) wait for the side stream first.
+    def _on_side(self, fn, *keep):
+        side = self.side
+        if side is None:
+            return fn()
+        side.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(side):
+            r = fn()
+        for t in keep:
+            t.record_stream(side)
+        return r
+
+    def join_side(self):
+        """make the current stream wait for every weight gradient issued so far"""
+        if self.side is not None:
+            torch.cuda.current_stream(self.device).wait_stream(self.side)
+
     def _wgrad(self, dy, x, dW, alpha=1.0):
-        """dW (fp32) += alpha * dy^T x. When the output tile grid is at or below one block per CU
-        the token dimension is split and the partial tiles go to a slab workspace (no atomics):
-        measured (tools/lin_wgrad_sweep.py, M=6000) 4096x1024 100 -> 72 us with 2 splits."""
+        """dW (fp32) += alpha * dy^T x (side stream). When the output tile grid is at or below one
+        block per CU the token dimension is split and the partial tiles go to a slab workspace
+        (no atomics): measured (tools/lin_wgrad_sweep.py, M=6000) 4096x1024 100 -> 72 us with 2 splits."""
         M, N = dy.shape
         K = x.shape[1]
         tiles = ((N + 127) // 128) * ((K + 127) // 128)
         splitk = 1 if tiles > 256 else max(1, min(16, 512 // max(tiles, 1), M // 512))
-        ws = None
-        if splitk > 1:
-            ws = torch.empty(splitk * N * K, device=dy.device, dtype=torch.float32)
-        ops.gemm(dy, x, dW, M=N, N=K, K=M, a_kmajor=False, b_kmajor=False, lda=dy.stride(0), ldb=x.stride(0),
-                 ldc=dW.stride(0), alpha=alpha, beta=1.0, splitk=splitk, ws=ws)
+
+        def run():
+            ws = None
+            if splitk > 1:
+                ws = torch.empty(splitk * N * K, device=dy.device, dtype=torch.float32)
+            ops.gemm(dy, x, dW, M=N, N=K, K=M, a_kmajor=False, b_kmajor=False, lda=dy.stride(0), ldb=x.stride(0),
+                     ldc=dW.stride(0), alpha=alpha, beta=1.0, splitk=splitk, ws=ws)
+        self._on_side(run, dy, x)
+
+    def _conv_wgrad(self, g, x, dy, dw):
+        self._on_side(lambda: ops.conv_bwd_weight(g, x, dy, dw), x, dy)
 
     def _bias_grad(self, g, db, alpha=1.0):
         ops.ew_bwd(g, db=db, alpha=alpha)
 
     # ------------------------------------------------------------------------ batch prep
+    def _stage(self, host_i32):
+        """one H2D copy of a host int32 vector through a ring of pinned staging buffers:
+        asynchronous (a pageable-memory copy makes the host wait for the stream to drain, which
+        starves the GPU while the next step's launches are issued); a ring slot is reused only
+        after the copy that last read it has executed."""
+        n = host_i32.numel()
+        ring = self._pinned
+        i = self._pin_next = (self._pin_next + 1) % len(ring)
+        buf, ev = ring[i]
+        if buf is None or buf.numel() < n:
+            buf = torch.empty(max(n, 4096), dtype=torch.int32, pin_memory=True)
+            ev = None
+        if ev is not None:
+            ev.synchronize()
+        buf[:n].copy_(host_i32)
+        dev = torch.empty(n, dtype=torch.int32, device=self.device)
+        dev.copy_(buf[:n], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        ring[i] = (buf, ev)
+        return dev
+
     def prepare(self, videos, audios, video_lengths, labels=None):
-        """host-side index tensors (labels / lengths are host data in the collator layout)."""
+        """index tensors of a batch (labels / lengths are host data in the collator layout; a
+        device tensor is read back once). All of them reach the device in ONE asynchronous copy."""
         B, _, T = videos.shape[:3]
         lens = video_lengths.detach().cpu().to(torch.int64)
-        b = {"B": B, "T": T, "lens_host": lens,
-             "lens": lens.to(torch.int32).to(self.device, non_blocking=True),
-             "full": bool((lens == T).all())}
+        b = {"B": B, "T": T, "lens_host": lens, "full": bool((lens == T).all())}
+        parts = [lens.to(torch.int32)]
         if labels is not None:
             lab = labels.detach().cpu()
             ys = [r[r != -1] for r in lab]
@@ -240,14 +294,21 @@ class Engine:
             Lmax = max(1, max(len(y) for y in ys))
             ctc_lab = torch.full((B, Lmax), -1, dtype=torch.int32)
             for i, y in enumerate(ys):
-                ys_in[i, 0] = self.V - 1
                 ys_in[i, 1:len(y) + 1] = y
                 ys_out[i, :len(y)] = y
                 ys_out[i, len(y)] = self.V - 1
                 ctc_lab[i, :len(y)] = y
-            b.update(L1=L1, ys_in=ys_in.flatten().to(self.device), ys_out=ys_out.flatten().to(self.device),
-                     ctc_lab=ctc_lab.to(self.device),
-                     ctc_len=torch.tensor([len(y) for y in ys], dtype=torch.int32).to(self.device))
+            parts += [ys_in.flatten(), ys_out.flatten(), ctc_lab.flatten(),
+                      torch.tensor([len(y) for y in ys], dtype=torch.int32)]
+        dev = self._stage(torch.cat(parts))
+        o = 0
+        views = []
+        for t in parts:
+            views.append(dev[o:o + t.numel()])
+            o += t.numel()
+        b["lens"] = views[0]
+        if labels is not None:
+            b.update(L1=L1, ys_in=views[1], ys_out=views[2], ctc_lab=views[3].view(B, Lmax), ctc_len=views[4])
         return b
 
     # ===================================================================== video frontend
@@ -351,7 +412,7 @@ class Engine:
                                     dgamma=self.g(p + "bn2.weight"), dbeta=self.g(p + "bn2.bias"))
                 dhd = None
             # conv2
-            ops.conv_bwd_weight(blk["g2"], blk["a1"], dh2, self.g(p + "conv2.weight"))
+            self._conv_wgrad(blk["g2"], blk["a1"], dh2, self.g(p + "conv2.weight"))
             da1 = self._e(M2, cout)
             ops.conv_bwd_data(blk["g2"], dh2, self.w(p + "conv2.weight"), da1)
             # bn1 + prelu1
@@ -359,7 +420,7 @@ class Engine:
             ops.bn_act_bwd(da1, blk["h1"], blk["st1"], self.arena.master(p + "relu1.weight"), dh1,
                            dprelu=self.g(p + "relu1.weight"), dgamma=self.g(p + "bn1.weight"),
                            dbeta=self.g(p + "bn1.bias"))
-            ops.conv_bwd_weight(blk["g1"], blk["x"], dh1, self.g(p + "conv1.weight"))
+            self._conv_wgrad(blk["g1"], blk["x"], dh1, self.g(p + "conv1.weight"))
             Mi = blk["x"].shape[0]
             if dz is not None:
                 dx = dz                      # identity shortcut: d(block input) starts as dz
@@ -367,7 +428,7 @@ class Engine:
             else:
                 dx = self._e(Mi, cin)
                 ops.conv_bwd_data(blk["g1"], dh1, self.w(p + "conv1.weight"), dx)
-                ops.conv_bwd_weight(blk["gd"], blk["x"], dhd, self.g(p + "downsample.0.weight"))
+                self._conv_wgrad(blk["gd"], blk["x"], dhd, self.g(p + "downsample.0.weight"))
                 ops.conv_bwd_data(blk["gd"], dhd, self.w(p + "downsample.0.weight"), dx, beta=1.0)
             dout = dx
         # stem
@@ -502,7 +563,7 @@ class Engine:
         dln2 = ops.linear_dgrad(dh, self.w(ff + "intermediate_dense.weight"))
         dx1 = self._ln_bwd(dln2, lc["x1"], p + "final_layer_norm", lc["m2"], lc["r2"], dres=dx2, dx=dx2)
         # x1 = x + drop(o Wo^T + bo)
-        go = g2
+        go = self._e(M, D)              # fresh: g2 may still be read by the side stream
         ops.ew_bwd(dx1, out=go, drop_p=lc["p_h"], seed=lc["sd_o"], db=self.g(a + "out_proj.bias"))
         self._wgrad(go, lc["o"], self.g(a + "out_proj.weight"))
         do = ops.linear_dgrad(go, self.w(a + "out_proj.weight"))
@@ -533,7 +594,7 @@ class Engine:
         for i in reversed(range(self.nl)):
             dx = self._enc_layer_bwd(i, ctx["layers"][i], dx, B, T, ctx["klen"])
             if self.on_grad_ready is not None:      # layers >= i (and everything after them) final
-                self.on_grad_ready(self._layer_decay_off[i])
+                self.on_grad_ready(self._layer_decay_off[i])   # (the reducer also waits for the side stream)
         # pos-conv block: x0 = drop(x + gelu(conv(x) + b))
         pc = self.pc
         if ctx["p_h"] > 0:
@@ -569,6 +630,7 @@ class Engine:
             ops.gemm(dv, self.w(EN + "feature_extractor_video.proj.weight"), dfeat, M=M, N=512, K=D, a_kmajor=True,
                      b_kmajor=False, lda=dv.stride(0), ldb=512, ldc=512, alpha=fgm)
             self.video_bwd(ctx["vctx"], dfeat)
+        self.join_side()
 
     # ============================================================================ decoder
     def decoder_fwd(self, enc, bt, train, save, seeds):
@@ -643,12 +705,12 @@ class Engine:
                  b_kmajor=False, lda=dlogits.stride(0), ldb=D, ldc=D)
         dy = ops.layernorm_bwd(dyn, ctx["y_last"], self.arena.master("decoder.after_norm.weight"), ctx["mf"], ctx["rf"],
                                dgamma=self.g("decoder.after_norm.weight"), dbeta=self.g("decoder.after_norm.bias"))
-        g = self._e(R, D)
         for i in reversed(range(self.dl)):
             lc = ctx["layers"][i]
             p = f"decoder.decoders.{i}."
             sa, ca, ff = p + "self_attn.", p + "src_attn.", p + "feed_forward."
-            # FFN
+            # FFN (each g is a fresh buffer: the previous one may still be read by the side stream)
+            g = self._e(R, D)
             ops.ew_bwd(dy, out=g, drop_p=p_d, seed=lc["s6"], db=self.g(ff + "w_2.bias"))
             self._wgrad(g, lc["a"], self.g(ff + "w_2.weight"))
             dh = ops.linear_dgrad(g, self.w(ff + "w_2.weight"), gate=lc["h"], act=RELU, drop_p=p_d, seed=lc["s5"])
@@ -658,6 +720,7 @@ class Engine:
             dy = ops.layernorm_bwd(dn3, lc["y2"], self.arena.master(p + "norm3.weight"), lc["m3"], lc["r3"], dx=dy, dres=dy,
                                    dgamma=self.g(p + "norm3.weight"), dbeta=self.g(p + "norm3.bias"))
             # source attention
+            g = self._e(R, D)
             ops.ew_bwd(dy, out=g, drop_p=p_d, seed=lc["s4"], db=self.g(ca + "linear_out.bias"))
             self._wgrad(g, lc["o2"], self.g(ca + "linear_out.weight"))
             do2 = ops.linear_dgrad(g, self.w(ca + "linear_out.weight"))
@@ -680,6 +743,7 @@ class Engine:
             dy = ops.layernorm_bwd(dn2, lc["y1"], self.arena.master(p + "norm2.weight"), lc["m2"], lc["r2"], dx=dy, dres=dy,
                                    dgamma=self.g(p + "norm2.weight"), dbeta=self.g(p + "norm2.bias"))
             # causal self attention
+            g = self._e(R, D)
             ops.ew_bwd(dy, out=g, drop_p=p_d, seed=lc["s2"], db=self.g(sa + "linear_out.bias"))
             self._wgrad(g, lc["o1"], self.g(sa + "linear_out.weight"))
             do1 = ops.linear_dgrad(g, self.w(sa + "linear_out.weight"))
@@ -778,6 +842,7 @@ class Engine:
         self.encoder_bwd(ctx["ectx"], denc)
         if self.after_backward is not None:
             self.after_backward()
+        self.join_side()
 
     # ========================================================================= inference
     def encode(self, audios, videos, video_lengths=None, train=False):

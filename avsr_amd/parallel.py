@@ -73,6 +73,7 @@ class GradReducer:
         self._next = 0
         self._works = []
         self.enabled = True          # False inside ArenaDDP.no_sync(): gradients accumulate locally
+        self.extra_streams = []      # other streams that produce gradients (the engine's side stream)
 
     def _reduce(self, a, b):
         w = dist.all_reduce(self.flat[a:b], op=dist.ReduceOp.SUM, group=self.group, async_op=self.stream is not None)
@@ -88,6 +89,8 @@ class GradReducer:
             return
         cur = torch.cuda.current_stream(self.flat.device)
         self.stream.wait_stream(cur)             # gradients of these ranges are complete
+        for s in self.extra_streams:             # ... including those computed on side streams
+            self.stream.wait_stream(s)
         with torch.cuda.stream(self.stream):
             for a, b in ranges:
                 self._reduce(a, b)
@@ -161,6 +164,8 @@ class ArenaDDP:
         arena.sync_shadow()
         self.reducer = GradReducer(arena.grad, bucket_bytes=bucket_bytes, group=group, use_stream=use_stream,
                                    segment=arena.segments["decay"])
+        if getattr(eng, "side", None) is not None:
+            self.reducer.extra_streams.append(eng.side)
         self.average = average
         self.broadcast_buffers = broadcast_buffers
         self.require_backward_grad_sync = True

@@ -202,6 +202,18 @@ def main():
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
+    # diagnostic (outside the timed region): host time to issue one step vs its device time
+    issue, dev_ms = [], []
+    for _ in range(3):
+        torch.cuda.synchronize()
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ev0.record()
+        h0 = time.perf_counter()
+        step()
+        issue.append((time.perf_counter() - h0) * 1e3)
+        ev1.record()
+        torch.cuda.synchronize()
+        dev_ms.append(ev0.elapsed_time(ev1))
     losses = out4.cpu().tolist()
     frames = args.steps * B * T * world
     value = frames / elapsed
@@ -233,6 +245,8 @@ def main():
         "model_tflops_per_s": round(value * fpf / world / 1e12, 1),
         "model_mfu": round(value * fpf / world / 1e12 / BF16_PEAK_TFLOPS, 4),
         "loss": [round(x, 4) for x in losses],
+        "host_issue_ms_per_step": round(sum(issue) / len(issue), 2),
+        "device_ms_per_step_synced": round(sum(dev_ms) / len(dev_ms), 2),
         "modality_drops": {"seed": args.seed, "video_off": drops.count("video_off"),
                            "audio_off": drops.count("audio_off"), "none": drops.count(None),
                            "note": "rank 0's timed steps; video_off skips the ResNet backward "
