@@ -170,6 +170,7 @@ class DecAttnParams(ctypes.Structure):
         ("dtype", _i), ("n", _i), ("H", _i), ("klen_max", _i), ("scale", _f),
         ("q", _c_p), ("ldq", _i64), ("k", _c_p), ("ldk", _i64), ("k_bstride", _i64),
         ("v", _c_p), ("ldv", _i64), ("v_bstride", _i64), ("klen", _c_p), ("o", _c_p), ("ldo", _i64),
+        ("kidx", _c_p),
     ]
 
 
@@ -181,6 +182,7 @@ class CtcPrefixParams(ctypes.Structure):
     _fields_ = [
         ("n", _i), ("T", _i), ("V", _i), ("P", _i), ("blank", _i), ("eos", _i), ("out_len", _i),
         ("logp", _c_p), ("r_prev", _c_p), ("last", _c_p), ("ids", _c_p), ("r_new", _c_p), ("psi", _c_p),
+        ("uidx", _c_p), ("logp_ustride", _i64), ("tlen", _c_p),
     ]
 
 
@@ -189,7 +191,7 @@ class BeamSelectParams(ctypes.Structure):
         ("n", _i), ("V", _i), ("P", _i), ("beam", _i), ("blank", _i), ("eos", _i), ("w_dec", _f), ("w_ctc", _f),
         ("dec", _c_p), ("ld", _i64), ("ids", _c_p), ("psi", _c_p), ("s_prev", _c_p), ("score", _c_p),
         ("out_prev", _c_p), ("out_tok", _c_p), ("out_col", _c_p), ("out_score", _c_p), ("out_dec", _c_p),
-        ("out_ctc", _c_p), ("out_s", _c_p),
+        ("out_ctc", _c_p), ("out_s", _c_p), ("nseg", _i), ("seg", _c_p),
     ]
 
 

@@ -80,8 +80,9 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(avsr_dec_attn_params p) {
   const int h = blockIdx.x, i = blockIdx.y;
   const int klen = p.klen ? min(p.klen[i], p.klen_max) : p.klen_max;
   const T* q = (const T*)p.q + (int64_t)i * p.ldq + h * 64;
-  const T* K = (const T*)p.k + (int64_t)i * p.k_bstride + h * 64;
-  const T* Vv = (const T*)p.v + (int64_t)i * p.v_bstride + h * 64;
+  const int kb = p.kidx ? p.kidx[i] : i;
+  const T* K = (const T*)p.k + (int64_t)kb * p.k_bstride + h * 64;
+  const T* Vv = (const T*)p.v + (int64_t)kb * p.v_bstride + h * 64;
   float qr[64];
 #pragma unroll
   for (int d = 0; d < 64; ++d) qr[d] = to_f(q[d]);
@@ -157,12 +158,16 @@ __global__ __launch_bounds__(256) void row_topk_kernel(avsr_topk_params p) {
 // hypothesis, lane j = its j-th scored token; the T recursion is sequential per lane.
 __global__ __launch_bounds__(64) void ctc_prefix_kernel(avsr_ctc_prefix_params p) {
   const int h = blockIdx.x, j = threadIdx.x;
-  const int T = p.T, V = p.V;
+  const int V = p.V;
+  const int u = p.uidx ? p.uidx[h] : 0;
+  const int T = p.uidx ? p.tlen[u] : p.T;         // this utterance's frames
+  const int TS = p.T;                              // row stride of r_prev / r_new
+  if (p.uidx) p.logp += (int64_t)u * p.logp_ustride;
   const bool act = j < p.P;
   const int id = act ? p.ids[h * p.P + j] : 0;
   const bool same = act && id == p.last[h];
-  const float* rp = p.r_prev ? p.r_prev + (int64_t)h * T * 2 : nullptr;
-  float* rn = act ? p.r_new + ((int64_t)h * p.P + j) * T * 2 : nullptr;
+  const float* rp = p.r_prev ? p.r_prev + (int64_t)h * TS * 2 : nullptr;
+  float* rn = act ? p.r_new + ((int64_t)h * p.P + j) * TS * 2 : nullptr;
   // r_prev at the first step: (logzero, cumsum of blank log-probs)
   auto rprev = [&](int t, int q, float cum) -> float { return rp ? rp[t * 2 + q] : (q == 0 ? LOGZERO : cum); };
   const int start = max(p.out_len, 1);
@@ -222,9 +227,13 @@ __global__ __launch_bounds__(256) void beam_select_kernel(avsr_beam_select_param
   int ti[KMAX];
 #pragma unroll
   for (int k = 0; k < KMAX; ++k) { tv[k] = -INFINITY; ti[k] = 0x7fffffff; }
-  const int total = p.n * p.V;
+  // segment (utterance) of this block: rows [r0, r0 + nrow); flat ids are segment-local
+  const int u = blockIdx.x;
+  const int r0 = p.nseg ? p.seg[u] : 0, nrow = p.nseg ? p.seg[u + 1] - r0 : p.n;
+  const int beam = min(p.beam, nrow * p.V);
+  const int total = nrow * p.V;
   for (int f = threadIdx.x; f < total; f += 256) {
-    const int h = f / p.V, v = f - h * p.V;
+    const int h = r0 + f / p.V, v = f - (f / p.V) * p.V;
     float psi = LOGZERO;
     if (v == p.eos) psi = p.psi[h * (p.P + 1) + p.P];
     else if (v != p.blank)
@@ -238,14 +247,14 @@ __global__ __launch_bounds__(256) void beam_select_kernel(avsr_beam_select_param
     int id = f;
 #pragma unroll
     for (int k = 0; k < KMAX; ++k) {
-      if (k < p.beam && (val > tv[k] || (val == tv[k] && id < ti[k]))) {
-        const float t = tv[k]; const int u = ti[k];
-        tv[k] = val; ti[k] = id; val = t; id = u;
+      if (k < beam && (val > tv[k] || (val == tv[k] && id < ti[k]))) {
+        const float t = tv[k]; const int w = ti[k];
+        tv[k] = val; ti[k] = id; val = t; id = w;
       }
     }
   }
   int head = 0;
-  for (int r = 0; r < p.beam; ++r) {
+  for (int r = 0; r < beam; ++r) {
     float v = -INFINITY; int id = 0x7fffffff;
 #pragma unroll
     for (int k = 0; k < KMAX; ++k) if (k == head) { v = tv[k]; id = ti[k]; }
@@ -253,20 +262,21 @@ __global__ __launch_bounds__(256) void beam_select_kernel(avsr_beam_select_param
     block_argmax256(v, id, shv, shi);
     if (mine == id && id != 0x7fffffff) ++head;
     if (threadIdx.x == 0) {
-      const int h = id / p.V, tok = id - h * p.V;
+      const int h = r0 + id / p.V, tok = id - (id / p.V) * p.V;
       int col = p.P - 1;                       // scoring_idmap == -1 -> python index -1
       for (int c = 0; c < p.P; ++c)
         if (p.ids[h * p.P + c] == tok) { col = c; break; }
       float psi = LOGZERO;
       if (tok == p.eos) psi = p.psi[h * (p.P + 1) + p.P];
       else if (tok != p.blank && p.ids[h * p.P + col] == tok) psi = p.psi[h * (p.P + 1) + col];
-      p.out_prev[r] = h;
-      p.out_tok[r] = tok;
-      p.out_col[r] = col;
-      p.out_score[r] = v;
-      p.out_dec[r] = p.dec[(int64_t)h * p.ld + tok];
-      p.out_ctc[r] = psi - p.s_prev[h];
-      p.out_s[r] = psi;
+      const int o = u * p.beam + r;
+      p.out_prev[o] = h;
+      p.out_tok[o] = tok;
+      p.out_col[o] = col;
+      p.out_score[o] = v;
+      p.out_dec[o] = p.dec[(int64_t)h * p.ld + tok];
+      p.out_ctc[o] = psi - p.s_prev[h];
+      p.out_s[o] = psi;
     }
   }
 }
@@ -329,8 +339,10 @@ extern "C" int avsr_ctc_prefix(const avsr_ctc_prefix_params* p, void* stream) {
 
 extern "C" int avsr_beam_select(const avsr_beam_select_params* p, void* stream) {
   if (!p || p->n <= 0) return AVSR_E_ARG;
-  if (p->beam < 1 || p->beam > KMAX || p->beam > p->n * p->V || p->P < 1) return AVSR_E_SHAPE;
-  hipLaunchKernelGGL(beam_select_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, *p);
+  if (p->beam < 1 || p->beam > KMAX || p->P < 1 || p->nseg < 0) return AVSR_E_SHAPE;
+  if (!p->nseg && p->beam > p->n * p->V) return AVSR_E_SHAPE;
+  if (p->nseg && !p->seg) return AVSR_E_ARG;
+  hipLaunchKernelGGL(beam_select_kernel, dim3(p->nseg ? p->nseg : 1), dim3(256), 0, (hipStream_t)stream, *p);
   AVSR_CHECK_LAUNCH();
   return 0;
 }

@@ -104,9 +104,11 @@ class BatchBeamSearch:
         return x, logp, mem
 
     # ----------------------------------------------------------------------- decoder step
-    def _decoder_step(self, eng, toks, pos, n, cache, mem, T):
+    def _decoder_step(self, eng, toks, pos, n, cache, mem, T, kidx=None, klen=None):
         """Decoder.forward_one_step for n prefixes whose last token (position pos) is toks:
-        returns log-probs (n, V) fp32; appends this position's self-attention K/V to cache."""
+        returns log-probs (n, V) fp32; appends this position's self-attention K/V to cache.
+        Batched utterances: memory rows [U*T][2D], hypothesis i attends to block kidx[i] over
+        klen[i] frames."""
         ar = eng.arena
         D, H = eng.dD, eng.dH
         x = eng._e(n, D)
@@ -132,7 +134,9 @@ class BatchBeamSearch:
             q2 = ops.linear_fwd(n2, eng.w(ca + "linear_q.weight"), ar.master(ca + "linear_q.bias"))
             o2 = eng._e(n, D)
             kv = mem[i]
-            ops.dec_attn(q2, kv[:, :D], kv[:, D:], o2, n=n, H=H, klen_max=T, k_bstride=0, v_bstride=0)
+            bs = 0 if kidx is None else T * kv.stride(0)
+            ops.dec_attn(q2, kv[:, :D], kv[:, D:], o2, n=n, H=H, klen_max=T, k_bstride=bs, v_bstride=bs,
+                         kidx=kidx, klen=klen)
             y2 = ops.linear_fwd(o2, eng.w(ca + "linear_out.weight"), ar.master(ca + "linear_out.bias"), res=y1)
             n3, _, _ = ops.layernorm_fwd(y2, ar.master(p + "norm3.weight"), ar.master(p + "norm3.bias"), 1e-12)
             a = ops.linear_fwd(n3, eng.w(ff + "w_1.weight"), ar.master(ff + "w_1.bias"), act=ops.L.ACT_RELU)
@@ -236,6 +240,131 @@ class BatchBeamSearch:
         if len(nbest) == 0:
             return [] if minlenratio < 0.1 else self.forward(x, maxlenratio, max(0.0, minlenratio - 0.1))
         return nbest
+
+    # ----------------------------------------------------------------- batched utterances
+    def decode_batch(self, xs, maxlenratio: float = 0.0, minlenratio: float = 0.0):
+        """Beam search of several utterances at once: xs = list of encoded utterances (T_u, d).
+        Every step runs the decoder, pre-beam, CTC prefix scoring and the per-utterance beam
+        selection for all running hypotheses of all utterances in the same launches (the
+        hypotheses of utterance u are rows [seg[u], seg[u+1])), with one host read-back per
+        step. Per utterance the search is exactly `self(x)`: same scores, same stopping rules
+        (maxlen = T_u, end detection, eos forced at the last step); an utterance that finishes
+        leaves the batch. Returns one n-best list per utterance."""
+        eng = self.e2e.engine()
+        dev = eng.device
+        U = len(xs)
+        if U == 0:
+            return []
+        Ts = [int(x.shape[0]) for x in xs]
+        Tm = max(Ts)
+        maxlens = [T if maxlenratio == 0 else (-int(maxlenratio) if maxlenratio < 0 else max(1, int(maxlenratio * T)))
+                   for T in Ts]
+        D, V, P, beam = eng.dD, self.n_vocab, self.pre_beam_size, self.beam_size
+        ar = eng.arena
+        # padded memory [U][Tm][D] -> CTC log-probs [U][Tm][V] and per-layer cross K/V [U*Tm][2D]
+        xp = torch.zeros(U, Tm, D, device=dev, dtype=eng.dtype)
+        for u, x in enumerate(xs):      # (the cast kernel converts fp32 encoder outputs to bf16 if needed)
+            ops.cast(x.to(dev).reshape(Ts[u], D).contiguous(), xp[u, :Ts[u]])
+        x2 = xp.view(U * Tm, D)
+        cl = eng._e(U * Tm, eng.Vp)
+        ops.linear_fwd(x2, eng.w("ctc.ctc_lo.weight"), ar.master("ctc.ctc_lo.bias"), out=cl[:, :eng.V])
+        logp = torch.empty(U, Tm, eng.V, device=dev, dtype=torch.float32)
+        ops.log_softmax_rows(cl, eng.V, logp.view(U * Tm, eng.V))
+        mem = []
+        for i in range(eng.dl):
+            ca = f"decoder.decoders.{i}.src_attn."
+            mem.append(ops.linear_fwd(x2, ar.span([ca + "linear_k.weight", ca + "linear_v.weight"]),
+                                      ar.span([ca + "linear_k.bias", ca + "linear_v.bias"], buf="master")))
+        tlen = torch.tensor(Ts, dtype=torch.int32).to(dev)
+        NM = U * beam
+        Lmax = max(maxlens) + 1
+        cache = torch.empty(eng.dl, 2, NM, Lmax, D, device=dev, dtype=eng.dtype)
+        cache2 = torch.empty_like(cache)
+        ids = torch.empty(NM, P, device=dev, dtype=torch.int32)
+        psi = torch.empty(NM, P + 1, device=dev, dtype=torch.float32)
+        r_new = torch.empty(NM, P, Tm, 2, device=dev, dtype=torch.float32)
+        r_prev = torch.empty(NM, Tm, 2, device=dev, dtype=torch.float32)
+        r_prev2 = torch.empty_like(r_prev)
+        out = {k: torch.empty(NM, device=dev, dtype=torch.int32) for k in ("prev", "tok", "col")}
+        out.update({k: torch.empty(NM, device=dev, dtype=torch.float32) for k in ("score", "dec", "ctc", "s")})
+        esz = cache.element_size()
+        # running hypotheses, grouped by utterance: host lists
+        run = [[dict(yseq=[self.sos], score=0.0, dec=0.0, ctc=0.0, s=0.0)] for _ in range(U)]
+        active = list(range(U))
+        ended = [[] for _ in range(U)]
+        first = True
+        i = 0
+        while active:
+            hyps = [(u, h) for u in active for h in run[u]]
+            n = len(hyps)
+            pos = i
+            seg_h = [0]
+            for u in active:
+                seg_h.append(seg_h[-1] + len(run[u]))
+            host = torch.tensor([h["yseq"][-1] for _, h in hyps] + [u for u, _ in hyps] +
+                                [Ts[u] for u, _ in hyps] + seg_h, dtype=torch.int32)
+            dv = host.to(dev, non_blocking=True)
+            toks, uidx, klen, seg = dv[:n], dv[n:2 * n], dv[2 * n:3 * n], dv[3 * n:]
+            dec = self._decoder_step(eng, toks, pos, n, cache, mem, Tm, kidx=uidx, klen=klen)
+            ops.row_topk(dec, V, P, ids[:n])
+            ops.ctc_prefix(logp, None if first else r_prev[:n], toks, ids[:n], r_new[:n], psi[:n], n=n, out_len=pos,
+                           blank=self.blank, eos=self.eos, uidx=uidx, tlen=tlen)
+            fv = torch.tensor([h["s"] for _, h in hyps] + [h["score"] for _, h in hyps], dtype=torch.float32)
+            fv = fv.to(dev, non_blocking=True)
+            ops.beam_select(dec, V, ids[:n], psi[:n], fv[:n], fv[n:], out, n=n, beam=beam, blank=self.blank,
+                            eos=self.eos, w_dec=self.w_dec, w_ctc=self.w_ctc, seg=seg)
+            nsel = len(active) * beam
+            res = {k: v[:nsel].cpu() for k, v in out.items()}     # the one host sync per step
+            prev, tok, col = res["prev"].tolist(), res["tok"].tolist(), res["col"].tolist()
+            keep_src, keep_col, still = [], [], []
+            for a, u in enumerate(active):
+                new = []
+                for r in range(beam):
+                    o = a * beam + r
+                    g = prev[o]
+                    h = hyps[g][1]
+                    new.append(dict(yseq=h["yseq"] + [tok[o]], score=float(res["score"][o]),
+                                    dec=h["dec"] + float(res["dec"][o]), ctc=h["ctc"] + float(res["ctc"][o]),
+                                    s=float(res["s"][o]), src=g, col=col[o]))
+                if i == maxlens[u] - 1:
+                    for hyp in new:
+                        hyp["yseq"] = hyp["yseq"] + [self.eos]
+                keep = []
+                for hyp in new:
+                    if hyp["yseq"][-1] == self.eos:
+                        ended[u].append(self._make_hyp(hyp))
+                    else:
+                        keep.append(hyp)
+                done = (maxlenratio == 0.0 and end_detect([h.asdict() for h in ended[u]], i)) or not keep \
+                    or i >= maxlens[u] - 1
+                if done:
+                    run[u] = []
+                    continue
+                run[u] = keep
+                still.append(u)
+                keep_src += [hyp["src"] for hyp in keep]
+                keep_col += [hyp["src"] * P + hyp["col"] for hyp in keep]
+            active = still
+            if not active:
+                break
+            m = len(keep_src)
+            idx = torch.tensor(keep_src + keep_col, dtype=torch.int32).to(dev, non_blocking=True)
+            row = Lmax * D * esz
+            ops.gather_rows(cache, cache2, idx[:m], groups=eng.dl * 2, n=m, row_bytes=(pos + 1) * D * esz,
+                            src_gstride=NM * row, src_rstride=row, dst_gstride=NM * row, dst_rstride=row)
+            cache, cache2 = cache2, cache
+            ops.gather_rows(r_new, r_prev2, idx[m:], groups=1, n=m, row_bytes=Tm * 2 * 4, src_gstride=0,
+                            src_rstride=Tm * 2 * 4, dst_gstride=0, dst_rstride=Tm * 2 * 4)
+            r_prev, r_prev2 = r_prev2, r_prev
+            first = False
+            i += 1
+        results = []
+        for u in range(U):
+            nbest = sorted(ended[u], key=lambda h: float(h.score), reverse=True)
+            if not nbest and minlenratio >= 0.1:
+                nbest = self.forward(xs[u], maxlenratio, max(0.0, minlenratio - 0.1))
+            results.append(nbest)
+        return results
 
     @staticmethod
     def _make_hyp(hyp):

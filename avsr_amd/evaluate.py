@@ -68,9 +68,19 @@ def gather_to_rank0(local, world):
     return [r for _, r in sorted((t for p in parts for t in p), key=lambda t: t[0])]
 
 
-def run_sharded(units, infer, rank=0, world=1):
-    """decode this rank's share with `infer(unit) -> text`; rank 0 returns all texts in order."""
-    return gather_to_rank0([(i, infer(u)) for i, u in shard(units, rank, world)], world)
+def run_sharded(units, infer, rank=0, world=1, infer_batch=None, batch=8):
+    """decode this rank's share with `infer(unit) -> text` (or `infer_batch(list of units) ->
+    texts`, `batch` units at a time: the engine's batched beam search); rank 0 returns all
+    texts in unit order."""
+    mine = shard(units, rank, world)
+    if infer_batch is None:
+        local = [(i, infer(u)) for i, u in mine]
+    else:
+        local = []
+        for s in range(0, len(mine), batch):
+            chunk = mine[s:s + batch]
+            local += list(zip([i for i, _ in chunk], infer_batch([u for _, u in chunk])))
+    return gather_to_rank0(local, world)
 
 
 def lrs2_set_wer(labels, outputs, norm=lambda s: s):
@@ -78,9 +88,34 @@ def lrs2_set_wer(labels, outputs, norm=lambda s: s):
     return wer([norm(l.replace("<unk>", "")) for l in labels], [norm(o.replace("<unk>", "")) for o in outputs])
 
 
-def avcocktail_chunk_wer(label_text, segments, norm=lambda s: s):
-    """eval_avcocktail for one chunk type: segments = [(start_time, output text)]."""
-    outs = [o for _, o in sorted(segments, key=lambda t: t[0])]
+def avcocktail_labels(captions, norm=lambda s: s):
+    """eval_avcocktail's label side (script/evaluation.py:410-434): captions = [(start, end,
+    text)] in file order; empty texts skipped; the session window is [min start, max end];
+    label texts sorted by (start, text) as `sorted(zip(...))` does, joined and normalised.
+    Returns (label_text, (window_start, window_end))."""
+    kept = [(a, b, t) for a, b, t in captions if t != ""]
+    if not kept:
+        raise ValueError("no non-empty caption")
+    start, end = min(a for a, _, _ in kept), max(b for _, b, _ in kept)
+    text = norm(" ".join(t for _, t in sorted((a, t) for a, _, t in kept)))
+    return text, (start, end)
+
+
+def in_window(seg_start, seg_end, window):
+    """a segment is scored unless it starts more than 1 s before the labelled span or ends more
+    than 1 s after it (script/evaluation.py:443-444)"""
+    return not (seg_start + 1 < window[0] or seg_end - 1 > window[1])
+
+
+def avcocktail_chunk_wer(label_text, segments, norm=lambda s: s, window=None):
+    """eval_avcocktail for one chunk type: segments = [(start_time, output text)] or
+    [(start_time, end_time, output text)]; with `window` (see avcocktail_labels) segments outside
+    it are dropped (callers should not decode them at all). Outputs are ordered as
+    `sorted(zip(start_times, outputs))`: by start, ties by text."""
+    segs = [(s[0], s[1], s[2]) if len(s) == 3 else (s[0], None, s[1]) for s in segments]
+    if window is not None:
+        segs = [x for x in segs if in_window(x[0], x[1] if x[1] is not None else x[0], window)]
+    outs = [o for _, o in sorted((a, o) for a, _, o in segs)]
     return wer(reference=label_text, hypothesis=norm(" ".join(outs).replace("<unk>", "")))
 
 

@@ -525,12 +525,13 @@ def log_softmax_rows(x, V, out):
     return out
 
 
-def dec_attn(q, k, v, o, *, n, H, klen_max, k_bstride, v_bstride, klen=None, scale=0.125):
+def dec_attn(q, k, v, o, *, n, H, klen_max, k_bstride, v_bstride, klen=None, scale=0.125, kidx=None):
     """one query per hypothesis: q/o rows i (ld = stride(0)), keys j of hypothesis i at
-    k[i*k_bstride + j*k.stride(-2)] (bstride 0: shared keys)."""
+    k[b*k_bstride + j*k.stride(-2)] with b = kidx[i] (kidx None: b = i; bstride 0: shared keys)."""
     _call("avsr_dec_attn", L.fill(L.DecAttnParams, dtype=dtype_code(q), n=n, H=H, klen_max=klen_max, scale=scale,
                                    q=q, ldq=q.stride(0), k=k, ldk=k.stride(-2), k_bstride=k_bstride, v=v,
-                                   ldv=v.stride(-2), v_bstride=v_bstride, klen=klen, o=o, ldo=o.stride(0)))
+                                   ldv=v.stride(-2), v_bstride=v_bstride, klen=klen, o=o, ldo=o.stride(0),
+                                   kidx=kidx))
     return o
 
 
@@ -539,20 +540,26 @@ def row_topk(x, V, K, ids):
     return ids
 
 
-def ctc_prefix(logp, r_prev, last, ids, r_new, psi, *, n, out_len, blank, eos):
-    T, V = logp.shape
+def ctc_prefix(logp, r_prev, last, ids, r_new, psi, *, n, out_len, blank, eos, uidx=None, tlen=None):
+    """logp (T, V) of one utterance, or (U, Tmax, V) with uidx (per-hypothesis utterance) and
+    tlen (per-utterance frames) for batched decoding"""
+    T, V = logp.shape[-2:]
     _call("avsr_ctc_prefix", L.fill(L.CtcPrefixParams, n=n, T=T, V=V, P=ids.shape[1], blank=blank, eos=eos,
                                      out_len=out_len, logp=logp, r_prev=r_prev, last=last, ids=ids, r_new=r_new,
-                                     psi=psi))
+                                     psi=psi, uidx=uidx, logp_ustride=T * V if uidx is not None else 0,
+                                     tlen=tlen))
 
 
-def beam_select(dec, V, ids, psi, s_prev, score, out, *, n, beam, blank, eos, w_dec, w_ctc):
-    """out: dict of device tensors prev/tok/col (int32) and score/dec/ctc/s (fp32), [beam]"""
+def beam_select(dec, V, ids, psi, s_prev, score, out, *, n, beam, blank, eos, w_dec, w_ctc, seg=None):
+    """out: dict of device tensors prev/tok/col (int32) and score/dec/ctc/s (fp32), [beam] —
+    or, with seg (int32 [U+1] row offsets of U utterances), one selection per utterance into
+    out[*][u*beam + r]"""
     _call("avsr_beam_select", L.fill(L.BeamSelectParams, n=n, V=V, P=ids.shape[1], beam=beam, blank=blank, eos=eos,
                                       w_dec=w_dec, w_ctc=w_ctc, dec=dec, ld=dec.stride(0), ids=ids, psi=psi,
                                       s_prev=s_prev, score=score, out_prev=out["prev"], out_tok=out["tok"],
                                       out_col=out["col"], out_score=out["score"], out_dec=out["dec"],
-                                      out_ctc=out["ctc"], out_s=out["s"]))
+                                      out_ctc=out["ctc"], out_s=out["s"],
+                                      nseg=0 if seg is None else seg.numel() - 1, seg=seg))
 
 
 def gather_rows(src, dst, idx, *, groups, n, row_bytes, src_gstride, src_rstride, dst_gstride, dst_rstride):

@@ -394,6 +394,10 @@ int avsr_adamw(const avsr_adamw_params* p, void* stream);
  *   score[h]; the beam best (h, v) in descending order -> out_prev/out_tok/out_score,
  *   out_dec = dec[h][v], out_ctc = psi - s_prev, out_s = psi, out_col = column of v in
  *   ids[h] (P-1 when v was not scored, the reference's scoring_idmap -1 index).
+ * Batched decoding (several utterances per step, avsr_amd.decode.BatchBeamSearch.decode_batch):
+ *   the optional kidx / uidx+tlen / nseg+seg fields route each hypothesis to its utterance's
+ *   memory, CTC log-probs and beam selection; the reference decodes one utterance at a time
+ *   (script/evaluation.py:280-296), results are identical per utterance.
  * avsr_gather_rows: dst[g][i] = src[g][idx[i]] for i < n, rows of row_bytes; sizes, strides and
  *   pointers multiples of 4 bytes (16-byte words when everything is 16-byte aligned).
  * ------------------------------------------------------------------------------------ */
@@ -408,6 +412,9 @@ typedef struct {
   const void* v; int64_t ldv, v_bstride;
   const int* klen;            /* [n] or NULL (= klen_max) */
   void* o; int64_t ldo;
+  const int* kidx;            /* [n] or NULL: hypothesis i reads key block kidx[i] (base kidx[i]*k_bstride,
+                                 v likewise) instead of block i — batched decoding of several
+                                 utterances whose memories sit in one [U][T][..] buffer */
 } avsr_dec_attn_params;
 int avsr_dec_attn(const avsr_dec_attn_params* p, void* stream);
 
@@ -427,6 +434,10 @@ typedef struct {
   const int* ids;             /* [n][P] */
   float* r_new;               /* [n][P][T][2] */
   float* psi;                 /* [n][P+1] */
+  /* batched utterances (uidx NULL: one utterance): hypothesis h scores utterance uidx[h],
+   * whose log-probs start at logp + uidx[h]*logp_ustride and whose length is tlen[uidx[h]]
+   * (<= T, the row stride of r_prev / r_new) */
+  const int* uidx; int64_t logp_ustride; const int* tlen;
 } avsr_ctc_prefix_params;
 int avsr_ctc_prefix(const avsr_ctc_prefix_params* p, void* stream);
 
@@ -441,6 +452,9 @@ typedef struct {
   const float* score;                  /* [n] */
   int* out_prev; int* out_tok; int* out_col;
   float* out_score; float* out_dec; float* out_ctc; float* out_s;
+  /* batched utterances (nseg 0: one selection over all n rows): selection u runs over rows
+   * [seg[u], seg[u+1]) and writes out_*[u*beam + r]; out_prev is the global row index */
+  int nseg; const int* seg;
 } avsr_beam_select_params;
 int avsr_beam_select(const avsr_beam_select_params* p, void* stream);
 

@@ -86,3 +86,24 @@ def test_sharded_eval_gloo_world2():
     assert res[0][1] == single
     refs = [f"hyp {u}" for u in UNITS]
     assert E.wer(refs, res[0][1]) == E.wer(refs, single) == 0.0
+
+
+def test_avcocktail_window_and_label_order():
+    """eval_avcocktail (script/evaluation.py:406-453): empty captions skipped, labels sorted by
+    (start, text), segments outside [start - 1, end + 1] dropped, outputs sorted by (start, text)."""
+    caps = [(5.0, 7.0, "c d"), (1.0, 3.0, "a b"), (4.0, 4.5, ""), (1.0, 2.0, "a a")]
+    text, win = E.avcocktail_labels(caps)
+    assert text == "a a a b c d" and win == (1.0, 7.0)
+    assert E.in_window(0.5, 3.0, win) and not E.in_window(-0.5, 3.0, win)
+    assert E.in_window(6.0, 8.0, win) and not E.in_window(6.0, 8.5, win)
+    segs = [(5.0, 7.0, "c d"), (1.0, 2.0, "a a a b"), (-2.0, 0.0, "zz"), (6.0, 9.0, "yy")]
+    assert E.avcocktail_chunk_wer(text, segs, window=win) == pytest.approx(0.0)
+    assert E.avcocktail_chunk_wer(text, segs) > 0.0
+    # ties on start time are broken by the text, like sorted(zip(starts, outputs))
+    assert E.avcocktail_chunk_wer("a b", [(1.0, "b"), (1.0, "a")]) == pytest.approx(0.0)
+
+
+def test_run_sharded_batched_single_process():
+    units = list(range(11))
+    got = E.run_sharded(units, None, infer_batch=lambda us: [str(u * 2) for u in us], batch=4)
+    assert got == [str(u * 2) for u in units]

@@ -101,6 +101,20 @@ def test_c1_decode_reference_encoder_output(g, model, state, beam):
     assert worst <= 1e-4
 
 
+@pytest.mark.parametrize("beam", [1, 3, 5])
+def test_c1_decode_batched(g, model, state, beam):
+    """the 8 C1 clips decoded together (BatchBeamSearch.decode_batch, one launch sequence for all
+    utterances) reproduce the reference's per-utterance best hypotheses."""
+    m = _fresh(model, state, torch.float32).eval()
+    bs = get_beam_search_decoder(m.avsr, TOKENS, ctc_weight=0.1, beam_size=beam)
+    hyps = bs.decode_batch([torch.from_numpy(g["c1_enc"][c]).cuda() for c in range(C1["B"])])
+    for c in range(C1["B"]):
+        best = hyps[c][0].asdict()
+        assert best["yseq"] == g[f"c1_yseq_b{beam}_{c}"].tolist(), (c, best["yseq"])
+        ref = float(g[f"c1_score_b{beam}_{c}"][0])
+        assert abs(best["score"] - ref) <= 1e-4 * abs(ref)
+
+
 def test_c1_module_api(g, model, state):
     """Decoder.batch_score (decoder.py:199-227) and CTC.log_softmax (ctc.py:163-170) as the
     reference's scorers call them."""
