@@ -56,6 +56,9 @@ class ConvParams(ctypes.Structure):
         ("splitk", _i),
         ("bias", _c_p), ("act", _i), ("preact", _c_p), ("res", _c_p),
         ("ws", _c_p),
+        ("bnr_h", _c_p), ("bnr_res", _c_p), ("bnr_scale", _c_p), ("bnr_shift", _c_p), ("bnr_prelu", _c_p),
+        ("bnr_mean", _c_p), ("bnr_invstd", _c_p), ("bnr_scale2", _c_p), ("bnr_shift2", _c_p),
+        ("bnr_mean2", _c_p), ("bnr_invstd2", _c_p), ("bnr_ws", _c_p),
     ]
 
 
@@ -94,6 +97,7 @@ class StemPoolParams(ctypes.Structure):
         ("h", _c_p), ("scale", _c_p), ("shift", _c_p), ("prelu", _c_p), ("y", _c_p), ("argmax", _c_p),
         ("dy", _c_p), ("dz", _c_p), ("mean", _c_p), ("invstd", _c_p),
         ("sums", _c_p), ("dprelu", _c_p), ("dgamma", _c_p), ("dbeta", _c_p), ("ws", _c_p),
+        ("hmax", _c_p), ("dh", _c_p),
     ]
 
 
@@ -216,6 +220,7 @@ SYMBOLS = {
     "avsr_conv_bwd_data": ([ctypes.POINTER(ConvParams), _c_p], _i),
     "avsr_conv_bwd_weight": ([ctypes.POINTER(ConvParams), _c_p], _i),
     "avsr_conv_stat_tiles": ([ctypes.POINTER(ConvParams)], _i),
+    "avsr_conv_bnr_tiles": ([ctypes.POINTER(ConvParams)], _i),
     "avsr_conv_wgrad_ws": ([ctypes.POINTER(ConvParams)], _i64),
     "avsr_layernorm_fwd": ([ctypes.POINTER(LayerNormParams), _c_p], _i),
     "avsr_layernorm_bwd": ([ctypes.POINTER(LayerNormParams), _c_p], _i),
@@ -224,7 +229,8 @@ SYMBOLS = {
     "avsr_bn_act_bwd_reduce": ([ctypes.POINTER(BnActParams), _c_p], _i),
     "avsr_bn_bwd_apply": ([ctypes.POINTER(BnActParams), _c_p], _i),
     "avsr_stem_pool_fwd": ([ctypes.POINTER(StemPoolParams), _c_p], _i),
-    "avsr_stem_pool_bwd_reduce": ([ctypes.POINTER(StemPoolParams), _c_p], _i),
+    "avsr_stem_pool_bwd_apply": ([ctypes.POINTER(StemPoolParams), _c_p], _i),
+    "avsr_bn_bwd_finalize": ([ctypes.POINTER(BnActParams), _i, _c_p], _i),
     "avsr_avgpool_fwd": ([_i, _i, _i, _i, _c_p, _c_p, _c_p], _i),
     "avsr_avgpool_bwd": ([_i, _i, _i, _i, _c_p, _c_p, _c_p], _i),
     "avsr_attn_fwd": ([ctypes.POINTER(AttnParams), _c_p], _i),

@@ -40,9 +40,12 @@ struct ConvArgs {
   int M, N, K, splits, kchunk;
   float* ws;                      // bwd_weight split-K slabs [groups][splits][M][N] (nullptr: direct / atomics)
   Epi e;
+  gemmg::BnrArgs bnr;             // K_DGRAD_BNR: BatchNorm-backward reduction of the stored tile
 };
 
-enum { K_FWD = 0, K_DGRAD = 1, K_WGRAD = 2 };
+// K_DGRAD_BNR + r: data-grad whose epilogue is gemmg::epilogue_bnr with residual mode r
+// (0 none, 1 identity, 2 under its own BN); bf16 LDS-DMA path only
+enum { K_FWD = 0, K_DGRAD = 1, K_WGRAD = 2, K_DGRAD_BNR = 3 };
 
 template <typename T, typename OutT, int WM, int WN, int KIND>
 __global__ __launch_bounds__(NT) void conv_kernel(ConvArgs a) {
@@ -363,7 +366,7 @@ __global__ __launch_bounds__(CF::NTH, CF::MINB) void conv_glds_kernel(ConvArgs a
       BConvK<CF::BM, CF::NW> la; la.init(pa, a.a_bytes, a.g, m0, a.M, wave, lane);
       gemmg::BDenseK<CF::BN, CF::NW> lb; lb.init(pb, a.b_bytes, a.K, n0, a.N, kend, wave, lane);
       gemmg::mainloop_glds<CF>(la, lb, kbeg, nk, acc, smem);
-    } else if constexpr (KIND == K_DGRAD) {
+    } else if constexpr (KIND == K_DGRAD || KIND >= K_DGRAD_BNR) {
       BConvKT<CF::BM, CF::NW> la; la.init(pa, a.a_bytes, a.g, m0, a.M, wave, lane);
       BWgtR<CF::BN, CF::NW> lb; lb.init(pb, a.b_bytes, a.g, n0, a.N, wave, lane);
       gemmg::mainloop_glds<CF>(la, lb, kbeg, nk, acc, smem);
@@ -376,7 +379,7 @@ __global__ __launch_bounds__(CF::NTH, CF::MINB) void conv_glds_kernel(ConvArgs a
     GConvK<CF::BM, CF::NW, false> la; la.init(pa, a.g, m0, a.M, kend, wave, lane);
     gemmg::GDenseK<CF::BN, CF::NW> lb; lb.init(pb, a.K, n0, a.N, kend, wave, lane);
     gemmg::mainloop_glds<CF>(la, lb, kbeg, nk, acc, smem);
-  } else if constexpr (KIND == K_DGRAD) {
+  } else if constexpr (KIND == K_DGRAD || KIND >= K_DGRAD_BNR) {
     GConvK<CF::BM, CF::NW, true> la; la.init(pa, a.g, m0, a.M, kend, wave, lane);
     GWgtR<CF::BN, CF::NW> lb; lb.init(pb, a.g, n0, a.N, kend, wave, lane);
     gemmg::mainloop_glds<CF>(la, lb, kbeg, nk, acc, smem);
@@ -384,6 +387,10 @@ __global__ __launch_bounds__(CF::NTH, CF::MINB) void conv_glds_kernel(ConvArgs a
     gemmg::GDenseR<CF::BM, CF::NW> la; la.init(pa, a.g.ldy, m0, a.M, kend, wave, lane);
     GConvR<CF::BN, CF::NW> lb; lb.init(pb, a.g, n0, a.N, kend, wave, lane);
     gemmg::mainloop_glds<CF>(la, lb, kbeg, nk, acc, smem);
+  }
+  if constexpr (KIND >= K_DGRAD_BNR) {
+    gemmg::epilogue_bnr<CF, KIND - K_DGRAD_BNR>(a.e, a.bnr, m0, n0, acc, smem);
+    return;
   }
   Epi e = a.e;
   if (KIND == K_WGRAD && a.ws) e.C = a.ws + ((int64_t)grp * a.splits + sp) * a.M * a.N;
@@ -515,6 +522,12 @@ extern "C" int avsr_conv_stat_tiles(const avsr_conv_params* p) {
   return (M + bm - 1) / bm;
 }
 
+extern "C" int avsr_conv_bnr_tiles(const avsr_conv_params* p) {
+  const int M = p->nimg * p->hin * p->win;
+  const int bm = tile_bm(M, p->cin);
+  return (M + bm - 1) / bm;
+}
+
 extern "C" int avsr_conv_fwd(const avsr_conv_params* p, void* stream) {
   if (!p) return AVSR_E_ARG;
   ConvArgs a;
@@ -555,6 +568,24 @@ extern "C" int avsr_conv_bwd_data(const avsr_conv_params* p, void* stream) {
               ((int64_t)p->nimg * p->hout * p->wout - 1) * p->ldy + p->cout, (int64_t)p->cout * a.K);
   base_epi(a.e);
   a.e.M = a.M; a.e.N = a.N; a.e.C = p->dx; a.e.ldc = p->ldx; a.e.alpha = p->alpha; a.e.beta = p->beta;
+  if (p->bnr_h) {
+    // BN-backward reduction in the epilogue: bf16 LDS-DMA path, one group, every operand of
+    // the epilogue 16-byte aligned with the row stride of dx
+    if (p->dtype != AVSR_BF16 || !conv_glds_enabled() || p->groups != 1 || !p->bnr_ws || !p->bnr_scale ||
+        !p->bnr_shift || !p->bnr_prelu || !p->bnr_mean || !p->bnr_invstd || (p->bnr_scale2 && !p->bnr_res) ||
+        (p->bnr_scale2 && (!p->bnr_shift2 || !p->bnr_mean2 || !p->bnr_invstd2)))
+      return AVSR_E_ARG;
+    if (!avsr_aligned16(p->bnr_h) || (p->bnr_res && !avsr_aligned16(p->bnr_res))) return AVSR_E_ALIGN;
+    a.bnr.h = (const bf16*)p->bnr_h; a.bnr.res = (const bf16*)p->bnr_res;
+    a.bnr.scale = p->bnr_scale; a.bnr.shift = p->bnr_shift; a.bnr.prelu = p->bnr_prelu;
+    a.bnr.mean = p->bnr_mean; a.bnr.invstd = p->bnr_invstd; a.bnr.scale2 = p->bnr_scale2;
+    a.bnr.shift2 = p->bnr_shift2; a.bnr.mean2 = p->bnr_mean2; a.bnr.invstd2 = p->bnr_invstd2; a.bnr.ws = p->bnr_ws;
+    if (a.M == 0) return 0;
+    hipStream_t st = (hipStream_t)stream;
+    if (p->bnr_scale2) return glds_by_tile<bf16, K_DGRAD_BNR + 2>(a, 1, st);
+    if (p->bnr_res) return glds_by_tile<bf16, K_DGRAD_BNR + 1>(a, 1, st);
+    return glds_by_tile<bf16, K_DGRAD_BNR>(a, 1, st);
+  }
   if (a.M == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
   if (p->dtype == AVSR_F32) return by_tile<float, float, K_DGRAD>(a, p->groups, st);

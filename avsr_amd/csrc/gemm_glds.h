@@ -383,6 +383,115 @@ AVSR_DEV void epilogue_g(const Epi& e, int m0, int n0, f32x4 (&acc)[CF::TM][CF::
   }
 }
 
+// BatchNorm(+PReLU) backward reduction fused into a data-gradient epilogue. The tile's
+// values v (alpha*acc + beta*C) are the gradient of y = prelu(z), z = h*scale + shift
+// (+ res | + res*scale2 + shift2); the epilogue stores dz = prelu'(z)*v instead of v and
+// writes the tile's per-column partial sums
+//   ws[tile_m][0][col] = sum dz, [1] = sum dz*xhat, [2] = sum dz*xhat2, [3] = sum v*z*[z<=0]
+// (xhat = (h-mean)*invstd, xhat2 the same for res under its BN) over the tile's valid rows.
+// h / res are laid out like C (row stride ldc). Requires N % 8 == 0 and the vector path.
+struct BnrArgs {
+  const bf16* h; const bf16* res;
+  const float *scale, *shift, *prelu, *mean, *invstd, *scale2, *shift2, *mean2, *invstd2;
+  float* ws;
+};
+
+// RES: 0 no residual, 1 identity residual, 2 residual under its own BN (downsample)
+template <class CF, int RES>
+AVSR_DEV void epilogue_bnr(const Epi& e, const BnrArgs& b, int m0, int n0, f32x4 (&acc)[CF::TM][CF::TN], char* smem) {
+  constexpr int BN = CF::BN, LDR = BN + 4, SR = CF::WM * 32, CG = BN / 8, RP = 33, IT = SR * CG / CF::NTH;
+  static_assert(CF::NTH % CG == 0 && (SR * CG) % CF::NTH == 0, "a thread's column group must be fixed");
+  static_assert(CF::NTH * RP * 4 <= CF::LDS_BYTES, "partials staging exceeds LDS");
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / CF::WN, wn = wave % CF::WN;
+  float* st = (float*)smem;
+  const int lc = (tid % CG) * 8, col = n0 + lc;
+  const bool colok = col < e.N;
+  const bool beta = e.beta != 0.f;
+  float sc[8], sh[8], pw[8], mu[8], is[8], sc2[8], sh2[8], mu2[8], is2[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int c = colok ? col + j : 0;
+    sc[j] = b.scale[c]; sh[j] = b.shift[c]; pw[j] = b.prelu[c]; mu[j] = b.mean[c]; is[j] = b.invstd[c];
+    if constexpr (RES == 2) { sc2[j] = b.scale2[c]; sh2[j] = b.shift2[c]; mu2[j] = b.mean2[c]; is2[j] = b.invstd2[c]; }
+  }
+  float s0[8], s1[8], s2[8], s3[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s0[j] = s1[j] = s2[j] = s3[j] = 0.f;
+  bf16* C = (bf16*)e.C;
+#pragma unroll
+  for (int i = 0; i < CF::FM; ++i) {
+    // this pass's epilogue operands (h, residual, old dx) are requested before the LDS
+    // staging barrier so their latency overlaps it
+    bf16x8 ph[IT], pr[IT], pc[IT];
+    int64_t off[IT];
+    bool ok[IT];
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+      const int lr = (tid + it * CF::NTH) / CG;
+      const int row = m0 + ((lr >> 5) * CF::FM + i) * 32 + (lr & 31);
+      ok[it] = row < e.M && colok;
+      off[it] = ok[it] ? (int64_t)row * e.ldc + col : 0;
+      ph[it] = *(const bf16x8*)(b.h + off[it]);
+      if constexpr (RES != 0) pr[it] = *(const bf16x8*)(b.res + off[it]);
+      if (beta) pc[it] = *(const bf16x8*)(C + off[it]);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int j = 0; j < CF::TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int lr = wm * 32 + h * 16 + 4 * (lane >> 4) + r;
+          st[lr * LDR + (wn * CF::TN + j) * 16 + (lane & 15)] = acc[2 * i + h][j][r];
+        }
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+      if (!ok[it]) continue;
+      const int lr = (tid + it * CF::NTH) / CG;
+      const f32x4 v0 = *(const f32x4*)(st + lr * LDR + lc), v1 = *(const f32x4*)(st + lr * LDR + lc + 4);
+      const float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+      bf16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float vj = v[j] * e.alpha;
+        if (beta) vj += e.beta * (float)pc[it][j];
+        const float hh = (float)ph[it][j];
+        float z = hh * sc[j] + sh[j];
+        float rr = 0.f;
+        if constexpr (RES != 0) rr = (float)pr[it][j];
+        if constexpr (RES == 1) z += rr;
+        if constexpr (RES == 2) z += rr * sc2[j] + sh2[j];
+        const bool pos = z > 0.f;
+        const float d = pos ? vj : vj * pw[j];
+        s3[j] += pos ? 0.f : vj * z;
+        s0[j] += d;
+        s1[j] += d * (hh - mu[j]) * is[j];
+        if constexpr (RES == 2) s2[j] += d * (rr - mu2[j]) * is2[j];
+        o[j] = (bf16)d;
+      }
+      *(bf16x8*)(C + off[it]) = o;
+    }
+  }
+  // per-column sums over the block: thread partials -> LDS (padded rows), then one thread per
+  // (sum, column) adds the NTH/CG threads that own that column group
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    st[tid * RP + j] = s0[j]; st[tid * RP + 8 + j] = s1[j];
+    st[tid * RP + 16 + j] = s2[j]; st[tid * RP + 24 + j] = s3[j];
+  }
+  __syncthreads();
+  for (int t = tid; t < 4 * BN; t += CF::NTH) {
+    const int q = t / BN, cc = t % BN, g = cc >> 3, j = cc & 7;
+    float s = 0.f;
+    for (int k = g; k < CF::NTH; k += CG) s += st[k * RP + q * 8 + j];
+    if (n0 + cc < e.N) b.ws[((int64_t)(m0 / CF::BM) * 4 + q) * e.N + n0 + cc] = s;
+  }
+}
+
 // XCD-aware block order: consecutive remapped ids run on one XCD (shared L2), bijective for
 // any grid size (nwg need not be a multiple of 8)
 AVSR_DEV int xcd_remap(int orig, int nwg) {

@@ -330,12 +330,11 @@ __global__ __launch_bounds__(256) void bn_grad_finalize_kernel(const float* ws, 
   }
 }
 
-// MODE 0: dy given per element; MODE 1: stem max-pool — dy gathered through the argmax
-// (sp.fd_w / sp.fd_hw: host-built fast divisions by W and H*W).
-struct StemGeo { FastDiv fw, fhw; };
-
-template <typename T, int MODE>
-__global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(BnArgs a, avsr_stem_pool_params sp, StemGeo geo) {
+// dz = prelu'(z)*dy with z recomputed; per-block channel partials of sum dz, sum dz*xhat,
+// sum dz*xhat2 and the PReLU-weight sum dy*z*[z<=0] -> ws[block][4][C]. Two vectors per
+// iteration (independent 16-byte loads in flight).
+template <typename T>
+__global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(BnArgs a) {
   constexpr int VE = VecW<T>::VE;
   __shared__ float lds[256 * VE];
   const int cpv = a.C / VE;
@@ -345,57 +344,40 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(BnArgs a, avsr_stem_
   for (int j = 0; j < VE; ++j) { s0[j] = s1[j] = s2[j] = s3[j] = 0.f; }
   const int64_t t0 = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int c0 = (int)(t0 % cpv) * VE;
-  float sc[VE], sh[VE], pw[VE], mu[VE], is[VE];
+  float sc[VE], sh[VE], pw[VE], mu[VE], is[VE], sc2[VE], sh2[VE], mu2[VE], is2[VE];
   chan_load(a.scale, c0, sc); chan_load(a.shift, c0, sh); chan_load(a.prelu, c0, pw);
   chan_load(a.mean, c0, mu); chan_load(a.invstd, c0, is);
+  chan_load(a.scale2, c0, sc2); chan_load(a.shift2, c0, sh2); chan_load(a.mean2, c0, mu2); chan_load(a.invstd2, c0, is2);
   const bool res = a.res != nullptr, res_bn = a.scale2 != nullptr;
-  for (int64_t v = t0; v < nv; v += stride) {
-    float h[VE], r[VE], d[VE];
-    ldv((const T*)a.h + v * VE, h);
-    if (res) ldv((const T*)a.res + v * VE, r);
-    if constexpr (MODE == 0) {
-      ldv((const T*)a.dy + v * VE, d);
-    } else {
-      // input pixel (n, ih, iw) of the stem max-pool; windows (oh, ow) with 2*o-1 <= i <= 2*o+1
-      const uint32_t pix = (uint32_t)(v >> (31 - __builtin_clz(cpv)));   // cpv | 256: a power of two
-      const uint32_t n = fdiv(pix, geo.fhw), rem = pix - n * geo.fhw.d;
-      const int ih = (int)fdiv(rem, geo.fw), iw = (int)(rem - ih * geo.fw.d);
+  for (int64_t v = t0; v < nv; v += 2 * stride) {
+    const bool two = v + stride < nv;
+    float h[2][VE], r[2][VE], d[2][VE];
 #pragma unroll
-      for (int j = 0; j < VE; ++j) d[j] = 0.f;
-      const int oh0 = (ih + 1) / 2 - 1, ow0 = (iw + 1) / 2 - 1;
+    for (int u = 0; u < 2; ++u) {
+      if (u == 1 && !two) break;
+      const int64_t w = v + u * stride;
+      ldv((const T*)a.h + w * VE, h[u]);
+      ldv((const T*)a.dy + w * VE, d[u]);
+      if (res) ldv((const T*)a.res + w * VE, r[u]);
+    }
 #pragma unroll
-      for (int dh = 0; dh < 2; ++dh) {
-        const int oh = oh0 + dh;
-        if (oh < 0 || oh >= sp.Ho || ih < 2 * oh - 1 || ih > 2 * oh + 1) continue;
+    for (int u = 0; u < 2; ++u) {
+      if (u == 1 && !two) break;
+      float dzo[VE];
 #pragma unroll
-        for (int dw = 0; dw < 2; ++dw) {
-          const int ow = ow0 + dw;
-          if (ow < 0 || ow >= sp.Wo || iw < 2 * ow - 1 || iw > 2 * ow + 1) continue;
-          const int64_t ov = (((int64_t)n * sp.Ho + oh) * sp.Wo + ow) * cpv + c0 / VE;
-          const uint8_t want = (uint8_t)((ih - 2 * oh + 1) * 3 + (iw - 2 * ow + 1));
-          float g[VE];
-          ldv((const T*)sp.dy + ov * VE, g);
-          uint8_t am[VE];
-          if constexpr (VE == 8) *(uint2*)am = *(const uint2*)(sp.argmax + ov * VE);
-          else *(uint32_t*)am = *(const uint32_t*)(sp.argmax + ov * VE);
-#pragma unroll
-          for (int j = 0; j < VE; ++j) d[j] += am[j] == want ? g[j] : 0.f;
-        }
+      for (int j = 0; j < VE; ++j) {
+        float z = h[u][j] * sc[j] + sh[j];
+        if (res) z += res_bn ? r[u][j] * sc2[j] + sh2[j] : r[u][j];
+        const bool pos = z > 0.f;
+        const float dz = pos ? d[u][j] : d[u][j] * pw[j];
+        s3[j] += pos ? 0.f : d[u][j] * z;
+        dzo[j] = dz;
+        s0[j] += dz;
+        s1[j] += dz * (h[u][j] - mu[j]) * is[j];
+        if (res_bn) s2[j] += dz * (r[u][j] - mu2[j]) * is2[j];
       }
+      stv((T*)a.dz + (v + u * stride) * VE, dzo);
     }
-    float dzo[VE];
-#pragma unroll
-    for (int j = 0; j < VE; ++j) {
-      float z = h[j] * sc[j] + sh[j];
-      if (res) z += res_bn ? r[j] * a.scale2[c0 + j] + a.shift2[c0 + j] : r[j];
-      const float dz = z > 0.f ? d[j] : d[j] * pw[j];
-      s3[j] += z > 0.f ? 0.f : d[j] * z;
-      dzo[j] = dz;
-      s0[j] += dz;
-      s1[j] += dz * (h[j] - mu[j]) * is[j];
-      if (res_bn) s2[j] += dz * (r[j] - a.mean2[c0 + j]) * a.invstd2[c0 + j];
-    }
-    stv((T*)a.dz + v * VE, dzo);
   }
   // channel partials of this block -> ws[block][q][C]; bn_grad_finalize sums the blocks
   float* wsb = a.ws + (int64_t)blockIdx.x * 4 * a.C;
@@ -403,6 +385,27 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(BnArgs a, avsr_stem_
   block_chan_partial<VE>(s1, lds, cpv, wsb + 1 * a.C);
   block_chan_partial<VE>(s2, lds, cpv, wsb + 2 * a.C);
   block_chan_partial<VE>(s3, lds, cpv, wsb + 3 * a.C);
+}
+
+// ws[nb][4][C] -> ws2[slices][4][C]: block (channel group of 64, slice); each wave takes every
+// 4th block row of the slice, lanes = channels (256-byte coalesced reads)
+__global__ __launch_bounds__(256) void bn_ws_fold_kernel(const float* ws, int nb, int C, int per, float* ws2) {
+  __shared__ float red[4][4][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane, sl = blockIdx.y;
+  const int b0 = sl * per, b1 = min(nb, b0 + per);
+  float s[4] = {0.f, 0.f, 0.f, 0.f};
+  if (c < C)
+    for (int b = b0 + wave; b < b1; b += 4)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) s[q] += ws[((int64_t)b * 4 + q) * C + c];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) red[wave][q][lane] = s[q];
+  __syncthreads();
+  if (wave == 0 && c < C)
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      ws2[((int64_t)sl * 4 + q) * C + c] = red[0][q][lane] + red[1][q][lane] + red[2][q][lane] + red[3][q][lane];
 }
 
 template <typename T>
@@ -486,10 +489,10 @@ __global__ __launch_bounds__(256) void stem_pool_fwd_kernel(avsr_stem_pool_param
     const int ih = min(max(2 * oh - 1 + q / 3, 0), p.H - 1), iw = min(max(2 * ow - 1 + q % 3, 0), p.W - 1);
     ldv(base + (ih * p.W + iw) * p.C, hv[q]);
   }
-  float best[VE];
+  float best[VE], bh[VE];
   uint8_t idx[VE];
 #pragma unroll
-  for (int j = 0; j < VE; ++j) { best[j] = -INFINITY; idx[j] = 0; }
+  for (int j = 0; j < VE; ++j) { best[j] = -INFINITY; bh[j] = 0.f; idx[j] = 0; }
 #pragma unroll
   for (int q = 0; q < 9; ++q) {
     const int ih = 2 * oh - 1 + q / 3, iw = 2 * ow - 1 + q % 3;
@@ -498,13 +501,82 @@ __global__ __launch_bounds__(256) void stem_pool_fwd_kernel(avsr_stem_pool_param
     for (int j = 0; j < VE; ++j) {
       const float z = hv[q][j] * sc[j] + sh[j];
       const float y = z > 0.f ? z : z * pw[j];
-      if (y > best[j]) { best[j] = y; idx[j] = (uint8_t)q; }
+      if (y > best[j]) { best[j] = y; bh[j] = hv[q][j]; idx[j] = (uint8_t)q; }
     }
   }
   const int64_t ov = (int64_t)n * per_img + v;
   stv((T*)p.y + ov * VE, best);
+  if (p.hmax) stv((T*)p.hmax + ov * VE, bh);
   if constexpr (VE == 8) *(uint2*)(p.argmax + ov * VE) = *(const uint2*)idx;
   else *(uint32_t*)(p.argmax + ov * VE) = *(const uint32_t*)idx;
+}
+
+// Stem backward, dense part. The BN reductions run over the pooled grid (h at the argmax,
+// saved by the forward as hmax; dz is nonzero only where an input pixel is some window's
+// argmax, so sum_p dz*xhat = sum_o dzp[o]*xhat(hmax[o])); here dz[p] = sum of dzp[o] over the
+// (at most 4) windows o whose argmax is p, and dh = scale*(dz - S0/M - xhat*S1/M).
+// Grid-stride over 16-byte vectors with the thread's channel group fixed (the stride is a
+// multiple of C/VE), so the per-channel coefficients are formed once per thread.
+template <typename T>
+__global__ __launch_bounds__(256) void stem_bwd_apply_kernel(avsr_stem_pool_params p, FastDiv fw, FastDiv fhw) {
+  constexpr int VE = VecW<T>::VE;
+  const int cpv = p.C / VE, cshift = 31 - __builtin_clz(cpv);
+  const int64_t nv = (int64_t)p.nimg * p.H * p.W * cpv, stride = (int64_t)gridDim.x * 256;
+  const int64_t t0 = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int cv = (int)(t0 % cpv), c0 = cv * VE;
+  const float invM = 1.f / ((float)p.nimg * p.H * p.W);
+  float ka[VE], kb[VE], kc[VE], km[VE];
+#pragma unroll
+  for (int j = 0; j < VE; ++j) {
+    const int c = c0 + j;
+    const float s0 = p.sums[c * 3 + 0] * invM, s1 = p.sums[c * 3 + 1] * invM;
+    ka[j] = p.scale[c]; kb[j] = -p.scale[c] * s1 * p.invstd[c]; kc[j] = -p.scale[c] * s0; km[j] = p.mean[c];
+  }
+  // two vectors per iteration: both h loads and all window gathers in flight together
+  for (int64_t v = t0; v < nv; v += 2 * stride) {
+    const bool two = v + stride < nv;
+    float h[2][VE], d[2][VE];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+#pragma unroll
+      for (int j = 0; j < VE; ++j) d[u][j] = 0.f;
+      if (u == 1 && !two) break;
+      const int64_t w = v + u * stride;
+      const uint32_t pix = (uint32_t)(w >> cshift);
+      const uint32_t n = fdiv(pix, fhw), rem = pix - n * fhw.d;
+      const int ih = (int)fdiv(rem, fw), iw = (int)(rem - ih * fw.d);
+      ldv((const T*)p.h + w * VE, h[u]);
+      // windows (oh, ow) with 2*o-1 <= i <= 2*o+1
+      const int oh0 = (ih + 1) / 2 - 1, ow0 = (iw + 1) / 2 - 1;
+#pragma unroll
+      for (int dh = 0; dh < 2; ++dh) {
+        const int oh = oh0 + dh;
+        if (oh < 0 || oh >= p.Ho || ih < 2 * oh - 1 || ih > 2 * oh + 1) continue;
+#pragma unroll
+        for (int dw = 0; dw < 2; ++dw) {
+          const int ow = ow0 + dw;
+          if (ow < 0 || ow >= p.Wo || iw < 2 * ow - 1 || iw > 2 * ow + 1) continue;
+          const int64_t ov = (((int64_t)n * p.Ho + oh) * p.Wo + ow) * cpv + cv;
+          const uint8_t want = (uint8_t)((ih - 2 * oh + 1) * 3 + (iw - 2 * ow + 1));
+          float g[VE];
+          ldv((const T*)p.dz + ov * VE, g);
+          uint8_t am[VE];
+          if constexpr (VE == 8) *(uint2*)am = *(const uint2*)(p.argmax + ov * VE);
+          else *(uint32_t*)am = *(const uint32_t*)(p.argmax + ov * VE);
+#pragma unroll
+          for (int j = 0; j < VE; ++j) d[u][j] += am[j] == want ? g[j] : 0.f;
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      if (u == 1 && !two) break;
+      float o[VE];
+#pragma unroll
+      for (int j = 0; j < VE; ++j) o[j] = ka[j] * d[u][j] + kb[j] * (h[u][j] - km[j]) + kc[j];
+      stv((T*)p.dh + (v + u * stride) * VE, o);
+    }
+  }
 }
 
 // =============================================================== avg pool
@@ -605,13 +677,32 @@ extern "C" int avsr_bn_act_bwd_reduce(const avsr_bn_act_params* p, void* stream)
   if (rc) return rc;
   if (!p->ws) return AVSR_E_ARG;
   BnArgs a = bn_args(p);
-  avsr_stem_pool_params sp = {};
   const int ve = p->dtype == AVSR_BF16 ? 8 : 4;
   const int g = bn_grid((int64_t)p->M * p->C / ve, p->C / ve);
-  if (p->dtype == AVSR_BF16) hipLaunchKernelGGL((bn_bwd_reduce_kernel<bf16, 0>), dim3(g), dim3(256), 0, (hipStream_t)stream, a, sp, StemGeo{});
-  else hipLaunchKernelGGL((bn_bwd_reduce_kernel<float, 0>), dim3(g), dim3(256), 0, (hipStream_t)stream, a, sp, StemGeo{});
-  hipLaunchKernelGGL(bn_grad_finalize_kernel, dim3(p->C), dim3(256), 0, (hipStream_t)stream, (const float*)p->ws, g,
-                     p->C, p->sums, p->dbeta, p->dgamma, p->dbeta2, p->scale2 ? p->dgamma2 : nullptr, p->dprelu);
+  if (p->dtype == AVSR_BF16) hipLaunchKernelGGL(bn_bwd_reduce_kernel<bf16>, dim3(g), dim3(256), 0, (hipStream_t)stream, a);
+  else hipLaunchKernelGGL(bn_bwd_reduce_kernel<float>, dim3(g), dim3(256), 0, (hipStream_t)stream, a);
+  AVSR_CHECK_LAUNCH();
+  return avsr_bn_bwd_finalize(p, g, stream);
+}
+
+// ws[tiles][4][C] (from the reduce kernel or a data-grad BN epilogue) -> sums + parameter
+// grads. More than 256 partial rows are first folded into 128 slices, stored after the
+// partials (ws holds AVSR_BN_FIN_WS(tiles, C) floats).
+extern "C" int avsr_bn_bwd_finalize(const avsr_bn_act_params* p, int tiles, void* stream) {
+  if (!p || !p->ws || p->C <= 0 || tiles <= 0) return AVSR_E_ARG;
+  const float* ws = p->ws;
+  int nb = tiles;
+  hipStream_t st = (hipStream_t)stream;
+  if (tiles > 256) {
+    constexpr int SL = 128;
+    const int per = (tiles + SL - 1) / SL;
+    float* ws2 = p->ws + (int64_t)tiles * 4 * p->C;
+    hipLaunchKernelGGL(bn_ws_fold_kernel, dim3((p->C + 63) / 64, SL), dim3(256), 0, st, (const float*)p->ws, tiles,
+                       p->C, per, ws2);
+    ws = ws2; nb = SL;
+  }
+  hipLaunchKernelGGL(bn_grad_finalize_kernel, dim3(p->C), dim3(256), 0, st, ws, nb, p->C, p->sums, p->dbeta,
+                     p->dgamma, p->dbeta2, p->dgamma2, p->dprelu);
   AVSR_CHECK_LAUNCH();
   return 0;
 }
@@ -642,22 +733,17 @@ extern "C" int avsr_stem_pool_fwd(const avsr_stem_pool_params* p, void* stream) 
   return 0;
 }
 
-extern "C" int avsr_stem_pool_bwd_reduce(const avsr_stem_pool_params* p, void* stream) {
-  if (!p) return AVSR_E_ARG;
+extern "C" int avsr_stem_pool_bwd_apply(const avsr_stem_pool_params* p, void* stream) {
+  if (!p || !p->dz || !p->dh || !p->sums || !p->argmax) return AVSR_E_ARG;
   const int ve = p->dtype == AVSR_BF16 ? 8 : 4;
-  if (p->C % ve || (256 % (p->C / ve))) return AVSR_E_SHAPE;
-  BnArgs a = {};
-  a.M = p->nimg * p->H * p->W; a.C = p->C; a.h = p->h; a.scale = p->scale; a.shift = p->shift;
-  a.prelu = p->prelu; a.dz = p->dz; a.mean = p->mean; a.invstd = p->invstd; a.sums = p->sums;
-  a.dprelu = p->dprelu; a.dgamma = p->dgamma; a.dbeta = p->dbeta; a.ws = p->ws;
-  if (!p->ws) return AVSR_E_ARG;
+  if (p->C % ve) return AVSR_E_SHAPE;
+  if (256 % (p->C / ve)) return AVSR_E_SHAPE;
   if ((int64_t)p->nimg * p->H * p->W >= (1ll << 31)) return AVSR_E_SHAPE;
-  const StemGeo geo{make_fastdiv(p->W), make_fastdiv(p->H * p->W)};
-  const int g = bn_grid((int64_t)a.M * p->C / ve, p->C / ve);
-  if (p->dtype == AVSR_BF16) hipLaunchKernelGGL((bn_bwd_reduce_kernel<bf16, 1>), dim3(g), dim3(256), 0, (hipStream_t)stream, a, *p, geo);
-  else hipLaunchKernelGGL((bn_bwd_reduce_kernel<float, 1>), dim3(g), dim3(256), 0, (hipStream_t)stream, a, *p, geo);
-  hipLaunchKernelGGL(bn_grad_finalize_kernel, dim3(p->C), dim3(256), 0, (hipStream_t)stream, (const float*)p->ws, g,
-                     p->C, p->sums, p->dbeta, p->dgamma, (float*)nullptr, (float*)nullptr, p->dprelu);
+  if (p->Ho != (p->H + 1) / 2 || p->Wo != (p->W + 1) / 2) return AVSR_E_SHAPE;
+  const int g = bn_grid((int64_t)p->nimg * p->H * p->W * p->C / ve, p->C / ve);
+  const FastDiv fw = make_fastdiv(p->W), fhw = make_fastdiv(p->H * p->W);
+  if (p->dtype == AVSR_BF16) hipLaunchKernelGGL(stem_bwd_apply_kernel<bf16>, dim3(g), dim3(256), 0, (hipStream_t)stream, *p, fw, fhw);
+  else hipLaunchKernelGGL(stem_bwd_apply_kernel<float>, dim3(g), dim3(256), 0, (hipStream_t)stream, *p, fw, fhw);
   AVSR_CHECK_LAUNCH();
   return 0;
 }

@@ -21,6 +21,7 @@ Design (MI355X-first):
     never stored; the loss and its gradient never leave the device (no host sync).
 """
 import math
+import os
 import random
 
 import numpy as np
@@ -31,6 +32,8 @@ from . import _lib as L
 from .arena import Arena
 
 GELU, RELU, NONE = L.ACT_GELU, L.ACT_RELU, L.ACT_NONE
+# BatchNorm-backward reductions in the ResNet data-grad epilogues (bf16); 0 = separate passes (A/B)
+_BN_FUSE = os.environ.get("AVSR_BN_FUSE", "1") == "1"
 
 
 def _pad8(n):
@@ -356,9 +359,10 @@ class Engine:
             ops.bn_finalize(st0, gam, bet, bn.running_mean, bn.running_var, training=False, eps=bn.eps)
         x = self._e(N * 22 * 22, 64)
         am = self._e(N * 22 * 22, 64, dtype=torch.uint8)
-        ops.stem_pool_fwd(h0, N, 44, 44, st0, self.arena.master(R + "frontend3D.2.weight"), x, am)
+        hmax = self._e(N * 22 * 22, 64) if save else None
+        ops.stem_pool_fwd(h0, N, 44, 44, st0, self.arena.master(R + "frontend3D.2.weight"), x, am, hmax=hmax)
         if save:
-            ctx.update(xp=xp, gs=gs, h0=h0, st0=st0, am=am)
+            ctx.update(xp=xp, gs=gs, h0=h0, st0=st0, am=am, hmax=hmax)
         blocks = []
         hw = 22
         for li, bi, cin, cout, s in self.RES_BLOCKS:
@@ -390,52 +394,82 @@ class Engine:
         return feat, ctx
 
     def video_bwd(self, ctx, dfeat):
+        """ResNet backward. With bf16 compute the BatchNorm+PReLU backward reduction of each
+        layer runs in the epilogue of the data-gradient that produces its output gradient
+        (conv2 dgrad -> bn1; a block's last dgrad -> the previous block's bn2 or, for the first
+        block, the stem on its pooled grid), so only the apply pass touches the tensors again."""
         N = ctx["N"]
         R = "encoder.feature_extractor_video.resnet."
         hw = ctx["hw_last"]
+        fuse = self.dtype == torch.bfloat16 and _BN_FUSE
+        blocks = ctx["blocks"]
         dout = self._e(N * hw * hw, 512)
         ops.avgpool_bwd(dfeat, N, hw * hw, 512, dout)
-        for blk in reversed(ctx["blocks"]):
+        red = None                 # (ws, tiles): dout already holds dz of the next bn2
+        for j in range(len(blocks) - 1, -1, -1):
+            blk = blocks[j]
             p, cout, cin = blk["p"], blk["cout"], blk["cin"]
             M2 = blk["h2"].shape[0]
-            dh2 = self._e(M2, cout)
-            if blk["gd"] is not None:
-                dhd = self._e(M2, cout)
-                ops.bn_act_bwd(dout, blk["h2"], blk["st2"], self.arena.master(p + "relu2.weight"), dh2,
-                               res=blk["hd"], st2=blk["std"], dh2=dhd, dprelu=self.g(p + "relu2.weight"),
-                               dgamma=self.g(p + "bn2.weight"), dbeta=self.g(p + "bn2.bias"),
-                               dgamma2=self.g(p + "downsample.1.weight"), dbeta2=self.g(p + "downsample.1.bias"))
-                dz = None
+            down = blk["gd"] is not None
+            res, rst = (blk["hd"], blk["std"]) if down else (blk["x"], None)
+            g2 = dict(dprelu=self.g(p + "relu2.weight"), dgamma=self.g(p + "bn2.weight"), dbeta=self.g(p + "bn2.bias"))
+            if down:
+                g2.update(dgamma2=self.g(p + "downsample.1.weight"), dbeta2=self.g(p + "downsample.1.bias"))
+            # bn2 + prelu2 (+ downsample BN)
+            if red is None:
+                dz2, sums2 = ops.bn_act_bwd_reduce(dout, blk["h2"], blk["st2"], self.arena.master(p + "relu2.weight"),
+                                                   res=res, st2=rst, **g2)
             else:
-                dz = ops.bn_act_bwd(dout, blk["h2"], blk["st2"], self.arena.master(p + "relu2.weight"), dh2,
-                                    res=blk["x"], dprelu=self.g(p + "relu2.weight"),
-                                    dgamma=self.g(p + "bn2.weight"), dbeta=self.g(p + "bn2.bias"))
-                dhd = None
-            # conv2
+                dz2, sums2 = dout, ops.bn_bwd_finalize(red[0], red[1], cout, **g2)
+            dh2 = self._e(M2, cout)
+            dhd = self._e(M2, cout) if down else None
+            ops.bn_bwd_apply(dz2, blk["h2"], blk["st2"], sums2, dh2, res=res, st2=rst, dh2=dhd)
+            # conv2 (its data-grad carries bn1 + prelu1's reduction when fused)
             self._conv_wgrad(blk["g2"], blk["a1"], dh2, self.g(p + "conv2.weight"))
             da1 = self._e(M2, cout)
-            ops.conv_bwd_data(blk["g2"], dh2, self.w(p + "conv2.weight"), da1)
-            # bn1 + prelu1
-            dh1 = self._e(M2, cout)
-            ops.bn_act_bwd(da1, blk["h1"], blk["st1"], self.arena.master(p + "relu1.weight"), dh1,
-                           dprelu=self.g(p + "relu1.weight"), dgamma=self.g(p + "bn1.weight"),
-                           dbeta=self.g(p + "bn1.bias"))
-            self._conv_wgrad(blk["g1"], blk["x"], dh1, self.g(p + "conv1.weight"))
-            Mi = blk["x"].shape[0]
-            if dz is not None:
-                dx = dz                      # identity shortcut: d(block input) starts as dz
-                ops.conv_bwd_data(blk["g1"], dh1, self.w(p + "conv1.weight"), dx, beta=1.0)
+            g1 = dict(dprelu=self.g(p + "relu1.weight"), dgamma=self.g(p + "bn1.weight"), dbeta=self.g(p + "bn1.bias"))
+            prelu1 = self.arena.master(p + "relu1.weight")
+            if fuse:
+                ws, tiles = ops.conv_bwd_data_bnr(blk["g2"], dh2, self.w(p + "conv2.weight"), da1, blk["h1"],
+                                                  blk["st1"], prelu1)
+                dz1, sums1 = da1, ops.bn_bwd_finalize(ws, tiles, cout, **g1)
             else:
-                dx = self._e(Mi, cin)
+                ops.conv_bwd_data(blk["g2"], dh2, self.w(p + "conv2.weight"), da1)
+                dz1, sums1 = ops.bn_act_bwd_reduce(da1, blk["h1"], blk["st1"], prelu1, **g1)
+            dh1 = self._e(M2, cout)
+            ops.bn_bwd_apply(dz1, blk["h1"], blk["st1"], sums1, dh1)
+            self._conv_wgrad(blk["g1"], blk["x"], dh1, self.g(p + "conv1.weight"))
+            # block input gradient: conv1 (+ downsample) data-grads (+ dz2 through an identity
+            # shortcut); the last one carries the reduction of the layer that produced the input
+            if fuse:
+                if j > 0:
+                    pb = blocks[j - 1]
+                    pdown = pb["gd"] is not None
+                    tgt = dict(h=pb["h2"], st=pb["st2"], prelu=self.arena.master(pb["p"] + "relu2.weight"),
+                               res=pb["hd"] if pdown else pb["x"], st2=pb["std"] if pdown else None)
+                else:
+                    tgt = dict(h=ctx["hmax"], st=ctx["st0"], prelu=self.arena.master(R + "frontend3D.2.weight"))
+            red = None
+            if not down:
+                dx = dz2                     # identity shortcut: d(block input) starts as dz2
+                if fuse:
+                    red = ops.conv_bwd_data_bnr(blk["g1"], dh1, self.w(p + "conv1.weight"), dx, beta=1.0, **tgt)
+                else:
+                    ops.conv_bwd_data(blk["g1"], dh1, self.w(p + "conv1.weight"), dx, beta=1.0)
+            else:
+                dx = self._e(blk["x"].shape[0], cin)
                 ops.conv_bwd_data(blk["g1"], dh1, self.w(p + "conv1.weight"), dx)
                 self._conv_wgrad(blk["gd"], blk["x"], dhd, self.g(p + "downsample.0.weight"))
-                ops.conv_bwd_data(blk["gd"], dhd, self.w(p + "downsample.0.weight"), dx, beta=1.0)
+                if fuse:
+                    red = ops.conv_bwd_data_bnr(blk["gd"], dhd, self.w(p + "downsample.0.weight"), dx, beta=1.0, **tgt)
+                else:
+                    ops.conv_bwd_data(blk["gd"], dhd, self.w(p + "downsample.0.weight"), dx, beta=1.0)
             dout = dx
-        # stem
+        # stem: BN/PReLU reduction on the pooled grid, then the argmax-routed apply
         dh0 = self._e(N * 44 * 44, 64)
-        ops.stem_pool_bwd(dout, ctx["am"], ctx["h0"], N, 44, 44, ctx["st0"], self.arena.master(R + "frontend3D.2.weight"),
-                          dh0, dprelu=self.g(R + "frontend3D.2.weight"), dgamma=self.g(R + "frontend3D.1.weight"),
-                          dbeta=self.g(R + "frontend3D.1.bias"))
+        ops.stem_pool_bwd(dout, ctx["am"], ctx["hmax"], ctx["h0"], N, 44, 44, ctx["st0"],
+                          self.arena.master(R + "frontend3D.2.weight"), dh0, dprelu=self.g(R + "frontend3D.2.weight"),
+                          dgamma=self.g(R + "frontend3D.1.weight"), dbeta=self.g(R + "frontend3D.1.bias"), reduced=red)
         gp = self._z(64, 7, 7, 8, dtype=torch.float32)
         ops.conv_bwd_weight(ctx["gs"], ctx["xp"], dh0, gp)
         ops.stem_wgrad_unpack(gp, self.g(R + "frontend3D.0.weight"))

@@ -181,6 +181,33 @@ def conv_bwd_data(g, dy, w, dx, alpha=1.0, beta=0.0):
     return dx
 
 
+def bn_fin_ws(tiles, C):
+    """floats of a BN-backward partials workspace (AVSR_BN_FIN_WS)"""
+    return (tiles + (128 if tiles > 256 else 0)) * 4 * C
+
+
+def conv_bwd_data_bnr(g, dy, w, dx, h, st, prelu, *, res=None, st2=None, alpha=1.0, beta=0.0):
+    """data-grad whose epilogue runs the BatchNorm+PReLU backward reduction of the layer that
+    produced the conv input: dx <- dz = prelu'(z) * (alpha*conv^T(dy) + beta*dx); returns the
+    partial sums (ws, tiles) for bn_bwd_finalize (bf16 only)."""
+    p = g.params(dtype_code(dy))
+    assert dy.dtype == w.dtype == dx.dtype == h.dtype == torch.bfloat16
+    lib = L.load()
+    tiles = lib.avsr_conv_bnr_tiles(ctypes.byref(p))
+    ws = torch.empty(bn_fin_ws(tiles, g.cin), device=dx.device)
+    p.dy, p.w, p.dx = dy.data_ptr(), w.data_ptr(), dx.data_ptr()
+    p.alpha, p.beta = alpha, beta
+    p.bnr_h, p.bnr_res = h.data_ptr(), None if res is None else res.data_ptr()
+    p.bnr_scale, p.bnr_shift, p.bnr_prelu = st.scale.data_ptr(), st.shift.data_ptr(), prelu.data_ptr()
+    p.bnr_mean, p.bnr_invstd = st.mean.data_ptr(), st.invstd.data_ptr()
+    if st2 is not None:
+        p.bnr_scale2, p.bnr_shift2 = st2.scale.data_ptr(), st2.shift.data_ptr()
+        p.bnr_mean2, p.bnr_invstd2 = st2.mean.data_ptr(), st2.invstd.data_ptr()
+    p.bnr_ws = ws.data_ptr()
+    L.check(lib.avsr_conv_bwd_data(ctypes.byref(p), L.stream_ptr()), "avsr_conv_bwd_data(bnr)")
+    return ws, tiles
+
+
 _WGRAD_SLAB = os.environ.get("AVSR_WGRAD_SLAB", "1") == "1"   # 0: atomic split-K (A/B runs)
 
 
@@ -265,47 +292,81 @@ def bn_act_fwd(h, st, prelu, y, res=None, st2=None):
     return y
 
 
+def _bn_params(h, st, *, M=None, res=None, st2=None, **kw):
+    M = h.shape[0] if M is None else M
+    C = h.shape[-1]
+    return L.fill(L.BnActParams, dtype=dtype_code(h), M=M, C=C, h=h, scale=st.scale, shift=st.shift, res=res,
+                  scale2=None if st2 is None else st2.scale, shift2=None if st2 is None else st2.shift,
+                  mean=st.mean, invstd=st.invstd, mean2=None if st2 is None else st2.mean,
+                  invstd2=None if st2 is None else st2.invstd, **kw)
+
+
+def bn_act_bwd_reduce(dy, h, st, prelu, *, res=None, st2=None, dz=None, sums=None, dprelu=None, dgamma=None,
+                      dbeta=None, dgamma2=None, dbeta2=None):
+    """dz = prelu'(z) * dy (z recomputed) and the BN sums [C][3]; accumulates the PReLU / BN
+    parameter gradients. Returns (dz, sums)."""
+    C = h.shape[-1]
+    dz = torch.empty_like(h) if dz is None else dz
+    sums = torch.empty(C, 3, device=h.device) if sums is None else sums
+    ws = torch.empty(bn_fin_ws(2048, C), device=h.device)
+    _call("avsr_bn_act_bwd_reduce", _bn_params(h, st, res=res, st2=st2, ws=ws, prelu=prelu, dy=dy, dz=dz, sums=sums,
+                                               dprelu=dprelu, dgamma=dgamma, dbeta=dbeta, dgamma2=dgamma2,
+                                               dbeta2=dbeta2))
+    return dz, sums
+
+
+def bn_bwd_finalize(ws, tiles, C, *, sums=None, dprelu=None, dgamma=None, dbeta=None, dgamma2=None, dbeta2=None):
+    """sums [C][3] + parameter gradients from the partials of a data-grad BN epilogue."""
+    sums = torch.empty(C, 3, device=ws.device) if sums is None else sums
+    p = L.fill(L.BnActParams, C=C, ws=ws, sums=sums, dprelu=dprelu, dgamma=dgamma, dbeta=dbeta, dgamma2=dgamma2,
+               dbeta2=dbeta2)
+    L.check(L.load().avsr_bn_bwd_finalize(ctypes.byref(p), tiles, L.stream_ptr()), "avsr_bn_bwd_finalize")
+    return sums
+
+
+def bn_bwd_apply(dz, h, st, sums, dh, *, res=None, st2=None, dh2=None, beta_acc=0.0):
+    """dh = scale*(dz - S0/M - xhat*S1/M) (+ beta_acc*dh); dh2 likewise for the downsample BN."""
+    _call("avsr_bn_bwd_apply", _bn_params(h, st, res=res, st2=st2, dz=dz, sums=sums, dh=dh, dh2=dh2,
+                                          beta_acc=beta_acc))
+    return dh
+
+
 def bn_act_bwd(dy, h, st, prelu, dh, *, res=None, st2=None, dh2=None, dz=None, sums=None,
                dprelu=None, dgamma=None, dbeta=None, dgamma2=None, dbeta2=None, beta_acc=0.0):
     """Backward of y = prelu(bn(h) + [bn2(res) | res]): returns dz (grad of the residual
     input when identity) and writes dh (and dh2 for the downsample BN)."""
-    M, C = h.shape
-    dz = torch.empty_like(h) if dz is None else dz
-    sums = torch.empty(C, 3, device=h.device) if sums is None else sums
-    ws = torch.empty(2048 * 4 * C, device=h.device)
-    p = L.fill(L.BnActParams, ws=ws, dtype=dtype_code(h), M=M, C=C, h=h, scale=st.scale, shift=st.shift, res=res,
-               scale2=None if st2 is None else st2.scale, shift2=None if st2 is None else st2.shift,
-               prelu=prelu, dy=dy, dz=dz, mean=st.mean, invstd=st.invstd,
-               mean2=None if st2 is None else st2.mean, invstd2=None if st2 is None else st2.invstd,
-               sums=sums, dprelu=dprelu, dgamma=dgamma, dbeta=dbeta, dgamma2=dgamma2, dbeta2=dbeta2,
-               dh=dh, dh2=dh2, beta_acc=beta_acc)
-    _call("avsr_bn_act_bwd_reduce", p)
-    _call("avsr_bn_bwd_apply", p)
+    dz, sums = bn_act_bwd_reduce(dy, h, st, prelu, res=res, st2=st2, dz=dz, sums=sums, dprelu=dprelu,
+                                 dgamma=dgamma, dbeta=dbeta, dgamma2=dgamma2, dbeta2=dbeta2)
+    bn_bwd_apply(dz, h, st, sums, dh, res=res, st2=st2, dh2=dh2, beta_acc=beta_acc)
     return dz
 
 
-def stem_pool_fwd(h, nimg, H, W, st, prelu, y, argmax):
+def stem_pool_fwd(h, nimg, H, W, st, prelu, y, argmax, hmax=None):
+    """y = maxpool3x3s2(prelu(bn(h))) with the argmax window index and (hmax) h at the argmax"""
     C = h.shape[-1]
     _call("avsr_stem_pool_fwd", L.fill(L.StemPoolParams, dtype=dtype_code(h), nimg=nimg, H=H, W=W, C=C,
                                         Ho=(H + 1) // 2, Wo=(W + 1) // 2, h=h, scale=st.scale, shift=st.shift,
-                                        prelu=prelu, y=y, argmax=argmax))
+                                        prelu=prelu, y=y, argmax=argmax, hmax=hmax))
     return y
 
 
-def stem_pool_bwd(dy, argmax, h, nimg, H, W, st, prelu, dh, *, dz=None, sums=None, dprelu=None,
-                  dgamma=None, dbeta=None):
-    """Backward through max-pool, PReLU and BN of the stem: writes dh (grad of the conv output)."""
+def stem_pool_bwd(dy, argmax, hmax, h, nimg, H, W, st, prelu, dh, *, dzp=None, sums=None, dprelu=None,
+                  dgamma=None, dbeta=None, reduced=None):
+    """Backward through max-pool, PReLU and BN of the stem: writes dh (grad of the conv output).
+    The BN/PReLU reduction runs on the pooled grid (h = hmax); `reduced` = (ws, tiles) when a
+    data-grad BN epilogue already stored the pooled dz in dy and wrote the partials."""
     C = h.shape[-1]
-    dz = torch.empty_like(h) if dz is None else dz
-    sums = torch.empty(C, 3, device=h.device) if sums is None else sums
-    ws = torch.empty(2048 * 4 * C, device=h.device)
-    sp = L.fill(L.StemPoolParams, ws=ws, dtype=dtype_code(h), nimg=nimg, H=H, W=W, C=C, Ho=(H + 1) // 2,
-                Wo=(W + 1) // 2, h=h, scale=st.scale, shift=st.shift, prelu=prelu, argmax=argmax, dy=dy, dz=dz,
-                mean=st.mean, invstd=st.invstd, sums=sums, dprelu=dprelu, dgamma=dgamma, dbeta=dbeta)
-    _call("avsr_stem_pool_bwd_reduce", sp)
-    M = nimg * H * W
-    _call("avsr_bn_bwd_apply", L.fill(L.BnActParams, dtype=dtype_code(h), M=M, C=C, h=h.view(M, C), scale=st.scale,
-                                       shift=st.shift, dz=dz, mean=st.mean, invstd=st.invstd, sums=sums, dh=dh))
+    Ho, Wo = (H + 1) // 2, (W + 1) // 2
+    Mo = nimg * Ho * Wo
+    if reduced is None:
+        dzp, sums = bn_act_bwd_reduce(dy.view(Mo, C), hmax.view(Mo, C), st, prelu, dz=dzp, sums=sums,
+                                      dprelu=dprelu, dgamma=dgamma, dbeta=dbeta)
+    else:
+        dzp = dy
+        sums = bn_bwd_finalize(reduced[0], reduced[1], C, sums=sums, dprelu=dprelu, dgamma=dgamma, dbeta=dbeta)
+    _call("avsr_stem_pool_bwd_apply", L.fill(L.StemPoolParams, dtype=dtype_code(h), nimg=nimg, H=H, W=W, C=C,
+                                              Ho=Ho, Wo=Wo, h=h, scale=st.scale, argmax=argmax, dz=dzp,
+                                              mean=st.mean, invstd=st.invstd, sums=sums, dh=dh))
     return dh
 
 

@@ -108,6 +108,17 @@ typedef struct {
    * laid out like y; used by the pos-conv: x + GELU(conv(x) + b)) */
   const float* bias; int act; void* preact; const void* res;
   float* ws;      /* bwd_weight split-K workspace of avsr_conv_wgrad_ws() floats, or NULL */
+  /* bwd_data, optional (bf16, groups 1): BatchNorm+PReLU backward reduction in the epilogue.
+   * The value v = alpha*conv_transpose(dy, w) + beta*dx is the gradient of prelu(z),
+   * z = h*scale + shift (+ res | + res*scale2 + shift2); dx receives dz = prelu'(z)*v and
+   * bnr_ws[avsr_conv_bnr_tiles()][4][cin] the per-tile column sums (sum dz, sum dz*xhat,
+   * sum dz*xhat2, sum v*z*[z<=0]) that avsr_bn_bwd_finalize folds. h / res laid out like dx.
+   * Replaces the separate avsr_bn_act_bwd_reduce pass over dx (resnet.py:45-62 backward). */
+  const void* bnr_h; const void* bnr_res;
+  const float* bnr_scale; const float* bnr_shift; const float* bnr_prelu;
+  const float* bnr_mean; const float* bnr_invstd;
+  const float* bnr_scale2; const float* bnr_shift2; const float* bnr_mean2; const float* bnr_invstd2;
+  float* bnr_ws;
 } avsr_conv_params;
 
 int avsr_conv_fwd(const avsr_conv_params* p, void* stream);
@@ -115,6 +126,8 @@ int avsr_conv_bwd_data(const avsr_conv_params* p, void* stream);
 int avsr_conv_bwd_weight(const avsr_conv_params* p, void* stream);
 /* number of row tiles the forward partial statistics are split into */
 int avsr_conv_stat_tiles(const avsr_conv_params* p);
+/* number of row tiles of a bwd_data with the BN-backward epilogue (rows of bnr_ws) */
+int avsr_conv_bnr_tiles(const avsr_conv_params* p);
 /* fp32 workspace (floats) bwd_weight uses when p->ws is given (0: it needs none) */
 int64_t avsr_conv_wgrad_ws(const avsr_conv_params* p);
 
@@ -187,26 +200,37 @@ typedef struct {
   void* dh; void* dh2; float beta_acc;             /* bwd_apply outputs (dh2 for the downsample BN) */
   float* ws;                                       /* bwd_reduce workspace >= AVSR_BN_WS(C) floats */
 } avsr_bn_act_params;
-#define AVSR_BN_WS(C) (2048 * 4 * (C))
+/* partial sums of `tiles` row blocks [tiles][4][C] plus the fold area finalize uses */
+#define AVSR_BN_FIN_WS(tiles, C) (((int64_t)(tiles) + ((tiles) > 256 ? 128 : 0)) * 4 * (C))
+#define AVSR_BN_WS(C) AVSR_BN_FIN_WS(2048, C)
 int avsr_bn_act_fwd(const avsr_bn_act_params* p, void* stream);
+/* reduce + finalize (sums, dgamma/dbeta, dprelu) */
 int avsr_bn_act_bwd_reduce(const avsr_bn_act_params* p, void* stream);
+/* finalize only, from partials ws[tiles][4][C] written by a data-grad BN epilogue
+ * (avsr_conv_params.bnr_ws, tiles = avsr_conv_bnr_tiles) */
+int avsr_bn_bwd_finalize(const avsr_bn_act_params* p, int tiles, void* stream);
 int avsr_bn_bwd_apply(const avsr_bn_act_params* p, void* stream);
 
-/* stem: y[n][oh][ow][c] = max_{3x3, s2, p1} prelu(bn(h)) (+argmax index),
- * resnet.py:132-136 (BatchNorm3d + PReLU + MaxPool3d((1,3,3),(1,2,2),(0,1,1))).
- * bwd_reduce: routes dy through the argmax and PReLU -> dz [n][h][w][c], with the BN
- * reductions of avsr_bn_act_bwd_reduce (then avsr_bn_bwd_apply). */
+/* stem: y[n][oh][ow][c] = max_{3x3, s2, p1} prelu(bn(h)) (+argmax index, + hmax = h at the
+ * argmax), resnet.py:132-136 (BatchNorm3d + PReLU + MaxPool3d((1,3,3),(1,2,2),(0,1,1))).
+ * Backward in the pooled domain: the BN/PReLU reduction is avsr_bn_act_bwd_reduce (or a
+ * data-grad BN epilogue) over the POOLED grid with h = hmax, dy = pooled gradient, giving the
+ * pooled dz and the sums over input pixels (dz vanishes off the argmax positions);
+ * bwd_apply: dh[n][h][w][c] = scale*(dz - S0/M - xhat*S1/M), dz routed back through the
+ * argmax (M = nimg*H*W). */
 typedef struct {
   int dtype, nimg, H, W, C, Ho, Wo;
   const void* h; const float* scale; const float* shift; const float* prelu;
   void* y; uint8_t* argmax;
-  const void* dy; void* dz;
+  const void* dy; void* dz;                        /* bwd_apply: dz = pooled dz [n][Ho][Wo][C] */
   const float* mean; const float* invstd;
   float* sums; float* dprelu; float* dgamma; float* dbeta;
-  float* ws;                                       /* >= AVSR_BN_WS(C) floats */
+  float* ws;
+  void* hmax;                                      /* fwd output [n][Ho][Wo][C] (optional) */
+  void* dh;                                        /* bwd_apply output [n][H][W][C] */
 } avsr_stem_pool_params;
 int avsr_stem_pool_fwd(const avsr_stem_pool_params* p, void* stream);
-int avsr_stem_pool_bwd_reduce(const avsr_stem_pool_params* p, void* stream);
+int avsr_stem_pool_bwd_apply(const avsr_stem_pool_params* p, void* stream);
 
 /* global average pool over P pixels: y[n][c] = mean_p x[n][p][c] (nn.AdaptiveAvgPool2d(1),
  * resnet.py:83,121); bwd: dx[n][p][c] = dy[n][c] / P */

@@ -73,3 +73,22 @@ def test_train_step_losses_and_grads(dev, g, dtype):
     for k, row in zip(g["bn_keys"], g["bn_after"]):
         got = bufs[k].flatten()[:8].cpu().numpy()
         np.testing.assert_allclose(got, row, rtol=t["bn"], atol=t["bn"] * 1e-1)
+
+
+def test_resnet_bn_fusion_ab(dev, g, monkeypatch):
+    """bf16: the ResNet backward with the BN reductions fused into the data-grad epilogues
+    (default) equals the separate-pass backward (AVSR_BN_FUSE=0) up to bf16 rounding of the
+    intermediate gradient the separate pass stores."""
+    from avsr_amd import engine as E
+    got = {}
+    for fuse in (True, False):
+        monkeypatch.setattr(E, "_BN_FUSE", fuse)
+        m = _model(g, torch.bfloat16).train()
+        out = m(**_batch(g, dev))
+        out.loss.backward()
+        got[fuse] = {k: p.grad.detach().double().clone() for k, p in m.named_parameters()
+                     if "feature_extractor_video" in k and p.grad is not None}
+    assert got[True].keys() == got[False].keys() and len(got[True]) > 10
+    bad = [(k, rel(got[True][k].cpu(), got[False][k].cpu().numpy())) for k in got[True]
+           if got[False][k].norm() > 0 and rel(got[True][k].cpu(), got[False][k].cpu().numpy()) > 3e-2]
+    assert not bad, bad[:10]

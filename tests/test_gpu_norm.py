@@ -113,7 +113,15 @@ def test_stem_pool(dev, dtype):
     ops.bn_finalize(st, gam.to(dev), bet.to(dev), None, None, partials=_partials(hd.float().cpu().view(-1, C)).to(dev))
     y = torch.empty(n, 22, 22, C, device=dev, dtype=dtype)
     am = torch.empty(n, 22, 22, C, device=dev, dtype=torch.uint8)
-    ops.stem_pool_fwd(hd, n, H, W, st, a.to(dev), y, am)
+    hmax = torch.empty(n, 22, 22, C, device=dev, dtype=dtype)
+    ops.stem_pool_fwd(hd, n, H, W, st, a.to(dev), y, am, hmax=hmax)
+    # hmax = h at the recorded argmax window position
+    q = am.long().cpu()
+    ih = (2 * torch.arange(22).view(1, 22, 1, 1) - 1 + q // 3).clamp(0, H - 1)
+    iw = (2 * torch.arange(22).view(1, 1, 22, 1) - 1 + q % 3).clamp(0, W - 1)
+    hc = hd.cpu()
+    pick = hc[torch.arange(n).view(n, 1, 1, 1), ih, iw, torch.arange(C).view(1, 1, 1, C)]
+    assert torch.equal(pick, hmax.cpu())
     hr = hd.double().cpu().permute(0, 3, 1, 2).requires_grad_()
     P = [t.double().requires_grad_() for t in (gam, bet, a)]
     z = F.prelu(F.batch_norm(hr, None, None, P[0], P[1], training=True, eps=1e-5), P[2])
@@ -123,12 +131,77 @@ def test_stem_pool(dev, dtype):
     ref.backward(dy.double())
     dh = torch.empty_like(hd)
     grads = [torch.zeros(C, device=dev) for _ in range(3)]
-    ops.stem_pool_bwd(dy.permute(0, 2, 3, 1).contiguous().to(dev, dtype), am, hd, n, H, W, st, a.to(dev), dh,
+    ops.stem_pool_bwd(dy.permute(0, 2, 3, 1).contiguous().to(dev, dtype), am, hmax, hd, n, H, W, st, a.to(dev), dh,
                       dgamma=grads[0], dbeta=grads[1], dprelu=grads[2])
     tol = _tol(dtype, 1e-4, 3e-2)
     assert _rel(dh.permute(0, 3, 1, 2), hr.grad) < tol
     for gg, pp in zip(grads, P):
         assert _rel(gg, pp.grad) < tol
+
+
+BNR_CASES = [
+    # nimg, hw (dgrad output = BN input grid), BN channels (conv cin), cout, k, stride, pad, residual
+    (6, 22, 64, 64, 3, 1, 1, "identity"),       # 256x64 tiles, layer 1
+    (5, 22, 64, 128, 1, 2, 0, "downsample"),    # a block's downsample dgrad into the previous bn2
+    (7, 6, 256, 256, 3, 1, 1, "plain"),         # 128x128 tiles, bn1 of layer 3
+    (9, 3, 512, 512, 3, 1, 1, "identity"),      # layer 4, ragged last row tile
+]
+
+
+@pytest.mark.parametrize("case", BNR_CASES)
+def test_conv_dgrad_bn_epilogue(dev, case):
+    """conv_bwd_data_bnr (BN + PReLU backward reduction in the data-grad epilogue) vs fp64:
+    dz = prelu'(z) * (conv^T(dy) + beta*dx_old) and the folded sums / parameter gradients."""
+    n, hw, cin, cout, k, s, p, mode = case
+    g = torch.Generator().manual_seed(n * 1000 + cin)
+    geom = ops.ConvGeom(n, hw, hw, cin, cout, k, k, (s, s), (p, p))
+    ho = geom.hout
+    M = n * hw * hw
+    bf = torch.bfloat16
+    dyt = torch.randn(n, cout, ho, ho, generator=g)
+    wt = torch.randn(cout, cin, k, k, generator=g) * (cout * k * k) ** -0.5
+    h = (torch.randn(M, cin, generator=g) * 1.3 + 0.2).to(bf)
+    r = (torch.randn(M, cin, generator=g) * 0.8 - 0.1).to(bf)
+    old = torch.randn(M, cin, generator=g).to(bf)
+    beta = 0.0 if mode == "plain" else 1.0
+
+    def state():
+        st = ops.BnState(cin, dev)
+        st.mean.copy_(0.1 * torch.randn(cin, generator=g)); st.invstd.copy_(0.5 + torch.rand(cin, generator=g))
+        st.scale.copy_(1 + 0.2 * torch.randn(cin, generator=g)); st.shift.copy_(0.2 * torch.randn(cin, generator=g))
+        return st
+    st = state()
+    st2 = state() if mode == "downsample" else None
+    a = 0.25 + 0.05 * torch.randn(cin, generator=g)
+    dx = old.to(dev).clone()
+    ws, tiles = ops.conv_bwd_data_bnr(geom, dyt.permute(0, 2, 3, 1).contiguous().to(dev, bf),
+                                      wt.permute(0, 2, 3, 1).contiguous().to(dev, bf), dx, h.to(dev), st, a.to(dev),
+                                      res=None if mode == "plain" else r.to(dev), st2=st2, beta=beta)
+    grads = [torch.zeros(cin, device=dev) for _ in range(5)]
+    sums = ops.bn_bwd_finalize(ws, tiles, cin, dbeta=grads[0], dgamma=grads[1], dprelu=grads[4],
+                               dbeta2=grads[2] if st2 else None, dgamma2=grads[3] if st2 else None)
+    # fp64 reference from the same bf16 operands
+    xr = torch.zeros(n, cin, hw, hw, dtype=torch.float64, requires_grad=True)
+    F.conv2d(xr, wt.to(bf).double(), stride=s, padding=p).backward(dyt.to(bf).double())
+    v = xr.grad.permute(0, 2, 3, 1).reshape(M, cin) + beta * old.double()
+    cpu = lambda t: t.double().cpu()
+    hd, rd = h.double(), r.double()
+    z = hd * cpu(st.scale) + cpu(st.shift)
+    if mode == "identity":
+        z = z + rd
+    elif mode == "downsample":
+        z = z + rd * cpu(st2.scale) + cpu(st2.shift)
+    dz = torch.where(z > 0, v, v * a.double())
+    assert _rel(dx.view(M, cin), dz) < 2e-2
+    s0 = dz.sum(0)
+    s1 = (dz * (hd - cpu(st.mean)) * cpu(st.invstd)).sum(0)
+    s3 = torch.where(z > 0, torch.zeros_like(v), v * z).sum(0)
+    tol = 1e-2
+    assert _rel(sums[:, 0], s0) < tol and _rel(sums[:, 1], s1) < tol
+    assert _rel(grads[0], s0) < tol and _rel(grads[1], s1) < tol and _rel(grads[4], s3) < tol
+    if st2 is not None:
+        s2 = (dz * (rd - cpu(st2.mean)) * cpu(st2.invstd)).sum(0)
+        assert _rel(sums[:, 2], s2) < tol and _rel(grads[3], s2) < tol and _rel(grads[2], s0) < tol
 
 
 def test_avgpool(dev):
