@@ -742,6 +742,45 @@ AVSR_DEV void load_img(bf16* img, const bf16* src, int64_t ld, int n, int nz, in
   }
 }
 
+// Two [n][64] row-major operands -> two padded LDS images (rows >= n zero), every global load
+// of a pass issued before any LDS write (one HBM round trip per pass of 4 vectors per thread
+// per image instead of one per vector); out-of-range rows load a clamped valid row and are
+// zeroed by a select, so no load sits behind a branch
+constexpr int LD_IT = 4;
+AVSR_DEV void load_pair(bf16* i1, const bf16* s1, int64_t ld1, bf16* i2, const bf16* s2, int64_t ld2, int n, int nz,
+                        int tid, int nthr) {
+  for (int base = 0; base < nz * 8; base += LD_IT * nthr) {
+    v16 x1[LD_IT], x2[LD_IT];
+#pragma unroll
+    for (int it = 0; it < LD_IT; ++it) {
+      const int id = base + it * nthr + tid, row = id >> 3, ch = (id & 7) * 8;
+      const int rr = min(row, n - 1);
+      x1[it] = *(const v16*)(s1 + (int64_t)rr * ld1 + ch);
+      x2[it] = *(const v16*)(s2 + (int64_t)rr * ld2 + ch);
+    }
+#pragma unroll
+    for (int it = 0; it < LD_IT; ++it) {
+      const int id = base + it * nthr + tid, row = id >> 3, ch = (id & 7) * 8;
+      if (id < nz * 8) {
+        const bool ok = row < n;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { x1[it].w[j] = ok ? x1[it].w[j] : 0u; x2[it].w[j] = ok ? x2[it].w[j] : 0u; }
+        *(v16*)&i1[row * ROW + ch] = x1[it];
+        *(v16*)&i2[row * ROW + ch] = x2[it];
+      }
+    }
+  }
+}
+
+// fragment row load without a branch: row index clamped by the caller's `ok`, value selected
+AVSR_DEV bf16x8 ldrow_sel(const bf16* base, int64_t ld, int row, int nrows, int col) {
+  const v16 x = *(const v16*)(base + (int64_t)min(row, nrows - 1) * ld + col);
+  v16 y;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) y.w[j] = row < nrows ? x.w[j] : 0u;
+  return *(const bf16x8*)&y;
+}
+
 // AttnDrop's 32-bit-index form (the dispatcher guarantees B*H*Lq*ceil(Lk/2) < 2^32) with the
 // golden-ratio premultiply distributed over the index: hash(g) = fmix32(g*G ^ pre) and
 // g*G = rowG + (k/2)*G (mod 2^32), so per pair only an add, a xor and the finaliser remain
@@ -770,13 +809,13 @@ __global__ __launch_bounds__(768) void attn_fwd_kernel(AttnArgs a) {
   const int nk = (a.Lk + 31) & ~31;
   bf16* Ks = sm;
   bf16* Vs = sm + nk * ROW;
-  load_img(Ks, (const bf16*)a.k + (int64_t)b * a.Lk * a.ldk + h * DH, a.ldk, a.Lk, nk, tid, nthr);
-  load_img(Vs, (const bf16*)a.v + (int64_t)b * a.Lk * a.ldv + h * DH, a.ldv, a.Lk, nk, tid, nthr);
   const int q0 = (blockIdx.y * (nthr >> 6) + w) * 32, qi = q0 + c;
   const bf16* Q = (const bf16*)a.q + (int64_t)b * a.Lq * a.ldq + h * DH;
   bf16x8 qf[4];
 #pragma unroll
-  for (int s = 0; s < 4; ++s) qf[s] = ldrow(Q + (int64_t)qi * a.ldq + s * 16 + 8 * hh, qi < a.Lq);
+  for (int s = 0; s < 4; ++s) qf[s] = ldrow_sel(Q, a.ldq, qi, a.Lq, s * 16 + 8 * hh);
+  load_pair(Ks, (const bf16*)a.k + (int64_t)b * a.Lk * a.ldk + h * DH, a.ldk,
+            Vs, (const bf16*)a.v + (int64_t)b * a.Lk * a.ldv + h * DH, a.ldv, a.Lk, nk, tid, nthr);
   const int klen = a.klen ? min(a.klen[b], a.Lk) : a.Lk;
   const int kend = a.causal ? min(klen, q0 + 32) : klen;
   const int nt = (kend + 31) >> 5;
@@ -860,39 +899,55 @@ __global__ __launch_bounds__(NT) void attn_bwd_dkdv_kernel(AttnArgs a) {
   float* dls = lss + nq;                              // delta (0 past Lq)
   const bf16* Q = (const bf16*)a.q + (int64_t)b * a.Lq * a.ldq + h * DH;
   const bf16* dO = (const bf16*)a.dout + (int64_t)b * a.Lq * a.lddo + h * DH;
-  load_img(Qs, Q, a.ldq, a.Lq, nq, tid, nthr);
-  load_img(dOs, dO, a.lddo, a.Lq, nq, tid, nthr);
-  for (int q = tid; q < nq; q += nthr) lss[q] = q < a.Lq ? a.lse[(int64_t)bh * a.Lq + q] * LOG2E : 0.f;
-  __syncthreads();
-  // delta[q] = sum_d dO * O: 8 lanes per query row (one 16-byte chunk each)
-  {
-    const bf16* O = (const bf16*)a.o + (int64_t)b * a.Lq * a.ldo + h * DH;
-    for (int id = tid; id < nq * 8; id += nthr) {
-      const int q = id >> 3, ch = (id & 7) * 8;
-      float sacc = 0.f;
-      if (q < a.Lq) {
-        const bf16x8 ov = *(const bf16x8*)(O + (int64_t)q * a.ldo + ch);
-        const bf16x8 dv = *(const bf16x8*)&dOs[q * ROW + ch];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) sacc += (float)ov[j] * (float)dv[j];
-      }
-      sacc += __shfl_xor(sacc, 1, 64);
-      sacc += __shfl_xor(sacc, 2, 64);
-      sacc += __shfl_xor(sacc, 4, 64);
-      if ((id & 7) == 0) {
-        dls[q] = sacc;
-        if (blockIdx.y == 0 && q < a.Lq) a.delta[(int64_t)bh * a.Lq + q] = sacc;
-      }
-    }
-  }
   const int kb0 = (blockIdx.y * (nthr >> 6) + w) * 32, key = kb0 + c;
   const bf16* K = (const bf16*)a.k + (int64_t)b * a.Lk * a.ldk + h * DH;
   const bf16* V = (const bf16*)a.v + (int64_t)b * a.Lk * a.ldv + h * DH;
   bf16x8 kf[4], vf[4];
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
-    kf[s] = ldrow(K + (int64_t)key * a.ldk + s * 16 + 8 * hh, key < a.Lk);
-    vf[s] = ldrow(V + (int64_t)key * a.ldv + s * 16 + 8 * hh, key < a.Lk);
+    kf[s] = ldrow_sel(K, a.ldk, key, a.Lk, s * 16 + 8 * hh);
+    vf[s] = ldrow_sel(V, a.ldv, key, a.Lk, s * 16 + 8 * hh);
+  }
+  // Q / dO images and delta[q] = sum_d dO * O in one pass: every load of a pass is issued
+  // first; 8 consecutive lanes hold one query row (one 16-byte chunk each)
+  {
+    const bf16* O = (const bf16*)a.o + (int64_t)b * a.Lq * a.ldo + h * DH;
+    for (int base = 0; base < nq * 8; base += LD_IT * nthr) {
+      v16 xq[LD_IT], xd[LD_IT], xo[LD_IT];
+      float ls[LD_IT];
+#pragma unroll
+      for (int it = 0; it < LD_IT; ++it) {
+        const int id = base + it * nthr + tid, rr = min(id >> 3, a.Lq - 1), ch = (id & 7) * 8;
+        xq[it] = *(const v16*)(Q + (int64_t)rr * a.ldq + ch);
+        xd[it] = *(const v16*)(dO + (int64_t)rr * a.lddo + ch);
+        xo[it] = *(const v16*)(O + (int64_t)rr * a.ldo + ch);
+        ls[it] = a.lse[(int64_t)bh * a.Lq + rr];
+      }
+#pragma unroll
+      for (int it = 0; it < LD_IT; ++it) {
+        const int id = base + it * nthr + tid, q = id >> 3, ch = (id & 7) * 8;
+        const bool ok = q < a.Lq;
+        float sacc = 0.f;
+        const bf16x8 ov = *(const bf16x8*)&xo[it], dv = *(const bf16x8*)&xd[it];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) sacc += (float)ov[j] * (float)dv[j];
+        sacc = ok ? sacc : 0.f;
+        sacc += __shfl_xor(sacc, 1, 64);
+        sacc += __shfl_xor(sacc, 2, 64);
+        sacc += __shfl_xor(sacc, 4, 64);
+        if (id < nq * 8) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) { xq[it].w[j] = ok ? xq[it].w[j] : 0u; xd[it].w[j] = ok ? xd[it].w[j] : 0u; }
+          *(v16*)&Qs[q * ROW + ch] = xq[it];
+          *(v16*)&dOs[q * ROW + ch] = xd[it];
+          if ((id & 7) == 0) {
+            dls[q] = sacc;
+            lss[q] = ok ? ls[it] * LOG2E : 0.f;
+            if (blockIdx.y == 0 && ok) a.delta[(int64_t)bh * a.Lq + q] = sacc;
+          }
+        }
+      }
+    }
   }
   const int klen = a.klen ? min(a.klen[b], a.Lk) : a.Lk;
   const float sl2 = a.scale * LOG2E;
@@ -972,8 +1027,6 @@ __global__ __launch_bounds__(768) void attn_bwd_dq_kernel(AttnArgs a, OutT* dq, 
   const int nk = (a.Lk + 31) & ~31;
   bf16* Ks = sm;
   bf16* Vs = sm + nk * ROW;
-  load_img(Ks, (const bf16*)a.k + (int64_t)b * a.Lk * a.ldk + h * DH, a.ldk, a.Lk, nk, tid, nthr);
-  load_img(Vs, (const bf16*)a.v + (int64_t)b * a.Lk * a.ldv + h * DH, a.ldv, a.Lk, nk, tid, nthr);
   const int q0 = (blockIdx.y * (nthr >> 6) + w) * 32, qi = q0 + c;
   const bool qok = qi < a.Lq;
   const bf16* Q = (const bf16*)a.q + (int64_t)b * a.Lq * a.ldq + h * DH;
@@ -981,12 +1034,15 @@ __global__ __launch_bounds__(768) void attn_bwd_dq_kernel(AttnArgs a, OutT* dq, 
   bf16x8 qf[4], of[4];
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
-    qf[s] = ldrow(Q + (int64_t)qi * a.ldq + s * 16 + 8 * hh, qok);
-    of[s] = ldrow(dO + (int64_t)qi * a.lddo + s * 16 + 8 * hh, qok);
+    qf[s] = ldrow_sel(Q, a.ldq, qi, a.Lq, s * 16 + 8 * hh);
+    of[s] = ldrow_sel(dO, a.lddo, qi, a.Lq, s * 16 + 8 * hh);
   }
-  const int64_t bhq = (int64_t)bh * a.Lq + qi;
-  const float lq = qok ? a.lse[bhq] * LOG2E : 0.f;
-  const float dl = qok ? a.delta[bhq] : 0.f;
+  const int64_t bhq = (int64_t)bh * a.Lq + min(qi, a.Lq - 1);
+  const float lq0 = a.lse[bhq], dl0 = a.delta[bhq];
+  load_pair(Ks, (const bf16*)a.k + (int64_t)b * a.Lk * a.ldk + h * DH, a.ldk,
+            Vs, (const bf16*)a.v + (int64_t)b * a.Lk * a.ldv + h * DH, a.ldv, a.Lk, nk, tid, nthr);
+  const float lq = qok ? lq0 * LOG2E : 0.f;
+  const float dl = qok ? dl0 : 0.f;
   const int klen = a.klen ? min(a.klen[b], a.Lk) : a.Lk;
   const int kend = a.causal ? min(klen, q0 + 32) : klen;
   const int nt = (kend + 31) >> 5;

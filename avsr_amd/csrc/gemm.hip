@@ -265,7 +265,7 @@ extern "C" int avsr_gemm(const avsr_gemm_params* p, void* stream) {
   a.sSplit = 0;
   if (slab) {   // partial tiles -> ws[b][split][M][N], reduced below
     e.C = p->ws; e.ldc = p->N; e.alpha = 1.f; e.beta = 0.f;
-    a.sC = (int64_t)splits * p->M * p->N; a.sSplit = (int64_t)p->M * p->N;
+    a.sSplit = (int64_t)p->M * p->N + AVSR_GEMM_SLAB_PAD; a.sC = (int64_t)splits * a.sSplit;
   }
   e.preact = p->preact; e.res = p->res; e.ldr = p->ldr; e.gate = p->gate;
   e.drop_p = p->drop_p; e.seed = p->seed; e.drop_base = 0; e.stats = nullptr; e.stats_tiles = 0;
@@ -278,9 +278,10 @@ extern "C" int avsr_gemm(const avsr_gemm_params* p, void* stream) {
   else rc = by_tile<bf16, bf16>(p, a, st);
   if (rc || !slab) return rc;
   const int64_t per = (int64_t)p->M * (p->N / 4);
-  const dim3 g((unsigned)avsr_grid(per, 256, 1024), p->batch);
-  hipLaunchKernelGGL(slab_reduce_kernel, g, dim3(256), 0, st, (const float*)p->ws, splits, p->M, p->N, (float*)p->C,
-                     p->ldc, p->strideC, p->alpha, p->beta);
+  if (per >= (1ll << 31)) return AVSR_E_SHAPE;
+  const dim3 g((unsigned)avsr_grid(per, 256, 4096), p->batch);
+  hipLaunchKernelGGL(slab_reduce_kernel, g, dim3(256), 0, st, (const float*)p->ws, splits, p->M, p->N,
+                     (int64_t)p->M * p->N + AVSR_GEMM_SLAB_PAD, (float*)p->C, p->ldc, p->strideC, p->alpha, p->beta);
   AVSR_CHECK_LAUNCH();
   return 0;
 }

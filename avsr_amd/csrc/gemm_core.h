@@ -525,18 +525,21 @@ AVSR_DEV void epilogue(const Epi& e, int m0, int n0, f32x16 (&acc)[2][2], char* 
   }
 }
 
-// split-K slab reduce: C[b] = alpha * sum_s ws[b][s] + beta * C[b]   (fp32, 4 columns/thread)
-static __global__ __launch_bounds__(256) void slab_reduce_kernel(const float* ws, int splits, int M, int N, float* C,
-                                                          int64_t ldc, int64_t sC, float alpha, float beta) {
+// split-K slab reduce: C[b] = alpha * sum_s ws[b][s] + beta * C[b]   (fp32, 4 columns/thread;
+// slab s of batch b at ws + (b*splits + s)*sS)
+static __global__ __launch_bounds__(256) void slab_reduce_kernel(const float* ws, int splits, int M, int N, int64_t sS,
+                                                                 float* C, int64_t ldc, int64_t sC, float alpha,
+                                                                 float beta) {
   const int nq = N / 4;
   const int64_t per = (int64_t)M * nq;
   const int b = blockIdx.y;
-  const int64_t mn = (int64_t)M * N;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < per; i += (int64_t)gridDim.x * 256) {
-    const int m = (int)(i / nq), n = (int)(i % nq) * 4;
-    const float* w = ws + (int64_t)b * splits * mn + (int64_t)m * N + n;
+  // per = M * N/4 < 2^31 (host-checked): 32-bit index math (a 64-bit division per vector
+  // made this kernel ALU-bound)
+  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < (uint32_t)per; i += gridDim.x * 256) {
+    const int m = (int)(i / (uint32_t)nq), n = (int)(i - (uint32_t)m * nq) * 4;
+    const float* w = ws + (int64_t)b * splits * sS + (int64_t)m * N + n;
     f32x4 s = *(const f32x4*)w;
-    for (int q = 1; q < splits; ++q) s += *(const f32x4*)(w + q * mn);
+    for (int q = 1; q < splits; ++q) s += *(const f32x4*)(w + q * sS);
     float* c = C + (int64_t)b * sC + (int64_t)m * ldc + n;
     f32x4 o = s * alpha;
     if (beta != 0.f) o += *(const f32x4*)c * beta;

@@ -253,26 +253,68 @@ __global__ __launch_bounds__(256) void sumsq_kernel(const float* x, int64_t n, f
   if (threadIdx.x == 0) atomicAdd(out, sh[0] + sh[1] + sh[2] + sh[3]);
 }
 
-template <typename S>
-__global__ __launch_bounds__(256) void adamw_kernel(avsr_adamw_params p) {
-  float coef = p.grad_scale;
+struct AdamCoef { float coef, step, rbc2, decay; };
+
+AVSR_DEV AdamCoef adam_coef(const avsr_adamw_params& p) {
+  AdamCoef c;
+  c.coef = p.grad_scale;
   if (p.sumsq) {
     const float tn = sqrtf(*p.sumsq) * p.grad_scale;
-    coef *= fminf(1.f, p.max_norm / (tn + 1e-6f));
+    c.coef *= fminf(1.f, p.max_norm / (tn + 1e-6f));
   }
-  const float step = p.lr / p.bias_corr1;
-  const float rbc2 = 1.f / sqrtf(p.bias_corr2);
-  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < p.n; i += (int64_t)gridDim.x * 256) {
-    const float g = p.grad[i] * coef;
-    float w = p.param[i];
-    w -= p.lr * p.weight_decay * w;
-    const float m = p.beta1 * p.exp_avg[i] + (1.f - p.beta1) * g;
-    const float v = p.beta2 * p.exp_avg_sq[i] + (1.f - p.beta2) * g * g;
-    p.exp_avg[i] = m;
-    p.exp_avg_sq[i] = v;
-    w -= step * m / (sqrtf(v) * rbc2 + p.eps);
-    p.param[i] = w;
-    if (p.shadow) ((S*)p.shadow)[i] = from_f<S>(w);
+  c.step = p.lr / p.bias_corr1;
+  c.rbc2 = 1.f / sqrtf(p.bias_corr2);
+  c.decay = p.lr * p.weight_decay;
+  return c;
+}
+
+// one element (torch.optim.AdamW arithmetic: decoupled decay, then the moment update)
+AVSR_DEV float adam_elem(const avsr_adamw_params& p, const AdamCoef& c, float g, float w, float& m, float& v) {
+  g *= c.coef;
+  w -= c.decay * w;
+  m = p.beta1 * m + (1.f - p.beta1) * g;
+  v = p.beta2 * v + (1.f - p.beta2) * g * g;
+  return w - c.step * m / (sqrtf(v) * c.rbc2 + p.eps);
+}
+
+// Four elements per thread and iteration with 16-byte loads / stores: elements [0, head) and
+// [head + 4*nv, n) (fewer than 4 each, to reach / past the 16-byte boundary) by block 0.
+template <typename S>
+__global__ __launch_bounds__(256) void adamw_kernel(avsr_adamw_params p, int head, int64_t nv) {
+  const AdamCoef c = adam_coef(p);
+  if (blockIdx.x == 0 && threadIdx.x < 8) {
+    const int t = threadIdx.x;
+    const int64_t i = t < 4 ? t : head + 4 * nv + (t - 4);
+    if ((t < 4 && t < head) || (t >= 4 && i < p.n)) {
+      float m = p.exp_avg[i], v = p.exp_avg_sq[i];
+      const float w = adam_elem(p, c, p.grad[i], p.param[i], m, v);
+      p.exp_avg[i] = m; p.exp_avg_sq[i] = v; p.param[i] = w;
+      if (p.shadow) ((S*)p.shadow)[i] = from_f<S>(w);
+    }
+  }
+  float* P = p.param + head; const float* G = p.grad + head;
+  float* M = p.exp_avg + head; float* V = p.exp_avg_sq + head;
+  for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < nv; q += (int64_t)gridDim.x * 256) {
+    const f32x4 g = *(const f32x4*)(G + 4 * q);
+    f32x4 w = *(const f32x4*)(P + 4 * q), m = *(const f32x4*)(M + 4 * q), v = *(const f32x4*)(V + 4 * q);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float mj = m[j], vj = v[j];
+      w[j] = adam_elem(p, c, g[j], w[j], mj, vj);
+      m[j] = mj; v[j] = vj;
+    }
+    *(f32x4*)(P + 4 * q) = w; *(f32x4*)(M + 4 * q) = m; *(f32x4*)(V + 4 * q) = v;
+    if (p.shadow) {
+      S* sh = (S*)p.shadow + head + 4 * q;
+      if constexpr (sizeof(S) == 2) {
+        bf16x4 o;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] = (bf16)w[j];
+        *(bf16x4*)sh = o;
+      } else {
+        *(f32x4*)sh = w;
+      }
+    }
   }
 }
 
@@ -291,8 +333,10 @@ int ew_launch(const avsr_ew_params* p, hipStream_t st) {
   if (p->db && !p->ws) return AVSR_E_ARG;
   const int nv = p->N / ve;
   dim3 grid((nv + 63) / 64, 1);
-  int gy = 2048 / (int)grid.x;
-  gy = gy < 16 ? 16 : (gy > 256 ? 256 : gy);
+  // ~4096 blocks (16 waves per CU) for latency hiding; at most AVSR_EW_ROWBLOCKS row blocks
+  // of column partials for colsum_finalize
+  int gy = 4096 / (int)grid.x;
+  gy = gy < 16 ? 16 : (gy > AVSR_EW_ROWBLOCKS ? AVSR_EW_ROWBLOCKS : gy);
   gy = gy > p->rows ? p->rows : gy;
   grid.y = gy;
   EwArgs a = ew_args(p);
@@ -447,9 +491,19 @@ extern "C" int avsr_sumsq(const float* x, int64_t n, float* out, void* stream) {
 extern "C" int avsr_adamw(const avsr_adamw_params* p, void* stream) {
   if (!p) return AVSR_E_ARG;
   if (p->n == 0) return 0;
-  const int g = avsr_grid(p->n, 256, 4096);
-  if (p->shadow_dtype == AVSR_F32) hipLaunchKernelGGL(adamw_kernel<float>, dim3(g), dim3(256), 0, (hipStream_t)stream, *p);
-  else hipLaunchKernelGGL(adamw_kernel<bf16>, dim3(g), dim3(256), 0, (hipStream_t)stream, *p);
+  // the four fp32 arrays share their offset modulo 16 bytes (one arena index); the shadow must
+  // then be 8-byte (bf16) / 16-byte (fp32) aligned at the same element
+  const uintptr_t a0 = (uintptr_t)p->param & 15;
+  if ((((uintptr_t)p->grad & 15) != a0) || (((uintptr_t)p->exp_avg & 15) != a0) || (((uintptr_t)p->exp_avg_sq & 15) != a0) || (a0 & 3))
+    return AVSR_E_ALIGN;
+  int head = (int)(((16 - a0) & 15) / 4);
+  if (head > p->n) head = (int)p->n;
+  const int64_t nv = (p->n - head) / 4;
+  const size_t ssz = p->shadow_dtype == AVSR_F32 ? 4 : 2;
+  if (p->shadow && (((uintptr_t)p->shadow + head * ssz) & (4 * ssz - 1))) return AVSR_E_ALIGN;
+  const int g = avsr_grid(nv > 0 ? nv : 1, 256, 4096);
+  if (p->shadow_dtype == AVSR_F32) hipLaunchKernelGGL(adamw_kernel<float>, dim3(g), dim3(256), 0, (hipStream_t)stream, *p, head, nv);
+  else hipLaunchKernelGGL(adamw_kernel<bf16>, dim3(g), dim3(256), 0, (hipStream_t)stream, *p, head, nv);
   AVSR_CHECK_LAUNCH();
   return 0;
 }

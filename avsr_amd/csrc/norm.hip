@@ -58,19 +58,23 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(LnArgs a) {
   if (lane == 0) { a.mean[row] = mean; a.rstd[row] = rstd; }
 }
 
-// grid-stride over rows (one wave per row at a time); dgamma/dbeta accumulated per lane in
-// registers, then one fp32 atomic per column per wave
+// grid-stride over rows (one wave per row at a time, 8 waves per block); dgamma/dbeta
+// accumulated per lane in registers, summed over the block's waves in LDS and written as
+// one partial row per block (colsum_finalize adds the blocks)
+constexpr int LN_BWD_WAVES = 8;
 template <typename T, int VPL>
-__global__ __launch_bounds__(256) void ln_bwd_kernel(LnArgs a) {
+__global__ __launch_bounds__(64 * LN_BWD_WAVES) void ln_bwd_kernel(LnArgs a) {
   constexpr int VE = VecW<T>::VE;
   const int lane = threadIdx.x & 63;
-  const int nw = gridDim.x * 4;
-  float dg[VPL][VE], db[VPL][VE];
+  const int nw = gridDim.x * LN_BWD_WAVES;
+  float dg[VPL][VE], db[VPL][VE], gm[VPL][VE];
 #pragma unroll
-  for (int i = 0; i < VPL; ++i)
+  for (int i = 0; i < VPL; ++i) {
+    const int c = (lane + i * 64) * VE;
 #pragma unroll
-    for (int j = 0; j < VE; ++j) { dg[i][j] = 0.f; db[i][j] = 0.f; }
-  for (int row = blockIdx.x * 4 + (threadIdx.x >> 6); row < a.rows; row += nw) {
+    for (int j = 0; j < VE; ++j) { dg[i][j] = 0.f; db[i][j] = 0.f; gm[i][j] = c < a.N ? a.gamma[c + j] : 0.f; }
+  }
+  for (int row = blockIdx.x * LN_BWD_WAVES + (threadIdx.x >> 6); row < a.rows; row += nw) {
     const T* x = (const T*)a.x + (int64_t)row * a.ldx;
     const T* dy = (const T*)a.dy + (int64_t)row * a.lddy;
     const float mean = a.mean[row], rstd = a.rstd[row];
@@ -86,7 +90,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(LnArgs a) {
 #pragma unroll
         for (int j = 0; j < VE; ++j) {
           xh[i][j] = (xv[j] - mean) * rstd;
-          g[i][j] = dv[j] * a.gamma[c + j];
+          g[i][j] = dv[j] * gm[i][j];
           s1 += g[i][j];
           s2 += g[i][j] * xh[i][j];
           dg[i][j] += dv[j] * xh[i][j];
@@ -117,8 +121,8 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(LnArgs a) {
     }
   }
   if (!a.dgamma) return;
-  // per-block column partials (4 waves summed in LDS) -> ws[block][2][N]
-  __shared__ float red[4 * 2048];
+  // per-block column partials (the block's waves summed in LDS) -> ws[block][2][N]
+  __shared__ float red[LN_BWD_WAVES * 2048];
   const int w = threadIdx.x >> 6;
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
@@ -131,8 +135,12 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(LnArgs a) {
         for (int j = 0; j < VE; ++j) red[w * a.N + c + j] = q == 0 ? dg[i][j] : db[i][j];
     }
     __syncthreads();
-    for (int c = threadIdx.x; c < a.N; c += 256)
-      a.ws[((int64_t)blockIdx.x * 2 + q) * a.N + c] = red[c] + red[a.N + c] + red[2 * a.N + c] + red[3 * a.N + c];
+    for (int c = threadIdx.x; c < a.N; c += 64 * LN_BWD_WAVES) {
+      float t = 0.f;
+#pragma unroll
+      for (int v = 0; v < LN_BWD_WAVES; ++v) t += red[v * a.N + c];
+      a.ws[((int64_t)blockIdx.x * 2 + q) * a.N + c] = t;
+    }
   }
 }
 
@@ -146,12 +154,15 @@ int ln_launch(const avsr_layernorm_params* p, bool bwd, hipStream_t st) {
   a.dres = p->dres; a.lddres = p->lddres; a.dgamma = p->dgamma; a.dbeta = p->dbeta; a.ws = p->ws;
   const int vpl = (p->N / VE + 63) / 64;
   int blocks = (p->rows + 3) / 4;
-  if (bwd) blocks = blocks < 256 ? blocks : 256;
+  if (bwd) {
+    blocks = (p->rows + LN_BWD_WAVES - 1) / LN_BWD_WAVES;
+    blocks = blocks < AVSR_LN_BLOCKS ? blocks : AVSR_LN_BLOCKS;
+  }
   if (bwd && p->dgamma && (!p->ws || p->N > 2048)) return AVSR_E_ARG;
 #define LNL(V)                                                                                   \
   if (vpl <= V) {                                                                                \
     if (bwd) {                                                                                   \
-      hipLaunchKernelGGL((ln_bwd_kernel<T, V>), dim3(blocks), dim3(256), 0, st, a);              \
+      hipLaunchKernelGGL((ln_bwd_kernel<T, V>), dim3(blocks), dim3(64 * LN_BWD_WAVES), 0, st, a); \
       if (p->dgamma) {                                                                           \
         hipLaunchKernelGGL(colsum_finalize_kernel, colsum_grid(2 * p->N), dim3(256), 0, st,     \
                            (const float*)p->ws, blocks, (int64_t)2 * p->N, 2 * p->N, p->dgamma, \

@@ -247,7 +247,7 @@ class Engine:
         def run():
             ws = None
             if splitk > 1:
-                ws = torch.empty(splitk * N * K, device=dy.device, dtype=torch.float32)
+                ws = torch.empty(ops.slab_ws(1, splitk, N, K), device=dy.device, dtype=torch.float32)
             ops.gemm(dy, x, dW, M=N, N=K, K=M, a_kmajor=False, b_kmajor=False, lda=dy.stride(0), ldb=x.stride(0),
                      ldc=dW.stride(0), alpha=alpha, beta=1.0, splitk=splitk, ws=ws)
         self._on_side(run, dy, x)

@@ -16,6 +16,13 @@ _DT = {torch.float32: L.AVSR_F32, torch.bfloat16: L.AVSR_BF16}
 # "events": [(start, end), ...]}} — HIP events recorded on the launching (current) stream
 PROBE = {}
 
+SLAB_PAD = 1088   # AVSR_GEMM_SLAB_PAD
+
+
+def slab_ws(batch, splitk, M, N):
+    """fp32 floats of a split-K slab workspace (AVSR_GEMM_SLAB_WS)"""
+    return batch * splitk * (M * N + SLAB_PAD)
+
 
 def dtype_code(t):
     try:
@@ -62,7 +69,7 @@ def gemm(A, B, C, *, M, N, K, a_kmajor, b_kmajor, lda, ldb, ldc, batch=1,
     p.drop_p, p.seed = float(drop_p), int(seed) & 0xFFFFFFFFFFFFFFFF
     p.splitk = int(splitk)
     if ws is not None:
-        assert ws.dtype == torch.float32 and ws.numel() >= batch * splitk * M * N
+        assert ws.dtype == torch.float32 and ws.numel() >= slab_ws(batch, splitk, M, N)
         p.ws = ws.data_ptr()
     probe = PROBE.get("gemm")
     if probe is not None and probe["match"](M, N, K, a_kmajor, b_kmajor, dt):
@@ -252,7 +259,7 @@ def layernorm_bwd(dy, x, gamma, mean, rstd, dx=None, dres=None, dgamma=None, dbe
     """dx = dres + LN-backward(dy); dgamma/dbeta (fp32) accumulate."""
     rows, N = x.shape
     dx = torch.empty_like(x) if dx is None else dx
-    ws = None if dgamma is None else torch.empty(256 * 2 * N, device=x.device)
+    ws = None if dgamma is None else torch.empty(256 * 2 * N, device=x.device)   # AVSR_LN_WS
     _call("avsr_layernorm_bwd", L.fill(L.LayerNormParams, dtype=dtype_code(x), rows=rows, N=N, eps=0.0,
                                         x=x, ldx=x.stride(0), ldy=N, gamma=gamma, mean=mean, rstd=rstd,
                                         dy=dy, lddy=dy.stride(0), dx=dx, lddx=dx.stride(0),
@@ -472,7 +479,7 @@ def loss_finalize(B, nll, row_loss, row_correct, mtlalpha, out):
 
 def ew_bwd(dy, *, out=None, gate=None, act=L.ACT_NONE, drop_p=0.0, seed=0, alpha=1.0, db=None):
     rows, N = dy.shape
-    ws = None if db is None else torch.empty(256 * N, device=dy.device)
+    ws = None if db is None else torch.empty(256 * N, device=dy.device)   # AVSR_EW_WS
     _call("avsr_ew_bwd", L.fill(L.EwParams, dtype=dtype_code(dy), rows=rows, N=N, dy=dy, lddy=dy.stride(0), ws=ws,
                                  out=out, ldout=0 if out is None else out.stride(0), gate=gate,
                                  ldgate=0 if gate is None else gate.stride(0), act=act, drop_p=float(drop_p),

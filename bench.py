@@ -190,13 +190,19 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     drops.clear()
+    ms0 = torch.cuda.memory_stats(dev)
+    host_t = []
     t0 = time.perf_counter()
     for _ in range(args.steps):
+        h0 = time.perf_counter()
         out4 = step()
+        host_t.append(time.perf_counter() - h0)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    ms1 = torch.cuda.memory_stats(dev)
+    timed_drops = list(drops)
     probe_ev = ops.PROBE.pop("gemm")["events"]
     if world > 1:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
@@ -247,8 +253,11 @@ def main():
         "loss": [round(x, 4) for x in losses],
         "host_issue_ms_per_step": round(sum(issue) / len(issue), 2),
         "device_ms_per_step_synced": round(sum(dev_ms) / len(dev_ms), 2),
-        "modality_drops": {"seed": args.seed, "video_off": drops.count("video_off"),
-                           "audio_off": drops.count("audio_off"), "none": drops.count(None),
+        "host_ms_per_step_timed": round(sum(host_t) / len(host_t) * 1e3, 2),
+        "allocator_timed": {k: ms1.get(k, 0) - ms0.get(k, 0) for k in
+                            ("num_device_alloc", "num_device_free", "num_alloc_retries", "num_sync_all_streams")},
+        "modality_drops": {"seed": args.seed, "video_off": timed_drops.count("video_off"),
+                           "audio_off": timed_drops.count("audio_off"), "none": timed_drops.count(None),
                            "note": "rank 0's timed steps; video_off skips the ResNet backward "
                                    "(its gradient is exactly zero, avhubert.py:480)"},
     }

@@ -69,10 +69,16 @@ typedef struct {
   float drop_p;              /* dropout probability (0 = off) */
   uint64_t seed;             /* counter-based dropout stream id */
   int splitk;                /* >1: K split over blocks (C must be fp32) */
-  float* ws;                 /* split-K slab workspace, batch*splitk*M*N fp32: each split stores its
-                                partial tile, a reduce pass writes C = alpha*sum + beta*C (plain
-                                epilogue only). NULL: C += alpha*acc by fp32 atomics */
+  float* ws;                 /* split-K slab workspace, AVSR_GEMM_SLAB_WS(batch, splitk, M, N) fp32:
+                                each split stores its partial tile, a reduce pass writes
+                                C = alpha*sum + beta*C (plain epilogue only). NULL: C += alpha*acc
+                                by fp32 atomics */
 } avsr_gemm_params;
+/* slabs are AVSR_GEMM_SLAB_PAD floats apart beyond M*N: power-of-two slab strides put the
+ * reduce pass's split-many reads of one vector on the same HBM channels (measured 0.55 TB/s for
+ * 8 slabs of 4 MiB) */
+#define AVSR_GEMM_SLAB_PAD 1088
+#define AVSR_GEMM_SLAB_WS(batch, splitk, M, N) ((int64_t)(batch) * (splitk) * ((int64_t)(M) * (N) + AVSR_GEMM_SLAB_PAD))
 
 int avsr_gemm(const avsr_gemm_params* p, void* stream);
 
@@ -153,7 +159,8 @@ typedef struct {
   float* dgamma; float* dbeta;              /* bwd: fp32 accumulators [N] or NULL */
   float* ws;                                /* bwd with dgamma: workspace >= AVSR_LN_WS(N) floats */
 } avsr_layernorm_params;
-#define AVSR_LN_WS(N) (256 * 2 * (N))
+#define AVSR_LN_BLOCKS 256
+#define AVSR_LN_WS(N) (AVSR_LN_BLOCKS * 2 * (N))
 int avsr_layernorm_fwd(const avsr_layernorm_params* p, void* stream);
 int avsr_layernorm_bwd(const avsr_layernorm_params* p, void* stream);
 
@@ -356,7 +363,8 @@ typedef struct {
   float* db;
   float* ws;                                       /* with db: workspace >= AVSR_EW_WS(N) floats */
 } avsr_ew_params;
-#define AVSR_EW_WS(N) (256 * (N))
+#define AVSR_EW_ROWBLOCKS 256
+#define AVSR_EW_WS(N) (AVSR_EW_ROWBLOCKS * (N))
 int avsr_ew_bwd(const avsr_ew_params* p, void* stream);
 int avsr_dropout_fwd(const avsr_ew_params* p, void* stream);
 int avsr_mask_rows(int dtype, int B, int T, int N, void* x, int64_t ldx, const int* len, void* stream);

@@ -120,7 +120,7 @@ def test_gemm_layouts_bf16(dev, gemm_tile, a_kmajor, b_kmajor, M, N, K, splitk):
     if splitk > 1:   # slab workspace mode: C = 0.5 * A.B + 1.0 * C_old, no atomics
         C0 = torch.randn(M, N, device=dev)
         C2 = C0.clone()
-        ws = torch.full((splitk * M * N,), float("nan"), device=dev)
+        ws = torch.full((ops.slab_ws(1, splitk, M, N),), float("nan"), device=dev)
         ops.gemm(A, B, C2, M=M, N=N, K=K, a_kmajor=a_kmajor, b_kmajor=b_kmajor,
                  lda=A.shape[1], ldb=B.shape[1], ldc=N, splitk=splitk, ws=ws, alpha=0.5, beta=1.0)
         err = (C2 - (0.5 * ref + C0)).abs().max().item() / ref.abs().max().item()

@@ -48,7 +48,7 @@ def wgrad(dy, x, dW):
     K = x.shape[1]
     tiles = ((N + 127) // 128) * ((K + 127) // 128)
     splitk = 1 if tiles > 256 else max(1, min(16, 512 // max(tiles, 1), Mt // 512))
-    ws = torch.empty(splitk * N * K, device=dy.device, dtype=torch.float32) if splitk > 1 else None
+    ws = torch.empty(ops.slab_ws(1, splitk, N, K), device=dy.device, dtype=torch.float32) if splitk > 1 else None
     ops.gemm(dy, x, dW, M=N, N=K, K=Mt, a_kmajor=False, b_kmajor=False, lda=dy.stride(0), ldb=x.stride(0),
              ldc=dW.stride(0), beta=1.0, splitk=splitk, ws=ws)
 

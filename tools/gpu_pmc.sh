@@ -1,8 +1,20 @@
+# SQ counter passes (MFMA busy, VALU / LDS / VMEM issue, waits, LDS conflicts) over the attention,
+# ResNet and GEMM microbenches. Usage: gpurun -- bash tools/gpu_pmc.sh TAG
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-for K in fwd dgrad wgrad; do timeout -k 10 100 python tools/conv_one.py $K 6000 22 64 64 3 1 >> gpurun_out/conv.log 2>&1 || exit 1; done
-for K in fwd dgrad wgrad; do timeout -k 10 100 python tools/conv_one.py $K 6000 11 128 128 3 1 >> gpurun_out/conv.log 2>&1 || exit 1; done
-timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/pmc_conv/a -o run --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_MISC SQ_INST_CYCLES_VMEM SQ_BUSY_CYCLES -- python tools/conv_one.py fwd 6000 22 64 64 3 1 5 > gpurun_out/pmc_conv.log 2>&1 || exit 1
-timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/pmc_conv/b -o run --pmc GRBM_GUI_ACTIVE SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_SALU SQ_INSTS_VMEM -- python tools/conv_one.py fwd 6000 22 64 64 3 1 5 >> gpurun_out/pmc_conv.log 2>&1 || exit 1
-echo rc=$?
+O=gpurun_out/${1:-pmc}; mkdir -p $O
+PA="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_WAIT_INST_LDS SQ_WAIT_ANY GRBM_GUI_ACTIVE"
+PB="SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_VMEM SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_SALU SQ_WAIT_INST_ANY"
+for prog in attn resnet gemm; do
+  case $prog in
+    attn) CMD="python3 tools/attn_bench.py";;
+    resnet) CMD="python3 tools/resnet_bench.py 1";;
+    gemm) CMD="python3 tools/gemm_sq.py 128";;
+  esac
+  for pass in A B; do
+    if [ $pass = A ]; then P="$PA"; else P="$PB"; fi
+    timeout -s KILL 240 rocprofv3 --pmc $P --output-format csv -d $O/$prog$pass -o run -- $CMD > $O/$prog$pass.log 2>&1 || { echo "$prog $pass failed"; tail -5 $O/$prog$pass.log; exit 1; }
+  done
+done
+echo rc=0
