@@ -826,47 +826,43 @@ __global__ __launch_bounds__(768) void attn_fwd_kernel(AttnArgs a) {
   f32x16 o0, o1;
   zacc(o0); zacc(o1);
   float m = -INFINITY, lsum = 0.f;
+  float mb = 0.f;                               // running row max, scaled by log2(e) * scale
   if (q0 < a.Lq) {
-    // pass 1: row max of the raw scores
+    // one pass, online softmax: per 32-key tile S^T = K Q^T, the row max over the tile (the
+    // two lane halves hold the same query, different keys), rescale of the running O^T / row
+    // sum when the max grows (per-lane scalar: the lane's accumulator column is its query),
+    // P = exp2(S*scale*log2e - max), dropout, O^T += V^T P^T
     for (int t = 0; t < nt; ++t) {
       f32x16 st;
       zacc(st);
 #pragma unroll
       for (int s = 0; s < 4; ++s) st = mfma32(rd8(Ks, t * 32 + c, s * 16 + 8 * hh), qf[s], st);
-      if (t * 32 + 32 <= klen && (!a.causal || t * 32 + 31 <= q0)) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) m = fmaxf(m, st[r]);
-      } else {
+      const bool full = t * 32 + 32 <= klen && (!a.causal || t * 32 + 31 <= q0);
+      if (!full) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int k = t * 32 + qrow(r, hh);
           const bool ok = (k < klen) & (!a.causal | (k <= qi));
-          m = fmaxf(m, ok ? st[r] : -INFINITY);
+          st[r] = ok ? st[r] : -INFINITY;
         }
       }
-    }
-    m = fmaxf(m, __shfl_xor(m, 32, 64));
-    const float mb = m == -INFINITY ? 0.f : m * sl2;
-    // pass 2: probabilities, row sum, dropout, O^T += V^T P^T
-    for (int t = 0; t < nt; ++t) {
-      f32x16 st;
-      zacc(st);
+      float mt = st[0];
 #pragma unroll
-      for (int s = 0; s < 4; ++s) st = mfma32(rd8(Ks, t * 32 + c, s * 16 + 8 * hh), qf[s], st);
-      if (t * 32 + 32 <= klen && (!a.causal || t * 32 + 31 <= q0)) {
+      for (int r = 1; r < 16; ++r) mt = fmaxf(mt, st[r]);
+      mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+      // branch-free (MFMAs below run for the whole wave): a query with no visible key so far
+      // keeps max -inf, mb 0, and contributes exp2(-inf) = 0
+      const float mn = fmaxf(m, mt);
+      const float mbn = mn == -INFINITY ? 0.f : mn * sl2;
+      const float alpha = m == -INFINITY ? 0.f : fexp2(mb - mbn);
+      m = mn; mb = mbn;
+      lsum *= alpha;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          st[r] = fexp2(fmaf(st[r], sl2, -mb));
-          lsum += st[r];
-        }
-      } else {
+      for (int r = 0; r < 16; ++r) { o0[r] *= alpha; o1[r] *= alpha; }
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int k = t * 32 + qrow(r, hh);
-          const bool ok = (k < klen) & (!a.causal | (k <= qi));
-          st[r] = ok ? fexp2(fmaf(st[r], sl2, -mb)) : 0.f;
-          lsum += st[r];
-        }
+      for (int r = 0; r < 16; ++r) {
+        st[r] = fexp2(fmaf(st[r], sl2, -mb));      // masked keys: exp2(-inf) = 0
+        lsum += st[r];
       }
       if (a.drop_p > 0.f) drop_tile(st, rowG + (uint32_t)(t * 16) * GOLD, drop, hh);
       const bf16x8 pa = accb(st, 0), pb = accb(st, 1);
