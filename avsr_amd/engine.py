@@ -36,6 +36,14 @@ GELU, RELU, NONE = L.ACT_GELU, L.ACT_RELU, L.ACT_NONE
 _BN_FUSE = os.environ.get("AVSR_BN_FUSE", "1") == "1"
 
 
+def wgrad_splitk(M, N, K):
+    """token-dimension split of a weight-gradient GEMM dW[N][K] += dy[M][N]^T x[M][K]: split
+    only when the 128x128 output grid is at or below one block per CU (slab workspace, no
+    atomics)."""
+    tiles = ((N + 127) // 128) * ((K + 127) // 128)
+    return 1 if tiles > 256 else max(1, min(16, 512 // max(tiles, 1), M // 512))
+
+
 def _pad8(n):
     return (n + 7) // 8 * 8
 
@@ -241,8 +249,7 @@ class Engine:
         (no atomics): measured (tools/lin_wgrad_sweep.py, M=6000) 4096x1024 100 -> 72 us with 2 splits."""
         M, N = dy.shape
         K = x.shape[1]
-        tiles = ((N + 127) // 128) * ((K + 127) // 128)
-        splitk = 1 if tiles > 256 else max(1, min(16, 512 // max(tiles, 1), M // 512))
+        splitk = wgrad_splitk(M, N, K)
 
         def run():
             ws = None

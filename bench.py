@@ -117,6 +117,34 @@ def frontend_timing(B, T, dev, reps=5):
             "what": f"{B} clips: log-fbank+stack4+LN of {640 * T} samples and crop/normalise of {T}x96x96 u8 frames"}
 
 
+def encoder_gemm_table(dev, M, D, F):
+    """the 12 GEMM shapes of one encoder layer (QKV, out-proj, FFN1, FFN2 x fwd / dgrad /
+    wgrad with the engine's split-K policy), each timed alone (HIP graph, plain epilogue,
+    N(0, 0.25) operands); outside the timed region. Returns per-shape TF/s and the worst."""
+    from avsr_amd import ops
+    from tools.gemm_table import timed, wgrad
+    g = torch.Generator(device="cpu").manual_seed(0)
+    rows = []
+    for name, (N, K) in {"qkv": (3 * D, D), "out": (D, D), "ffn1": (F, D), "ffn2": (D, F)}.items():
+        x = (torch.randn(M, K, generator=g) * 0.5).to(dev, torch.bfloat16)
+        W = (torch.randn(N, K, generator=g) * 0.05).to(dev, torch.bfloat16)
+        dy = (torch.randn(M, N, generator=g) * 0.5).to(dev, torch.bfloat16)
+        dW = torch.zeros(N, K, device=dev)
+        fl = 2.0 * M * N * K
+        for op, fn in (("fwd", lambda: ops.linear_fwd(x, W)), ("dgrad", lambda: ops.linear_dgrad(dy, W)),
+                       ("wgrad", lambda: wgrad(dy, x, dW))):
+            us = timed(fn)
+            tf = fl / us / 1e6
+            rows.append({"gemm": f"{name} {op}", "us": round(us, 1), "tflops": round(tf, 1),
+                         "frac": round(tf / BF16_PEAK_TFLOPS, 4)})
+    worst = min(rows, key=lambda r: r["frac"])
+    tot_us = sum(r["us"] for r in rows)
+    tot_fl = sum(2.0 * M * N * K for (N, K) in ((3 * D, D), (D, D), (F, D), (D, F))) * 3
+    return {"per_shape": rows, "worst": worst, "layer_us": round(tot_us, 1),
+            "layer_frac": round(tot_fl / tot_us / 1e6 / BF16_PEAK_TFLOPS, 4),
+            "note": "isolated launches, plain epilogue (tools/gemm_table.py); the in-step probe is `roofline`"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -262,6 +290,9 @@ def main():
                                    "(its gradient is exactly zero, avhubert.py:480)"},
     }
     result["frontend"] = frontend_timing(B, T, dev)
+    if args.layers is None:
+        result["encoder_gemms"] = encoder_gemm_table(dev, B * T, cfg.hidden_size, cfg.intermediate_size)
+        result["roofline"]["worst_encoder_gemm"] = result["encoder_gemms"]["worst"]
     if state_cpu is not None:
         threads = min(16, os.cpu_count() or 1)
         fps, dt = cpu_baseline(cfg, state_cpu, T, threads)

@@ -13,6 +13,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
 from avsr_amd import ops  # noqa: E402
+from avsr_amd.engine import wgrad_splitk  # noqa: E402
 
 PEAK = 2500.0
 dev = torch.device("cuda")
@@ -46,8 +47,7 @@ def wgrad(dy, x, dW):
     grid is at or below one block per CU)"""
     Mt, N = dy.shape
     K = x.shape[1]
-    tiles = ((N + 127) // 128) * ((K + 127) // 128)
-    splitk = 1 if tiles > 256 else max(1, min(16, 512 // max(tiles, 1), Mt // 512))
+    splitk = wgrad_splitk(Mt, N, K)
     ws = torch.empty(ops.slab_ws(1, splitk, N, K), device=dy.device, dtype=torch.float32) if splitk > 1 else None
     ops.gemm(dy, x, dW, M=N, N=K, K=Mt, a_kmajor=False, b_kmajor=False, lda=dy.stride(0), ldb=x.stride(0),
              ldc=dW.stride(0), beta=1.0, splitk=splitk, ws=ws)
