@@ -41,6 +41,9 @@ def wgrad_splitk(M, N, K):
     only when the 128x128 output grid is at or below one block per CU (slab workspace, no
     atomics)."""
     tiles = ((N + 127) // 128) * ((K + 127) // 128)
+    forced = os.environ.get("AVSR_WGRAD_SPLIT")          # experiments (tools/gemm_table.py)
+    if forced:
+        return max(1, min(int(forced), M // 256))
     return 1 if tiles > 256 else max(1, min(16, 512 // max(tiles, 1), M // 512))
 
 
