@@ -61,7 +61,7 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(LnArgs a) {
 // grid-stride over rows (one wave per row at a time, 8 waves per block); dgamma/dbeta
 // accumulated per lane in registers, summed over the block's waves in LDS and written as
 // one partial row per block (colsum_finalize adds the blocks)
-constexpr int LN_BWD_WAVES = 8;
+constexpr int LN_BWD_WAVES = 4;
 template <typename T, int VPL>
 __global__ __launch_bounds__(64 * LN_BWD_WAVES) void ln_bwd_kernel(LnArgs a) {
   constexpr int VE = VecW<T>::VE;
