@@ -185,31 +185,33 @@ static inline int avsr_grid(long work, int per_block = 256, int cap = 2048) {
 
 // Column sums of a row-block partial workspace: out[c] += sum_b ws[b*ld + c] for c < N, or,
 // when out1 != nullptr, columns [N1, N) go to out1[c - N1] (LayerNorm dgamma/dbeta in one
-// launch). Block = 32 columns (one 128-byte line per row) x 8 row lanes, 4 independent
-// accumulators per lane, LDS reduce: the partial rows are read in parallel, not as a serial
-// dependent chain.
-static __global__ __launch_bounds__(256) void colsum_finalize_kernel(const float* ws, int nb, int64_t ld, int N,
-                                                                     float* out, int N1, float* out1) {
-  __shared__ float red[8][33];
+// launch). Block = 32 columns (one 128-byte line per row) x 32 row lanes (1024 threads): each
+// thread adds nb/32 partial rows with four independent accumulators, then the row lanes are
+// summed in a fixed order (deterministic). (8 row lanes: ~6.7 us per 256 x 1024 workspace,
+// a latency-bound chain of 32 loads per thread.)
+constexpr int COLSUM_THREADS = 1024;
+static __global__ __launch_bounds__(COLSUM_THREADS) void colsum_finalize_kernel(const float* ws, int nb, int64_t ld, int N,
+                                                                                 float* out, int N1, float* out1) {
+  __shared__ float red[32][33];
   const int cl = threadIdx.x & 31, rl = threadIdx.x >> 5;
   const int c = blockIdx.x * 32 + cl;
   float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
   if (c < N) {
     int b = rl;
-    for (; b + 24 < nb; b += 32) {
+    for (; b + 96 < nb; b += 128) {
       s0 += ws[(int64_t)b * ld + c];
-      s1 += ws[(int64_t)(b + 8) * ld + c];
-      s2 += ws[(int64_t)(b + 16) * ld + c];
-      s3 += ws[(int64_t)(b + 24) * ld + c];
+      s1 += ws[(int64_t)(b + 32) * ld + c];
+      s2 += ws[(int64_t)(b + 64) * ld + c];
+      s3 += ws[(int64_t)(b + 96) * ld + c];
     }
-    for (; b < nb; b += 8) s0 += ws[(int64_t)b * ld + c];
+    for (; b < nb; b += 32) s0 += ws[(int64_t)b * ld + c];
   }
   red[rl][cl] = (s0 + s1) + (s2 + s3);
   __syncthreads();
   if (rl == 0 && c < N) {
     float s = 0.f;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) s += red[i][cl];
+    for (int i = 0; i < 32; ++i) s += red[i][cl];
     if (out1 && c >= N1) out1[c - N1] += s;
     else out[c] += s;
   }

@@ -343,7 +343,7 @@ int ew_launch(const avsr_ew_params* p, hipStream_t st) {
   if (p->dtype == AVSR_BF16) hipLaunchKernelGGL(ew_bwd_kernel<bf16>, grid, dim3(256), 0, st, a);
   else hipLaunchKernelGGL(ew_bwd_kernel<float>, grid, dim3(256), 0, st, a);
   if (p->db)
-    hipLaunchKernelGGL(colsum_finalize_kernel, colsum_grid(p->N), dim3(256), 0, st, (const float*)p->ws,
+    hipLaunchKernelGGL(colsum_finalize_kernel, colsum_grid(p->N), dim3(COLSUM_THREADS), 0, st, (const float*)p->ws,
                        (int)grid.y, (int64_t)p->N, p->N, p->db, 0, (float*)nullptr);
   AVSR_CHECK_LAUNCH();
   return 0;

@@ -164,7 +164,7 @@ int ln_launch(const avsr_layernorm_params* p, bool bwd, hipStream_t st) {
     if (bwd) {                                                                                   \
       hipLaunchKernelGGL((ln_bwd_kernel<T, V>), dim3(blocks), dim3(64 * LN_BWD_WAVES), 0, st, a); \
       if (p->dgamma) {                                                                           \
-        hipLaunchKernelGGL(colsum_finalize_kernel, colsum_grid(2 * p->N), dim3(256), 0, st,     \
+        hipLaunchKernelGGL(colsum_finalize_kernel, colsum_grid(2 * p->N), dim3(COLSUM_THREADS), 0, st,\
                            (const float*)p->ws, blocks, (int64_t)2 * p->N, 2 * p->N, p->dgamma, \
                            p->N, p->dbeta);                                                      \
       }                                                                                          \
@@ -187,13 +187,16 @@ int ln_check(const avsr_layernorm_params* p) {
 }
 
 // =============================================================== BatchNorm
-__global__ __launch_bounds__(256) void bn_finalize_kernel(avsr_bn_finalize_params a) {
+// one block of BNF_THREADS per channel: Chan-merge of the conv epilogue's (count, mean, M2)
+// tile partials (the stem has ~45 k tiles per channel: 1024 threads keep that under ~40 us)
+constexpr int BNF_THREADS = 1024;
+__global__ __launch_bounds__(BNF_THREADS) void bn_finalize_kernel(avsr_bn_finalize_params a) {
   const int c = blockIdx.x;
-  __shared__ double sn[256], sm[256], sq[256];
+  __shared__ double sn[BNF_THREADS], sm[BNF_THREADS], sq[BNF_THREADS];
   double n = 0, mean = 0, m2 = 0;
   if (a.training) {
     const float* pp = a.partials + (int64_t)c * a.tiles * 3;
-    for (int t = threadIdx.x; t < a.tiles; t += 256) {
+    for (int t = threadIdx.x; t < a.tiles; t += blockDim.x) {
       const double nb = pp[t * 3 + 0], mb = pp[t * 3 + 1], qb = pp[t * 3 + 2];
       if (nb > 0) {
         const double nn = n + nb, d = mb - mean;
@@ -204,7 +207,7 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(avsr_bn_finalize_param
     }
     sn[threadIdx.x] = n; sm[threadIdx.x] = mean; sq[threadIdx.x] = m2;
     __syncthreads();
-    for (int o = 128; o > 0; o >>= 1) {
+    for (int o = blockDim.x / 2; o > 0; o >>= 1) {     // blockDim.x: 256 or 1024
       if (threadIdx.x < o) {
         const double na = sn[threadIdx.x], nb = sn[threadIdx.x + o];
         if (nb > 0) {
@@ -659,7 +662,8 @@ extern "C" int avsr_bn_finalize(const avsr_bn_finalize_params* p, void* stream) 
   if (!p || p->C <= 0) return AVSR_E_ARG;
   if (p->training && !p->partials) return AVSR_E_ARG;
   if (!p->training && (!p->running_mean || !p->running_var)) return AVSR_E_ARG;
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3(p->C), dim3(256), 0, (hipStream_t)stream, *p);
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3(p->C), dim3(p->training && p->tiles > 2048 ? BNF_THREADS : 256), 0,
+                     (hipStream_t)stream, *p);
   AVSR_CHECK_LAUNCH();
   return 0;
 }
