@@ -234,6 +234,7 @@ SYMBOLS = {
     "avsr_avgpool_fwd": ([_i, _i, _i, _i, _c_p, _c_p, _c_p], _i),
     "avsr_avgpool_bwd": ([_i, _i, _i, _i, _c_p, _c_p, _c_p], _i),
     "avsr_attn_fwd": ([ctypes.POINTER(AttnParams), _c_p], _i),
+    "avsr_debug_attn_stamps": ([_c_p], _i),
     "avsr_attn_bwd_prep": ([ctypes.POINTER(AttnParams), _c_p], _i),
     "avsr_attn_bwd": ([ctypes.POINTER(AttnParams), _c_p], _i),
     "avsr_row_lse": ([ctypes.POINTER(XentParams), _c_p], _i),

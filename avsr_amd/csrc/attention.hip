@@ -728,6 +728,22 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs a, OutT* dq, 
 // which split the 16 queries' hashes and swap halves (__shfl_xor 1).
 namespace res {
 using namespace v2;
+
+// diagnostic only (avsr_debug_attn_stamps): per workgroup [start, after loads, after compute,
+// end] s_memrealtime ticks (100 MHz) and the hardware id, written by lane 0 of wave 0 to a
+// buffer of its own; no output depends on it
+__device__ unsigned long long* g_stamps = nullptr;
+AVSR_DEV void stamp(int slot) {
+  unsigned long long* st = g_stamps;
+  if (st != nullptr && threadIdx.x == 0) {
+    const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+    st[(blockIdx.y * gridDim.x + blockIdx.x) * 6 + slot] = t;
+    if (slot == 0) {
+      st[(blockIdx.y * gridDim.x + blockIdx.x) * 6 + 4] = (unsigned long long)__builtin_amdgcn_s_getreg((4) | (0 << 6) | (31 << 11));
+      st[(blockIdx.y * gridDim.x + blockIdx.x) * 6 + 5] = (unsigned long long)__builtin_amdgcn_s_getreg((20) | (0 << 6) | (31 << 11));
+    }
+  }
+}
 constexpr int MAXR = 384;           // resident rows per (b, h)
 constexpr int MAXW = MAXR / 32;     // waves per workgroup (768 threads)
 constexpr uint32_t GOLD = 0x9E3779B1u;
@@ -804,6 +820,7 @@ AVSR_DEV void drop_tile(f32x16& x, uint32_t tG, const AttnDrop& d, int hh) {
 
 __global__ __launch_bounds__(768) void attn_fwd_kernel(AttnArgs a) {
   extern __shared__ __attribute__((aligned(16))) bf16 sm[];
+  stamp(0);
   const int bh = blockIdx.x, b = bh / a.H, h = bh % a.H;
   const int tid = threadIdx.x, nthr = blockDim.x, w = tid >> 6, l = tid & 63, c = l & 31, hh = l >> 5;
   const int nk = (a.Lk + 31) & ~31;
@@ -814,25 +831,63 @@ __global__ __launch_bounds__(768) void attn_fwd_kernel(AttnArgs a) {
   bf16x8 qf[4];
 #pragma unroll
   for (int s = 0; s < 4; ++s) qf[s] = ldrow_sel(Q, a.ldq, qi, a.Lq, s * 16 + 8 * hh);
-  load_pair(Ks, (const bf16*)a.k + (int64_t)b * a.Lk * a.ldk + h * DH, a.ldk,
-            Vs, (const bf16*)a.v + (int64_t)b * a.Lk * a.ldv + h * DH, a.ldv, a.Lk, nk, tid, nthr);
+  // K/V images: when one pass of LD_IT vectors per thread covers them, all loads are issued
+  // here and the images are written round by round inside the tile loop (round r = rows
+  // [r*nthr/8, (r+1)*nthr/8)), so later rounds' HBM latency hides behind the first tiles'
+  // compute (one workgroup per head per CU leaves nothing else to hide it); the barriers are
+  // raw s_barrier after lgkmcnt(0), which do not drain the outstanding loads
+  const bf16* Kg = (const bf16*)a.k + (int64_t)b * a.Lk * a.ldk + h * DH;
+  const bf16* Vg = (const bf16*)a.v + (int64_t)b * a.Lk * a.ldv + h * DH;
+  const bool pipe = nk * 8 <= LD_IT * nthr;
+  const int rtot = pipe ? (nk * 8 + nthr - 1) / nthr : 0;     // rounds to write (uniform)
+  const int rpr = nthr >> 3;                                    // image rows per round
+  v16 xk[LD_IT], xv[LD_IT];
+  if (pipe) {
+#pragma unroll
+    for (int it = 0; it < LD_IT; ++it) {
+      const int id = it * nthr + tid, rr = min(id >> 3, a.Lk - 1), ch = (id & 7) * 8;
+      xk[it] = *(const v16*)(Kg + (int64_t)rr * a.ldk + ch);
+      xv[it] = *(const v16*)(Vg + (int64_t)rr * a.ldv + ch);
+    }
+  } else {
+    load_pair(Ks, Kg, a.ldk, Vs, Vg, a.ldv, a.Lk, nk, tid, nthr);
+  }
   const int klen = a.klen ? min(a.klen[b], a.Lk) : a.Lk;
   const int kend = a.causal ? min(klen, q0 + 32) : klen;
   const int nt = (kend + 31) >> 5;
   const float sl2 = a.scale * LOG2E;
   const AttnDrop drop(a.drop_p, a.seed, a.B, a.H, a.Lq, a.Lk);
   const uint32_t rowG = ((uint32_t)bh * (uint32_t)a.Lq + (uint32_t)min(qi, a.Lq - 1)) * drop.npair * GOLD;
-  __syncthreads();
+  if (!pipe) __syncthreads();
   f32x16 o0, o1;
   zacc(o0); zacc(o1);
   float m = -INFINITY, lsum = 0.f;
   float mb = 0.f;                               // running row max, scaled by log2(e) * scale
-  if (q0 < a.Lq) {
+  int t = 0;                                    // next key tile
+#pragma unroll
+  for (int it = 0; it < LD_IT; ++it) {
+    if (pipe && it < rtot) {
+      const int id = it * nthr + tid, row = id >> 3, ch = (id & 7) * 8;
+      if (id < nk * 8) {
+        const bool ok = row < a.Lk;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { xk[it].w[j] = ok ? xk[it].w[j] : 0u; xv[it].w[j] = ok ? xv[it].w[j] : 0u; }
+        *(v16*)&Ks[row * ROW + ch] = xk[it];
+        *(v16*)&Vs[row * ROW + ch] = xv[it];
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (it == 0) stamp(1);
+    }
+    // tiles whose 32 keys are all in LDS after this round
+    const int tend = (!pipe || it + 1 >= rtot) ? nt : min(nt, ((it + 1) * rpr) >> 5);
+    if (q0 >= a.Lq) continue;
     // one pass, online softmax: per 32-key tile S^T = K Q^T, the row max over the tile (the
     // two lane halves hold the same query, different keys), rescale of the running O^T / row
     // sum when the max grows (per-lane scalar: the lane's accumulator column is its query),
     // P = exp2(S*scale*log2e - max), dropout, O^T += V^T P^T
-    for (int t = 0; t < nt; ++t) {
+    for (; t < tend; ++t) {
       f32x16 st;
       zacc(st);
 #pragma unroll
@@ -871,16 +926,21 @@ __global__ __launch_bounds__(768) void attn_fwd_kernel(AttnArgs a) {
       o1 = mfma32(rdT(Vs, t * 32, 32, l), pa, o1);
       o1 = mfma32(rdT(Vs, t * 32 + 16, 32, l), pb, o1);
     }
+  }
+  if (q0 < a.Lq) {
     lsum += __shfl_xor(lsum, 32, 64);
     if (hh == 0 && qi < a.Lq)
       a.lse[(int64_t)bh * a.Lq + qi] = lsum > 0.f ? (mb + log2f(lsum)) * LN2 : -INFINITY;
   }
   __syncthreads();                         // K/V images no longer read: reuse LDS as store slabs
+  stamp(2);
   if (q0 < a.Lq) {
     const float inv = lsum > 0.f ? 1.f / lsum : 0.f;
     bf16* O = (bf16*)a.o + ((int64_t)b * a.Lq + q0) * a.ldo + h * DH;
     store_t<bf16>(o0, o1, inv, (float*)sm + w * 32 * 65, O, a.ldo, a.Lq - q0);
   }
+  __syncthreads();
+  stamp(3);
 }
 
 template <int NT>
@@ -1126,6 +1186,12 @@ int check(const avsr_attn_params* p) {
 }
 
 }  // namespace
+
+// diagnostic: device buffer of 6 x uint64 per workgroup for the resident forward kernel
+// (nullptr: off). Not part of the product path.
+extern "C" int avsr_debug_attn_stamps(unsigned long long* buf) {
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(res::g_stamps), &buf, sizeof(buf));
+}
 
 extern "C" int avsr_attn_fwd(const avsr_attn_params* p, void* stream) {
   int rc = check(p);

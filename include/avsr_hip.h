@@ -280,6 +280,10 @@ typedef struct {
    * otherwise bf16 writes dq (fp32) with plain stores (= accumulate onto a zeroed buffer) */
   void* dq_out; int64_t lddq_out;
 } avsr_attn_params;
+/* diagnostic (not product path): per-workgroup s_memrealtime stamps of the resident attention
+ * forward into buf[6 * workgroups] (start, first K/V round, compute done, end, HW_ID, XCC_ID);
+ * buf = NULL turns them off */
+int avsr_debug_attn_stamps(unsigned long long* buf);
 int avsr_attn_fwd(const avsr_attn_params* p, void* stream);
 int avsr_attn_bwd_prep(const avsr_attn_params* p, void* stream);   /* delta = rowsum(dO * O) */
 int avsr_attn_bwd(const avsr_attn_params* p, void* stream);
