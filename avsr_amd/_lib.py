@@ -297,14 +297,15 @@ def check(rc, op):
 
 
 _raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+_get_device = getattr(torch._C, "_cuda_getDevice", None) or torch.cuda.current_device
 
 
 def stream_ptr(device=None):
     """the current HIP stream of `device` (default: the current device) as a void pointer;
     the raw-stream query skips building a torch Stream object on every launch"""
     if _raw_stream is not None:
-        idx = torch.cuda.current_device() if device is None else torch.device(device).index
+        idx = _get_device() if device is None else torch.device(device).index
         if idx is None:
-            idx = torch.cuda.current_device()
+            idx = _get_device()
         return ctypes.c_void_p(_raw_stream(idx))
     return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)

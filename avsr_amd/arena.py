@@ -137,20 +137,32 @@ class Arena:
     def _cbuf(self):
         return self.shadow if self.shadow is not None else self.data
 
+    def _view(self, kind, buf, name, make):
+        """per-(buffer, parameter) view cache: the arena buffers are allocated once, so a view
+        stays valid; building it anew on every launch costs the step a few ms of host time"""
+        key = (kind, id(buf), name)
+        v = self._vc.get(key) if hasattr(self, "_vc") else None
+        if v is None:
+            if not hasattr(self, "_vc"):
+                self._vc = {}
+            v = self._vc[key] = make()
+        return v
+
     def w(self, name):
         """compute-dtype weight in PHYSICAL layout (e.g. conv: [cout][kh][kw][cin])."""
-        return self._phys(self._cbuf(), self.meta[name])
+        buf = self._cbuf()
+        return self._view("w", buf, name, lambda: self._phys(buf, self.meta[name]))
 
     def w_padded(self, name):
         m = self.meta[name]
         return self._cbuf()[m["off"]:m["off"] + m["numel"]].view(m["phys_alloc"])
 
     def master(self, name):
-        return self._phys(self.data, self.meta[name])
+        return self._view("m", self.data, name, lambda: self._phys(self.data, self.meta[name]))
 
     def g(self, name):
         """fp32 gradient accumulator in PHYSICAL layout."""
-        return self._phys(self.grad, self.meta[name])
+        return self._view("g", self.grad, name, lambda: self._phys(self.grad, self.meta[name]))
 
     def g_padded(self, name):
         m = self.meta[name]
