@@ -2,6 +2,9 @@
 // forward and backward, for the AVSR hot path (declarations and reference call sites in
 // include/avsr_hip.h). All are HBM-bound: 16-byte vector loads/stores, fp32 statistics,
 // one pass per tensor where the math allows.
+#include <algorithm>
+#include <cstdlib>
+
 #include "common.h"
 
 namespace {
@@ -58,15 +61,15 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(LnArgs a) {
   if (lane == 0) { a.mean[row] = mean; a.rstd[row] = rstd; }
 }
 
-// grid-stride over rows (one wave per row at a time, 8 waves per block); dgamma/dbeta
-// accumulated per lane in registers, summed over the block's waves in LDS and written as
-// one partial row per block (colsum_finalize adds the blocks)
-constexpr int LN_BWD_WAVES = 4;
-template <typename T, int VPL>
-__global__ __launch_bounds__(64 * LN_BWD_WAVES) void ln_bwd_kernel(LnArgs a) {
+// grid-stride over rows, W waves per block, each wave R rows at a time with all their loads
+// (x, dy, dres) issued together; dgamma/dbeta accumulated per lane in registers, summed over
+// the block's waves in LDS (dynamic, W*N floats) and written as one partial row per block
+// (colsum_finalize adds the blocks)
+template <typename T, int VPL, int W, int R>
+__global__ __launch_bounds__(64 * W) void ln_bwd_kernel(LnArgs a) {
   constexpr int VE = VecW<T>::VE;
   const int lane = threadIdx.x & 63;
-  const int nw = gridDim.x * LN_BWD_WAVES;
+  const int nw = gridDim.x * W;
   float dg[VPL][VE], db[VPL][VE], gm[VPL][VE];
 #pragma unroll
   for (int i = 0; i < VPL; ++i) {
@@ -74,55 +77,67 @@ __global__ __launch_bounds__(64 * LN_BWD_WAVES) void ln_bwd_kernel(LnArgs a) {
 #pragma unroll
     for (int j = 0; j < VE; ++j) { dg[i][j] = 0.f; db[i][j] = 0.f; gm[i][j] = c < a.N ? a.gamma[c + j] : 0.f; }
   }
-  for (int row = blockIdx.x * LN_BWD_WAVES + (threadIdx.x >> 6); row < a.rows; row += nw) {
-    const T* x = (const T*)a.x + (int64_t)row * a.ldx;
-    const T* dy = (const T*)a.dy + (int64_t)row * a.lddy;
-    const float mean = a.mean[row], rstd = a.rstd[row];
-    float xh[VPL][VE], g[VPL][VE];
-    float s1 = 0.f, s2 = 0.f;
+  for (int row0 = blockIdx.x * W + (threadIdx.x >> 6); row0 < a.rows; row0 += R * nw) {
+    float xv[R][VPL][VE], dv[R][VPL][VE], rv[R][VPL][VE];
+    float mean[R], rstd[R];
+    bool live[R];
 #pragma unroll
-    for (int i = 0; i < VPL; ++i) {
-      const int c = (lane + i * 64) * VE;
-      if (c < a.N) {
-        float xv[VE], dv[VE];
-        ldv(x + c, xv);
-        ldv(dy + c, dv);
+    for (int u = 0; u < R; ++u) {
+      const int row = min(row0 + u * nw, a.rows - 1);
+      live[u] = row0 + u * nw < a.rows;
+      const T* x = (const T*)a.x + (int64_t)row * a.ldx;
+      const T* dy = (const T*)a.dy + (int64_t)row * a.lddy;
+      const T* dr = a.dres ? (const T*)a.dres + (int64_t)row * a.lddres : nullptr;
+      mean[u] = a.mean[row]; rstd[u] = a.rstd[row];
 #pragma unroll
-        for (int j = 0; j < VE; ++j) {
-          xh[i][j] = (xv[j] - mean) * rstd;
-          g[i][j] = dv[j] * gm[i][j];
-          s1 += g[i][j];
-          s2 += g[i][j] * xh[i][j];
-          dg[i][j] += dv[j] * xh[i][j];
-          db[i][j] += dv[j];
-        }
-      } else {
-#pragma unroll
-        for (int j = 0; j < VE; ++j) { xh[i][j] = 0.f; g[i][j] = 0.f; }
-      }
-    }
-    s1 = wave_sum(s1) / a.N;
-    s2 = wave_sum(s2) / a.N;
-    T* dx = (T*)a.dx + (int64_t)row * a.lddx;
-    const T* dr = a.dres ? (const T*)a.dres + (int64_t)row * a.lddres : nullptr;
-#pragma unroll
-    for (int i = 0; i < VPL; ++i) {
-      const int c = (lane + i * 64) * VE;
-      if (c < a.N) {
-        float o[VE], r[VE];
-        if (dr) ldv(dr + c, r);
+      for (int i = 0; i < VPL; ++i) {
+        const int c = min((lane + i * 64) * VE, a.N - VE);
+        ldv(x + c, xv[u][i]);
+        ldv(dy + c, dv[u][i]);
+        if (dr) ldv(dr + c, rv[u][i]);
         else
 #pragma unroll
-          for (int j = 0; j < VE; ++j) r[j] = 0.f;
+          for (int j = 0; j < VE; ++j) rv[u][i][j] = 0.f;
+      }
+    }
 #pragma unroll
-        for (int j = 0; j < VE; ++j) o[j] = r[j] + rstd * (g[i][j] - s1 - xh[i][j] * s2);
-        stv(dx + c, o);
+    for (int u = 0; u < R; ++u) {
+      float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int i = 0; i < VPL; ++i) {
+        const bool cok = (lane + i * 64) * VE < a.N && live[u];
+#pragma unroll
+        for (int j = 0; j < VE; ++j) {
+          const float xh = (xv[u][i][j] - mean[u]) * rstd[u];
+          const float g = cok ? dv[u][i][j] * gm[i][j] : 0.f;
+          s1 += g;
+          s2 += g * xh;
+          dg[i][j] += cok ? dv[u][i][j] * xh : 0.f;
+          db[i][j] += cok ? dv[u][i][j] : 0.f;
+          xv[u][i][j] = xh;             // keep xhat and g for the output pass
+          dv[u][i][j] = g;
+        }
+      }
+      s1 = wave_sum(s1) / a.N;
+      s2 = wave_sum(s2) / a.N;
+      if (live[u]) {
+        T* dx = (T*)a.dx + (int64_t)(row0 + u * nw) * a.lddx;
+#pragma unroll
+        for (int i = 0; i < VPL; ++i) {
+          const int c = (lane + i * 64) * VE;
+          if (c < a.N) {
+            float o[VE];
+#pragma unroll
+            for (int j = 0; j < VE; ++j) o[j] = rv[u][i][j] + rstd[u] * (dv[u][i][j] - s1 - xv[u][i][j] * s2);
+            stv(dx + c, o);
+          }
+        }
       }
     }
   }
   if (!a.dgamma) return;
   // per-block column partials (the block's waves summed in LDS) -> ws[block][2][N]
-  __shared__ float red[LN_BWD_WAVES * 2048];
+  extern __shared__ float red[];                 // [W][N]
   const int w = threadIdx.x >> 6;
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
@@ -135,13 +150,24 @@ __global__ __launch_bounds__(64 * LN_BWD_WAVES) void ln_bwd_kernel(LnArgs a) {
         for (int j = 0; j < VE; ++j) red[w * a.N + c + j] = q == 0 ? dg[i][j] : db[i][j];
     }
     __syncthreads();
-    for (int c = threadIdx.x; c < a.N; c += 64 * LN_BWD_WAVES) {
+    for (int c = threadIdx.x; c < a.N; c += 64 * W) {
       float t = 0.f;
 #pragma unroll
-      for (int v = 0; v < LN_BWD_WAVES; ++v) t += red[v * a.N + c];
+      for (int v = 0; v < W; ++v) t += red[v * a.N + c];
       a.ws[((int64_t)blockIdx.x * 2 + q) * a.N + c] = t;
     }
   }
+}
+
+// LayerNorm backward launch shape: AVSR_LN_BWD = "W,R" (waves per block, rows in flight per
+// wave) for experiments. Default 4,1: in isolation (tools/ln_bench.py) 6000 x 1024 takes
+// 18.6-20.4 us under every shape, and 8-16 waves lose 2x at N = 2048
+static void ln_bwd_shape(int& W, int& R) {
+  W = 4; R = 1;
+  const char* e = getenv("AVSR_LN_BWD");
+  if (e && e[0] && e[1] == ',') { W = e[0] == '1' ? 16 : e[0] - '0'; R = atoi(e + 2); }
+  if (W != 4 && W != 8 && W != 16) W = 8;
+  if (R != 1 && R != 2) R = 2;
 }
 
 template <typename T>
@@ -154,15 +180,23 @@ int ln_launch(const avsr_layernorm_params* p, bool bwd, hipStream_t st) {
   a.dres = p->dres; a.lddres = p->lddres; a.dgamma = p->dgamma; a.dbeta = p->dbeta; a.ws = p->ws;
   const int vpl = (p->N / VE + 63) / 64;
   int blocks = (p->rows + 3) / 4;
+  int W = 4, R = 1;
   if (bwd) {
-    blocks = (p->rows + LN_BWD_WAVES - 1) / LN_BWD_WAVES;
+    ln_bwd_shape(W, R);
+    blocks = (p->rows + W - 1) / W;
     blocks = blocks < AVSR_LN_BLOCKS ? blocks : AVSR_LN_BLOCKS;
   }
   if (bwd && p->dgamma && (!p->ws || p->N > 2048)) return AVSR_E_ARG;
+  while (W > 4 && (size_t)W * p->N * sizeof(float) > 64 * 1024) W >>= 1;   // default dynamic-LDS limit
+  if (bwd) blocks = std::min((p->rows + W - 1) / W, AVSR_LN_BLOCKS);
+  const size_t red = (size_t)W * p->N * sizeof(float);
+#define LNB(V, W_, R_) hipLaunchKernelGGL((ln_bwd_kernel<T, V, W_, R_>), dim3(blocks), dim3(64 * W_), red, st, a)
 #define LNL(V)                                                                                   \
   if (vpl <= V) {                                                                                \
     if (bwd) {                                                                                   \
-      hipLaunchKernelGGL((ln_bwd_kernel<T, V>), dim3(blocks), dim3(64 * LN_BWD_WAVES), 0, st, a); \
+      if (W == 16) { if (R == 2) LNB(V, 16, 2); else LNB(V, 16, 1); }                            \
+      else if (W == 8) { if (R == 2) LNB(V, 8, 2); else LNB(V, 8, 1); }                          \
+      else { if (R == 2) LNB(V, 4, 2); else LNB(V, 4, 1); }                                      \
       if (p->dgamma) {                                                                           \
         hipLaunchKernelGGL(colsum_finalize_kernel, colsum_grid(2 * p->N), dim3(COLSUM_THREADS), 0, st,\
                            (const float*)p->ws, blocks, (int64_t)2 * p->N, 2 * p->N, p->dgamma, \
@@ -176,6 +210,7 @@ int ln_launch(const avsr_layernorm_params* p, bool bwd, hipStream_t st) {
   }
   LNL(1) LNL(2) LNL(4) LNL(8)
 #undef LNL
+#undef LNB
   return AVSR_E_SHAPE;
 }
 
