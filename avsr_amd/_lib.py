@@ -206,6 +206,16 @@ class FbankParams(ctypes.Structure):
     ]
 
 
+class TimeMaskParams(ctypes.Structure):
+    _fields_ = [("B", _i), ("L", _i), ("nspan", _i), ("row_bytes", _i64), ("clip_stride_bytes", _i64),
+                ("x", _c_p), ("spans", _c_p)]
+
+
+class AddNoiseParams(ctypes.Structure):
+    _fields_ = [("B", _i), ("L", _i), ("x", _c_p), ("ldx", _i64), ("noise", _c_p), ("ldn", _i64),
+                ("lengths", _c_p), ("snr_db", _c_p), ("y", _c_p), ("ldy", _i64), ("ws", _c_p)]
+
+
 class VideoNormParams(ctypes.Structure):
     _fields_ = [
         ("B", _i), ("T", _i), ("H", _i), ("W", _i), ("crop", _i), ("oy", _i), ("ox", _i),
@@ -266,6 +276,9 @@ SYMBOLS = {
     "avsr_gather_rows": ([_i, _i, _i64, _c_p, _i64, _i64, _c_p, _i64, _i64, _c_p, _c_p], _i),
     "avsr_fbank_stack": ([ctypes.POINTER(FbankParams), _c_p], _i),
     "avsr_video_normalize": ([ctypes.POINTER(VideoNormParams), _c_p], _i),
+    "avsr_time_mask": ([ctypes.POINTER(TimeMaskParams), _c_p], _i),
+    "avsr_add_noise": ([ctypes.POINTER(AddNoiseParams), _c_p], _i),
+    "avsr_rgb_to_gray": ([_c_p, _c_p, _i64, _c_p], _i),
 }
 
 _lib = None

@@ -1,6 +1,9 @@
-"""Input front end on the GPU (SURVEY.md §8 f2): the collator's per-clip audio / video transforms
+"""Input front end on the GPU (SURVEY.md §8 f2, f3): the collator's per-clip audio / video transforms
 as HIP kernels (avsr_fbank_stack, avsr_video_normalize in libavsr_hip.so), producing the
-`audios` (B, 104, T) and `videos` (B, 1, T, 88, 88) tensors `AVHubertAVSR.forward` takes.
+`audios` (B, 104, T) and `videos` (B, 1, T, 88, 88) tensors `AVHubertAVSR.forward` takes, and
+the train-time augmentations (AdaptiveTimeMask, AddNoise, AddMultiSpk, RGB -> gray: avsr_time_mask,
+avsr_add_noise, avsr_rgb_to_gray). Media decoding (torchcodec) stays outside: these take decoded
+device tensors.
 
 Mirrors src/dataset/avhubert_dataset.py: `cut_or_pad` (:22-33), `FBanksAndStack` (:86-116),
 `VideoTransform` (:225-246, eval branch; train RandomCrop = explicit crop offsets), and the
@@ -9,6 +12,7 @@ CPU path (the library raises AvsrLibError when it is missing).
 """
 import ctypes
 import math
+import random
 
 import torch
 
@@ -111,3 +115,145 @@ def collate(wavs, frames):
     audios = audio_features(wav, ns, T=tmax)
     lengths = torch.tensor(lens, dtype=torch.int64)
     return {"videos": videos, "audios": audios, "video_lengths": lengths, "audio_lengths": lengths.clone()}
+
+
+# ---------------------------------------------------------------------------------------
+# train-time augmentation (src/dataset/avhubert_dataset.py:131-222)
+# ---------------------------------------------------------------------------------------
+
+def time_mask(x, spans):
+    """Zero time steps [start, end) of each clip in place: x (B, L, ...) contiguous device tensor
+    of any dtype, spans = one list of (start, end) pairs per clip (host ints; ends past L clip)."""
+    assert x.is_cuda and x.is_contiguous() and x.dim() >= 2
+    B, Lx = x.shape[0], x.shape[1]
+    ns = max((len(s) for s in spans), default=0)
+    if ns == 0 or B == 0:
+        return x
+    tab = torch.zeros(B, ns, 2, dtype=torch.int32)
+    for b, sp in enumerate(spans):
+        for i, (a, e) in enumerate(sp):
+            tab[b, i, 0], tab[b, i, 1] = int(a), int(e)
+    tab = tab.to(x.device)
+    row = x[0, 0].numel() * x.element_size()
+    p = L.fill(L.TimeMaskParams, B=B, L=Lx, nspan=ns, row_bytes=row, clip_stride_bytes=x.stride(0) * x.element_size(),
+               x=x, spans=tab)
+    L.check(L.load().avsr_time_mask(ctypes.byref(p), L.stream_ptr()), "avsr_time_mask")
+    return x
+
+
+def adaptive_time_mask_spans(length, window, stride):
+    """AdaptiveTimeMask.forward's draws (avhubert_dataset.py:140-150), same RNG calls in the same
+    order (torch.randint for the pairs, Python's random.randrange for the starts): the spans
+    [t_start, t_start + t_end) it zeroes."""
+    n_mask = int((length + stride - 0.1) // stride)
+    ts = torch.randint(0, window, size=(n_mask, 2))
+    spans = []
+    for t, t_end in ts.tolist():
+        if length - t <= 0:
+            continue
+        t_start = random.randrange(0, length - t)
+        if t_start == t_start + t:
+            continue
+        spans.append((t_start, t_start + t_end))
+    return spans
+
+
+class AdaptiveTimeMask(torch.nn.Module):
+    """avhubert_dataset.py:131-151 on a device tensor x (T, ...): returns a masked copy."""
+
+    def __init__(self, window, stride):
+        super().__init__()
+        self.window, self.stride = window, stride
+
+    def forward(self, x):
+        out = x.clone().contiguous()
+        spans = adaptive_time_mask_spans(out.size(0), self.window, self.stride)
+        time_mask(out.unsqueeze(0), [spans])
+        return out
+
+
+def add_noise(waveform, noise, snr, lengths=None, out=None):
+    """torchaudio.functional.add_noise as the reference calls it (avhubert_dataset.py:178, 214,
+    220): waveform, noise (B, L) or (L,) float32 device tensors, snr (B,) or scalar dB:
+    y = x + 10^((snr0 - snr) / 20) * noise, snr0 = 10 log10(|x|^2 / |n|^2) over each clip (its first
+    lengths[b] samples when given)."""
+    one = waveform.dim() == 1
+    x = waveform.reshape(1, -1) if one else waveform
+    n = noise.reshape(1, -1) if one else noise
+    assert x.is_cuda and x.dtype == n.dtype == torch.float32 and x.shape == n.shape
+    assert x.stride(1) == 1 and n.stride(1) == 1
+    B, Lx = x.shape
+    snr_t = torch.as_tensor(snr, dtype=torch.float32).reshape(-1).expand(B).contiguous().to(x.device)
+    y = torch.empty_like(x) if out is None else out.reshape(B, Lx)
+    ws = torch.empty(2 * 64 * B, dtype=torch.float64, device=x.device)
+    lens = None if lengths is None else torch.as_tensor(lengths, dtype=torch.int32).to(x.device)
+    p = L.fill(L.AddNoiseParams, B=B, L=Lx, x=x, ldx=x.stride(0), noise=n, ldn=n.stride(0), lengths=lens,
+               snr_db=snr_t, y=y, ldy=y.stride(0), ws=ws)
+    L.check(L.load().avsr_add_noise(ctypes.byref(p), L.stream_ptr()), "avsr_add_noise")
+    return y.reshape(-1) if one else y
+
+
+class AddNoise(torch.nn.Module):
+    """avhubert_dataset.py:154-179: `noise` is the decoded noise waveform on the device ((1, N) or
+    (N,), 16 kHz; the reference loads it from `noise_filename` with torchaudio)."""
+
+    def __init__(self, noise=None, snr_target=None):
+        super().__init__()
+        self.snr_levels = [snr_target] if snr_target else [-5, 0, 5, 10, 15, 20, 999999]
+        self.noise = None if noise is None else noise.reshape(1, -1)
+
+    def forward(self, speech):
+        # speech: T x 1 -> T x 1
+        if self.noise is None:
+            return speech
+        s = speech.t()
+        start_idx = random.randint(0, self.noise.shape[1] - s.shape[1])
+        seg = self.noise[:, start_idx:start_idx + s.shape[1]].contiguous()
+        snr = random.choice(self.snr_levels)
+        return add_noise(s.contiguous(), seg, snr).t()
+
+
+class AddMultiSpk(torch.nn.Module):
+    """avhubert_dataset.py:181-222: mixes 0-2 interfering speakers. `load_audio(entry)` returns
+    an entry's decoded waveform (T, 1) on the device (the reference decodes `entry['video']`)."""
+
+    def __init__(self, speech_dataset=None, snr_target=None, interferer_spk=None, load_audio=None):
+        super().__init__()
+        self.snr_levels = [snr_target] if snr_target else [-5, 0, 5, 10, 15, 20]
+        self.interferer_spk = [interferer_spk] if interferer_spk else [0, 0, 1, 2]
+        self.speech_dataset = speech_dataset
+        self.load_audio = load_audio
+
+    def forward(self, speech):
+        if self.speech_dataset is None:
+            return speech
+        speech_length = speech.size(0) / 16000
+        if speech_length < 2:
+            return speech
+        num_interferer = random.choice(self.interferer_spk)
+        interferer_signal = None
+        for _ in range(num_interferer):
+            interferer = self.load_audio(random.choice(self.speech_dataset))
+            interferer_length = interferer.size(0) / 16000
+            if 2 <= interferer_length <= 10:
+                interferer = cut_or_pad(interferer, len(speech))
+                if interferer_signal is None:
+                    interferer_signal = interferer
+                else:
+                    snr_level = random.choice([-5, 0, 5, 10, 15])
+                    interferer_signal = add_noise(interferer_signal.t().contiguous(), interferer.t().contiguous(),
+                                                  snr_level).t()
+        if interferer_signal is None:
+            return speech
+        snr_level = random.choice(self.snr_levels)
+        return add_noise(speech.t().contiguous(), interferer_signal.t().contiguous(), snr_level).t()
+
+
+def rgb_to_gray(frames):
+    """uint8 (..., 3) RGB device frames -> uint8 (...) = cv2.cvtColor(f, cv2.COLOR_RGB2GRAY)
+    (load_video, avhubert_dataset.py:45), fixed point (R*4899 + G*9617 + B*1868 + 8192) >> 14."""
+    assert frames.is_cuda and frames.dtype == torch.uint8 and frames.shape[-1] == 3 and frames.is_contiguous()
+    out = torch.empty(frames.shape[:-1], dtype=torch.uint8, device=frames.device)
+    L.check(L.load().avsr_rgb_to_gray(ctypes.c_void_p(frames.data_ptr()), ctypes.c_void_p(out.data_ptr()),
+                                      out.numel(), L.stream_ptr()), "avsr_rgb_to_gray")
+    return out

@@ -533,6 +533,41 @@ typedef struct {
 } avsr_video_norm_params;
 int avsr_video_normalize(const avsr_video_norm_params* p, void* stream);
 
+/* ------------------------------------------------------------------------------------
+ * Train-time augmentation on device (the collator's CPU transforms).
+ * avsr_time_mask: zero spans of rows of x [B][L][row_bytes] (any dtype: row_bytes bytes per
+ *   time step): rows [spans[b][s][0], spans[b][s][1]) of clip b for s < nspan (empty / negative
+ *   spans ignored). Replaces AdaptiveTimeMask.forward's `cloned[t_start:t_end] = 0`
+ *   (src/dataset/avhubert_dataset.py:131-151; the span draws stay on the host, :141-149).
+ * avsr_add_noise: y[b] = x[b] + s_b * n[b] over the first len_b samples of each clip, with
+ *   s_b = 10^((snr0_b - snr_b) / 20), snr0_b = 10 (log10 |x_b|^2 - log10 |n_b|^2) (energies in
+ *   fp64 over the clip) — torchaudio.functional.add_noise as AddNoise / AddMultiSpk call it
+ *   (avhubert_dataset.py:154-222: :178, :214, :220). y may alias x. ws: 2 * B * 64 doubles.
+ * avsr_rgb_to_gray: uint8 RGB [n][3] -> uint8 gray [n], cv2.COLOR_RGB2GRAY fixed point
+ *   (R*4899 + G*9617 + B*1868 + 8192) >> 14 (load_video, avhubert_dataset.py:45).
+ * ------------------------------------------------------------------------------------ */
+typedef struct {
+  int B, L, nspan;
+  int64_t row_bytes, clip_stride_bytes;     /* bytes per time step, bytes between clips */
+  void* x;
+  const int* spans;                         /* device [B][nspan][2] */
+} avsr_time_mask_params;
+int avsr_time_mask(const avsr_time_mask_params* p, void* stream);
+
+typedef struct {
+  int B, L;
+  const float* x; int64_t ldx;
+  const float* noise; int64_t ldn;
+  const int* lengths;                       /* device [B] or NULL (all L) */
+  const float* snr_db;                      /* device [B] */
+  float* y; int64_t ldy;
+  double* ws;                               /* >= AVSR_NOISE_WS(B) doubles */
+} avsr_add_noise_params;
+#define AVSR_NOISE_WS(B) (2 * 64 * (int64_t)(B))
+int avsr_add_noise(const avsr_add_noise_params* p, void* stream);
+
+int avsr_rgb_to_gray(const uint8_t* rgb, uint8_t* gray, int64_t n, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
