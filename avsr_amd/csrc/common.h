@@ -78,6 +78,23 @@ AVSR_DEV float drop_scale(float p, uint64_t seed, uint64_t idx) {
   return mix32(seed, idx) >= thr ? 1.0f / (1.0f - p) : 0.0f;
 }
 
+// drop_scale over indices d0 .. d0+7, multiplied into v: when the 8 indices share their high
+// word the mix32_hi finaliser is computed once (same mask as drop_scale element by element)
+AVSR_DEV void drop8(float p, uint64_t seed, uint64_t d0, float* v) {
+  const uint32_t thr = (uint32_t)(p * 4294967296.0f);
+  const float ks = 1.0f / (1.0f - p);
+  const uint32_t lo = (uint32_t)d0;
+  if (lo <= 0xFFFFFFF8u) {
+    const uint32_t pre = mix32_hi(seed, (uint32_t)(d0 >> 32));
+    const uint32_t g0 = lo * 0x9E3779B1u;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v[q] *= fmix32((g0 + (uint32_t)q * 0x9E3779B1u) ^ pre) >= thr ? ks : 0.0f;
+  } else {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v[q] *= drop_scale(p, seed, d0 + q);
+  }
+}
+
 AVSR_DEV float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
 AVSR_DEV float gelu_erf_grad(float x) {
   float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752f));
@@ -98,6 +115,33 @@ AVSR_DEV float gelu_fast(float x) {
 AVSR_DEV float gelu_fast_grad(float x) {
   const float z = x * 0.70710678118654752f, e = __expf(-z * z);
   return 0.5f * (1.0f + erf_as(z, e)) + x * 0.39894228040143268f * e;
+}
+// two elements at a time: the polynomial, the scalings and the final blend in packed fp32
+// (v_pk_fma_f32 / v_pk_mul_f32), only rcp and exp per element
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+AVSR_DEV f32x2 erf_as2(f32x2 z, f32x2 ez2) {
+  const f32x2 az = {fabsf(z.x), fabsf(z.y)};
+  const f32x2 d = az * 0.3275911f + 1.0f;
+  const f32x2 t = {__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+  f32x2 p = t * 1.061405429f + -1.453152027f;
+  p = p * t + 1.421413741f;
+  p = p * t + -0.284496736f;
+  p = p * t + 0.254829592f;
+  const f32x2 r = 1.0f - (p * t) * ez2;
+  return f32x2{copysignf(r.x, z.x), copysignf(r.y, z.y)};
+}
+AVSR_DEV f32x2 exp_negsq2(f32x2 z) {
+  const f32x2 q = z * z;
+  return f32x2{__expf(-q.x), __expf(-q.y)};
+}
+AVSR_DEV f32x2 gelu_fast2(f32x2 x) {
+  const f32x2 z = x * 0.70710678118654752f;
+  const f32x2 hx = x * 0.5f;
+  return hx + hx * erf_as2(z, exp_negsq2(z));
+}
+AVSR_DEV f32x2 gelu_fast_grad2(f32x2 x) {
+  const f32x2 z = x * 0.70710678118654752f, e = exp_negsq2(z);
+  return 0.5f + 0.5f * erf_as2(z, e) + (x * 0.39894228040143268f) * e;
 }
 template <typename T> AVSR_DEV float act_fwd_t(int act, float h) {
   if constexpr (sizeof(T) == 2) return act == AVSR_ACT_GELU ? gelu_fast(h) : (act == AVSR_ACT_RELU ? fmaxf(h, 0.f) : h);

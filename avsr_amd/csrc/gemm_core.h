@@ -406,27 +406,37 @@ AVSR_DEV void epi_vec8(const Epi& e, int row, int col, float (&v)[8]) {
     }
     if (e.preact) st8((T*)e.preact + off, v);
     if (e.act) {
+      if (sizeof(T) == 2 && e.act == AVSR_ACT_GELU) {
 #pragma unroll
-      for (int q = 0; q < 8; ++q) v[q] = act_fwd_t<T>(e.act, v[q]);
-    }
-    if (e.drop_p > 0.f) {
+        for (int q = 0; q < 8; q += 2) {
+          const f32x2 r = gelu_fast2(f32x2{v[q], v[q + 1]});
+          v[q] = r.x; v[q + 1] = r.y;
+        }
+      } else {
 #pragma unroll
-      for (int q = 0; q < 8; ++q) v[q] *= drop_scale(e.drop_p, e.seed, d0 + q);
+        for (int q = 0; q < 8; ++q) v[q] = act_fwd_t<T>(e.act, v[q]);
+      }
     }
+    if (e.drop_p > 0.f) drop8(e.drop_p, e.seed, d0, v);
     if (e.res) {
       ld8((const T*)e.res + (int64_t)row * e.ldr + col, t);
 #pragma unroll
       for (int q = 0; q < 8; ++q) v[q] += t[q];
     }
   } else {
-    if (e.drop_p > 0.f) {
-#pragma unroll
-      for (int q = 0; q < 8; ++q) v[q] *= drop_scale(e.drop_p, e.seed, d0 + q);
-    }
+    if (e.drop_p > 0.f) drop8(e.drop_p, e.seed, d0, v);
     if (e.gate) {
       ld8((const T*)e.gate + off, t);
+      if (sizeof(T) == 2 && e.act == AVSR_ACT_GELU) {
 #pragma unroll
-      for (int q = 0; q < 8; ++q) v[q] *= act_bwd_t<T>(e.act, t[q]);
+        for (int q = 0; q < 8; q += 2) {
+          const f32x2 r = gelu_fast_grad2(f32x2{t[q], t[q + 1]});
+          v[q] *= r.x; v[q + 1] *= r.y;
+        }
+      } else {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] *= act_bwd_t<T>(e.act, t[q]);
+      }
     }
   }
   if (e.beta != 0.f) {

@@ -112,7 +112,8 @@ class Engine:
         self.side = (torch.cuda.Stream(device=self.device)
                      if self.device.type == "cuda" and os.environ.get("AVSR_SIDE_STREAM", "1") == "1" else None)
         # reused events: a stream wait binds the record that precedes it
-        self._side_ev = [torch.cuda.Event() for _ in range(8)] if self.side is not None else []
+        self._side_ev = [torch.cuda.Event() for _ in range(int(os.environ.get("AVSR_SIDE_EV", "8")))] \
+            if self.side is not None else []
         self._side_i = 0
         E = "encoder.encoder.layers"
         groups = []
@@ -239,10 +240,13 @@ class Engine:
             return fn()
         # order the side stream after the work queued so far on the current stream: one raw
         # event record + wait (torch's wait_stream builds Stream / Event objects per call)
-        ev = self._side_ev[self._side_i]
-        self._side_i = (self._side_i + 1) % len(self._side_ev)
-        ev.record()
-        side.wait_event(ev)
+        if self._side_ev:
+            ev = self._side_ev[self._side_i]
+            self._side_i = (self._side_i + 1) % len(self._side_ev)
+            ev.record()
+            side.wait_event(ev)
+        else:
+            side.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(side):
             r = fn()
         for t in keep:

@@ -257,3 +257,64 @@ def rgb_to_gray(frames):
     L.check(L.load().avsr_rgb_to_gray(ctypes.c_void_p(frames.data_ptr()), ctypes.c_void_p(out.data_ptr()),
                                       out.numel(), L.stream_ptr()), "avsr_rgb_to_gray")
     return out
+
+
+def random_crop_offsets(h, w, th=88, tw=88):
+    """torchvision RandomCrop.get_params draws (avhubert_dataset.py:230): top, left."""
+    if h == th and w == tw:
+        return 0, 0
+    i = torch.randint(0, h - th + 1, size=(1,)).item()
+    j = torch.randint(0, w - tw + 1, size=(1,)).item()
+    return i, j
+
+
+class TrainCollator:
+    """DataCollator (avhubert_dataset.py:313-353) with the train transforms (VideoTransform /
+    AudioTransform 'train', :225-275) on decoded device clips: per clip, in the reference's
+    order, RandomCrop(88) + AdaptiveTimeMask(10, 25) on the frames, then cut_or_pad to 640 T
+    samples, AdaptiveTimeMask(6400, 16000), AddMultiSpk, AddNoise and FBanksAndStack on the
+    audio; collate_pad's zero padding. `noise` / `speech_dataset` + `load_audio` as for AddNoise /
+    AddMultiSpk (None: those steps pass the clip through, as in the reference)."""
+
+    def __init__(self, noise=None, speech_dataset=None, load_audio=None, text_transform=None):
+        self.vmask = AdaptiveTimeMask(10, 25)
+        self.amask = AdaptiveTimeMask(6400, 16000)
+        self.multispk = AddMultiSpk(speech_dataset=speech_dataset, load_audio=load_audio)
+        self.noise = AddNoise(noise)
+        self.text_transform = text_transform
+
+    def __call__(self, wavs, frames, labels=None):
+        """wavs: list of (S_i,) or (S_i, 1) float32 device waveforms; frames: list of (T_i, H, W)
+        uint8 device frames (gray); labels: optional list of strings (needs text_transform) or
+        token lists."""
+        dev = frames[0].device
+        lens = [f.shape[0] for f in frames]
+        tmax = max(lens)
+        B = len(frames)
+        videos = torch.zeros(B, 1, tmax, 88, 88, device=dev, dtype=torch.float32)
+        wav = torch.zeros(B, RATE_RATIO * tmax, device=dev, dtype=torch.float32)
+        for b in range(B):
+            f = frames[b]
+            oy, ox = random_crop_offsets(f.shape[1], f.shape[2])
+            spans = adaptive_time_mask_spans(f.shape[0], 10, 25)
+            fr = f.contiguous().clone()
+            time_mask(fr.unsqueeze(0), [spans])          # zero frames == zero after /255 and crop
+            video_transform(fr.unsqueeze(0), offsets=(oy, ox), out=videos[b:b + 1, :, :lens[b]])
+            a = cut_or_pad(wavs[b].reshape(-1, 1), RATE_RATIO * lens[b])
+            a = self.amask(a)
+            a = self.multispk(a)
+            a = self.noise(a)
+            wav[b, :RATE_RATIO * lens[b]] = a.reshape(-1)
+        ns = torch.tensor([RATE_RATIO * t for t in lens], dtype=torch.int64)
+        audios = audio_features(wav, ns, T=tmax)
+        lengths = torch.tensor(lens, dtype=torch.int64)
+        out = {"videos": videos, "audios": audios, "video_lengths": lengths, "audio_lengths": lengths.clone()}
+        if labels is not None:
+            toks = [self.text_transform.tokenize(l) if isinstance(l, str) else torch.as_tensor(l) for l in labels]
+            Lm = max(len(t) for t in toks)
+            lab = torch.full((B, Lm), -1, dtype=torch.int64)
+            for b, t in enumerate(toks):
+                lab[b, :len(t)] = torch.as_tensor(t, dtype=torch.int64)
+            out["labels"] = lab
+            out["label_lengths"] = torch.tensor([len(t) for t in toks], dtype=torch.int64)
+        return out

@@ -99,3 +99,61 @@ def test_rgb_to_gray(dev):
     rgb = torch.randint(0, 256, (5, 96, 96, 3), generator=g, dtype=torch.uint8)
     got = F.rgb_to_gray(rgb.to(dev)).cpu().numpy()
     assert np.array_equal(got, A.rgb_to_gray(rgb.numpy()))
+
+
+def _oracle_multispk(speech, pool):
+    """AddMultiSpk.forward's draws (avhubert_dataset.py:196-222) on numpy (S, 1) clips."""
+    if speech.shape[0] / 16000 < 2:
+        return speech
+    sig = None
+    for _ in range(random.choice([0, 0, 1, 2])):
+        itf = pool[random.choice(list(range(len(pool))))]
+        if 2 <= itf.shape[0] / 16000 <= 10:
+            itf = F.cut_or_pad(torch.from_numpy(itf), len(speech)).numpy()
+            if sig is None:
+                sig = itf
+            else:
+                sig = A.add_noise(sig.T, itf.T, np.array([random.choice([-5, 0, 5, 10, 15])])).T
+    if sig is None:
+        return speech
+    return A.add_noise(speech.T, sig.T, np.array([random.choice([-5, 0, 5, 10, 15, 20])])).T
+
+
+def test_train_collator(dev):
+    """DataCollator with the 'train' transforms (avhubert_dataset.py:225-275, 313-353): the device
+    collator against the same pipeline on numpy, with the RNG draws replayed in the same order."""
+    from oracle import frontend_oracle as O
+    g = torch.Generator().manual_seed(5)
+    ts = [75, 60]
+    frames = [torch.randint(0, 256, (t, 96, 96), generator=g, dtype=torch.uint8) for t in ts]
+    wavs = [0.2 * torch.randn(640 * t - 50, generator=g) for t in ts]
+    noise = 0.3 * torch.randn(1, 200000, generator=g)
+    pool = [0.2 * torch.randn(int(16000 * s), 1, generator=g) for s in (2.5, 4.0, 11.0)]
+    col = F.TrainCollator(noise=noise.to(dev), speech_dataset=list(range(3)), load_audio=lambda i: pool[i].to(dev))
+    for seed in range(3):
+        torch.manual_seed(seed); random.seed(100 + seed)
+        out = col([w.to(dev) for w in wavs], [f.to(dev) for f in frames], labels=[[3, 9, 4], [7]])
+        torch.manual_seed(seed); random.seed(100 + seed)
+        vids, auds = [], []
+        for f, w, t in zip(frames, wavs, ts):
+            oy = torch.randint(0, 96 - 88 + 1, size=(1,)).item()
+            ox = torch.randint(0, 96 - 88 + 1, size=(1,)).item()
+            x = f.numpy()[:, oy:oy + 88, ox:ox + 88].astype(np.float32) / np.float32(255.0)
+            x = A.adaptive_time_mask(x, 10, 25)
+            vids.append((x - np.float32(0.421)) / np.float32(0.165))
+            a = O.cut_or_pad(w.numpy(), 640 * t)[:, None]
+            a = A.adaptive_time_mask(a, 6400, 16000)
+            a = _oracle_multispk(a, [p.numpy() for p in pool])
+            start = random.randint(0, noise.shape[1] - a.shape[0])
+            snr = random.choice([-5, 0, 5, 10, 15, 20, 999999])
+            a = A.add_noise(a.T, noise[:, start:start + a.shape[0]].numpy(), np.array([snr])).T
+            auds.append(a[:, 0].astype(np.float32))
+        v = out["videos"].cpu().numpy()
+        assert v.shape == (2, 1, 75, 88, 88)
+        for b, t in enumerate(ts):
+            assert np.abs(v[b, 0, :t] - vids[b]).max() < 1e-5, seed
+            assert (v[b, 0, t:] == 0).all()
+        ref = O.collate_audio(auds, ts)
+        assert (out["audios"].cpu() - torch.from_numpy(ref)).abs().max().item() < 2e-3, seed
+        assert out["labels"].tolist() == [[3, 9, 4], [7, -1, -1]]
+        assert out["video_lengths"].tolist() == ts and out["label_lengths"].tolist() == [3, 1]

@@ -1,12 +1,13 @@
-# A/B: slab vs atomic conv weight-gradient, bench + kernel profile
+# A/B of env settings on the full bench (default vs each "NAME=VALUE" argument), same box
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 O=gpurun_out/ab; mkdir -p $O
-timeout -k 10 300 python -u bench.py --steps 10 --warmup 3 --no-cpu-baseline > $O/a1.log 2>&1 || exit 1
-AVSR_WGRAD_SLAB=0 timeout -k 10 300 python -u bench.py --steps 10 --warmup 3 --no-cpu-baseline > $O/b1.log 2>&1 || exit 1
-timeout -k 10 300 python -u bench.py --steps 10 --warmup 3 --no-cpu-baseline > $O/a2.log 2>&1 || exit 1
-AVSR_WGRAD_SLAB=0 timeout -k 10 300 python -u bench.py --steps 10 --warmup 3 --no-cpu-baseline > $O/b2.log 2>&1 || exit 1
-timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 bench.py --steps 4 --warmup 2 --no-cpu-baseline > $O/prof.log 2>&1 || exit 1
-for f in a1 b1 a2 b2; do echo $f; grep -o '"ms_per_step": [0-9.]*' $O/$f.log; done
-echo rc=0
+run() {  # label, env assignment
+  env $2 timeout -k 10 300 python -u bench.py --no-cpu-baseline > $O/$1.log 2>&1 || { echo "$1 failed"; tail -20 $O/$1.log; exit 1; }
+  tail -1 $O/$1.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('$1', '$2', d['value'], d['ms_per_step'], d['host_ms_per_step_timed'], d['device_ms_per_step_synced'], d['host_issue_ms_per_step'])"
+}
+run base AVSR_NOP=1
+i=0
+for a in "$@"; do i=$((i+1)); run v$i "$a"; done
+run base2 AVSR_NOP=1
