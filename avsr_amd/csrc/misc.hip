@@ -35,9 +35,18 @@ __global__ __launch_bounds__(256) void ew_bwd_kernel(EwArgs a) {
       ldv((const T*)a.dy + (int64_t)r * a.lddy + cv * VE, d);
       if (a.gate) ldv((const T*)a.gate + (int64_t)r * a.ldgate + cv * VE, g);
 #pragma unroll
+      for (int j = 0; j < VE; ++j) d[j] *= a.alpha;
+      if (a.drop_p > 0.f) {
+        const uint64_t i0 = (uint64_t)r * a.N + cv * VE;
+        if constexpr (VE == 8) drop8(a.drop_p, a.seed, i0, d);
+        else {
+#pragma unroll
+          for (int j = 0; j < VE; ++j) d[j] *= drop_scale(a.drop_p, a.seed, i0 + j);
+        }
+      }
+#pragma unroll
       for (int j = 0; j < VE; ++j) {
-        float v = d[j] * a.alpha;
-        if (a.drop_p > 0.f) v *= drop_scale(a.drop_p, a.seed, (uint64_t)r * a.N + cv * VE + j);
+        float v = d[j];
         if (a.gate) v *= act_bwd_t<T>(a.act, g[j]);
         acc[j] += v;
         d[j] = v;

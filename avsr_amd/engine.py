@@ -105,6 +105,7 @@ class Engine:
         if getattr(cfg, "modality", "av") not in ("av", "audio", "video"):
             raise ValueError(f"unknown modality {cfg.modality!r}")
         self.last_modality = None
+        self.force_modality = None   # (modality,): skip the draw (bench warm-up of every variant)
         self.capture = None          # tests: a dict receives the last forward's enc / logits / batch
         self._pinned = [(None, None)] * 4
         self._pin_next = 0
@@ -115,6 +116,9 @@ class Engine:
         self._side_ev = [torch.cuda.Event() for _ in range(int(os.environ.get("AVSR_SIDE_EV", "8")))] \
             if self.side is not None else []
         self._side_i = 0
+        # operands the side stream reads stay referenced until join_side() (instead of
+        # record_stream, whose deferred frees keep the caching allocator growing for steps)
+        self._side_keep = [] if os.environ.get("AVSR_SIDE_KEEP", "1") == "1" else None
         E = "encoder.encoder.layers"
         groups = []
         for i in range(self.nl):
@@ -232,7 +236,7 @@ class Engine:
     # weight gradients run on a side stream: nothing on the backward's critical path (the data-
     # gradient chain) waits for them, so they fill the CUs the chain's kernels leave idle (grid
     # tails, one-block-per-CU attention, small LayerNorm / bias kernels). Their inputs are kept
-    # alive for the side stream (record_stream) and never overwritten afterwards; gradient
+    # alive for the side stream (_side_keep) and never overwritten afterwards; gradient
     # consumers (all-reduce buckets, the optimizer) wait for the side stream first.
     def _on_side(self, fn, *keep):
         side = self.side
@@ -249,14 +253,20 @@ class Engine:
             side.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(side):
             r = fn()
-        for t in keep:
-            t.record_stream(side)
+        if self._side_keep is not None:
+            self._side_keep.extend(keep)
+        else:
+            for t in keep:
+                t.record_stream(side)
         return r
 
     def join_side(self):
         """make the current stream wait for every weight gradient issued so far"""
         if self.side is not None:
             torch.cuda.current_stream(self.device).wait_stream(self.side)
+            if self._side_keep:
+                # freed blocks return to the current stream's pool behind this wait
+                self._side_keep.clear()
 
     def _wgrad(self, dy, x, dW, alpha=1.0):
         """dW (fp32) += alpha * dy^T x (side stream). When the output tile grid is at or below one
@@ -831,7 +841,7 @@ class Engine:
         bt = self.prepare(videos, audios, video_lengths, labels)
         B, T = bt["B"], bt["T"]
         M = B * T
-        modality = self.draw_modality(train)
+        modality = self.draw_modality(train) if self.force_modality is None else self.force_modality[0]
         self.last_modality = modality
         enc, ectx = self.encoder_fwd(audios.to(self.device), videos.to(self.device), bt, train, need_grad, seeds, modality)
         # CTC branch: ctc_lo(dropout(enc))

@@ -19,6 +19,7 @@ resume) drives the engine instead:
     loss scaling). Otherwise the engine computes in fp32.
 """
 import copy
+import gc
 
 import torch
 from transformers import Trainer
@@ -50,6 +51,10 @@ class AVSRTrainer(Trainer):
         super().__init__(**kw)
         self.valid_data_collator = valid_data_collator
         self.ddp = ArenaDDP(self.model, average=True)
+        # the import-time heap (torch, transformers) moves to the collector's permanent
+        # generation: a full collection during a step otherwise stalls the host for ~0.1 s
+        gc.collect()
+        gc.freeze()
         # keep accelerate from wrapping the engine model in DistributedDataParallel
         prepare_model = self.accelerator.prepare_model
 

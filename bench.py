@@ -15,6 +15,7 @@ stream it is launched on; `cpu_baseline` times the repo's CPU restatement of the
 (oracle/, "port") on the host cores on a bounded sample.
 """
 import argparse
+import gc
 import json
 import os
 import sys
@@ -192,6 +193,23 @@ def main():
     d_ctc = torch.full((1,), mtl, device=dev)
     d_att = torch.full((1,), 1.0 - mtl, device=dev)
 
+    # the import-time heap goes to the collector's permanent generation (a full collection
+    # inside a step stalled the host for 0.1-0.15 s once per run)
+    if os.environ.get("AVSR_BENCH_GCFREEZE", "1") == "1":
+        gc.collect()
+        gc.freeze()
+    # untimed warm-up of each modality variant's step first (no RNG draws): every allocation
+    # pattern the timed steps can take is in the caching allocator's pool before timing
+    for forced in ((None, "video_off", "audio_off") if os.environ.get("AVSR_BENCH_PRIME", "1") == "1" else ()):
+        eng.force_modality = (forced,)
+        arena.zero_grad()
+        _, ctx = eng.forward(v, a, lens, lab, train=True, need_grad=True, seed=1)
+        eng.backward(ctx, d_ctc, d_att)
+        del ctx
+    eng.force_modality = None
+    torch.cuda.synchronize()
+    arena.zero_grad()
+
     # modality dropout (avhubert.py:476-482) draws from numpy's global RNG like the reference;
     # seeded here so that the timed steps' decisions are reproducible and reported
     np.random.seed(args.seed + 7919 * rank)
@@ -220,10 +238,13 @@ def main():
     drops.clear()
     ms0 = torch.cuda.memory_stats(dev)
     host_t = []
+    step_ev = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    step_ev[0].record()
+    for i in range(args.steps):
         h0 = time.perf_counter()
         out4 = step()
+        step_ev[i + 1].record()
         host_t.append(time.perf_counter() - h0)
     torch.cuda.synchronize()
     if world > 1:
@@ -264,7 +285,8 @@ def main():
             traffic = rec["traffic_bytes"]
     result = {
         "metric": METRIC, "value": round(value, 2), "unit": "AV-frames/s", "n_gpus": world,
-        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "steps": args.steps, "warmup": args.warmup,
+        "warmup_note": "plus one untimed fwd+bwd per modality variant (none / video_off / audio_off) before the warm-up steps", "ms_per_step": round(elapsed / args.steps * 1e3, 3),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
         "data": "synthetic (SURVEY d1 recipe: uint8 lip frames, normal+LN 104-d audio, U[1,5047] labels)",
         "config": {"workload": f"C2/C3: AVHubertAVSR fwd+bwd+AdamW, {B}x{T / 25:.0f}s clips per GPU "
@@ -282,6 +304,8 @@ def main():
         "host_issue_ms_per_step": round(sum(issue) / len(issue), 2),
         "device_ms_per_step_synced": round(sum(dev_ms) / len(dev_ms), 2),
         "host_ms_per_step_timed": round(sum(host_t) / len(host_t) * 1e3, 2),
+        "host_ms_steps": [round(t * 1e3, 1) for t in host_t],
+        "stream_ms_steps": [round(step_ev[i].elapsed_time(step_ev[i + 1]), 1) for i in range(args.steps)],
         "allocator_timed": {k: ms1.get(k, 0) - ms0.get(k, 0) for k in
                             ("num_device_alloc", "num_device_free", "num_alloc_retries", "num_sync_all_streams")},
         "modality_drops": {"seed": args.seed, "video_off": timed_drops.count("video_off"),
