@@ -25,6 +25,7 @@ static int make_geom(const avsr_conv_params* p, ConvGeom& g) {
   g.f_w_in = make_fastdiv((uint32_t)p->win);
   g.f_kw = make_fastdiv((uint32_t)p->kw);
   g.cin_shift = ilog2(p->cin); g.cout_shift = ilog2(p->cout);
+  g.ktot_w = p->kh * p->kw * p->cin; g.tap_kfw = p->kw; g.tap_kh0 = 0; g.tap_kw0 = 0; g.tap_step = 1;
   const int ve = p->dtype == AVSR_BF16 ? 8 : 4;
   if (g.cin_shift < 0 || g.cout_shift < 0 || p->cin < ve || p->cout < ve) return AVSR_E_SHAPE;
   if (p->ldx % ve || p->ldy % ve) return AVSR_E_ALIGN;
@@ -289,7 +290,7 @@ template <int R, int NW> struct BWgtR {
   uint32_t vo[SLOTS];
   AVSR_DEV void init(const bf16* base, uint32_t bytes, const ConvGeom& g_, int r0, int rext, int wave, int lane) {
     rs = make_rsrc(base, bytes); g = g_;
-    const int ktot = g.kh * g.kw * g.cin;
+    const int ktot = g.ktot_w;
 #pragma unroll
     for (int i = 0; i < SLOTS; ++i) {
       const int pc = i * NW + wave, pk = pc * RPP + lane / CPR;
@@ -298,8 +299,13 @@ template <int R, int NW> struct BWgtR {
     }
   }
   AVSR_DEV void issue(char* img, int k0, int wave) const {
-    const int ktot = g.kh * g.kw * g.cin;
-    const uint32_t so = (uint32_t)((((int64_t)(k0 & ((1 << g.cout_shift) - 1))) * ktot + (int64_t)(k0 >> g.cout_shift) * g.cin) * 2);
+    const int ktot = g.ktot_w;
+    int tap = k0 >> g.cout_shift;
+    if (g.tap_step != 1) {      // parity class of a stride-2 data-grad: class tap (u, v) -> kernel tap
+      const int u = (int)fdiv(tap, g.f_kw), v = tap - u * (int)g.f_kw.d;
+      tap = (g.tap_kh0 + g.tap_step * u) * g.tap_kfw + g.tap_kw0 + g.tap_step * v;
+    }
+    const uint32_t so = (uint32_t)((((int64_t)(k0 & ((1 << g.cout_shift) - 1))) * ktot + (int64_t)tap * g.cin) * 2);
 #pragma unroll
     for (int i = 0; i < SLOTS; ++i) bglds16(rs, vo[i], so, img + (i * NW + wave) * 1024);
   }
@@ -464,6 +470,7 @@ static void base_epi(Epi& e) {
   e.alpha = 1.f; e.beta = 0.f; e.bias = nullptr; e.act = 0; e.bwd = 0; e.atomic = 0;
   e.preact = nullptr; e.res = nullptr; e.ldr = 0; e.gate = nullptr; e.drop_p = 0.f; e.seed = 0;
   e.drop_base = 0; e.stats = nullptr; e.stats_tiles = 0;
+  e.rm_wc = 0; e.rm_hc = 0; e.rm_hin = 0; e.rm_win = 0; e.rm_a = 0; e.rm_b = 0;
 }
 
 // weight-gradient split-K plan. The LDS-DMA path writes per-split fp32 slabs (plain stores)
@@ -514,6 +521,66 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* ws, int 
   }
 }
 
+// Stride-2 data-grad by parity class of the input pixel. Class (a, b) = pixels (2i+a, 2j+b)
+// receives contributions only from the taps kh = kh0 + 2u, kh0 = (a + ph) mod 2 (kw likewise),
+// through dy at (i + ci - u, j + cj - v), ci = (a + ph - kh0) / 2: a stride-1 data-grad over
+// the class grid. The four class GEMMs do 1/4 of the multiply-adds of the full one, whose
+// other taps land on the zeros between the strided output pixels. A class with no taps (1x1
+// kernels) still runs its epilogue (zeros, or the fused BatchNorm reduction of beta * dx).
+struct S2Class { int a, b, hc, wc, nkh, nkw, kh0, kw0, ci, cj; };
+
+static void s2_classes(const avsr_conv_params* p, S2Class (&c)[4]) {
+  for (int q = 0; q < 4; ++q) {
+    S2Class& k = c[q];
+    k.a = q >> 1; k.b = q & 1;
+    k.hc = (p->hin - k.a + 1) / 2; k.wc = (p->win - k.b + 1) / 2;
+    k.kh0 = (k.a + p->ph) & 1; k.kw0 = (k.b + p->pw) & 1;
+    k.nkh = k.kh0 < p->kh ? (p->kh - k.kh0 + 1) / 2 : 0;
+    k.nkw = k.kw0 < p->kw ? (p->kw - k.kw0 + 1) / 2 : 0;
+    k.ci = (k.a + p->ph - k.kh0) / 2; k.cj = (k.b + p->pw - k.kw0) / 2;
+  }
+}
+
+// the parity-class path: bf16 buffer-DMA loaders (tap-uniform K-tiles), one group, stride 2
+static bool s2_phase(const avsr_conv_params* p) {
+  const char* e = getenv("AVSR_CONV_S2PHASE");
+  if (e && e[0] == '0') return false;
+  if (p->sh != 2 || p->sw != 2 || p->groups != 1 || p->dtype != AVSR_BF16 || !conv_glds_enabled()) return false;
+  if (p->cout % 64) return false;
+  ConvArgs t;
+  set_extents(t, p, true, ((int64_t)p->nimg * p->hout * p->wout - 1) * p->ldy + p->cout,
+              (int64_t)p->cout * p->kh * p->kw * p->cin);
+  return t.a_bytes != 0;
+}
+
+template <int KIND>
+static int s2_launch(const ConvArgs& a0, const avsr_conv_params* p, hipStream_t st) {
+  S2Class cl[4];
+  s2_classes(p, cl);
+  int64_t tile_off = 0;
+  for (int q = 0; q < 4; ++q) {
+    const S2Class& k = cl[q];
+    const int Mc = p->nimg * k.hc * k.wc;
+    if (Mc == 0) continue;
+    ConvArgs a = a0;
+    a.g.hin = k.hc; a.g.win = k.wc; a.g.kh = k.nkh; a.g.kw = k.nkw; a.g.sh = 1; a.g.sw = 1;
+    a.g.ph = k.ci; a.g.pw = k.cj;
+    a.g.f_hw_in = make_fastdiv((uint32_t)(k.hc * k.wc));
+    a.g.f_w_in = make_fastdiv((uint32_t)k.wc);
+    a.g.f_kw = make_fastdiv((uint32_t)(k.nkw > 0 ? k.nkw : 1));
+    a.g.tap_kh0 = k.kh0; a.g.tap_kw0 = k.kw0; a.g.tap_step = 2;
+    a.M = Mc; a.K = k.nkh * k.nkw * p->cout; a.kchunk = a.K;
+    a.e.M = Mc;
+    a.e.rm_wc = k.wc; a.e.rm_hc = k.hc; a.e.rm_hin = p->hin; a.e.rm_win = p->win; a.e.rm_a = k.a; a.e.rm_b = k.b;
+    if (KIND >= K_DGRAD_BNR) a.bnr.ws = a0.bnr.ws + tile_off * 4 * a.N;
+    tile_off += (Mc + tile_bm(Mc, a.N) - 1) / tile_bm(Mc, a.N);
+    if (KIND == K_DGRAD && a.K == 0 && a.e.beta == 1.f) continue;   // dx += 0
+    const int rc = glds_by_tile<bf16, KIND>(a, 1, st);
+    if (rc) return rc;
+  }
+  return 0;
+}
+
 }  // namespace
 
 extern "C" int avsr_conv_stat_tiles(const avsr_conv_params* p) {
@@ -523,6 +590,16 @@ extern "C" int avsr_conv_stat_tiles(const avsr_conv_params* p) {
 }
 
 extern "C" int avsr_conv_bnr_tiles(const avsr_conv_params* p) {
+  if (s2_phase(p)) {
+    S2Class cl[4];
+    s2_classes(p, cl);
+    int t = 0;
+    for (int q = 0; q < 4; ++q) {
+      const int Mc = p->nimg * cl[q].hc * cl[q].wc;
+      if (Mc) t += (Mc + tile_bm(Mc, p->cin) - 1) / tile_bm(Mc, p->cin);
+    }
+    return t;
+  }
   const int M = p->nimg * p->hin * p->win;
   const int bm = tile_bm(M, p->cin);
   return (M + bm - 1) / bm;
@@ -582,6 +659,11 @@ extern "C" int avsr_conv_bwd_data(const avsr_conv_params* p, void* stream) {
     a.bnr.shift2 = p->bnr_shift2; a.bnr.mean2 = p->bnr_mean2; a.bnr.invstd2 = p->bnr_invstd2; a.bnr.ws = p->bnr_ws;
     if (a.M == 0) return 0;
     hipStream_t st = (hipStream_t)stream;
+    if (s2_phase(p)) {
+      if (p->bnr_scale2) return s2_launch<K_DGRAD_BNR + 2>(a, p, st);
+      if (p->bnr_res) return s2_launch<K_DGRAD_BNR + 1>(a, p, st);
+      return s2_launch<K_DGRAD_BNR>(a, p, st);
+    }
     if (p->bnr_scale2) return glds_by_tile<bf16, K_DGRAD_BNR + 2>(a, 1, st);
     if (p->bnr_res) return glds_by_tile<bf16, K_DGRAD_BNR + 1>(a, 1, st);
     return glds_by_tile<bf16, K_DGRAD_BNR>(a, 1, st);
@@ -589,6 +671,7 @@ extern "C" int avsr_conv_bwd_data(const avsr_conv_params* p, void* stream) {
   if (a.M == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
   if (p->dtype == AVSR_F32) return by_tile<float, float, K_DGRAD>(a, p->groups, st);
+  if (s2_phase(p)) return s2_launch<K_DGRAD>(a, p, st);
   if (p->dtype == AVSR_BF16)
     return conv_glds_enabled() ? glds_by_tile<bf16, K_DGRAD>(a, p->groups, st)
                                : by_tile<bf16, bf16, K_DGRAD>(a, p->groups, st);

@@ -269,6 +269,7 @@ extern "C" int avsr_gemm(const avsr_gemm_params* p, void* stream) {
   }
   e.preact = p->preact; e.res = p->res; e.ldr = p->ldr; e.gate = p->gate;
   e.drop_p = p->drop_p; e.seed = p->seed; e.drop_base = 0; e.stats = nullptr; e.stats_tiles = 0;
+  e.rm_wc = 0; e.rm_hc = 0; e.rm_hin = 0; e.rm_win = 0; e.rm_a = 0; e.rm_b = 0;
   hipStream_t st = (hipStream_t)stream;
   if (p->K == 0) return AVSR_E_SHAPE;
   int rc;

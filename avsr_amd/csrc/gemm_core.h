@@ -37,6 +37,11 @@ struct ConvGeom {
   FastDiv f_hw_in, f_w_in;          // division by hin*win, win
   FastDiv f_kw;                     // division by kw
   int cin_shift, cout_shift;        // log2(cin), log2(cout)
+  // data-grad weight taps: K-tile tap t = (u, v) over the (kh, kw) grid above reads the weight
+  // tap (tap_kh0 + tap_step*u, tap_kw0 + tap_step*v) of a tap_kfh x tap_kfw kernel whose rows
+  // hold ktot_w = tap_kfh*tap_kfw*cin elements (tap_step 1: the plain kernel; 2: one parity
+  // class of a stride-2 data-grad)
+  int ktot_w, tap_kfw, tap_kh0, tap_kw0, tap_step;
 };
 
 // ---------------------------------------------------------------- dense loaders
@@ -318,7 +323,18 @@ struct Epi {
   float drop_p; uint64_t seed; uint64_t drop_base;
   float* stats;        // BN partials: [N][stats_tiles][3] = (count, mean, M2) of the stored values
   int stats_tiles;
+  // output row map of a stride-2 data-grad parity class: GEMM row r = (n, i, j) over an
+  // rm_hc x rm_wc grid stores to pixel (n, 2i + rm_a, 2j + rm_b) of an rm_hin x rm_win image;
+  // rm_wc == 0: row r is stored at row r
+  int rm_wc, rm_hc, rm_hin, rm_win, rm_a, rm_b;
 };
+
+AVSR_DEV int epi_row(const Epi& e, int r) {
+  if (e.rm_wc == 0) return r;
+  const int q = r / e.rm_wc, j = r - q * e.rm_wc;
+  const int n = q / e.rm_hc, i = q - n * e.rm_hc;
+  return (n * e.rm_hin + 2 * i + e.rm_a) * e.rm_win + 2 * j + e.rm_b;
+}
 
 // row/col of accumulator register r of tile (i, j)
 AVSR_DEV int acc_row(int wm, int i, int r, int lane) { return wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5); }

@@ -372,11 +372,12 @@ AVSR_DEV void epilogue_g(const Epi& e, int m0, int n0, f32x4 (&acc)[CF::TM][CF::
       if (row < e.M && col < e.N) {
         const f32x4 v0 = *(const f32x4*)(st + lr * LDR + lc), v1 = *(const f32x4*)(st + lr * LDR + lc + 4);
         float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+        const int orow = epi_row(e, row);
         if (vec && col + 8 <= e.N) {
-          epi_vec8<T, OutT>(e, row, col, v);
+          epi_vec8<T, OutT>(e, orow, col, v);
         } else {
-          epi_elems<T, OutT, 4>(e, row, col, v);
-          if (col + 4 < e.N) epi_elems<T, OutT, 4>(e, row, col + 4, v + 4);
+          epi_elems<T, OutT, 4>(e, orow, col, v);
+          if (col + 4 < e.N) epi_elems<T, OutT, 4>(e, orow, col + 4, v + 4);
         }
       }
     }
@@ -431,7 +432,7 @@ AVSR_DEV void epilogue_bnr(const Epi& e, const BnrArgs& b, int m0, int n0, f32x4
       const int lr = (tid + it * CF::NTH) / CG;
       const int row = m0 + ((lr >> 5) * CF::FM + i) * 32 + (lr & 31);
       ok[it] = row < e.M && colok;
-      off[it] = ok[it] ? (int64_t)row * e.ldc + col : 0;
+      off[it] = ok[it] ? (int64_t)epi_row(e, row) * e.ldc + col : 0;
       ph[it] = *(const bf16x8*)(b.h + off[it]);
       if constexpr (RES != 0) pr[it] = *(const bf16x8*)(b.res + off[it]);
       if (beta) pc[it] = *(const bf16x8*)(C + off[it]);

@@ -19,6 +19,8 @@ CASES = [
     (5, 22, 22, 64, 128, 3, 2, 1),
     (5, 22, 22, 64, 128, 1, 2, 0),
     (7, 6, 6, 256, 512, 3, 2, 1),
+    (5, 11, 11, 128, 256, 3, 2, 1),   # odd input: parity classes of unequal size
+    (5, 11, 11, 128, 256, 1, 2, 0),
     (4, 3, 3, 512, 512, 3, 1, 1),
     (3, 88, 88, 8, 64, 7, 2, 3),      # stem as 2-D conv over 8 packed channels
 ]
@@ -129,3 +131,29 @@ def test_wgrad_slab_accumulates(dev, case, splitk):
     ref = wr.grad.permute(0, 2, 3, 1) + init.double()
     assert _rel(dw, ref) < 2e-2
     assert _rel(dw - init.to(dev), dwa - init.to(dev)) < 1e-4
+
+
+S2_CASES = [(5, 22, 22, 64, 128, 3, 2, 1), (5, 11, 11, 128, 256, 3, 2, 1), (7, 6, 6, 256, 512, 3, 2, 1),
+            (5, 11, 11, 128, 256, 1, 2, 0), (3, 22, 22, 64, 128, 1, 2, 0)]
+
+
+@pytest.mark.parametrize("beta", [0.0, 1.0])
+@pytest.mark.parametrize("case", S2_CASES)
+def test_stride2_dgrad_parity_classes_match_full(dev, case, beta, monkeypatch):
+    """The stride-2 data-grad split into input-pixel parity classes (conv.hip s2_launch) adds
+    the same non-zero products in the same order as the full col2im GEMM: bit-identical."""
+    n, h, w, cin, cout, k, s, p = case
+    g = torch.Generator().manual_seed(n * 7 + cin + k)
+    geom = ops.ConvGeom(n, h, w, cin, cout, k, k, (s, s), (p, p))
+    bf = torch.bfloat16
+    dy = torch.randn(n, geom.hout, geom.wout, cout, generator=g).to(dev, bf)
+    wd = (torch.randn(cout, k, k, cin, generator=g) * (cin * k * k) ** -0.5).to(dev, bf)
+    old = torch.randn(n, h, w, cin, generator=g).to(dev, bf)
+    outs = []
+    for mode in ("1", "0"):
+        monkeypatch.setenv("AVSR_CONV_S2PHASE", mode)
+        dx = old.clone()
+        ops.conv_bwd_data(geom, dy, wd, dx, beta=beta)
+        outs.append(dx)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])

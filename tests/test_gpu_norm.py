@@ -145,6 +145,8 @@ BNR_CASES = [
     (5, 22, 64, 128, 1, 2, 0, "downsample"),    # a block's downsample dgrad into the previous bn2
     (7, 6, 256, 256, 3, 1, 1, "plain"),         # 128x128 tiles, bn1 of layer 3
     (9, 3, 512, 512, 3, 1, 1, "identity"),      # layer 4, ragged last row tile
+    (4, 11, 128, 256, 3, 2, 1, "identity"),     # stride 2 by parity class, odd grid
+    (4, 11, 128, 256, 1, 2, 0, "downsample"),   # 1x1 stride 2: three classes epilogue-only
 ]
 
 

@@ -39,13 +39,25 @@ def once(fuse):
     return ev[0].elapsed_time(ev[1]), ev[1].elapsed_time(ev[2])
 
 
-for f in (True, False):
-    once(f)
-res = {True: [], False: []}
+# variants: (label, BN fusion, AVSR_CONV_S2PHASE)
+mode = sys.argv[2] if len(sys.argv) > 2 else "fuse"
+variants = [("fuse=1", True, "1"), ("fuse=0", False, "1")] if mode == "fuse" else \
+    [("s2phase=1", True, "1"), ("s2phase=0", True, "0")]
+
+
+def run(var):
+    os.environ["AVSR_CONV_S2PHASE"] = var[2]
+    return once(var[1])
+
+
+for var in variants:
+    run(var)
+res = {var[0]: [] for var in variants}
 for _ in range(reps):
-    for f in (True, False):
-        res[f].append(once(f))
-for f in (True, False):
-    fw = sorted(x[0] for x in res[f])[len(res[f]) // 2]
-    bw = sorted(x[1] for x in res[f])[len(res[f]) // 2]
-    print(f"fuse={int(f)}: video fwd {fw:.3f} ms  bwd {bw:.3f} ms (median of {reps})", flush=True)
+    for var in variants:
+        res[var[0]].append(run(var))
+for var in variants:
+    r = res[var[0]]
+    fw = sorted(x[0] for x in r)[len(r) // 2]
+    bw = sorted(x[1] for x in r)[len(r) // 2]
+    print(f"{var[0]}: video fwd {fw:.3f} ms  bwd {bw:.3f} ms (median of {reps})", flush=True)
