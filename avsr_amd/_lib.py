@@ -38,6 +38,8 @@ class GemmParams(ctypes.Structure):
         ("seed", ctypes.c_uint64),
         ("splitk", _i),
         ("ws", _c_p),
+        ("db", _c_p),
+        ("db_ws", _c_p),
     ]
 
 

@@ -470,7 +470,7 @@ static void base_epi(Epi& e) {
   e.alpha = 1.f; e.beta = 0.f; e.bias = nullptr; e.act = 0; e.bwd = 0; e.atomic = 0;
   e.preact = nullptr; e.res = nullptr; e.ldr = 0; e.gate = nullptr; e.drop_p = 0.f; e.seed = 0;
   e.drop_base = 0; e.stats = nullptr; e.stats_tiles = 0;
-  e.rm_wc = 0; e.rm_hc = 0; e.rm_hin = 0; e.rm_win = 0; e.rm_a = 0; e.rm_b = 0;
+  e.rm_wc = 0; e.rm_hc = 0; e.rm_hin = 0; e.rm_win = 0; e.rm_a = 0; e.rm_b = 0; e.colsum = nullptr;
 }
 
 // weight-gradient split-K plan. The LDS-DMA path writes per-split fp32 slabs (plain stores)

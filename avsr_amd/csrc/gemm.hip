@@ -151,6 +151,23 @@ int tile_cfg(const avsr_gemm_params* p, int splits) {
   return 0;
 }
 
+// row-tile height of a configuration (the fused column-sum partials are per row tile)
+int cfg_bm(int cfg, bool ak) {
+  switch (cfg) {
+    case 1: return Cfg256::BM;
+    case 2: return Cfg256x128::BM;
+    case 3: return Cfg128x256::BM;
+    case 4: return Cfg128s3::BM;
+    case 5: return Cfg128s4::BM;
+    case 6: return Cfg128w8s3::BM;
+    case 7: return Cfg128w8s4::BM;
+    case 8: return gemmpp::BM;
+    case 9: return ak ? Cfg96::BM : Cfg128::BM;   // as launch_cfg
+    case 10: return Cfg128x64::BM;
+    default: return Cfg128::BM;
+  }
+}
+
 template <typename OutT, bool AK, bool BK>
 int launch_cfg(int cfg, const DenseArgs& a, int batch, hipStream_t st) {
   switch (cfg) {
@@ -270,6 +287,17 @@ extern "C" int avsr_gemm(const avsr_gemm_params* p, void* stream) {
   e.preact = p->preact; e.res = p->res; e.ldr = p->ldr; e.gate = p->gate;
   e.drop_p = p->drop_p; e.seed = p->seed; e.drop_base = 0; e.stats = nullptr; e.stats_tiles = 0;
   e.rm_wc = 0; e.rm_hc = 0; e.rm_hin = 0; e.rm_win = 0; e.rm_a = 0; e.rm_b = 0;
+  e.colsum = nullptr;
+  int colsum_bm = 0;
+  if (p->db) {   // fused bias gradient: the LDS-DMA bf16 path's vector epilogue, one K pass
+    if (!glds || p->dtype != AVSR_BF16 || p->c_f32 || splits > 1 || p->batch != 1 || !p->db_ws || (p->N % 8) ||
+        (p->ldc % 8) || (p->ldr % 8) || !avsr_aligned16(p->C) || (p->gate && !avsr_aligned16(p->gate)) ||
+        (p->preact && !avsr_aligned16(p->preact)) || (p->res && (!avsr_aligned16(p->res) || (p->ldr % 8))) ||
+        (p->bias && !avsr_aligned16(p->bias)))
+      return AVSR_E_ARG;
+    colsum_bm = cfg_bm(tile_cfg(p, splits), p->a_kmajor != 0);
+    e.colsum = p->db_ws;
+  }
   hipStream_t st = (hipStream_t)stream;
   if (p->K == 0) return AVSR_E_SHAPE;
   int rc;
@@ -277,7 +305,14 @@ extern "C" int avsr_gemm(const avsr_gemm_params* p, void* stream) {
   else if (p->dtype == AVSR_F32) rc = by_tile<float, float>(p, a, st);
   else if (p->c_f32) rc = by_tile<bf16, float>(p, a, st);
   else rc = by_tile<bf16, bf16>(p, a, st);
-  if (rc || !slab) return rc;
+  if (rc) return rc;
+  if (colsum_bm) {
+    const int tiles = (p->M + colsum_bm - 1) / colsum_bm;
+    hipLaunchKernelGGL(colsum_finalize_kernel, colsum_grid(p->N), dim3(COLSUM_THREADS), 0, st, (const float*)p->db_ws,
+                       tiles, (int64_t)p->N, p->N, p->db, 0, (float*)nullptr);
+    AVSR_CHECK_LAUNCH();
+  }
+  if (!slab) return 0;
   const int64_t per = (int64_t)p->M * (p->N / 4);
   if (per >= (1ll << 31)) return AVSR_E_SHAPE;
   const dim3 g((unsigned)avsr_grid(per, 256, 4096), p->batch);

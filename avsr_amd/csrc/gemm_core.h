@@ -327,6 +327,7 @@ struct Epi {
   // rm_hc x rm_wc grid stores to pixel (n, 2i + rm_a, 2j + rm_b) of an rm_hin x rm_win image;
   // rm_wc == 0: row r is stored at row r
   int rm_wc, rm_hc, rm_hin, rm_win, rm_a, rm_b;
+  float* colsum;       // [row tiles][N]: per-tile column sums of the stored values (or nullptr)
 };
 
 AVSR_DEV int epi_row(const Epi& e, int r) {

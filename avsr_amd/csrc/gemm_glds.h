@@ -352,6 +352,10 @@ AVSR_DEV void epilogue_g(const Epi& e, int m0, int n0, f32x4 (&acc)[CF::TM][CF::
       }
     }
   }
+  static_assert(CF::NTH % (BN / 8) == 0, "a thread's column group must be fixed");
+  float cs[8];          // column sums of this thread's stored values (e.colsum)
+#pragma unroll
+  for (int j = 0; j < 8; ++j) cs[j] = 0.f;
 #pragma unroll
   for (int i = 0; i < CF::FM; ++i) {
     __syncthreads();
@@ -375,11 +379,28 @@ AVSR_DEV void epilogue_g(const Epi& e, int m0, int n0, f32x4 (&acc)[CF::TM][CF::
         const int orow = epi_row(e, row);
         if (vec && col + 8 <= e.N) {
           epi_vec8<T, OutT>(e, orow, col, v);
+          if (e.colsum) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) cs[j] += v[j];
+          }
         } else {
           epi_elems<T, OutT, 4>(e, orow, col, v);
           if (col + 4 < e.N) epi_elems<T, OutT, 4>(e, orow, col + 4, v + 4);
         }
       }
+    }
+  }
+  if (e.colsum) {       // (host-checked: vector path, N % 8 == 0) block reduction per column
+    constexpr int CG = BN / 8, RP = 9;
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 8; ++j) st[tid * RP + j] = cs[j];
+    __syncthreads();
+    for (int t = tid; t < BN; t += CF::NTH) {
+      const int g = t >> 3, j = t & 7;
+      float s = 0.f;
+      for (int k = g; k < CF::NTH; k += CG) s += st[k * RP + j];
+      if (n0 + t < e.N) e.colsum[(int64_t)(m0 / CF::BM) * e.N + n0 + t] = s;
     }
   }
 }

@@ -34,6 +34,8 @@ from .arena import Arena
 GELU, RELU, NONE = L.ACT_GELU, L.ACT_RELU, L.ACT_NONE
 # BatchNorm-backward reductions in the ResNet data-grad epilogues (bf16); 0 = separate passes (A/B)
 _BN_FUSE = os.environ.get("AVSR_BN_FUSE", "1") == "1"
+# bias gradients reduced in the epilogue of the data-grad GEMM that produces their operand
+_DB_FUSE = os.environ.get("AVSR_DB_FUSE", "1") == "1"
 
 
 def wgrad_splitk(M, N, K):
@@ -287,7 +289,15 @@ class Engine:
     def _conv_wgrad(self, g, x, dy, dw):
         self._on_side(lambda: ops.conv_bwd_weight(g, x, dy, dw), x, dy)
 
-    def _bias_grad(self, g, db, alpha=1.0):
+    def _fused_db(self, name):
+        """bias-gradient target handed to the data-grad that produces its operand (ops.linear_dgrad
+        reduces it in the GEMM epilogue, or in a separate pass where that core does not apply)"""
+        return self.g(name) if _DB_FUSE else None
+
+    def _bias_grad(self, g, db, alpha=1.0, fused=False):
+        """db += alpha * column sums of g (skipped when the producing data-grad already did it)"""
+        if fused and _DB_FUSE:
+            return
         ops.ew_bwd(g, db=db, alpha=alpha)
 
     # ------------------------------------------------------------------------ batch prep
@@ -623,8 +633,9 @@ class Engine:
         g2 = self._e(M, D)
         ops.ew_bwd(dx2, out=g2, drop_p=lc["p_h"], seed=lc["sd_f"], db=self.g(ff + "output_dense.bias"))
         self._wgrad(g2, lc["act"], self.g(ff + "output_dense.weight"))
-        dh = ops.linear_dgrad(g2, self.w(ff + "output_dense.weight"), gate=lc["h"], act=GELU, drop_p=lc["p_a"], seed=lc["sd_a"])
-        self._bias_grad(dh, self.g(ff + "intermediate_dense.bias"))
+        dh = ops.linear_dgrad(g2, self.w(ff + "output_dense.weight"), gate=lc["h"], act=GELU, drop_p=lc["p_a"],
+                              seed=lc["sd_a"], db=self._fused_db(ff + "intermediate_dense.bias"))
+        self._bias_grad(dh, self.g(ff + "intermediate_dense.bias"), fused=True)
         self._wgrad(dh, lc["ln2"], self.g(ff + "intermediate_dense.weight"))
         dln2 = ops.linear_dgrad(dh, self.w(ff + "intermediate_dense.weight"))
         dx1 = self._ln_bwd(dln2, lc["x1"], p + "final_layer_norm", lc["m2"], lc["r2"], dres=dx2, dx=dx2)
@@ -779,8 +790,9 @@ class Engine:
             g = self._e(R, D)
             ops.ew_bwd(dy, out=g, drop_p=p_d, seed=lc["s6"], db=self.g(ff + "w_2.bias"))
             self._wgrad(g, lc["a"], self.g(ff + "w_2.weight"))
-            dh = ops.linear_dgrad(g, self.w(ff + "w_2.weight"), gate=lc["h"], act=RELU, drop_p=p_d, seed=lc["s5"])
-            self._bias_grad(dh, self.g(ff + "w_1.bias"))
+            dh = ops.linear_dgrad(g, self.w(ff + "w_2.weight"), gate=lc["h"], act=RELU, drop_p=p_d, seed=lc["s5"],
+                                  db=self._fused_db(ff + "w_1.bias"))
+            self._bias_grad(dh, self.g(ff + "w_1.bias"), fused=True)
             self._wgrad(dh, lc["n3"], self.g(ff + "w_1.weight"))
             dn3 = ops.linear_dgrad(dh, self.w(ff + "w_1.weight"))
             dy = ops.layernorm_bwd(dn3, lc["y2"], self.arena.master(p + "norm3.weight"), lc["m3"], lc["r3"], dx=dy, dres=dy,

@@ -38,7 +38,7 @@ def _ptr(t):
 def gemm(A, B, C, *, M, N, K, a_kmajor, b_kmajor, lda, ldb, ldc, batch=1,
          strideA=0, strideB=0, strideC=0, alpha=1.0, beta=0.0, bias=None, act=L.ACT_NONE,
          epi_bwd=False, preact=None, res=None, ldr=None, strideR=0, gate=None, drop_p=0.0, seed=0,
-         splitk=1, ws=None):
+         splitk=1, ws=None, db=None, db_ws=None):
     """Raw GEMM launch: C[b,m,n] = epi(alpha * sum_k A(b,m,k) B(b,n,k)). See avsr_hip.h."""
     lib = L.load()
     assert A.is_cuda and B.is_cuda and C.is_cuda
@@ -71,6 +71,10 @@ def gemm(A, B, C, *, M, N, K, a_kmajor, b_kmajor, lda, ldb, ldc, batch=1,
     if ws is not None:
         assert ws.dtype == torch.float32 and ws.numel() >= slab_ws(batch, splitk, M, N)
         p.ws = ws.data_ptr()
+    if db is not None:
+        assert db.dtype == torch.float32 and db.numel() >= N and db_ws is not None and db_ws.dtype == torch.float32
+        assert db_ws.numel() >= ((M + 63) // 64) * N
+        p.db, p.db_ws = db.data_ptr(), db_ws.data_ptr()
     probe = PROBE.get("gemm")
     if probe is not None and probe["match"](M, N, K, a_kmajor, b_kmajor, dt):
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -100,14 +104,23 @@ def linear_fwd(x, W, bias=None, *, act=L.ACT_NONE, preact=None, res=None, drop_p
     return out
 
 
-def linear_dgrad(dy, W, *, gate=None, act=L.ACT_NONE, drop_p=0.0, seed=0, out=None, beta=0.0):
-    """dx = (dy W) [* dropout mask][* act'(gate)]  — gradient w.r.t. the layer input."""
+def linear_dgrad(dy, W, *, gate=None, act=L.ACT_NONE, drop_p=0.0, seed=0, out=None, beta=0.0, db=None):
+    """dx = (dy W) [* dropout mask][* act'(gate)]  — gradient w.r.t. the layer input.
+    db (fp32 [K]): += column sums of dx (the bias gradient of the layer dx is the output
+    gradient of), reduced in the GEMM epilogue."""
     M, N = dy.shape
     K = W.shape[1]
     if out is None:
         out = torch.empty(M, K, device=dy.device, dtype=dy.dtype)
+    # the epilogue reduction needs the LDS-DMA bf16 core (avsr_gemm: glds_ok) and 8-column vectors
+    fused = (db is not None and dy.dtype == torch.bfloat16 and M >= 128 and K >= 128 and K % 8 == 0
+             and out.stride(0) % 8 == 0 and os.environ.get("AVSR_GEMM_NOGLDS", "0") != "1")
+    ws = torch.empty(((M + 63) // 64) * K, device=dy.device) if fused else None   # AVSR_GEMM_COLSUM_WS
     gemm(dy, W, out, M=M, N=K, K=N, a_kmajor=True, b_kmajor=False, lda=dy.stride(0), ldb=W.stride(0),
-         ldc=out.stride(0), epi_bwd=True, gate=gate, act=act, drop_p=drop_p, seed=seed, beta=beta)
+         ldc=out.stride(0), epi_bwd=True, gate=gate, act=act, drop_p=drop_p, seed=seed, beta=beta,
+         db=db if fused else None, db_ws=ws)
+    if db is not None and not fused:
+        ew_bwd(out, db=db)
     return out
 
 

@@ -73,7 +73,12 @@ typedef struct {
                                 each split stores its partial tile, a reduce pass writes
                                 C = alpha*sum + beta*C (plain epilogue only). NULL: C += alpha*acc
                                 by fp32 atomics */
+  float* db;                 /* optional: db[n] += sum_m C[m][n] of the stored tile values (the
+                                bias gradient of the layer whose output gradient C is, e.g.
+                                FFN1's bias from the FFN2 data-grad); bf16, N % 8 == 0, no split */
+  float* db_ws;              /* its row-tile partials, AVSR_GEMM_COLSUM_WS(M, N) fp32 */
 } avsr_gemm_params;
+#define AVSR_GEMM_COLSUM_WS(M, N) ((int64_t)(((M) + 63) / 64) * (N))
 /* slabs are AVSR_GEMM_SLAB_PAD floats apart beyond M*N: power-of-two slab strides put the
  * reduce pass's split-many reads of one vector on the same HBM channels (measured 0.55 TB/s for
  * 8 slabs of 4 MiB) */

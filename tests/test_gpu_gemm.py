@@ -146,3 +146,22 @@ def test_gemm_batched_strided_bf16(dev, gemm_tile):
     ref = torch.bmm(A.float(), B.float())
     err = (C - ref).abs().max().item() / ref.abs().max().item()
     assert err < 2e-3, err
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,N,K", [(1000, 1024, 4096), (6000, 256, 1024), (200, 512, 136), (96, 512, 256)])
+def test_dgrad_fused_bias_grad(dev, gemm_tile, M, N, K):
+    """linear_dgrad(..., db=) reduces the bias gradient of its output (column sums of the stored
+    values, here after GELU' and dropout) in the GEMM epilogue, per row tile of every tile
+    configuration; ragged M, and M < 128 (separate reduction pass). Reference: fp64 column sums
+    of the returned bf16 tensor (the fused sums use the fp32 values before rounding: 2e-3)."""
+    g = torch.Generator().manual_seed(M + N)
+    dy = torch.randn(M, N, generator=g).to(dev, torch.bfloat16)
+    W = (torch.randn(N, K, generator=g) * N ** -0.5).to(dev, torch.bfloat16)
+    h = torch.randn(M, K, generator=g).to(dev, torch.bfloat16)
+    db0 = torch.randn(K, generator=g).to(dev)
+    db = db0.clone()
+    out = ops.linear_dgrad(dy, W, gate=h, act=L.ACT_GELU, drop_p=0.1, seed=11, db=db)
+    ref = out.double().sum(0)
+    err = ((db.double() - db0.double()) - ref).abs().max().item() / ref.abs().max().item()
+    assert err < 2e-3, err
