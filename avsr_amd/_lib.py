@@ -256,6 +256,8 @@ SYMBOLS = {
     "avsr_ctc_bwd": ([ctypes.POINTER(CtcParams), _c_p], _i),
     "avsr_loss_finalize": ([_i, _c_p, _i, _c_p, _c_p, _f, _c_p, _c_p], _i),
     "avsr_ew_bwd": ([ctypes.POINTER(EwParams), _c_p], _i),
+    "avsr_colsum_defer": ([_i], _i),
+    "avsr_colsum_flush": ([_c_p], _i),
     "avsr_dropout_fwd": ([ctypes.POINTER(EwParams), _c_p], _i),
     "avsr_mask_rows": ([_i, _i, _i, _i, _c_p, _i64, _c_p, _c_p], _i),
     "avsr_embed_fwd": ([ctypes.POINTER(EmbedParams), _c_p], _i),

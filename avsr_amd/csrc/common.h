@@ -234,11 +234,10 @@ static inline int avsr_grid(long work, int per_block = 256, int cap = 2048) {
 // summed in a fixed order (deterministic). (8 row lanes: ~6.7 us per 256 x 1024 workspace,
 // a latency-bound chain of 32 loads per thread.)
 constexpr int COLSUM_THREADS = 1024;
-static __global__ __launch_bounds__(COLSUM_THREADS) void colsum_finalize_kernel(const float* ws, int nb, int64_t ld, int N,
-                                                                                 float* out, int N1, float* out1) {
+AVSR_DEV void colsum_block(const float* ws, int nb, int64_t ld, int N, float* out, int N1, float* out1, int cb) {
   __shared__ float red[32][33];
   const int cl = threadIdx.x & 31, rl = threadIdx.x >> 5;
-  const int c = blockIdx.x * 32 + cl;
+  const int c = cb * 32 + cl;
   float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
   if (c < N) {
     int b = rl;
@@ -260,4 +259,14 @@ static __global__ __launch_bounds__(COLSUM_THREADS) void colsum_finalize_kernel(
     else out[c] += s;
   }
 }
+static __global__ __launch_bounds__(COLSUM_THREADS) void colsum_finalize_kernel(const float* ws, int nb, int64_t ld, int N,
+                                                                                 float* out, int N1, float* out1) {
+  colsum_block(ws, nb, ld, N, out, N1, out1, blockIdx.x);
+}
 static inline dim3 colsum_grid(int N) { return dim3((N + 31) / 32); }
+
+// The row-block partial workspaces of bias / LayerNorm parameter gradients are finalised by
+// colsum_launch: at once, or — between avsr_colsum_defer(1) and avsr_colsum_flush() — queued
+// host-side and reduced by ONE batched launch per flush (misc.hip). Callers keep the
+// workspaces alive until the flush.
+int colsum_launch(const float* ws, int nb, int64_t ld, int N, float* out, int N1, float* out1, hipStream_t st);

@@ -308,9 +308,8 @@ extern "C" int avsr_gemm(const avsr_gemm_params* p, void* stream) {
   if (rc) return rc;
   if (colsum_bm) {
     const int tiles = (p->M + colsum_bm - 1) / colsum_bm;
-    hipLaunchKernelGGL(colsum_finalize_kernel, colsum_grid(p->N), dim3(COLSUM_THREADS), 0, st, (const float*)p->db_ws,
-                       tiles, (int64_t)p->N, p->N, p->db, 0, (float*)nullptr);
-    AVSR_CHECK_LAUNCH();
+    rc = colsum_launch((const float*)p->db_ws, tiles, (int64_t)p->N, p->N, p->db, 0, nullptr, st);
+    if (rc) return rc;
   }
   if (!slab) return 0;
   const int64_t per = (int64_t)p->M * (p->N / 4);

@@ -4,6 +4,7 @@
 // packing, pos-conv weight norm, and the fused clip-grad-norm + AdamW step.
 // All HBM-bound: 16-byte vectors where the layout allows, grid-stride loops.
 #include "common.h"
+#include <vector>
 
 namespace {
 
@@ -351,14 +352,65 @@ int ew_launch(const avsr_ew_params* p, hipStream_t st) {
   EwArgs a = ew_args(p);
   if (p->dtype == AVSR_BF16) hipLaunchKernelGGL(ew_bwd_kernel<bf16>, grid, dim3(256), 0, st, a);
   else hipLaunchKernelGGL(ew_bwd_kernel<float>, grid, dim3(256), 0, st, a);
-  if (p->db)
-    hipLaunchKernelGGL(colsum_finalize_kernel, colsum_grid(p->N), dim3(COLSUM_THREADS), 0, st, (const float*)p->ws,
-                       (int)grid.y, (int64_t)p->N, p->N, p->db, 0, (float*)nullptr);
+  AVSR_CHECK_LAUNCH();
+  if (p->db) return colsum_launch((const float*)p->ws, (int)grid.y, (int64_t)p->N, p->N, p->db, 0, nullptr, st);
+  return 0;
+}
+
+// ---- deferred column-sum finalisation (one launch per flush) ----------------------------
+constexpr int COLSUM_BATCH = 32;
+struct ColsumBatch {
+  const float* ws[COLSUM_BATCH]; float* out[COLSUM_BATCH]; float* out1[COLSUM_BATCH];
+  int64_t ld[COLSUM_BATCH]; int nb[COLSUM_BATCH], N[COLSUM_BATCH], N1[COLSUM_BATCH];
+};
+__global__ __launch_bounds__(COLSUM_THREADS) void colsum_batch_kernel(ColsumBatch b) {
+  const int d = blockIdx.y;
+  if ((int)blockIdx.x * 32 >= b.N[d]) return;          // block-uniform
+  colsum_block(b.ws[d], b.nb[d], b.ld[d], b.N[d], b.out[d], b.N1[d], b.out1[d], blockIdx.x);
+}
+struct ColsumQueue { bool on = false; std::vector<ColsumBatch> full; ColsumBatch cur; int n = 0; int maxn = 0; };
+ColsumQueue g_colsum;
+
+}  // namespace
+
+int colsum_launch(const float* ws, int nb, int64_t ld, int N, float* out, int N1, float* out1, hipStream_t st) {
+  if (!g_colsum.on) {
+    hipLaunchKernelGGL(colsum_finalize_kernel, colsum_grid(N), dim3(COLSUM_THREADS), 0, st, ws, nb, ld, N, out, N1, out1);
+    AVSR_CHECK_LAUNCH();
+    return 0;
+  }
+  ColsumQueue& q = g_colsum;
+  const int i = q.n % COLSUM_BATCH;
+  q.cur.ws[i] = ws; q.cur.nb[i] = nb; q.cur.ld[i] = ld; q.cur.N[i] = N; q.cur.out[i] = out; q.cur.N1[i] = N1;
+  q.cur.out1[i] = out1;
+  q.n++;
+  q.maxn = q.maxn > N ? q.maxn : N;
+  if (q.n % COLSUM_BATCH == 0) q.full.push_back(q.cur);
+  return 0;
+}
+
+extern "C" int avsr_colsum_defer(int on) {
+  const int was = g_colsum.on ? 1 : 0;
+  g_colsum.on = on != 0;
+  if (!g_colsum.on && g_colsum.n) {   // switched off with passes still queued (an aborted step):
+    g_colsum.full.clear();            // drop them rather than reduce workspaces that may be gone
+    g_colsum.n = 0; g_colsum.maxn = 0;
+  }
+  return was;
+}
+
+extern "C" int avsr_colsum_flush(void* stream) {
+  ColsumQueue& q = g_colsum;
+  hipStream_t st = (hipStream_t)stream;
+  const dim3 gx = colsum_grid(q.maxn > 0 ? q.maxn : 1);
+  for (const ColsumBatch& b : q.full) hipLaunchKernelGGL(colsum_batch_kernel, dim3(gx.x, COLSUM_BATCH), dim3(COLSUM_THREADS), 0, st, b);
+  const int rest = q.n % COLSUM_BATCH;
+  if (rest) hipLaunchKernelGGL(colsum_batch_kernel, dim3(gx.x, rest), dim3(COLSUM_THREADS), 0, st, q.cur);
+  q.full.clear(); q.n = 0; q.maxn = 0;
   AVSR_CHECK_LAUNCH();
   return 0;
 }
 
-}  // namespace
 
 extern "C" int avsr_ew_bwd(const avsr_ew_params* p, void* stream) {
   if (!p) return AVSR_E_ARG;

@@ -198,9 +198,9 @@ int ln_launch(const avsr_layernorm_params* p, bool bwd, hipStream_t st) {
       else if (W == 8) { if (R == 2) LNB(V, 8, 2); else LNB(V, 8, 1); }                          \
       else { if (R == 2) LNB(V, 4, 2); else LNB(V, 4, 1); }                                      \
       if (p->dgamma) {                                                                           \
-        hipLaunchKernelGGL(colsum_finalize_kernel, colsum_grid(2 * p->N), dim3(COLSUM_THREADS), 0, st,\
-                           (const float*)p->ws, blocks, (int64_t)2 * p->N, 2 * p->N, p->dgamma, \
-                           p->N, p->dbeta);                                                      \
+        AVSR_CHECK_LAUNCH();                                                                     \
+        return colsum_launch((const float*)p->ws, blocks, (int64_t)2 * p->N, 2 * p->N, p->dgamma, \
+                             p->N, p->dbeta, st);                                                \
       }                                                                                          \
     } else {                                                                                     \
       hipLaunchKernelGGL((ln_fwd_kernel<T, V>), dim3(blocks), dim3(256), 0, st, a);              \

@@ -36,6 +36,8 @@ GELU, RELU, NONE = L.ACT_GELU, L.ACT_RELU, L.ACT_NONE
 _BN_FUSE = os.environ.get("AVSR_BN_FUSE", "1") == "1"
 # bias gradients reduced in the epilogue of the data-grad GEMM that produces their operand
 _DB_FUSE = os.environ.get("AVSR_DB_FUSE", "1") == "1"
+# parameter-gradient column-sum finalise passes batched per flush (ops.colsum_defer)
+_COLSUM_DEFER = os.environ.get("AVSR_COLSUM_DEFER", "1") == "1"
 
 
 def wgrad_splitk(M, N, K):
@@ -670,6 +672,7 @@ class Engine:
         dx = self._ln_bwd(dout, ctx["x_last"], E + "layer_norm", ctx["mf"], ctx["rf"])
         for i in reversed(range(self.nl)):
             dx = self._enc_layer_bwd(i, ctx["layers"][i], dx, B, T, ctx["klen"])
+            ops.colsum_flush()                      # this layer's bias / LayerNorm gradients
             if self.on_grad_ready is not None:      # layers >= i (and everything after them) final
                 self.on_grad_ready(self._layer_decay_off[i])   # (the reducer also waits for the side stream)
         # pos-conv block: x0 = drop(x + gelu(conv(x) + b))
@@ -903,6 +906,23 @@ class Engine:
         d_att = d_att.reshape(1).to(torch.float32)
         if self.before_backward is not None:
             self.before_backward()
+        # bias / LayerNorm parameter-gradient finalise passes are batched: one launch per
+        # encoder layer (flushed before its on_grad_ready) and one for the rest at the end
+        prev = ops.colsum_defer(_COLSUM_DEFER)
+        try:
+            self._backward(ctx, d_ctc, d_att)
+            ops.colsum_flush()
+        finally:
+            ops.colsum_defer(prev)
+        if self.after_backward is not None:
+            self.after_backward()
+        self.join_side()
+
+    def _backward(self, ctx, d_ctc, d_att):
+        cfg = self.cfg
+        bt = ctx["bt"]
+        B, T = bt["B"], bt["T"]
+        M = B * T
         # attention loss -> decoder
         dl = ctx["dlog"]
         ddl = self._e(dl.shape[0], self.Vp)
@@ -918,9 +938,6 @@ class Engine:
                  seed=ctx["sd_c"])
         self.decoder_bwd(ctx["dctx"], ddl, ctx["enc"], denc, bt)
         self.encoder_bwd(ctx["ectx"], denc)
-        if self.after_backward is not None:
-            self.after_backward()
-        self.join_side()
 
     # ========================================================================= inference
     def encode(self, audios, videos, video_lengths=None, train=False):

@@ -115,7 +115,7 @@ def linear_dgrad(dy, W, *, gate=None, act=L.ACT_NONE, drop_p=0.0, seed=0, out=No
     # the epilogue reduction needs the LDS-DMA bf16 core (avsr_gemm: glds_ok) and 8-column vectors
     fused = (db is not None and dy.dtype == torch.bfloat16 and M >= 128 and K >= 128 and K % 8 == 0
              and out.stride(0) % 8 == 0 and os.environ.get("AVSR_GEMM_NOGLDS", "0") != "1")
-    ws = torch.empty(((M + 63) // 64) * K, device=dy.device) if fused else None   # AVSR_GEMM_COLSUM_WS
+    ws = _colsum_ws(((M + 63) // 64) * K, dy.device) if fused else None   # AVSR_GEMM_COLSUM_WS
     gemm(dy, W, out, M=M, N=K, K=N, a_kmajor=True, b_kmajor=False, lda=dy.stride(0), ldb=W.stride(0),
          ldc=out.stride(0), epi_bwd=True, gate=gate, act=act, drop_p=drop_p, seed=seed, beta=beta,
          db=db if fused else None, db_ws=ws)
@@ -272,7 +272,7 @@ def layernorm_bwd(dy, x, gamma, mean, rstd, dx=None, dres=None, dgamma=None, dbe
     """dx = dres + LN-backward(dy); dgamma/dbeta (fp32) accumulate."""
     rows, N = x.shape
     dx = torch.empty_like(x) if dx is None else dx
-    ws = None if dgamma is None else torch.empty(256 * 2 * N, device=x.device)   # AVSR_LN_WS
+    ws = None if dgamma is None else _colsum_ws(256 * 2 * N, x.device)   # AVSR_LN_WS
     _call("avsr_layernorm_bwd", L.fill(L.LayerNormParams, dtype=dtype_code(x), rows=rows, N=N, eps=0.0,
                                         x=x, ldx=x.stride(0), ldy=N, gamma=gamma, mean=mean, rstd=rstd,
                                         dy=dy, lddy=dy.stride(0), dx=dx, lddx=dx.stride(0),
@@ -490,9 +490,37 @@ def loss_finalize(B, nll, row_loss, row_correct, mtlalpha, out):
 # Elementwise / data movement
 # ---------------------------------------------------------------------------------------
 
+# deferred column-sum finalisation (avsr_colsum_defer / avsr_colsum_flush): the partial
+# workspaces of the queued passes stay referenced here until the flush has been enqueued
+_COLSUM = {"on": False, "keep": []}
+
+
+def _colsum_ws(n, device):
+    ws = torch.empty(n, device=device)
+    if _COLSUM["on"]:
+        _COLSUM["keep"].append(ws)
+    return ws
+
+
+def colsum_defer(on):
+    """queue (True) or run at once (False) the finalise passes of bias / LayerNorm parameter
+    gradients; returns the previous setting"""
+    prev = _COLSUM["on"]
+    L.load().avsr_colsum_defer(int(bool(on)))
+    _COLSUM["on"] = bool(on)
+    return prev
+
+
+def colsum_flush():
+    """one batched launch for every queued finalise pass (current stream)"""
+    if _COLSUM["on"] or _COLSUM["keep"]:
+        L.check(L.load().avsr_colsum_flush(L.stream_ptr()), "avsr_colsum_flush")
+        _COLSUM["keep"].clear()
+
+
 def ew_bwd(dy, *, out=None, gate=None, act=L.ACT_NONE, drop_p=0.0, seed=0, alpha=1.0, db=None):
     rows, N = dy.shape
-    ws = None if db is None else torch.empty(256 * N, device=dy.device)   # AVSR_EW_WS
+    ws = None if db is None else _colsum_ws(256 * N, dy.device)   # AVSR_EW_WS
     _call("avsr_ew_bwd", L.fill(L.EwParams, dtype=dtype_code(dy), rows=rows, N=N, dy=dy, lddy=dy.stride(0), ws=ws,
                                  out=out, ldout=0 if out is None else out.stride(0), gate=gate,
                                  ldgate=0 if gate is None else gate.stride(0), act=act, drop_p=float(drop_p),

@@ -375,6 +375,14 @@ typedef struct {
 #define AVSR_EW_ROWBLOCKS 256
 #define AVSR_EW_WS(N) (AVSR_EW_ROWBLOCKS * (N))
 int avsr_ew_bwd(const avsr_ew_params* p, void* stream);
+/* Deferred finalisation of the column-sum partials (bias gradients of avsr_ew_bwd /
+ * avsr_gemm db, LayerNorm dgamma/dbeta): between avsr_colsum_defer(1) and avsr_colsum_flush the
+ * finalise passes are queued on the host and a flush reduces all of them in one batched launch
+ * on `stream` (stream-ordered after the producers). The caller keeps the partial workspaces
+ * alive until the flush. avsr_colsum_defer returns the previous setting. (A training step's
+ * ~200 separate 5 us finalise launches become one per encoder layer.) */
+int avsr_colsum_defer(int on);
+int avsr_colsum_flush(void* stream);
 int avsr_dropout_fwd(const avsr_ew_params* p, void* stream);
 int avsr_mask_rows(int dtype, int B, int T, int N, void* x, int64_t ldx, const int* len, void* stream);
 
