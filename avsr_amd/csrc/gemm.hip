@@ -135,6 +135,9 @@ using Cfg128w8s3 = gemmg::GCfg<2, 4, 2, 1, 3>;   // 128x128, 8 waves (64x32 each
 using Cfg128w8s4 = gemmg::GCfg<2, 4, 2, 1, 4>;   // 128x128, 8 waves, 4 stages
 using Cfg96 = gemmg::GCfg<3, 2, 1, 2, 2>;        // 96x128, 6 waves (32x64 each), 2 stages, 2 blocks/CU
 using Cfg128x64 = gemmg::GCfg<4, 1, 1, 2, 2>;    // 128x64, 4 waves (32x64 each), 2 stages, 3 blocks/CU
+using Cfg192 = gemmg::GCfg<2, 2, 3, 2, 2>;       // 192x128, 4 waves (96x64 each), 2 stages (80 KiB), 2 blocks/CU
+using Cfg192x256 = gemmg::GCfg<2, 4, 3, 2, 2>;   // 192x256, 8 waves (96x64 each), 2 stages (112 KiB)
+using Cfg192s3 = gemmg::GCfg<2, 2, 3, 2, 3>;     // 192x128, 4 waves, 3 stages (120 KiB)
 
 // tile choice: AVSR_GEMM_TILE=128|256|256x128|128x256 forces one (benchmarks); otherwise the
 // configuration with the fewest block rounds x per-tile work (wave quantisation over 256 CUs)
@@ -143,11 +146,23 @@ int tile_cfg(const avsr_gemm_params* p, int splits) {
   const int forced = !e ? -1 : !strcmp(e, "128") ? 0 : !strcmp(e, "256") ? 1 : !strcmp(e, "256x128") ? 2
                    : !strcmp(e, "128x256") ? 3 : !strcmp(e, "128s3") ? 4 : !strcmp(e, "128s4") ? 5
                    : !strcmp(e, "128w8s3") ? 6 : !strcmp(e, "128w8s4") ? 7 : !strcmp(e, "pp") ? 8
-                   : !strcmp(e, "96") ? 9 : !strcmp(e, "128x64") ? 10 : -1;
+                   : !strcmp(e, "96") ? 9 : !strcmp(e, "128x64") ? 10 : !strcmp(e, "192") ? 11
+                   : !strcmp(e, "192x256") ? 12 : !strcmp(e, "192s3") ? 13 : -1;
   if (forced >= 0) return forced;
-  // The 128x128 two-blocks-per-CU tile is the fastest configuration on every encoder shape
-  // (tools/gemm_table.py, profiles/r02_gemm_table.json: the 256x256 ping-pong core loses
-  // 8-36 % at M = 6000, the 96x128 / 128x64 / 3-stage variants are within +-4 % or slower)
+  // 128x128 at two blocks per CU is the default (tools/gemm_table.py, profiles/r02_gemm_table.*:
+  // the 256x256 ping-pong core loses 8-36 % at M = 6000, the 3-stage / 8-wave variants are
+  // slower). The 192x128 tile (96x64 per wave: 48 MFMAs per 20 fragment reads and 10 DMAs
+  // instead of 32 per 16 and 8) wins where it still runs >= 2 blocks per CU and its rounds
+  // carry no more work than 128x128's: the M = 6000 encoder GEMMs with N >= 3072 (QKV / FFN1
+  // fwd, FFN2 dgrad: -7..-15 %, profiles/r02_gemm_table192.txt). With one block per CU
+  // (N = 1024) it loses 4-18 %. k-major A only (r-contiguous A images need BM % 64 == 0).
+  if (p->a_kmajor) {
+    const long tiles_z = (long)p->batch * splits;
+    const long t128 = (long)((p->M + 127) / 128) * ((p->N + 127) / 128) * tiles_z;
+    const long t192 = (long)((p->M + 191) / 192) * ((p->N + 127) / 128) * tiles_z;
+    const long n128 = (t128 + 255) / 256, n192 = (t192 + 255) / 256;   // blocks on the busiest CU
+    if (n192 >= 2 && 3 * n192 * 50 <= 2 * n128 * 51) return 11;      // 1.5 n192 <= 1.02 n128
+  }
   return 0;
 }
 
@@ -164,6 +179,9 @@ int cfg_bm(int cfg, bool ak) {
     case 8: return gemmpp::BM;
     case 9: return ak ? Cfg96::BM : Cfg128::BM;   // as launch_cfg
     case 10: return Cfg128x64::BM;
+    case 11: return ak ? Cfg192::BM : Cfg128::BM;
+    case 12: return ak ? Cfg192x256::BM : Cfg128::BM;
+    case 13: return ak ? Cfg192s3::BM : Cfg128::BM;
     default: return Cfg128::BM;
   }
 }
@@ -183,6 +201,15 @@ int launch_cfg(int cfg, const DenseArgs& a, int batch, hipStream_t st) {
       if constexpr (AK) return launch_glds<OutT, AK, BK, Cfg96>(a, batch, st);   // r-contiguous A needs BM % 64 == 0
       else return launch_glds<OutT, AK, BK, Cfg128>(a, batch, st);
     case 10: return launch_glds<OutT, AK, BK, Cfg128x64>(a, batch, st);
+    case 11:   // BM = 192: r-contiguous A needs BM % 64 == 0 (weight-grads stay on 128x128)
+      if constexpr (AK) return launch_glds<OutT, AK, BK, Cfg192>(a, batch, st);
+      else return launch_glds<OutT, AK, BK, Cfg128>(a, batch, st);
+    case 12:
+      if constexpr (AK) return launch_glds<OutT, AK, BK, Cfg192x256>(a, batch, st);
+      else return launch_glds<OutT, AK, BK, Cfg128>(a, batch, st);
+    case 13:
+      if constexpr (AK) return launch_glds<OutT, AK, BK, Cfg192s3>(a, batch, st);
+      else return launch_glds<OutT, AK, BK, Cfg128>(a, batch, st);
     default: return launch_glds<OutT, AK, BK, Cfg128>(a, batch, st);
   }
 }

@@ -93,7 +93,7 @@ def _ref_gemm(A, B, a_kmajor, b_kmajor):
     return Af @ Bf.t()
 
 
-@pytest.fixture(params=["auto", "128", "256", "256x128", "128x256", "128s3", "128w8s3", "pp"])
+@pytest.fixture(params=["auto", "128", "256", "256x128", "128x256", "128s3", "128w8s3", "pp", "192", "192x256"])
 def gemm_tile(request, monkeypatch):
     """forces each LDS-DMA tile configuration (AVSR_GEMM_TILE, read per launch by avsr_gemm)"""
     if request.param != "auto":
@@ -165,3 +165,37 @@ def test_dgrad_fused_bias_grad(dev, gemm_tile, M, N, K):
     ref = out.double().sum(0)
     err = ((db.double() - db0.double()) - ref).abs().max().item() / ref.abs().max().item()
     assert err < 2e-3, err
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tile", ["192", "192x256", "256x128", "pp"])
+def test_tile_configs_bit_identical(dev, monkeypatch, tile):
+    """Every tile configuration accumulates each output over the same K order (64-deep K-tiles,
+    the same 16x16x32 MFMA sequence), so the fused-epilogue results must equal the 128x128
+    tile's bit for bit: FFN1-style forward (bias, GELU, pre-activation store, residual,
+    dropout) and FFN2-style data-grad (GELU' gate, dropout, fused bias gradient); ragged M/N/K."""
+    M, N, K = 1000, 776, 328
+    g = torch.Generator().manual_seed(17)
+    x = torch.randn(M, K, generator=g).to(dev, torch.bfloat16)
+    W = (torch.randn(N, K, generator=g) * K ** -0.5).to(dev, torch.bfloat16)
+    b = torch.randn(N, generator=g).to(dev)
+    r = torch.randn(M, N, generator=g).to(dev, torch.bfloat16)
+    dy = torch.randn(M, N, generator=g).to(dev, torch.bfloat16)
+    hg = torch.randn(M, K, generator=g).to(dev, torch.bfloat16)
+
+    def run():
+        h = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+        y = ops.linear_fwd(x, W, b, act=L.ACT_GELU, preact=h, res=r, drop_p=0.1, seed=7)
+        db = torch.zeros(K, device=dev)
+        dx = ops.linear_dgrad(dy, W, gate=hg, act=L.ACT_GELU, drop_p=0.1, seed=9, db=db)
+        torch.cuda.synchronize()
+        return y, h, dx, db
+
+    monkeypatch.setenv("AVSR_GEMM_TILE", "128")
+    ref = run()
+    monkeypatch.setenv("AVSR_GEMM_TILE", tile)
+    got = run()
+    for a_, b_, name in zip(got[:3], ref[:3], ("y", "preact", "dx")):
+        assert torch.equal(a_, b_), (tile, name, (a_.float() - b_.float()).abs().max().item())
+    # the bias gradient sums per-row-tile partials: a different row-tile height re-associates
+    assert _rel(got[3], ref[3]) < 1e-5
