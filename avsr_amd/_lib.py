@@ -10,7 +10,7 @@ import os
 import torch  # noqa: F401  (must precede the library load: shared HIP runtime)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libavsr_hip.so")
+LIB_PATH = os.environ.get("AVSR_LIB_PATH_AB") or os.path.join(_HERE, "libavsr_hip.so")   # override: A/B tools only
 
 AVSR_F32, AVSR_BF16 = 0, 1
 ACT_NONE, ACT_GELU, ACT_RELU = 0, 1, 2

@@ -817,6 +817,17 @@ AVSR_DEV void drop_tile(f32x16& x, uint32_t tG, const AttnDrop& d, int hh) {
     x[r + 1] *= keep16(h, true, d.thr, d.scale);
   }
 }
+// same mask, selection form: dropped elements -> 0, kept ones unscaled (the 1/(1-p) factor is
+// applied once to the tile's output sums by the caller)
+AVSR_DEV void drop_tile_sel(f32x16& x, uint32_t tG, const AttnDrop& d, int hh) {
+#pragma unroll
+  for (int r = 0; r < 16; r += 2) {
+    const uint32_t kp = (uint32_t)(((r & 3) >> 1) + 4 * (r >> 2) + 2 * hh);     // (qrow(r, hh) >> 1)
+    const uint32_t h = hashG(tG + kp * GOLD, d.pre);
+    x[r] = (h & 0xFFFFu) >= d.thr ? x[r] : 0.f;
+    x[r + 1] = (h >> 16) >= d.thr ? x[r + 1] : 0.f;
+  }
+}
 
 __global__ __launch_bounds__(768) void attn_fwd_kernel(AttnArgs a) {
   extern __shared__ __attribute__((aligned(16))) bf16 sm[];
@@ -861,8 +872,11 @@ __global__ __launch_bounds__(768) void attn_fwd_kernel(AttnArgs a) {
   if (!pipe) __syncthreads();
   f32x16 o0, o1;
   zacc(o0); zacc(o1);
-  float m = -INFINITY, lsum = 0.f;
-  float mb = 0.f;                               // running row max, scaled by log2(e) * scale
+  float lsum = 0.f;
+  // reference max (log2 units, scale * log2(e) applied): -inf until the row sees a key; it only
+  // moves when a tile's max exceeds it by more than 8, so P = exp2(s - mb) <= 256 and the
+  // rescale of O / the row sum (exact: softmax does not depend on the reference) is rare
+  float mb = -INFINITY;
   int t = 0;                                    // next key tile
 #pragma unroll
   for (int it = 0; it < LD_IT; ++it) {
@@ -904,22 +918,24 @@ __global__ __launch_bounds__(768) void attn_fwd_kernel(AttnArgs a) {
       float mt = st[0];
 #pragma unroll
       for (int r = 1; r < 16; ++r) mt = fmaxf(mt, st[r]);
-      mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
-      // branch-free (MFMAs below run for the whole wave): a query with no visible key so far
-      // keeps max -inf, mb 0, and contributes exp2(-inf) = 0
-      const float mn = fmaxf(m, mt);
-      const float mbn = mn == -INFINITY ? 0.f : mn * sl2;
-      const float alpha = m == -INFINITY ? 0.f : fexp2(mb - mbn);
-      m = mn; mb = mbn;
-      lsum *= alpha;
+      mt = fmaxf(mt, __shfl_xor(mt, 32, 64)) * sl2;
+      // a query with no visible key so far keeps mb = -inf (exponent reference 0) and
+      // contributes exp2(-inf) = 0; the MFMAs below run for the whole wave
+      const bool grow = mt > mb + 8.f;
+      if (__any(grow)) {                            // wave-uniform: rare after the first tile
+        const float alpha = grow ? (mb == -INFINITY ? 0.f : fexp2(mb - mt)) : 1.f;
+        mb = grow ? mt : mb;
+        lsum *= alpha;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) { o0[r] *= alpha; o1[r] *= alpha; }
+        for (int r = 0; r < 16; ++r) { o0[r] *= alpha; o1[r] *= alpha; }
+      }
+      const float mbu = mb == -INFINITY ? 0.f : mb;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        st[r] = fexp2(fmaf(st[r], sl2, -mb));      // masked keys: exp2(-inf) = 0
+        st[r] = fexp2(fmaf(st[r], sl2, -mbu));     // masked keys: exp2(-inf) = 0
         lsum += st[r];
       }
-      if (a.drop_p > 0.f) drop_tile(st, rowG + (uint32_t)(t * 16) * GOLD, drop, hh);
+      if (a.drop_p > 0.f) drop_tile_sel(st, rowG + (uint32_t)(t * 16) * GOLD, drop, hh);
       const bf16x8 pa = accb(st, 0), pb = accb(st, 1);
       o0 = mfma32(rdT(Vs, t * 32, 0, l), pa, o0);
       o0 = mfma32(rdT(Vs, t * 32 + 16, 0, l), pb, o0);
@@ -935,7 +951,7 @@ __global__ __launch_bounds__(768) void attn_fwd_kernel(AttnArgs a) {
   __syncthreads();                         // K/V images no longer read: reuse LDS as store slabs
   stamp(2);
   if (q0 < a.Lq) {
-    const float inv = lsum > 0.f ? 1.f / lsum : 0.f;
+    const float inv = lsum > 0.f ? (a.drop_p > 0.f ? drop.scale : 1.f) / lsum : 0.f;
     bf16* O = (bf16*)a.o + ((int64_t)b * a.Lq + q0) * a.ldo + h * DH;
     store_t<bf16>(o0, o1, inv, (float*)sm + w * 32 * 65, O, a.ldo, a.Lq - q0);
   }
@@ -1011,6 +1027,7 @@ __global__ __launch_bounds__(NT) void attn_bwd_dkdv_kernel(AttnArgs a) {
   const uint32_t nG = drop.npair * GOLD;
   const uint32_t keyG = ((uint32_t)bh * (uint32_t)a.Lq * drop.npair + (uint32_t)(min(key, a.Lk - 1) >> 1)) * GOLD;
   const bool odd = c & 1;
+  const float dscale = a.drop_p > 0.f ? drop.scale : 1.f;
   __syncthreads();
   f32x16 dv0, dv1, dk0, dk1;
   zacc(dv0); zacc(dv1); zacc(dk0); zacc(dk1);
@@ -1035,14 +1052,17 @@ __global__ __launch_bounds__(NT) void attn_bwd_dkdv_kernel(AttnArgs a) {
         const f32x4 ds = *(const f32x4*)&dls[qt0 + 8 * i + 4 * hh];
         // dropout: this lane pair (keys 2j, 2j+1) splits the 4 queries' hashes: even lanes
         // hash queries 0, 1, odd lanes 2, 3, then the two swap (static registers only)
-        float kp[4] = {1.f, 1.f, 1.f, 1.f};
+        // keep bits; P' = dropout(P) is stored unscaled (the 1/(1-p) factor goes on dV at the
+        // store), dP' = dropout(dP) scaled; the softmax scale of dS goes on dK at the store
+        bool kb[4] = {true, true, true, true};
         if (a.drop_p > 0.f) {
 #pragma unroll
           for (int u = 0; u < 2; ++u) {
             const uint32_t mine = hashG(tG + (uint32_t)(8 * i + (odd ? 2 : 0) + u) * nG, drop.pre);
             const uint32_t other = __shfl_xor(mine, 1, 64);
-            kp[u] = keep16(odd ? other : mine, odd, drop.thr, drop.scale);
-            kp[u + 2] = keep16(odd ? mine : other, odd, drop.thr, drop.scale);
+            const uint32_t h0 = odd ? other : mine, h1 = odd ? mine : other;
+            kb[u] = (odd ? (h0 >> 16) : (h0 & 0xFFFFu)) >= drop.thr;
+            kb[u + 2] = (odd ? (h1 >> 16) : (h1 & 0xFFFFu)) >= drop.thr;
           }
         }
 #pragma unroll
@@ -1050,8 +1070,8 @@ __global__ __launch_bounds__(NT) void attn_bwd_dkdv_kernel(AttnArgs a) {
           const int r = 4 * i + e, ql = qt0 + 8 * i + 4 * hh + e;
           const bool ok = full || (kok & (ql < a.Lq) & (!a.causal | (key <= ql)));
           const float p = ok ? fexp2(fmaf(sc[r], sl2, -ls[e])) : 0.f;
-          sc[r] = p * kp[e];                                    // P' = dropout(P)
-          dp[r] = p * (dp[r] * kp[e] - ds[e]) * a.scale;        // dS (scaled)
+          sc[r] = kb[e] ? p : 0.f;
+          dp[r] = p * ((kb[e] ? dp[r] * dscale : 0.f) - ds[e]);
         }
       }
       const bf16x8 pa = accb(sc, 0), pb = accb(sc, 1), sa = accb(dp, 0), sb = accb(dp, 1);
@@ -1069,9 +1089,9 @@ __global__ __launch_bounds__(NT) void attn_bwd_dkdv_kernel(AttnArgs a) {
   if (kb0 < a.Lk) {
     float* scr = (float*)sm + w * 32 * 65;
     bf16* DK = (bf16*)a.dk + ((int64_t)b * a.Lk + kb0) * a.lddk + h * DH;
-    store_t<bf16>(dk0, dk1, 1.f, scr, DK, a.lddk, a.Lk - kb0);
+    store_t<bf16>(dk0, dk1, a.scale, scr, DK, a.lddk, a.Lk - kb0);
     bf16* DV = (bf16*)a.dv + ((int64_t)b * a.Lk + kb0) * a.lddv + h * DH;
-    store_t<bf16>(dv0, dv1, 1.f, scr, DV, a.lddv, a.Lk - kb0);
+    store_t<bf16>(dv0, dv1, dscale, scr, DV, a.lddv, a.Lk - kb0);
   }
 }
 
@@ -1105,6 +1125,7 @@ __global__ __launch_bounds__(768) void attn_bwd_dq_kernel(AttnArgs a, OutT* dq, 
   const float sl2 = a.scale * LOG2E;
   const AttnDrop drop(a.drop_p, a.seed, a.B, a.H, a.Lq, a.Lk);
   const uint32_t rowG = ((uint32_t)bh * (uint32_t)a.Lq + (uint32_t)min(qi, a.Lq - 1)) * drop.npair * GOLD;
+  const float dscale = drop.scale;
   __syncthreads();
   f32x16 dq0, dq1;
   zacc(dq0); zacc(dq1);
@@ -1117,15 +1138,18 @@ __global__ __launch_bounds__(768) void attn_bwd_dq_kernel(AttnArgs a, OutT* dq, 
         st = mfma32(rd8(Ks, t * 32 + c, s * 16 + 8 * hh), qf[s], st);
         dpt = mfma32(rd8(Vs, t * 32 + c, s * 16 + 8 * hh), of[s], dpt);
       }
-      f32x16 keep;
+      // dP' = dropout(dP): kept elements scaled by 1/(1-p) (dscale), dropped ones 0; the
+      // softmax scale of dS is applied to dQ once, at the store
+      if (a.drop_p > 0.f) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) keep[r] = 1.f;
-      if (a.drop_p > 0.f) drop_tile(keep, rowG + (uint32_t)(t * 16) * GOLD, drop, hh);
+        for (int r = 0; r < 16; ++r) dpt[r] *= dscale;
+        drop_tile_sel(dpt, rowG + (uint32_t)(t * 16) * GOLD, drop, hh);
+      }
       if (t * 32 + 32 <= klen && (!a.causal || t * 32 + 31 <= q0)) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const float p = fexp2(fmaf(st[r], sl2, -lq));
-          dpt[r] = p * (dpt[r] * keep[r] - dl) * a.scale;
+          dpt[r] = p * (dpt[r] - dl);
         }
       } else {
 #pragma unroll
@@ -1133,7 +1157,7 @@ __global__ __launch_bounds__(768) void attn_bwd_dq_kernel(AttnArgs a, OutT* dq, 
           const int k = t * 32 + qrow(r, hh);
           const bool ok = (k < klen) & (!a.causal | (k <= qi));
           const float p = ok ? fexp2(fmaf(st[r], sl2, -lq)) : 0.f;
-          dpt[r] = p * (dpt[r] * keep[r] - dl) * a.scale;
+          dpt[r] = p * (dpt[r] - dl);
         }
       }
       const bf16x8 sa = accb(dpt, 0), sb = accb(dpt, 1);
@@ -1146,7 +1170,7 @@ __global__ __launch_bounds__(768) void attn_bwd_dq_kernel(AttnArgs a, OutT* dq, 
   __syncthreads();
   if (q0 < a.Lq) {
     OutT* DQ = dq + ((int64_t)b * a.Lq + q0) * lddq + h * DH;
-    store_t<OutT>(dq0, dq1, 1.f, (float*)sm + w * 32 * 65, DQ, lddq, a.Lq - q0);
+    store_t<OutT>(dq0, dq1, a.scale, (float*)sm + w * 32 * 65, DQ, lddq, a.Lq - q0);
   }
 }
 
