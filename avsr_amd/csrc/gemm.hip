@@ -12,8 +12,6 @@ namespace {
 
 struct DenseArgs {
   int M, N, K, splits, kchunk;
-  int dbg;                     // timing experiments only (AVSR_GEMM_DBG): 1 = no epilogue, 2 = no main loop,
-                               // 3 = epilogue without its global stores
   uint32_t a_bytes, b_bytes;   // buffer extents of one batch's A / B (buffer-DMA loaders); 0 = pointer loaders
   int64_t sSplit;      // slab mode: C offset between K splits (0: atomics / no split)
   const void* A; int64_t lda, sA;
@@ -56,7 +54,7 @@ __global__ __launch_bounds__(CF::NTH, CF::MINB) void dense_glds_kernel(DenseArgs
   const int kbeg = sp * a.kchunk, kend = min(a.K, kbeg + a.kchunk);
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   f32x4 acc[CF::TM][CF::TN];
-  const int nk = a.dbg == 2 ? 0 : (kend - kbeg + gemmg::GBK - 1) / gemmg::GBK;
+  const int nk = (kend - kbeg + gemmg::GBK - 1) / gemmg::GBK;
   if (a.a_bytes) {   // buffer-DMA loaders (operands < 2 GiB)
     using LA = typename std::conditional<AK, gemmg::BDenseK<CF::BM, CF::NW>, gemmg::BDenseR<CF::BM, CF::NW>>::type;
     using LB = typename std::conditional<BK, gemmg::BDenseK<CF::BN, CF::NW>, gemmg::BDenseR<CF::BN, CF::NW>>::type;
@@ -76,16 +74,6 @@ __global__ __launch_bounds__(CF::NTH, CF::MINB) void dense_glds_kernel(DenseArgs
   if (e.preact) e.preact = (bf16*)e.preact + (int64_t)bz * a.sC;
   if (e.gate) e.gate = (const bf16*)e.gate + (int64_t)bz * a.sC;
   e.drop_base = (uint64_t)bz * (uint64_t)a.M * (uint64_t)a.N;
-  if (a.dbg == 1) {   // timing experiment: keep the main loop live, skip the epilogue
-    float t = 0.f;
-#pragma unroll
-    for (int i = 0; i < CF::TM; ++i)
-#pragma unroll
-      for (int j = 0; j < CF::TN; ++j) t += acc[i][j][0];
-    if (t == 1234.5f) ((float*)e.C)[threadIdx.x] = t;
-    return;
-  }
-  if (a.dbg == 3) { gemmg::epilogue_g<bf16, OutT, CF, true>(e, m0, n0, acc, smem); return; }
   gemmg::epilogue_g<bf16, OutT, CF>(e, m0, n0, acc, smem);
 }
 
@@ -113,141 +101,6 @@ __global__ __launch_bounds__(gemmpp::NTH, 1) void dense_pp_kernel(DenseArgs a, i
   if (e.gate) e.gate = (const bf16*)e.gate + (int64_t)bz * a.sC;
   e.drop_base = (uint64_t)bz * (uint64_t)a.M * (uint64_t)a.N;
   gemmg::epilogue_g<bf16, OutT, gemmpp::CF>(e, m0, n0, acc, smem);
-}
-
-// ---------------------------------------------------------------- stream-K (persistent)
-// One block per CU slot walks a contiguous range of (tile, K-tile) iterations, so tile
-// boundaries -- and with them the epilogues' HBM stores -- fall at different times on the
-// blocks sharing a CU, overlapping one block's stores with the other's MFMAs (a grid of whole
-// tiles runs its blocks in lockstep: every epilogue at once, MFMA idle; and 1504 tiles over
-// 512 slots leave the last round 94 % full). Tiles are first divided among the 8 XCDs (whole
-// tiles, contiguous), then the XCD's iterations among its blocks: a block's predecessor on a
-// shared tile is the previous block of the same XCD (hardware id - 8), dispatched before it,
-// so the wait below cannot deadlock. The block that runs a tile's last K-tile owns it: it adds
-// the fp32 partial(s) of the predecessor(s) that ran the tile's first K-tiles, then runs the
-// ordinary epilogue. Partial hand-off: plain stores, vmcnt(0), barrier, agent-scope release,
-// flag = launch epoch; the owner polls the flag (relaxed, agent scope), acquires once, reads.
-constexpr int SK_REGIONS = 4, SK_MAXG = 2048;
-__device__ unsigned g_sk_flag[SK_REGIONS * SK_MAXG];
-
-template <typename OutT, bool AK, bool BK, class CF>
-__global__ __launch_bounds__(CF::NTH, CF::MINB) void dense_sk_kernel(DenseArgs a, int tiles_m, int tiles_n, int nkt,
-                                                                      float* ws, unsigned epoch) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int G = gridDim.x, h = blockIdx.x;
-  const int xcd = h & 7, nb = G >> 3, q = h >> 3;           // G % 8 == 0 (host)
-  const int tiles = tiles_m * tiles_n;
-  const int t_lo = (int)((int64_t)tiles * xcd / 8), t_hi = (int)((int64_t)tiles * (xcd + 1) / 8);
-  const int64_t xit = (int64_t)(t_hi - t_lo) * nkt;           // iterations of this XCD
-  auto range_start = [&](int qq) { return (int64_t)t_lo * nkt + xit * qq / nb; };
-  const int64_t it0 = range_start(q), it1 = range_start(q + 1);
-  unsigned* flag = g_sk_flag + (epoch % SK_REGIONS) * SK_MAXG;
-  float* myws = ws + (int64_t)h * (CF::TM * CF::TN * 4) * CF::NTH;   // slot stride: see launch_sk
-  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  f32x4 acc[CF::TM][CF::TN];
-  // one segment = K-tiles [k_lo, k_hi) of one tile. Order: the range's trailing partial tile
-  // first (published early for the next block, which owns that tile), then the whole tiles,
-  // then the leading segment, which this block owns and completes with the predecessor's
-  // partial (published at the predecessor's start)
-  auto segment = [&](int tile, int k_lo, int k_hi) {
-    int tm, tn, z;
-    gemmg::tile_of(tile, tiles_m, tiles_n, tm, tn, z);
-    const int m0 = tm * CF::BM, n0 = tn * CF::BN;
-    {
-      using LA = typename std::conditional<AK, gemmg::BDenseK<CF::BM, CF::NW>, gemmg::BDenseR<CF::BM, CF::NW>>::type;
-      using LB = typename std::conditional<BK, gemmg::BDenseK<CF::BN, CF::NW>, gemmg::BDenseR<CF::BN, CF::NW>>::type;
-      LA la; la.init((const bf16*)a.A, a.a_bytes, a.lda, m0, a.M, a.K, wave, lane);
-      LB lb; lb.init((const bf16*)a.B, a.b_bytes, a.ldb, n0, a.N, a.K, wave, lane);
-      gemmg::mainloop_glds<CF>(la, lb, k_lo * gemmg::GBK, k_hi - k_lo, acc, smem);   // ends in a barrier
-    }
-    if (k_hi < nkt) {          // not the owner: publish the partial
-#pragma unroll
-      for (int i = 0; i < CF::TM; ++i)
-#pragma unroll
-        for (int j = 0; j < CF::TN; ++j) *(f32x4*)(myws + ((int64_t)(i * CF::TN + j) * CF::NTH + tid) * 4) = acc[i][j];
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (tid == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_store(flag + h, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      return;
-    }
-    if (k_lo > 0) {
-      // predecessors (same XCD, hardware ids h-8, h-16, ...) hold the tile's first K-tiles
-      const int64_t tstart = (int64_t)tile * nkt;
-      for (int pq = q - 1; pq >= 0; --pq) {
-        const int ph = pq * 8 + xcd;
-        if (tid == 0) {
-          while (__hip_atomic_load(flag + ph, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch)
-            __builtin_amdgcn_s_sleep(1);
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        __syncthreads();
-        const float* pw = ws + (int64_t)ph * (CF::TM * CF::TN * 4) * CF::NTH;
-#pragma unroll
-        for (int i = 0; i < CF::TM; ++i)
-#pragma unroll
-          for (int j = 0; j < CF::TN; ++j) {
-            const f32x4 v = *(const f32x4*)(pw + ((int64_t)(i * CF::TN + j) * CF::NTH + tid) * 4);
-            acc[i][j] += v;
-          }
-        if (range_start(pq) <= tstart) break;
-      }
-    }
-    Epi e = a.e;
-    e.drop_base = 0;
-    gemmg::epilogue_g<bf16, OutT, CF>(e, m0, n0, acc, smem);
-    __syncthreads();   // the epilogue's LDS staging is read before the next segment's DMA lands
-  };
-  const int t0 = (int)(it0 / nkt), tl = (int)((it1 - 1) / nkt);
-  const int k0 = (int)(it0 - (int64_t)t0 * nkt), kl = (int)(it1 - (int64_t)tl * nkt);   // kl in [1, nkt]
-  if (t0 == tl) {
-    segment(t0, k0, kl);
-  } else {
-    if (kl < nkt) segment(tl, 0, kl);                       // trailing partial tile, published first
-    for (int t = t0 + 1; t < (kl < nkt ? tl : tl + 1); ++t) segment(t, 0, nkt);
-    segment(t0, k0, nkt);                                   // leading segment (owned; may wait)
-  }
-}
-
-static float* g_sk_ws = nullptr;       // [SK_REGIONS][SK_MAXG] partial tiles, allocated once
-static unsigned g_sk_epoch = 0;
-static int g_cus = 0;
-
-template <typename OutT, bool AK, bool BK, class CF>
-int launch_sk(const DenseArgs& a, hipStream_t st) {
-  constexpr int64_t SK_PER = 24576;                                  // floats of the largest partial (192x128)
-  constexpr int64_t per = (int64_t)CF::TM * CF::TN * 4 * CF::NTH;    // floats of one partial tile
-  static_assert(per <= SK_PER, "partial tile exceeds its workspace slot");
-  constexpr int64_t region = SK_PER * (SK_MAXG / SK_REGIONS);        // G <= SK_MAXG / SK_REGIONS
-  if (!g_cus) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&g_cus, hipDeviceAttributeMultiprocessorCount, dev);
-    if (g_cus <= 0) g_cus = 256;
-  }
-  if (!g_sk_ws) {
-    const hipError_t rc = hipMalloc((void**)&g_sk_ws, sizeof(float) * region * SK_REGIONS);
-    if (rc != hipSuccess) { g_sk_ws = nullptr; return (int)rc; }
-  }
-  const int tm = (a.M + CF::BM - 1) / CF::BM, tn = (a.N + CF::BN - 1) / CF::BN;
-  const int nkt = (a.K + gemmg::GBK - 1) / gemmg::GBK;
-  const int64_t total = (int64_t)tm * tn * nkt;
-  int G = g_cus * CF::MINB;
-  if (G > SK_MAXG / SK_REGIONS) G = SK_MAXG / SK_REGIONS;
-  G &= ~7;
-  if ((int64_t)tm * tn < 8 || total < G) return AVSR_E_SHAPE;   // every block needs >= 1 iteration
-  // every XCD's share of iterations must cover its blocks
-  if ((int64_t)(tm * tn / 8) * nkt < G / 8) return AVSR_E_SHAPE;
-  const unsigned epoch = ++g_sk_epoch;
-  float* ws = g_sk_ws + (int64_t)(epoch % SK_REGIONS) * region;
-  hipLaunchKernelGGL((dense_sk_kernel<OutT, AK, BK, CF>), dim3(G), dim3(CF::NTH), CF::LDS_BYTES, st, a, tm, tn, nkt, ws,
-                     epoch);
-  AVSR_CHECK_LAUNCH();
-  return 0;
 }
 
 template <typename OutT, bool AK, bool BK>
@@ -290,7 +143,7 @@ using Cfg192s3 = gemmg::GCfg<2, 2, 3, 2, 3>;     // 192x128, 4 waves, 3 stages (
 // configuration with the fewest block rounds x per-tile work (wave quantisation over 256 CUs)
 int tile_cfg(const avsr_gemm_params* p, int splits) {
   const char* e = getenv("AVSR_GEMM_TILE");
-  const int forced = !e ? -1 : !strcmp(e, "128") || !strcmp(e, "128sk") ? 0 : !strcmp(e, "192sk") ? 11 : !strcmp(e, "256") ? 1 : !strcmp(e, "256x128") ? 2
+  const int forced = !e ? -1 : !strcmp(e, "128") ? 0 : !strcmp(e, "256") ? 1 : !strcmp(e, "256x128") ? 2
                    : !strcmp(e, "128x256") ? 3 : !strcmp(e, "128s3") ? 4 : !strcmp(e, "128s4") ? 5
                    : !strcmp(e, "128w8s3") ? 6 : !strcmp(e, "128w8s4") ? 7 : !strcmp(e, "pp") ? 8
                    : !strcmp(e, "96") ? 9 : !strcmp(e, "128x64") ? 10 : !strcmp(e, "192") ? 11
@@ -361,39 +214,9 @@ int launch_cfg(int cfg, const DenseArgs& a, int batch, hipStream_t st) {
   }
 }
 
-// stream-K for one-batch, unsplit GEMMs on the buffer-DMA loaders (AVSR_GEMM_SK=0 disables;
-// AVSR_GEMM_TILE=128sk|192sk forces it with that tile)
-template <typename OutT, bool AK, bool BK>
-int launch_sk_cfg(int cfg, const DenseArgs& a, hipStream_t st) {
-  if constexpr (AK) {
-    if (cfg == 11) return launch_sk<OutT, AK, BK, Cfg192>(a, st);
-  }
-  return launch_sk<OutT, AK, BK, Cfg128>(a, st);
-}
-
-bool sk_wanted(const avsr_gemm_params* p, const DenseArgs& a, int& cfg) {
-  const char* t = getenv("AVSR_GEMM_TILE");
-  if (t && !strcmp(t, "128sk")) { cfg = 0; return true; }
-  if (t && !strcmp(t, "192sk")) { cfg = p->a_kmajor ? 11 : 0; return true; }
-  if (t) return false;
-  const char* e = getenv("AVSR_GEMM_SK");
-  if (!e || e[0] != '1') return false;
-  if (p->batch != 1 || a.splits != 1 || !a.a_bytes) return false;
-  return cfg == 0 || cfg == 11;
-}
-
 template <typename OutT>
 int glds_by_layout(const avsr_gemm_params* p, const DenseArgs& a, hipStream_t st) {
-  int cfg = tile_cfg(p, a.splits);
-  if (p->batch == 1 && a.splits == 1 && a.a_bytes && sk_wanted(p, a, cfg)) {
-    int rc;
-    if (p->a_kmajor && p->b_kmajor) rc = launch_sk_cfg<OutT, true, true>(cfg, a, st);
-    else if (p->a_kmajor) rc = launch_sk_cfg<OutT, true, false>(cfg, a, st);
-    else if (p->b_kmajor) rc = launch_sk_cfg<OutT, false, true>(cfg, a, st);
-    else rc = launch_sk_cfg<OutT, false, false>(cfg, a, st);
-    if (rc != AVSR_E_SHAPE) return rc;
-    cfg = tile_cfg(p, a.splits) == 11 && p->a_kmajor ? 11 : 0;   // too small for stream-K
-  }
+  const int cfg = tile_cfg(p, a.splits);
   if (p->a_kmajor && p->b_kmajor) return launch_cfg<OutT, true, true>(cfg, a, p->batch, st);
   if (p->a_kmajor) return launch_cfg<OutT, true, false>(cfg, a, p->batch, st);
   if (p->b_kmajor) return launch_cfg<OutT, false, true>(cfg, a, p->batch, st);
@@ -463,7 +286,6 @@ extern "C" int avsr_gemm(const avsr_gemm_params* p, void* stream) {
     return AVSR_E_ARG;
   DenseArgs a;
   a.M = p->M; a.N = p->N; a.K = p->K;
-  { static const char* d = getenv("AVSR_GEMM_DBG"); a.dbg = d ? atoi(d) : 0; }
   a.splits = splits;
   const bool glds = glds_ok(p) && !getenv_flag_noglds();
   const int kq = glds ? gemmg::GBK : BKE;

@@ -291,7 +291,7 @@ AVSR_DEV void mainloop_glds(const LA& la, const LB& lb, int kbeg, int nk, f32x4 
 // through LDS and writing it row-major, 8 consecutive columns per thread (one 16-byte store
 // per bf16 output row segment; 16-byte preact/residual/gate reads). Accumulator tile (ti, tj) register r sits at wave-local row
 // 16ti + 4(lane>>4) + r, column 16tj + (lane&15).
-template <typename T, typename OutT, class CF, bool NOSTORE = false>   // NOSTORE: timing experiments only
+template <typename T, typename OutT, class CF>
 AVSR_DEV void epilogue_g(const Epi& e, int m0, int n0, f32x4 (&acc)[CF::TM][CF::TN], char* smem) {
   constexpr int BN = CF::BN, LDR = BN + 4, SR = CF::WM * 32;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -377,9 +377,7 @@ AVSR_DEV void epilogue_g(const Epi& e, int m0, int n0, f32x4 (&acc)[CF::TM][CF::
         const f32x4 v0 = *(const f32x4*)(st + lr * LDR + lc), v1 = *(const f32x4*)(st + lr * LDR + lc + 4);
         float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
         const int orow = epi_row(e, row);
-        if constexpr (NOSTORE) {
-          if (v[0] + v[7] == 1234.5f) ((float*)e.C)[tid] = v[1];
-        } else if (vec && col + 8 <= e.N) {
+        if (vec && col + 8 <= e.N) {
           epi_vec8<T, OutT>(e, orow, col, v);
           if (e.colsum) {
 #pragma unroll

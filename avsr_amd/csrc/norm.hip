@@ -628,6 +628,75 @@ __global__ __launch_bounds__(256) void stem_bwd_apply_kernel(avsr_stem_pool_para
   }
 }
 
+// Same result for even H, W (Ho = H/2, Wo = W/2), one thread per 2x2 pixel block (2oh+dy, 2ow+dx)
+// and channel group: the block's pixels lie in windows (oh, ow), (oh, ow+1) [dx = 1],
+// (oh+1, ow) [dy = 1], (oh+1, ow+1) [both], so the four windows' dz / argmax are loaded once
+// for four outputs (2.25 window gathers per pixel otherwise), with no per-pixel divisions and
+// every load of the block issued together. Windows are added in the per-pixel kernel's order
+// (bit-identical).
+template <typename T>
+__global__ __launch_bounds__(256) void stem_bwd_apply2_kernel(avsr_stem_pool_params p) {
+  constexpr int VE = VecW<T>::VE;
+  const int cpv = p.C / VE;
+  const int64_t nv = (int64_t)p.nimg * p.Ho * p.Wo * cpv, stride = (int64_t)gridDim.x * 256;
+  const int64_t t0 = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int cv = (int)(t0 % cpv), c0 = cv * VE;
+  const float invM = 1.f / ((float)p.nimg * p.H * p.W);
+  float ka[VE], kb[VE], kc[VE], km[VE];
+#pragma unroll
+  for (int j = 0; j < VE; ++j) {
+    const int c = c0 + j;
+    const float s0 = p.sums[c * 3 + 0] * invM, s1 = p.sums[c * 3 + 1] * invM;
+    ka[j] = p.scale[c]; kb[j] = -p.scale[c] * s1 * p.invstd[c]; kc[j] = -p.scale[c] * s0; km[j] = p.mean[c];
+  }
+  for (int64_t v = t0; v < nv; v += stride) {
+    const int64_t blk = v / cpv;                       // (n, oh, ow)
+    const int ow = (int)(blk % p.Wo), oh = (int)((blk / p.Wo) % p.Ho);
+    const int64_t n = blk / ((int64_t)p.Wo * p.Ho);
+    // windows w = (oh + a, ow + b), a, b in {0, 1}; out-of-range windows contribute nothing
+    float g[4][VE];
+    uint8_t am[4][VE];
+    bool wok[4];
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const int wa = w >> 1, wb = w & 1;
+      wok[w] = oh + wa < p.Ho && ow + wb < p.Wo;
+      const int64_t ov = ((n * p.Ho + min(oh + wa, p.Ho - 1)) * p.Wo + min(ow + wb, p.Wo - 1)) * cpv + cv;
+      ldv((const T*)p.dz + ov * VE, g[w]);
+      if constexpr (VE == 8) *(uint2*)am[w] = *(const uint2*)(p.argmax + ov * VE);
+      else *(uint32_t*)am[w] = *(const uint32_t*)(p.argmax + ov * VE);
+    }
+    float h[4][VE];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int ih = 2 * oh + (q >> 1), iw = 2 * ow + (q & 1);
+      ldv((const T*)p.h + (((n * p.H + ih) * p.W + iw) * cpv + cv) * VE, h[q]);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int dy = q >> 1, dx = q & 1;
+      float d[VE];
+#pragma unroll
+      for (int j = 0; j < VE; ++j) d[j] = 0.f;
+      // pixel (2oh+dy, 2ow+dx) sits at window-local position (dy+1, dx+1) of window (oh, ow)
+      // and at (dy-1, dx+1), (dy+1, dx-1), (dy-1, dx-1) of the others (rows: 3 per window)
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        const int wa = w >> 1, wb = w & 1;
+        if ((wa && !dy) || (wb && !dx)) continue;      // the pixel is not in that window
+        const uint8_t want = (uint8_t)((dy - 2 * wa + 1) * 3 + (dx - 2 * wb + 1));
+#pragma unroll
+        for (int j = 0; j < VE; ++j) d[j] += (wok[w] && am[w][j] == want) ? g[w][j] : 0.f;
+      }
+      float o[VE];
+#pragma unroll
+      for (int j = 0; j < VE; ++j) o[j] = ka[j] * d[j] + kb[j] * (h[q][j] - km[j]) + kc[j];
+      const int ih = 2 * oh + dy, iw = 2 * ow + dx;
+      stv((T*)p.dh + (((n * p.H + ih) * p.W + iw) * cpv + cv) * VE, o);
+    }
+  }
+}
+
 // =============================================================== avg pool
 template <typename T>
 __global__ __launch_bounds__(256) void avgpool_fwd_kernel(int nimg, int P, int C, const T* x, T* y) {
@@ -790,6 +859,15 @@ extern "C" int avsr_stem_pool_bwd_apply(const avsr_stem_pool_params* p, void* st
   if (256 % (p->C / ve)) return AVSR_E_SHAPE;
   if ((int64_t)p->nimg * p->H * p->W >= (1ll << 31)) return AVSR_E_SHAPE;
   if (p->Ho != (p->H + 1) / 2 || p->Wo != (p->W + 1) / 2) return AVSR_E_SHAPE;
+  const char* pp = getenv("AVSR_STEM_APPLY_PIXEL");   // A/B: the per-pixel kernel
+  const bool per_pixel = pp && pp[0] == '1';
+  if (!(p->H & 1) && !(p->W & 1) && !per_pixel) {     // 2x2-block kernel (same result)
+    const int g2 = bn_grid((int64_t)p->nimg * p->Ho * p->Wo * p->C / ve, p->C / ve);
+    if (p->dtype == AVSR_BF16) hipLaunchKernelGGL(stem_bwd_apply2_kernel<bf16>, dim3(g2), dim3(256), 0, (hipStream_t)stream, *p);
+    else hipLaunchKernelGGL(stem_bwd_apply2_kernel<float>, dim3(g2), dim3(256), 0, (hipStream_t)stream, *p);
+    AVSR_CHECK_LAUNCH();
+    return 0;
+  }
   const int g = bn_grid((int64_t)p->nimg * p->H * p->W * p->C / ve, p->C / ve);
   const FastDiv fw = make_fastdiv(p->W), fhw = make_fastdiv(p->H * p->W);
   if (p->dtype == AVSR_BF16) hipLaunchKernelGGL(stem_bwd_apply_kernel<bf16>, dim3(g), dim3(256), 0, (hipStream_t)stream, *p, fw, fhw);

@@ -200,41 +200,3 @@ def test_tile_configs_bit_identical(dev, monkeypatch, tile):
     # the bias gradient sums per-row-tile partials: a different row-tile height re-associates
     assert _rel(got[3], ref[3]) < 1e-5
 
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("tile", ["128sk", "192sk"])
-@pytest.mark.parametrize("M,N,K", [(1999, 1000, 1000), (6000, 1024, 1024), (4096, 3072, 136)])
-def test_stream_k_matches_tiles(dev, monkeypatch, tile, M, N, K):
-    """Stream-K (persistent blocks over (tile, K-tile) ranges, fp32 partial hand-off between the
-    blocks sharing a tile) against the whole-tile kernel: same fused epilogues (bias, GELU,
-    pre-activation, residual, dropout; GELU' gate, dropout, fused bias gradient) and fp32
-    output. Only the fp32 summation order of a shared tile differs: bf16 outputs within one
-    rounding step (2e-2 of the output scale), fp32 within 1e-5."""
-    g = torch.Generator().manual_seed(M + N + K)
-    x = torch.randn(M, K, generator=g).to(dev, torch.bfloat16)
-    W = (torch.randn(N, K, generator=g) * K ** -0.5).to(dev, torch.bfloat16)
-    b = torch.randn(N, generator=g).to(dev)
-    r = torch.randn(M, N, generator=g).to(dev, torch.bfloat16)
-    dy = torch.randn(M, N, generator=g).to(dev, torch.bfloat16)
-    hg = torch.randn(M, K, generator=g).to(dev, torch.bfloat16)
-
-    def run():
-        h = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
-        y = ops.linear_fwd(x, W, b, act=L.ACT_GELU, preact=h, res=r, drop_p=0.1, seed=7)
-        db = torch.zeros(K, device=dev)
-        dx = ops.linear_dgrad(dy, W, gate=hg, act=L.ACT_GELU, drop_p=0.1, seed=9, db=db)
-        C = torch.zeros(M, N, device=dev)
-        ops.gemm(x, W, C, M=M, N=N, K=K, a_kmajor=True, b_kmajor=True, lda=K, ldb=K, ldc=N)
-        torch.cuda.synchronize()
-        return y, h, dx, db, C
-
-    monkeypatch.setenv("AVSR_GEMM_TILE", "128")
-    ref = run()
-    monkeypatch.setenv("AVSR_GEMM_TILE", tile)
-    for rep in range(2):          # twice: the partial hand-off flags are per-launch epochs
-        got = run()
-        for a_, b_, name in zip(got, ref, ("y", "preact", "dx", "db", "C")):
-            tol = 1e-5 if name in ("db", "C") else 2e-2
-            assert _rel(a_, b_) < tol, (tile, name, rep, _rel(a_, b_))
-        # dropout masks are identical (index hash), so zeros coincide
-        assert torch.equal(got[0] == 0, ref[0] == 0) or _rel(got[0], ref[0]) < 2e-2

@@ -139,6 +139,38 @@ def test_stem_pool(dev, dtype):
         assert _rel(gg, pp.grad) < tol
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("n,H,W", [(6, 44, 44), (3, 10, 14), (2, 9, 7)])
+def test_stem_bwd_apply_block_kernel(dev, dtype, monkeypatch, n, H, W):
+    """the 2x2-block stem backward apply (even H, W) reproduces the per-pixel kernel (same windows,
+    same addition order; the final fma contraction may differ: 1e-6 relative); odd sizes take
+    the per-pixel kernel either way"""
+    C = 64
+    g = torch.Generator().manual_seed(n * H + W)
+    hd = torch.randn(n, H, W, C, generator=g).to(dev, dtype)
+    st = ops.BnState(C, dev)
+    ops.bn_finalize(st, (1 + 0.1 * torch.randn(C, generator=g)).to(dev), (0.1 * torch.randn(C, generator=g)).to(dev),
+                    None, None, partials=_partials(hd.float().cpu().view(-1, C)).to(dev))
+    a = (0.25 + 0.05 * torch.randn(C, generator=g)).to(dev)
+    Ho, Wo = (H + 1) // 2, (W + 1) // 2
+    y = torch.empty(n, Ho, Wo, C, device=dev, dtype=dtype)
+    am = torch.empty(n, Ho, Wo, C, device=dev, dtype=torch.uint8)
+    hmax = torch.empty(n, Ho, Wo, C, device=dev, dtype=dtype)
+    ops.stem_pool_fwd(hd, n, H, W, st, a, y, am, hmax=hmax)
+    dy = torch.randn(n, Ho, Wo, C, generator=g).to(dev, dtype)
+    out = []
+    for pix in ("1", "0"):
+        monkeypatch.setenv("AVSR_STEM_APPLY_PIXEL", pix)
+        dh = torch.full_like(hd, float("nan"))
+        grads = [torch.zeros(C, device=dev) for _ in range(3)]
+        ops.stem_pool_bwd(dy, am, hmax, hd, n, H, W, st, a, dh, dgamma=grads[0], dbeta=grads[1], dprelu=grads[2])
+        torch.cuda.synchronize()
+        out.append((dh, grads))
+    assert _rel(out[0][0], out[1][0]) < (1e-6 if dtype == torch.float32 else 8e-3)
+    for g0, g1 in zip(out[0][1], out[1][1]):
+        assert torch.equal(g0, g1)
+
+
 BNR_CASES = [
     # nimg, hw (dgrad output = BN input grid), BN channels (conv cin), cout, k, stride, pad, residual
     (6, 22, 64, 64, 3, 1, 1, "identity"),       # 256x64 tiles, layer 1
