@@ -410,6 +410,7 @@ __global__ __launch_bounds__(CF::NTH, CF::MINB) void conv_glds_kernel(ConvArgs a
 using CCfg128 = gemmg::GCfg<2, 2, 2, 2, 2>;    // 128x128
 using CCfg256x64 = gemmg::GCfg<4, 1, 2, 2, 2>; // 256x64  (N <= 64: cout / cin = 64)
 using CCfg64x256 = gemmg::GCfg<1, 4, 2, 2, 2>; // 64x256  (M <= 64: weight-grad with cout = 64)
+using CCfg192 = gemmg::GCfg<2, 2, 3, 2, 2>;    // 192x128 (96x64 per wave), k-major A (fwd / data-grad)
 
 template <typename OutT, int KIND, class CF>
 int launch_glds(const ConvArgs& a, int groups, hipStream_t st) {
@@ -428,8 +429,23 @@ static bool conv_glds_enabled() {
   return !(e && e[0] == '1');
 }
 
+// 192x128 for the k-major-A directions (forward, data-grad) where it still runs >= 2 blocks per
+// CU and its rounds carry no more work than 128x128's (the dense rule, gemm.hip tile_cfg):
+// ResNet stages 2-3 at C2; AVSR_CONV_192=0 disables it (A/B)
+static bool conv192(int M, int N, int groups) {
+  if (N <= 64 || M <= 64 || !conv_glds_enabled()) return false;
+  const char* e = getenv("AVSR_CONV_192");
+  if (e && e[0] == '0') return false;
+  const long tn = (long)((N + 127) / 128) * groups;
+  const long n128 = ((long)((M + 127) / 128) * tn + 255) / 256, n192 = ((long)((M + 191) / 192) * tn + 255) / 256;
+  return n192 >= 2 && 3 * n192 * 50 <= 2 * n128 * 51;
+}
+
 template <typename OutT, int KIND>
 int glds_by_tile(const ConvArgs& a, int groups, hipStream_t st) {
+  if constexpr (KIND != K_WGRAD) {
+    if (conv192(a.M, a.N, groups)) return launch_glds<OutT, KIND, CCfg192>(a, groups, st);
+  }
   if (a.N <= 64) return launch_glds<OutT, KIND, CCfg256x64>(a, groups, st);
   if (a.M <= 64) return launch_glds<OutT, KIND, CCfg64x256>(a, groups, st);
   return launch_glds<OutT, KIND, CCfg128>(a, groups, st);
@@ -455,6 +471,8 @@ int by_tile(const ConvArgs& a, int groups, hipStream_t st) {
 }
 
 static int tile_bm(int M, int N) { return N <= 64 ? 256 : (M <= 64 ? 64 : 128); }
+// row-tile height of a forward / data-grad launch (glds_by_tile): per-tile BN partials
+static int tile_bm_k(int M, int N) { return conv192(M, N, 1) ? 192 : tile_bm(M, N); }
 
 // extents (elements, one group) of the A / B operands -> buffer-DMA loaders when allowed
 static void set_extents(ConvArgs& a, const avsr_conv_params* p, bool tap_uniform, int64_t ea, int64_t eb) {
@@ -573,7 +591,7 @@ static int s2_launch(const ConvArgs& a0, const avsr_conv_params* p, hipStream_t 
     a.e.M = Mc;
     a.e.rm_wc = k.wc; a.e.rm_hc = k.hc; a.e.rm_hin = p->hin; a.e.rm_win = p->win; a.e.rm_a = k.a; a.e.rm_b = k.b;
     if (KIND >= K_DGRAD_BNR) a.bnr.ws = a0.bnr.ws + tile_off * 4 * a.N;
-    tile_off += (Mc + tile_bm(Mc, a.N) - 1) / tile_bm(Mc, a.N);
+    tile_off += (Mc + tile_bm_k(Mc, a.N) - 1) / tile_bm_k(Mc, a.N);
     if (KIND == K_DGRAD && a.K == 0 && a.e.beta == 1.f) continue;   // dx += 0
     const int rc = glds_by_tile<bf16, KIND>(a, 1, st);
     if (rc) return rc;
@@ -585,7 +603,7 @@ static int s2_launch(const ConvArgs& a0, const avsr_conv_params* p, hipStream_t 
 
 extern "C" int avsr_conv_stat_tiles(const avsr_conv_params* p) {
   const int M = p->nimg * p->hout * p->wout;
-  const int bm = tile_bm(M, p->cout);
+  const int bm = tile_bm_k(M, p->cout);
   return (M + bm - 1) / bm;
 }
 
@@ -596,12 +614,12 @@ extern "C" int avsr_conv_bnr_tiles(const avsr_conv_params* p) {
     int t = 0;
     for (int q = 0; q < 4; ++q) {
       const int Mc = p->nimg * cl[q].hc * cl[q].wc;
-      if (Mc) t += (Mc + tile_bm(Mc, p->cin) - 1) / tile_bm(Mc, p->cin);
+      if (Mc) t += (Mc + tile_bm_k(Mc, p->cin) - 1) / tile_bm_k(Mc, p->cin);
     }
     return t;
   }
   const int M = p->nimg * p->hin * p->win;
-  const int bm = tile_bm(M, p->cin);
+  const int bm = tile_bm_k(M, p->cin);
   return (M + bm - 1) / bm;
 }
 

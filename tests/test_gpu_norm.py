@@ -246,3 +246,43 @@ def test_avgpool(dev):
     dx = torch.empty_like(x)
     ops.avgpool_bwd(y, 50, 9, 512, dx)
     assert _rel(dx, y[:, None, :].expand_as(x) / 9) < 1e-6
+
+
+@pytest.mark.parametrize("case", [(140, 22, 128, 128, 3, 1, 1, "identity"), (150, 22, 128, 128, 3, 1, 1, "plain")])
+def test_conv_192_tiles_match_128(dev, monkeypatch, case):
+    """the 192x128 row tiles of the forward / data-grad convolutions (AVSR_CONV_192, chosen for
+    the large-M ResNet stages) against 128x128: identical stored outputs (same K order), BN
+    partial statistics and fused BN-backward sums equal up to the per-tile grouping (1e-5)."""
+    n, hw, cin, cout, k, s, p, mode = case
+    g = torch.Generator().manual_seed(n + hw)
+    geom = ops.ConvGeom(n, hw, hw, cin, cout, k, k, (s, s), (p, p))
+    M = n * hw * hw
+    bf = torch.bfloat16
+    x = torch.randn(M, cin, generator=g).to(dev, bf)
+    w = (torch.randn(cout, k, k, cin, generator=g) * (cin * k * k) ** -0.5).to(dev, bf)
+    dy = torch.randn(geom.out_pixels, cout, generator=g).to(dev, bf)
+    h = (torch.randn(M, cin, generator=g) * 1.3 + 0.2).to(dev, bf)
+    r = (torch.randn(M, cin, generator=g) * 0.8 - 0.1).to(dev, bf)
+    st = ops.BnState(cin, dev)
+    st.mean.copy_(0.1 * torch.randn(cin, generator=g)); st.invstd.copy_(0.5 + torch.rand(cin, generator=g))
+    st.scale.copy_(1 + 0.2 * torch.randn(cin, generator=g)); st.shift.copy_(0.2 * torch.randn(cin, generator=g))
+    a = (0.25 + 0.05 * torch.randn(cin, generator=g)).to(dev)
+    out = {}
+    for flag in ("0", "1"):
+        monkeypatch.setenv("AVSR_CONV_192", flag)
+        y = torch.empty(geom.out_pixels, cout, device=dev, dtype=bf)
+        part = torch.empty(cout, ops.conv_stat_tiles(geom), 3, device=dev)
+        ops.conv_fwd(geom, x, w, y, stats=part)
+        bst = ops.BnState(cout, dev)
+        ops.bn_finalize(bst, torch.ones(cout, device=dev), torch.zeros(cout, device=dev), None, None, partials=part)
+        dx = torch.zeros(M, cin, device=dev, dtype=bf)
+        ws, tiles = ops.conv_bwd_data_bnr(geom, dy, w, dx, h, st, a, res=None if mode == "plain" else r,
+                                          beta=0.0)
+        sums = ops.bn_bwd_finalize(ws, tiles, cin)
+        torch.cuda.synchronize()
+        out[flag] = (y, bst.mean.clone(), bst.invstd.clone(), dx, sums, part.shape[1], tiles)
+    o0, o1 = out["0"], out["1"]
+    assert o1[5] < o0[5] and o1[6] < o0[6], "the 192-row tiles were not selected"
+    assert torch.equal(o0[0], o1[0]) and torch.equal(o0[3], o1[3])
+    assert _rel(o1[1], o0[1]) < 1e-5 and _rel(o1[2], o0[2]) < 1e-5
+    assert _rel(o1[4], o0[4]) < 1e-5

@@ -42,11 +42,13 @@ def once(fuse):
 # variants: (label, BN fusion, AVSR_CONV_S2PHASE)
 mode = sys.argv[2] if len(sys.argv) > 2 else "fuse"
 variants = [("fuse=1", True, "1"), ("fuse=0", False, "1")] if mode == "fuse" else \
+    [("c192=1", True, "1", "1"), ("c192=0", True, "1", "0")] if mode == "c192" else \
     [("s2phase=1", True, "1"), ("s2phase=0", True, "0")]
 
 
 def run(var):
     os.environ["AVSR_CONV_S2PHASE"] = var[2]
+    os.environ["AVSR_CONV_192"] = var[3] if len(var) > 3 else "1"
     return once(var[1])
 
 
