@@ -152,25 +152,37 @@ __global__ __launch_bounds__(256) void cast_flat_f32_bf16_kernel(int64_t n8, con
   }
 }
 
+// grid (clip x chunk of PACK_TC frames, pixel blocks): a thread walks one pixel through a
+// chunk of output frames, loading each of the chunk's PACK_TC + 4 source frames once (all
+// loads issued first) instead of 5 loads per output (the source video is read ~1.25x, not 5x)
+constexpr int PACK_TC = 16;
 template <typename T>
 __global__ __launch_bounds__(256) void stem_pack_kernel(int B, int T_, const float* video, T* out) {
   constexpr int HW = 88 * 88;
-  const int64_t total = (int64_t)B * T_ * HW;
-  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
-    const int64_t frame = i / HW;
-    const int pix = (int)(i % HW);
-    const int b = (int)(frame / T_), t = (int)(frame % T_);
+  const int pix = blockIdx.y * 256 + threadIdx.x;
+  if (pix >= HW) return;
+  const int nch = (T_ + PACK_TC - 1) / PACK_TC;
+  const int b = blockIdx.x / nch, t0 = (blockIdx.x - b * nch) * PACK_TC;
+  const float* src = video + (int64_t)b * T_ * HW + pix;
+  float f[PACK_TC + 4];
+#pragma unroll
+  for (int k = 0; k < PACK_TC + 4; ++k) {
+    const int tt = t0 + k - 2;
+    f[k] = (tt >= 0 && tt < T_) ? src[(int64_t)tt * HW] : 0.f;
+  }
+#pragma unroll
+  for (int u = 0; u < PACK_TC; ++u) {
+    const int t = t0 + u;
+    if (t >= T_) break;
     float o[8];
 #pragma unroll
-    for (int c = 0; c < 8; ++c) {
-      const int tt = t + c - 2;
-      o[c] = (c < 5 && tt >= 0 && tt < T_) ? video[((int64_t)b * T_ + tt) * HW + pix] : 0.f;
-    }
+    for (int c = 0; c < 8; ++c) o[c] = c < 5 ? f[u + c] : 0.f;
+    T* dst = out + (((int64_t)b * T_ + t) * HW + pix) * 8;
     if constexpr (sizeof(T) == 2) {
-      stv(out + i * 8, o);
+      stv(dst, o);
     } else {
-      stv(out + i * 8, o);
-      stv(out + i * 8 + 4, o + 4);
+      stv(dst, o);
+      stv(dst + 4, o + 4);
     }
   }
 }
@@ -491,9 +503,12 @@ extern "C" int avsr_cast(int sd, int dd, int rows, int cols, const void* src, in
 }
 
 extern "C" int avsr_stem_pack(int dtype, int B, int T, const float* video, void* out, void* stream) {
-  const int g = avsr_grid((int64_t)B * T * 88 * 88);
-  if (dtype == AVSR_BF16) hipLaunchKernelGGL(stem_pack_kernel<bf16>, dim3(g), dim3(256), 0, (hipStream_t)stream, B, T, video, (bf16*)out);
-  else hipLaunchKernelGGL(stem_pack_kernel<float>, dim3(g), dim3(256), 0, (hipStream_t)stream, B, T, video, (float*)out);
+  if ((int64_t)B * T == 0) return 0;
+  const int64_t nx = (int64_t)B * ((T + PACK_TC - 1) / PACK_TC);
+  if (nx > 0x7fffffffLL) return AVSR_E_SHAPE;
+  const dim3 g((unsigned)nx, (88 * 88 + 255) / 256);
+  if (dtype == AVSR_BF16) hipLaunchKernelGGL(stem_pack_kernel<bf16>, g, dim3(256), 0, (hipStream_t)stream, B, T, video, (bf16*)out);
+  else hipLaunchKernelGGL(stem_pack_kernel<float>, g, dim3(256), 0, (hipStream_t)stream, B, T, video, (float*)out);
   AVSR_CHECK_LAUNCH();
   return 0;
 }

@@ -256,3 +256,21 @@ def test_adamw_clip(dev):
     # fp32 params of magnitude ~1 after updates of ~1e-3: compare the params themselves
     assert (pd.cpu() - ref.detach()).abs().max().item() < 2e-6
     assert _rel(sh, pd) < 1e-2
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_stem_pack_exact(dev, dtype):
+    """time-stacked stem input: channel c of frame t = frame t + c - 2 (zero outside the clip,
+    channels 5..7 zero); T spans several frame chunks of the kernel with a ragged last one"""
+    B, T = 2, 37
+    g = torch.Generator().manual_seed(9)
+    vid = torch.randn(B, 1, T, 88, 88, generator=g)
+    xp = torch.full((B * T, 88, 88, 8), float("nan"), device=dev, dtype=dtype)
+    ops.stem_pack(vid.to(dev).contiguous(), xp)
+    ref = torch.zeros(B, T, 88, 88, 8)
+    for c in range(5):
+        for t in range(T):
+            tt = t + c - 2
+            if 0 <= tt < T:
+                ref[:, t, :, :, c] = vid[:, 0, tt]
+    assert torch.equal(xp.cpu().float().view(B, T, 88, 88, 8), ref.to(dtype).float())
