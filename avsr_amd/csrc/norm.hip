@@ -560,6 +560,74 @@ __global__ __launch_bounds__(256) void stem_pool_fwd_kernel(avsr_stem_pool_param
   else *(uint32_t*)(p.argmax + ov * VE) = *(const uint32_t*)idx;
 }
 
+// Same outputs for H = 2*Ho, W = 2*Wo: one thread per 2x2 block of pooled outputs and channel
+// group. The block's four 3x3 windows cover a 5x5 input patch: each input is loaded and put
+// through BN+PReLU once (25 per 4 outputs instead of 36), row by row; every window still
+// visits its taps in row-major order with the strict '>' (same maximum, same argmax on ties).
+// Grid-stride with the channel group fixed (per-channel coefficients loaded once).
+template <typename T>
+__global__ __launch_bounds__(256) void stem_pool_fwd2_kernel(avsr_stem_pool_params p) {
+  constexpr int VE = VecW<T>::VE;
+  const int cpv = p.C / VE;
+  const int bho = p.Ho >> 1, bwo = p.Wo >> 1;
+  const int64_t nv = (int64_t)p.nimg * bho * bwo * cpv, stride = (int64_t)gridDim.x * 256;
+  const int64_t t0 = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int cv = (int)(t0 % cpv), c0 = cv * VE;
+  float sc[VE], sh[VE], pw[VE];
+  chan_load(p.scale, c0, sc); chan_load(p.shift, c0, sh); chan_load(p.prelu, c0, pw);
+  for (int64_t v = t0; v < nv; v += stride) {
+    const int64_t blk = v / cpv;
+    const int bw = (int)(blk % bwo), bh = (int)((blk / bwo) % bho);
+    const int64_t n = blk / ((int64_t)bwo * bho);
+    const int ih0 = 4 * bh - 1, iw0 = 4 * bw - 1;        // patch origin (may be -1)
+    const T* base = (const T*)p.h + n * p.H * p.W * p.C + c0;
+    float best[4][VE], bhv[4][VE];
+    uint8_t idx[4][VE];
+#pragma unroll
+    for (int o = 0; o < 4; ++o)
+#pragma unroll
+      for (int j = 0; j < VE; ++j) { best[o][j] = -INFINITY; bhv[o][j] = 0.f; idx[o][j] = 0; }
+#pragma unroll
+    for (int r = 0; r < 5; ++r) {
+      const int ih = ih0 + r;
+      const bool rok = ih >= 0 && ih < p.H;
+      float hv[5][VE];
+#pragma unroll
+      for (int c = 0; c < 5; ++c) {
+        const int iw = min(max(iw0 + c, 0), p.W - 1);
+        ldv(base + ((int64_t)min(max(ih, 0), p.H - 1) * p.W + iw) * p.C, hv[c]);
+      }
+      if (!rok) continue;
+#pragma unroll
+      for (int c = 0; c < 5; ++c) {
+        const int iw = iw0 + c;
+        if (iw < 0 || iw >= p.W) continue;
+#pragma unroll
+        for (int o = 0; o < 4; ++o) {
+          const int a = o >> 1, b = o & 1;
+          const int wr = r - 2 * a, wc = c - 2 * b;       // tap position in window o
+          if (wr < 0 || wr > 2 || wc < 0 || wc > 2) continue;
+#pragma unroll
+          for (int j = 0; j < VE; ++j) {
+            const float z = hv[c][j] * sc[j] + sh[j];
+            const float y = z > 0.f ? z : z * pw[j];
+            if (y > best[o][j]) { best[o][j] = y; bhv[o][j] = hv[c][j]; idx[o][j] = (uint8_t)(wr * 3 + wc); }
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int o = 0; o < 4; ++o) {
+      const int oh = 2 * bh + (o >> 1), ow = 2 * bw + (o & 1);
+      const int64_t ov = ((n * p.Ho + oh) * p.Wo + ow) * cpv + cv;
+      stv((T*)p.y + ov * VE, best[o]);
+      if (p.hmax) stv((T*)p.hmax + ov * VE, bhv[o]);
+      if constexpr (VE == 8) *(uint2*)(p.argmax + ov * VE) = *(const uint2*)idx[o];
+      else *(uint32_t*)(p.argmax + ov * VE) = *(const uint32_t*)idx[o];
+    }
+  }
+}
+
 // Stem backward, dense part. The BN reductions run over the pooled grid (h at the argmax,
 // saved by the forward as hmax; dz is nonzero only where an input pixel is some window's
 // argmax, so sum_p dz*xhat = sum_o dzp[o]*xhat(hmax[o])); here dz[p] = sum of dzp[o] over the
@@ -844,6 +912,15 @@ extern "C" int avsr_stem_pool_fwd(const avsr_stem_pool_params* p, void* stream) 
   const int ve = p->dtype == AVSR_BF16 ? 8 : 4;
   if (p->C % ve) return AVSR_E_SHAPE;
   if (p->nimg > 65535) return AVSR_E_SHAPE;
+  const char* pp = getenv("AVSR_STEM_APPLY_PIXEL");   // A/B: the per-pixel kernels
+  if (p->H == 2 * p->Ho && p->W == 2 * p->Wo && !(p->Ho & 1) && !(p->Wo & 1) && !(pp && pp[0] == '1') &&
+      256 % (p->C / ve) == 0) {
+    const int g2 = bn_grid((int64_t)p->nimg * (p->Ho / 2) * (p->Wo / 2) * p->C / ve, p->C / ve);
+    if (p->dtype == AVSR_BF16) hipLaunchKernelGGL(stem_pool_fwd2_kernel<bf16>, dim3(g2), dim3(256), 0, (hipStream_t)stream, *p);
+    else hipLaunchKernelGGL(stem_pool_fwd2_kernel<float>, dim3(g2), dim3(256), 0, (hipStream_t)stream, *p);
+    AVSR_CHECK_LAUNCH();
+    return 0;
+  }
   const dim3 g((p->Ho * p->Wo * p->C / ve + 255) / 256, p->nimg);
   const FastDiv fwo = make_fastdiv(p->Wo);
   if (p->dtype == AVSR_BF16) hipLaunchKernelGGL(stem_pool_fwd_kernel<bf16>, g, dim3(256), 0, (hipStream_t)stream, *p, fwo);

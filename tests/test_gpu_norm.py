@@ -140,7 +140,7 @@ def test_stem_pool(dev, dtype):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("n,H,W", [(6, 44, 44), (3, 10, 14), (2, 9, 7)])
+@pytest.mark.parametrize("n,H,W", [(6, 44, 44), (3, 12, 16), (3, 10, 14), (2, 9, 7)])
 def test_stem_bwd_apply_block_kernel(dev, dtype, monkeypatch, n, H, W):
     """the 2x2-block stem backward apply (even H, W) reproduces the per-pixel kernel (same windows,
     same addition order; the final fma contraction may differ: 1e-6 relative); odd sizes take
@@ -153,10 +153,18 @@ def test_stem_bwd_apply_block_kernel(dev, dtype, monkeypatch, n, H, W):
                     None, None, partials=_partials(hd.float().cpu().view(-1, C)).to(dev))
     a = (0.25 + 0.05 * torch.randn(C, generator=g)).to(dev)
     Ho, Wo = (H + 1) // 2, (W + 1) // 2
-    y = torch.empty(n, Ho, Wo, C, device=dev, dtype=dtype)
-    am = torch.empty(n, Ho, Wo, C, device=dev, dtype=torch.uint8)
-    hmax = torch.empty(n, Ho, Wo, C, device=dev, dtype=dtype)
-    ops.stem_pool_fwd(hd, n, H, W, st, a, y, am, hmax=hmax)
+    fw = []
+    for pix in ("1", "0"):          # forward: 2x2 output blocks (even Ho, Wo) vs per-output windows
+        monkeypatch.setenv("AVSR_STEM_APPLY_PIXEL", pix)
+        y = torch.full((n, Ho, Wo, C), float("nan"), device=dev, dtype=dtype)
+        am = torch.full((n, Ho, Wo, C), 255, device=dev, dtype=torch.uint8)
+        hmax = torch.full((n, Ho, Wo, C), float("nan"), device=dev, dtype=dtype)
+        ops.stem_pool_fwd(hd, n, H, W, st, a, y, am, hmax=hmax)
+        torch.cuda.synchronize()
+        fw.append((y, am, hmax))
+    for t0, t1 in zip(*fw):
+        assert torch.equal(t0, t1)
+    y, am, hmax = fw[1]
     dy = torch.randn(n, Ho, Wo, C, generator=g).to(dev, dtype)
     out = []
     for pix in ("1", "0"):
