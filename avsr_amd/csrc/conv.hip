@@ -415,6 +415,7 @@ using CCfg192 = gemmg::GCfg<2, 2, 3, 2, 2>;    // 192x128 (96x64 per wave), k-ma
 template <typename OutT, int KIND, class CF>
 int launch_glds(const ConvArgs& a, int groups, hipStream_t st) {
   const int tm = (a.M + CF::BM - 1) / CF::BM, tn = (a.N + CF::BN - 1) / CF::BN;
+  if (a.e.stats && a.e.stats_tiles != tm) return AVSR_E_SHAPE;   // partials sized for another tile height
   const long nwg = (long)tm * tn * groups * a.splits;
   if (nwg > 0x7fffffffL) return AVSR_E_SHAPE;
   hipLaunchKernelGGL((conv_glds_kernel<OutT, KIND, CF>), dim3((unsigned)nwg), dim3(CF::NTH), CF::LDS_BYTES, st, a,
@@ -456,6 +457,7 @@ int launch(const ConvArgs& a, int groups, hipStream_t st) {
   // operand kinds per convolution direction (fwd: K/K, dgrad: K/R, wgrad: R/R)
   using TL = Tile<T, WM, WN, KIND != K_WGRAD, KIND == K_FWD>;
   dim3 grid((a.N + TL::BN - 1) / TL::BN, (a.M + TL::BM - 1) / TL::BM, groups * a.splits);
+  if (a.e.stats && a.e.stats_tiles != (int)grid.y) return AVSR_E_SHAPE;   // partials sized for another tile height
   if (grid.y > 65535) return AVSR_E_SHAPE;
   hipLaunchKernelGGL((conv_kernel<T, OutT, WM, WN, KIND>), grid, dim3(NT), TL::LDS_BYTES, st, a);
   AVSR_CHECK_LAUNCH();
@@ -471,8 +473,11 @@ int by_tile(const ConvArgs& a, int groups, hipStream_t st) {
 }
 
 static int tile_bm(int M, int N) { return N <= 64 ? 256 : (M <= 64 ? 64 : 128); }
-// row-tile height of a forward / data-grad launch (glds_by_tile): per-tile BN partials
-static int tile_bm_k(int M, int N) { return conv192(M, N, 1) ? 192 : tile_bm(M, N); }
+// row-tile height of a forward / data-grad launch: per-tile BN partials. 192 rows only on the
+// bf16 LDS-DMA path (glds_by_tile); the fp32 / register-staged path keeps tile_bm
+static int tile_bm_k(int M, int N, int dtype) {
+  return dtype == AVSR_BF16 && conv192(M, N, 1) ? 192 : tile_bm(M, N);
+}
 
 // extents (elements, one group) of the A / B operands -> buffer-DMA loaders when allowed
 static void set_extents(ConvArgs& a, const avsr_conv_params* p, bool tap_uniform, int64_t ea, int64_t eb) {
@@ -591,7 +596,7 @@ static int s2_launch(const ConvArgs& a0, const avsr_conv_params* p, hipStream_t 
     a.e.M = Mc;
     a.e.rm_wc = k.wc; a.e.rm_hc = k.hc; a.e.rm_hin = p->hin; a.e.rm_win = p->win; a.e.rm_a = k.a; a.e.rm_b = k.b;
     if (KIND >= K_DGRAD_BNR) a.bnr.ws = a0.bnr.ws + tile_off * 4 * a.N;
-    tile_off += (Mc + tile_bm_k(Mc, a.N) - 1) / tile_bm_k(Mc, a.N);
+    tile_off += (Mc + tile_bm_k(Mc, a.N, AVSR_BF16) - 1) / tile_bm_k(Mc, a.N, AVSR_BF16);
     if (KIND == K_DGRAD && a.K == 0 && a.e.beta == 1.f) continue;   // dx += 0
     const int rc = glds_by_tile<bf16, KIND>(a, 1, st);
     if (rc) return rc;
@@ -603,7 +608,7 @@ static int s2_launch(const ConvArgs& a0, const avsr_conv_params* p, hipStream_t 
 
 extern "C" int avsr_conv_stat_tiles(const avsr_conv_params* p) {
   const int M = p->nimg * p->hout * p->wout;
-  const int bm = tile_bm_k(M, p->cout);
+  const int bm = tile_bm_k(M, p->cout, p->dtype);
   return (M + bm - 1) / bm;
 }
 
@@ -614,12 +619,12 @@ extern "C" int avsr_conv_bnr_tiles(const avsr_conv_params* p) {
     int t = 0;
     for (int q = 0; q < 4; ++q) {
       const int Mc = p->nimg * cl[q].hc * cl[q].wc;
-      if (Mc) t += (Mc + tile_bm_k(Mc, p->cin) - 1) / tile_bm_k(Mc, p->cin);
+      if (Mc) t += (Mc + tile_bm_k(Mc, p->cin, p->dtype) - 1) / tile_bm_k(Mc, p->cin, p->dtype);
     }
     return t;
   }
   const int M = p->nimg * p->hin * p->win;
-  const int bm = tile_bm_k(M, p->cin);
+  const int bm = tile_bm_k(M, p->cin, p->dtype);
   return (M + bm - 1) / bm;
 }
 

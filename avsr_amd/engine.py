@@ -368,7 +368,7 @@ class Engine:
         bn, gam, bet = self._bn(bnprefix)
         st = ops.BnState(g.cout, self.device)
         if train:
-            part = self._e(g.cout, ops.conv_stat_tiles(g), 3, dtype=torch.float32)
+            part = self._e(g.cout, ops.conv_stat_tiles(g, ops.dtype_code(x)), 3, dtype=torch.float32)
             ops.conv_fwd(g, x, self.w(wname), h, part)
             ops.bn_finalize(st, gam, bet, bn.running_mean, bn.running_var, partials=part, training=True,
                             momentum=bn.momentum, eps=bn.eps)
@@ -393,7 +393,7 @@ class Engine:
         bn, gam, bet = self._bn(R + "frontend3D.1")
         st0 = ops.BnState(64, self.device)
         if train:
-            part = self._e(64, ops.conv_stat_tiles(gs), 3, dtype=torch.float32)
+            part = self._e(64, ops.conv_stat_tiles(gs, ops.dtype_code(xp)), 3, dtype=torch.float32)
             ops.conv_fwd(gs, xp, wp, h0, part)
             ops.bn_finalize(st0, gam, bet, bn.running_mean, bn.running_var, partials=part, training=True,
                             momentum=bn.momentum, eps=bn.eps)
@@ -779,7 +779,7 @@ class Engine:
         klen = ctx["klen"]
         p_d, p_att = ctx["p_d"], ctx["p_att"]
         self._bias_grad(dlogits, self.arena.g_padded("decoder.output_layer.bias"))
-        self._wgrad(dlogits[:, :self.V], ctx["yn"], self.g("decoder.output_layer.weight"))
+        self._wgrad(dlogits, ctx["yn"], self.arena.g_padded("decoder.output_layer.weight"))   # padded vocab
         dyn = self._e(R, D)
         ops.gemm(dlogits, self.arena.w_padded("decoder.output_layer.weight"), dyn, M=R, N=D, K=self.Vp, a_kmajor=True,
                  b_kmajor=False, lda=dlogits.stride(0), ldb=D, ldc=D)
@@ -932,7 +932,9 @@ class Engine:
         dcl = self._e(M, self.Vp)
         ops.ctc_bwd(ctx["cp"], d_ctc, 1.0 / B, dcl)
         self._bias_grad(dcl, self.arena.g_padded("ctc.ctc_lo.bias"))
-        self._wgrad(dcl[:, :self.V], ctx["xin"], self.g("ctc.ctc_lo.weight"))
+        # padded vocab (the backward writes zeros to columns V..Vp): Vp rows keep the weight-grad on
+        # the LDS-DMA core (r-contiguous operands need a multiple of 8); the pad rows get exact zeros
+        self._wgrad(dcl, ctx["xin"], self.arena.g_padded("ctc.ctc_lo.weight"))
         ops.gemm(dcl, self.arena.w_padded("ctc.ctc_lo.weight"), denc, M=M, N=self.D, K=self.Vp, a_kmajor=True,
                  b_kmajor=False, lda=dcl.stride(0), ldb=self.D, ldc=self.D, epi_bwd=True, drop_p=ctx["p_c"],
                  seed=ctx["sd_c"])

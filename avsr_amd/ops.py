@@ -172,7 +172,9 @@ class ConvGeom:
         return self.nimg * self.hin * self.win
 
 
-def conv_stat_tiles(g, dtype=L.AVSR_BF16):
+def conv_stat_tiles(g, dtype):
+    """output row tiles of conv_fwd(g, x of dtype code `dtype`, ..., stats): the tile height (hence
+    the partial-statistics count) depends on the path the dtype takes"""
     p = g.params(dtype)
     return L.load().avsr_conv_stat_tiles(ctypes.byref(p))
 
@@ -181,6 +183,11 @@ def conv_fwd(g, x, w, y, stats=None, bias=None, act=L.ACT_NONE, preact=None, res
     """y[pix, co] = act(conv(x, w) + bias) + res; stats: fp32 [cout, tiles, 3] BN partials."""
     p = g.params(dtype_code(x))
     assert x.dtype == w.dtype == y.dtype and x.is_cuda
+    if stats is not None:
+        # the kernel writes one (count, mean, M2) per output row tile of the launched tile height
+        tiles = L.load().avsr_conv_stat_tiles(ctypes.byref(p))
+        if stats.dtype != torch.float32 or stats.numel() < g.groups * g.cout * tiles * 3 or not stats.is_contiguous():
+            raise ValueError(f"conv_fwd stats: need fp32 [{g.cout}, {tiles}, 3], got {tuple(stats.shape)}")
     p.x, p.w, p.y = x.data_ptr(), w.data_ptr(), y.data_ptr()
     p.stats = None if stats is None else stats.data_ptr()
     p.bias = None if bias is None else bias.data_ptr()

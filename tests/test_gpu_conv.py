@@ -39,7 +39,7 @@ def test_conv2d(dev, dtype, case):
     xd = x.permute(0, 2, 3, 1).contiguous().to(dev, dtype)
     wd = wt.permute(0, 2, 3, 1).contiguous().to(dev, dtype)
     y = torch.empty(n, ho, wo, cout, device=dev, dtype=dtype)
-    tiles = ops.conv_stat_tiles(geom)
+    tiles = ops.conv_stat_tiles(geom, ops.dtype_code(xd))
     stats = torch.empty(cout, tiles, 3, device=dev)
     ops.conv_fwd(geom, xd, wd, y, stats)
     tol = 3e-5 if dtype == torch.float32 else 2e-2

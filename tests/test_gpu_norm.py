@@ -279,7 +279,7 @@ def test_conv_192_tiles_match_128(dev, monkeypatch, case):
     for flag in ("0", "1"):
         monkeypatch.setenv("AVSR_CONV_192", flag)
         y = torch.empty(geom.out_pixels, cout, device=dev, dtype=bf)
-        part = torch.empty(cout, ops.conv_stat_tiles(geom), 3, device=dev)
+        part = torch.empty(cout, ops.conv_stat_tiles(geom, ops.dtype_code(x)), 3, device=dev)
         ops.conv_fwd(geom, x, w, y, stats=part)
         bst = ops.BnState(cout, dev)
         ops.bn_finalize(bst, torch.ones(cout, device=dev), torch.zeros(cout, device=dev), None, None, partials=part)
