@@ -40,6 +40,24 @@ _DB_FUSE = os.environ.get("AVSR_DB_FUSE", "1") == "1"
 _COLSUM_DEFER = os.environ.get("AVSR_COLSUM_DEFER", "1") == "1"
 
 
+_STEP_STREAMS = {}
+
+
+def prioritize_step_stream(device):
+    """Make a high-priority stream the current stream of `device` for the training step; the
+    weight-gradient side stream keeps the default priority, so the data-gradient chain (which
+    bounds the step) wins CU slots over it (bench A/B, profiles/r02_stream_priority_ab.txt:
+    +1.5 %). AVSR_MAIN_PRIO=0 keeps the default stream. Returns the stream (or None)."""
+    if device.type != "cuda" or os.environ.get("AVSR_MAIN_PRIO", "1") != "1":
+        return None
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    s = _STEP_STREAMS.get(idx)
+    if s is None:
+        s = _STEP_STREAMS[idx] = torch.cuda.Stream(device=idx, priority=-1)
+    torch.cuda.set_stream(s)
+    return s
+
+
 def wgrad_splitk(M, N, K):
     """token-dimension split of a weight-gradient GEMM dW[N][K] += dy[M][N]^T x[M][K]: split
     only when the 128x128 output grid is at or below one block per CU (slab workspace, no

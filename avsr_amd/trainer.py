@@ -24,6 +24,7 @@ import gc
 import torch
 from transformers import Trainer
 
+from .engine import prioritize_step_stream
 from .optim import ArenaAdamW
 from .parallel import ArenaDDP
 
@@ -42,6 +43,7 @@ class AVSRTrainer(Trainer):
         if not str(getattr(optim, "value", optim)).startswith("adamw"):
             raise NotImplementedError(f"optim={args.optim}: the arena optimizer implements AdamW")
         model.setup_engine(args.device, self.engine_dtype)
+        prioritize_step_stream(args.device)   # data-grad chain ahead of the side stream's weight-grads
         kw = dict(model=model, args=args, data_collator=data_collator, train_dataset=train_dataset,
                   eval_dataset=eval_dataset, processing_class=processing_class, model_init=model_init,
                   compute_loss_func=compute_loss_func, compute_metrics=compute_metrics, callbacks=callbacks,

@@ -165,6 +165,8 @@ def main():
     assert world == args.gpus, f"--gpus {args.gpus} but WORLD_SIZE {world}"
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    from avsr_amd.engine import prioritize_step_stream
+    prioritize_step_stream(dev)      # the step's stream above the weight-grad side stream (AVSR_MAIN_PRIO=0: off)
     from avsr_amd import ops
     from avsr_amd.avhubert_avsr_model import AVHubertAVSR
     from avsr_amd.configuration_avhubert_avsr import AVHubertAVSRConfig
