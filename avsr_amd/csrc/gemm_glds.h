@@ -429,7 +429,7 @@ AVSR_DEV void epilogue_bnr(const Epi& e, const BnrArgs& b, int m0, int n0, f32x4
   float* st = (float*)smem;
   const int lc = (tid % CG) * 8, col = n0 + lc;
   const bool colok = col < e.N;
-  const bool beta = e.beta != 0.f;
+  const bool beta = e.beta != 0.f, alpha1 = e.alpha == 1.f;
   float sc[8], sh[8], pw[8], mu[8], is[8], sc2[8], sh2[8], mu2[8], is2[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
@@ -474,12 +474,19 @@ AVSR_DEV void epilogue_bnr(const Epi& e, const BnrArgs& b, int m0, int n0, f32x4
       if (!ok[it]) continue;
       const int lr = (tid + it * CF::NTH) / CG;
       const f32x4 v0 = *(const f32x4*)(st + lr * LDR + lc), v1 = *(const f32x4*)(st + lr * LDR + lc + 4);
-      const float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+      float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+      if (alpha1) {
+        if (beta)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] = fmaf(e.beta, (float)pc[it][j], v[j]);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = beta ? fmaf(e.beta, (float)pc[it][j], v[j] * e.alpha) : v[j] * e.alpha;
+      }
       bf16x8 o;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        float vj = v[j] * e.alpha;
-        if (beta) vj += e.beta * (float)pc[it][j];
+        const float vj = v[j];
         const float hh = (float)ph[it][j];
         float z = hh * sc[j] + sh[j];
         float rr = 0.f;
@@ -488,14 +495,19 @@ AVSR_DEV void epilogue_bnr(const Epi& e, const BnrArgs& b, int m0, int n0, f32x4
         if constexpr (RES == 2) z += rr * sc2[j] + sh2[j];
         const bool pos = z > 0.f;
         const float d = pos ? vj : vj * pw[j];
-        s3[j] += pos ? 0.f : vj * z;
+        s3[j] = fmaf(vj, pos ? 0.f : z, s3[j]);
         s0[j] += d;
-        s1[j] += d * (hh - mu[j]) * is[j];
-        if constexpr (RES == 2) s2[j] += d * (rr - mu2[j]) * is2[j];
+        s1[j] = fmaf(d, hh - mu[j], s1[j]);                 // x invstd once per column, below
+        if constexpr (RES == 2) s2[j] = fmaf(d, rr - mu2[j], s2[j]);
         o[j] = (bf16)d;
       }
       *(bf16x8*)(C + off[it]) = o;
     }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    s1[j] *= is[j];
+    if constexpr (RES == 2) s2[j] *= is2[j];
   }
   // per-column sums over the block: thread partials -> LDS (padded rows), then one thread per
   // (sum, column) adds the NTH/CG threads that own that column group

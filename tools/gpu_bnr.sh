@@ -1,0 +1,9 @@
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+O=gpurun_out/${1:-bnr}; mkdir -p $O
+timeout -k 10 300 python -u -m pytest tests/test_gpu_norm.py tests/test_gpu_conv.py tests/test_gpu_model_parity.py -x -q --timeout 120 --timeout-method thread > $O/tests.log 2>&1 || { echo tests failed; tail -30 $O/tests.log; exit 1; }
+tail -1 $O/tests.log
+timeout -k 10 300 python -u tools/resnet_bench.py 7 fuse > $O/rn.txt 2>&1 || { echo rn failed; tail -20 $O/rn.txt; exit 1; }
+grep -v amdgpu.ids $O/rn.txt
+echo rc=0
