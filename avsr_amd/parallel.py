@@ -36,6 +36,9 @@ def init_from_env(backend=None):
             backend = "nccl" if torch.cuda.is_available() else "gloo"
         if backend == "nccl":
             torch.cuda.set_device(local)
+            # RCCL's internal streams at high priority: the step runs on a high-priority stream
+            # (engine.prioritize_step_stream) and the gradient exchange must not queue behind it
+            os.environ.setdefault("TORCH_NCCL_HIGH_PRIORITY", "1")
         dist.init_process_group(backend=backend, rank=rank, world_size=world)
     return rank, world, local
 
@@ -69,7 +72,10 @@ class GradReducer:
         self.tail = [(a, min(n, a + step)) for a in range(d1, n, step)]
         if d0 > 0:
             self.tail = [(a, min(d0, a + step)) for a in range(0, d0, step)] + self.tail
-        self.stream = torch.cuda.Stream(device=flat_grad.device) if (use_stream and flat_grad.is_cuda) else None
+        # high priority like the step stream (engine.prioritize_step_stream): bucket all-reduces
+        # start as soon as their gradients are ready instead of waiting behind the backward
+        self.stream = (torch.cuda.Stream(device=flat_grad.device, priority=-1)
+                       if (use_stream and flat_grad.is_cuda) else None)
         self._next = 0
         self._works = []
         self.enabled = True          # False inside ArenaDDP.no_sync(): gradients accumulate locally
