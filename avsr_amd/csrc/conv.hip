@@ -513,7 +513,8 @@ static WgradPlan wgrad_plan(const avsr_conv_params* p, bool glds, bool with_ws) 
   if (splits <= 0) {
     // slab: ~2 full rounds of 512 block slots (2 per CU), rounded DOWN so the last round is
     // not a 1-block tail (513 blocks cost 2 rounds: measured 812 -> ~550 us on stage 1)
-    const long target = w.slab ? 1024 : 2048;
+    static const long env_target = getenv("AVSR_CONV_WGRAD_TARGET") ? atol(getenv("AVSR_CONV_WGRAD_TARGET")) : 0;
+    const long target = env_target > 0 ? env_target : (w.slab ? 1024 : 2048);   // env: A/B experiments
     const long want = w.slab ? (target / tiles > 0 ? target / tiles : 1) : (target + tiles - 1) / tiles;
     const long maxs = w.slab ? (K + 1023) / 1024 : (K + 2047) / 2048;
     splits = want < maxs ? want : maxs;

@@ -66,7 +66,8 @@ def wgrad_splitk(M, N, K):
     forced = os.environ.get("AVSR_WGRAD_SPLIT")          # experiments (tools/gemm_table.py)
     if forced:
         return max(1, min(int(forced), M // 256))
-    return 1 if tiles > 256 else max(1, min(16, 512 // max(tiles, 1), M // 512))
+    target = int(os.environ.get("AVSR_WGRAD_TARGET", "512"))   # block target (A/B experiments)
+    return 1 if tiles > target // 2 else max(1, min(16, target // max(tiles, 1), M // 512))
 
 
 def _pad8(n):
