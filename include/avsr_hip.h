@@ -34,7 +34,9 @@ enum { AVSR_E_SHAPE = 1001, AVSR_E_ALIGN = 1002, AVSR_E_DTYPE = 1003, AVSR_E_ARG
 const char* avsr_version(void);
 
 /* ------------------------------------------------------------------------------------
- * GEMM with fused epilogue (bf16 MFMA 32x32x16 tiles, fp32 accumulate).
+ * GEMM with fused epilogue, fp32 accumulate: v_mfma_f32_16x16x32_bf16 on the LDS-DMA core
+ * (128x128 / 192x128 tiles, bf16), v_mfma_f32_32x32x16_bf16 on the register-staged core
+ * (fp32 parity mode: bf16 hi/lo split; shapes under 128 rows / columns).
  *   C[b][m][n] = epi( alpha * sum_k A(b,m,k) * B(b,n,k) )
  *   A(m,k) = A[m*lda + k] if a_kmajor else A[k*lda + m]
  *   B(n,k) = B[n*ldb + k] if b_kmajor else B[k*ldb + n]
