@@ -258,6 +258,7 @@ SYMBOLS = {
     "avsr_ew_bwd": ([ctypes.POINTER(EwParams), _c_p], _i),
     "avsr_colsum_defer": ([_i], _i),
     "avsr_colsum_flush": ([_c_p], _i),
+    "avsr_colsum_inline": ([_i], _i),
     "avsr_dropout_fwd": ([ctypes.POINTER(EwParams), _c_p], _i),
     "avsr_mask_rows": ([_i, _i, _i, _i, _c_p, _i64, _c_p, _c_p], _i),
     "avsr_embed_fwd": ([ctypes.POINTER(EmbedParams), _c_p], _i),

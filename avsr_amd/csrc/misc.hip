@@ -380,13 +380,13 @@ __global__ __launch_bounds__(COLSUM_THREADS) void colsum_batch_kernel(ColsumBatc
   if ((int)blockIdx.x * 32 >= b.N[d]) return;          // block-uniform
   colsum_block(b.ws[d], b.nb[d], b.ld[d], b.N[d], b.out[d], b.N1[d], b.out1[d], blockIdx.x);
 }
-struct ColsumQueue { bool on = false; std::vector<ColsumBatch> full; ColsumBatch cur; int n = 0; int maxn = 0; };
+struct ColsumQueue { bool on = false, inl = false; std::vector<ColsumBatch> full; ColsumBatch cur; int n = 0; int maxn = 0; };
 ColsumQueue g_colsum;
 
 }  // namespace
 
 int colsum_launch(const float* ws, int nb, int64_t ld, int N, float* out, int N1, float* out1, hipStream_t st) {
-  if (!g_colsum.on) {
+  if (!g_colsum.on || g_colsum.inl) {
     hipLaunchKernelGGL(colsum_finalize_kernel, colsum_grid(N), dim3(COLSUM_THREADS), 0, st, ws, nb, ld, N, out, N1, out1);
     AVSR_CHECK_LAUNCH();
     return 0;
@@ -408,6 +408,12 @@ extern "C" int avsr_colsum_defer(int on) {
     g_colsum.full.clear();            // drop them rather than reduce workspaces that may be gone
     g_colsum.n = 0; g_colsum.maxn = 0;
   }
+  return was;
+}
+
+extern "C" int avsr_colsum_inline(int on) {
+  const int was = g_colsum.inl ? 1 : 0;
+  g_colsum.inl = on != 0;
   return was;
 }
 

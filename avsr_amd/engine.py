@@ -38,6 +38,8 @@ _BN_FUSE = os.environ.get("AVSR_BN_FUSE", "1") == "1"
 _DB_FUSE = os.environ.get("AVSR_DB_FUSE", "1") == "1"
 # parameter-gradient column-sum finalise passes batched per flush (ops.colsum_defer)
 _COLSUM_DEFER = os.environ.get("AVSR_COLSUM_DEFER", "1") == "1"
+# bias gradients of operands only the side stream's weight-grads read run on the side stream
+_SIDE_BIAS = os.environ.get("AVSR_SIDE_BIAS", "1") == "1"
 
 
 _STEP_STREAMS = {}
@@ -320,6 +322,13 @@ class Engine:
         if fused and _DB_FUSE:
             return
         ops.ew_bwd(g, db=db, alpha=alpha)
+
+    def _bias_grad_side(self, g, db):
+        """db += column sums of g on the weight-grad side stream (off the data-gradient chain; g is
+        an operand the side stream's weight-grad reads anyway), finalised there at once"""
+        if self.side is None or not _SIDE_BIAS:
+            return self._bias_grad(g, db)
+        self._on_side(lambda: ops.ew_bwd(g, db=db, inline=True), g)
 
     # ------------------------------------------------------------------------ batch prep
     def _stage(self, host_i32):
@@ -677,7 +686,7 @@ class Engine:
             ops.cast(dq32, dqkv[:, :D])
         names_b = [a + "q_proj.bias", a + "k_proj.bias", a + "v_proj.bias"]
         names_w = [a + "q_proj.weight", a + "k_proj.weight", a + "v_proj.weight"]
-        self._bias_grad(dqkv, self.arena.span(names_b, buf="g"))
+        self._bias_grad_side(dqkv, self.arena.span(names_b, buf="g"))
         self._wgrad(dqkv, lc["ln1"], self.arena.span(names_w, buf="g"))
         dln1 = ops.linear_dgrad(dqkv, self.arena.span(names_w))
         return self._ln_bwd(dln1, lc["x"], p + "layer_norm", lc["m1"], lc["r1"], dres=dx1, dx=dx1)

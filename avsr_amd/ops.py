@@ -525,13 +525,25 @@ def colsum_flush():
         _COLSUM["keep"].clear()
 
 
-def ew_bwd(dy, *, out=None, gate=None, act=L.ACT_NONE, drop_p=0.0, seed=0, alpha=1.0, db=None):
+def ew_bwd(dy, *, out=None, gate=None, act=L.ACT_NONE, drop_p=0.0, seed=0, alpha=1.0, db=None, inline=False):
+    """elementwise backward (dropout / activation gate) and/or bias gradient db += alpha * column
+    sums; inline=True finalises the column sums at once on the current stream even while the
+    finalise passes are deferred (a bias gradient issued on the weight-grad side stream)"""
     rows, N = dy.shape
-    ws = None if db is None else _colsum_ws(256 * N, dy.device)   # AVSR_EW_WS
-    _call("avsr_ew_bwd", L.fill(L.EwParams, dtype=dtype_code(dy), rows=rows, N=N, dy=dy, lddy=dy.stride(0), ws=ws,
-                                 out=out, ldout=0 if out is None else out.stride(0), gate=gate,
-                                 ldgate=0 if gate is None else gate.stride(0), act=act, drop_p=float(drop_p),
-                                 seed=int(seed) & (2 ** 64 - 1), alpha=alpha, db=db))
+    lib = L.load()
+    if inline and db is not None:
+        ws = torch.empty(256 * N, device=dy.device)       # consumed by the inline finalise
+        prev = lib.avsr_colsum_inline(1)
+    else:
+        ws = None if db is None else _colsum_ws(256 * N, dy.device)   # AVSR_EW_WS
+    try:
+        _call("avsr_ew_bwd", L.fill(L.EwParams, dtype=dtype_code(dy), rows=rows, N=N, dy=dy, lddy=dy.stride(0),
+                                     ws=ws, out=out, ldout=0 if out is None else out.stride(0), gate=gate,
+                                     ldgate=0 if gate is None else gate.stride(0), act=act, drop_p=float(drop_p),
+                                     seed=int(seed) & (2 ** 64 - 1), alpha=alpha, db=db))
+    finally:
+        if inline and db is not None:
+            lib.avsr_colsum_inline(prev)
     return out
 
 

@@ -385,6 +385,10 @@ int avsr_ew_bwd(const avsr_ew_params* p, void* stream);
  * ~200 separate 5 us finalise launches become one per encoder layer.) */
 int avsr_colsum_defer(int on);
 int avsr_colsum_flush(void* stream);
+/* avsr_colsum_inline(1): finalise passes launch at once on their producer's stream even while
+ * deferral is on (the queue is left untouched) -- for a column sum issued on another stream
+ * than the flush (the weight-grad side stream); returns the previous setting */
+int avsr_colsum_inline(int on);
 int avsr_dropout_fwd(const avsr_ew_params* p, void* stream);
 int avsr_mask_rows(int dtype, int B, int T, int N, void* x, int64_t ldx, const int* len, void* stream);
 
