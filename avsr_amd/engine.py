@@ -40,6 +40,8 @@ _DB_FUSE = os.environ.get("AVSR_DB_FUSE", "1") == "1"
 _COLSUM_DEFER = os.environ.get("AVSR_COLSUM_DEFER", "1") == "1"
 # bias gradients of operands only the side stream's weight-grads read run on the side stream
 _SIDE_BIAS = os.environ.get("AVSR_SIDE_BIAS", "1") == "1"
+# the CTC branch of the forward runs on the side stream beside the decoder forward
+_CTC_SIDE = os.environ.get("AVSR_CTC_SIDE", "1") == "1"
 
 
 _STEP_STREAMS = {}
@@ -887,26 +889,35 @@ class Engine:
         modality = self.draw_modality(train) if self.force_modality is None else self.force_modality[0]
         self.last_modality = modality
         enc, ectx = self.encoder_fwd(audios.to(self.device), videos.to(self.device), bt, train, need_grad, seeds, modality)
-        # CTC branch: ctc_lo(dropout(enc))
+        # CTC branch: ctc_lo(dropout(enc)). It runs on the side stream (idle during the forward),
+        # beside the decoder forward, whose small launches leave most CUs free; buffers are
+        # allocated on the step stream, which waits for the branch before the loss combine
         sd_c = seeds.next()
         p_c = cfg.dropout_rate if train else 0.0
-        xin = enc
-        if p_c > 0:
-            xin = self._e(M, self.D)
-            ops.dropout_fwd(enc, xin, p_c, sd_c)
+        xin = self._e(M, self.D) if p_c > 0 else enc
         clog = self._e(M, self.Vp)
-        ops.linear_fwd(xin, self.w("ctc.ctc_lo.weight"), self.arena.master("ctc.ctc_lo.bias"), out=clog[:, :self.V])
         clse = self._e(M, dtype=torch.float32)
-        ops.row_lse(clog, self.V, clse)
         Lmax = bt["ctc_lab"].shape[1]
         S = 2 * Lmax + 1
         alpha = self._e(B, T, S, dtype=torch.float32)
         gamma = self._e(B, T, S, dtype=torch.float32)
         nll = self._e(B, dtype=torch.float32)
         cp = ops.ctc_params(clog, B, T, self.V, bt["ctc_lab"], bt["ctc_len"], bt["lens"], clse, alpha, gamma, nll)
-        ops.ctc_fwd(cp)
+
+        def ctc_branch():
+            if p_c > 0:
+                ops.dropout_fwd(enc, xin, p_c, sd_c)
+            ops.linear_fwd(xin, self.w("ctc.ctc_lo.weight"), self.arena.master("ctc.ctc_lo.bias"),
+                           out=clog[:, :self.V])
+            ops.row_lse(clog, self.V, clse)
+            ops.ctc_fwd(cp)
+        if _CTC_SIDE:
+            self._on_side(ctc_branch, enc, xin, clog, clse, alpha, gamma, nll, bt["ctc_lab"], bt["ctc_len"], bt["lens"])
+        else:
+            ctc_branch()
         # attention branch
         dlog, dctx = self.decoder_fwd(enc, bt, train, need_grad, seeds)
+        self.join_side()
         R = dlog.shape[0]
         dlse = self._e(R, dtype=torch.float32)
         rloss = self._e(R, dtype=torch.float32)
