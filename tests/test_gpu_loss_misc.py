@@ -214,8 +214,10 @@ def test_stem_as_2d_conv(dev, dtype):
     assert _rel(gw, wr.grad) < (1e-4 if dtype == torch.float32 else 2e-2)
 
 
-def test_weightnorm(dev):
-    O, K, C = 96, 16, 8
+@pytest.mark.parametrize("O,K,C", [(96, 16, 8), (1024, 128, 64), (40, 6, 6)])
+def test_weightnorm(dev, O, K, C):
+    """weight norm over dims (0, 1) of the torch (out, in/groups, k) weight: vectorised
+    reduction (C % 4 == 0, incl. the pos-conv shape) and the scalar one (C = 6)"""
     g = torch.Generator().manual_seed(2)
     v = torch.randn(O, C, K, generator=g)          # torch layout (out, in/groups, k)
     gg = 1 + 0.1 * torch.randn(1, 1, K, generator=g)
