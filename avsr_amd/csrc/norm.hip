@@ -4,6 +4,7 @@
 // one pass per tensor where the math allows.
 #include <algorithm>
 #include <cstdlib>
+#include <cstring>
 
 #include "common.h"
 
@@ -165,7 +166,8 @@ __global__ __launch_bounds__(64 * W) void ln_bwd_kernel(LnArgs a) {
 static void ln_bwd_shape(int& W, int& R) {
   W = 4; R = 1;
   const char* e = getenv("AVSR_LN_BWD");
-  if (e && e[0] && e[1] == ',') { W = e[0] == '1' ? 16 : e[0] - '0'; R = atoi(e + 2); }
+  const char* comma = e ? strchr(e, ',') : nullptr;
+  if (comma) { W = atoi(e); R = atoi(comma + 1); }
   if (W != 4 && W != 8 && W != 16) W = 8;
   if (R != 1 && R != 2) R = 2;
 }
