@@ -168,8 +168,15 @@ static void ln_bwd_shape(int& W, int& R) {
   const char* e = getenv("AVSR_LN_BWD");
   const char* comma = e ? strchr(e, ',') : nullptr;
   if (comma) { W = atoi(e); R = atoi(comma + 1); }
-  if (W != 4 && W != 8 && W != 16) W = 8;
+  if (W != 2 && W != 4 && W != 8 && W != 16) W = 8;
   if (R != 1 && R != 2) R = 2;
+}
+
+// AVSR_LN_BWD_BLOCKS caps the backward grid below AVSR_LN_BLOCKS (the workspace bound)
+static int ln_bwd_blocks() {
+  const char* e = getenv("AVSR_LN_BWD_BLOCKS");
+  const int b = e ? atoi(e) : 0;
+  return b > 0 && b < AVSR_LN_BLOCKS ? b : AVSR_LN_BLOCKS;
 }
 
 template <typename T>
@@ -190,7 +197,7 @@ int ln_launch(const avsr_layernorm_params* p, bool bwd, hipStream_t st) {
   }
   if (bwd && p->dgamma && (!p->ws || p->N > 2048)) return AVSR_E_ARG;
   while (W > 4 && (size_t)W * p->N * sizeof(float) > 64 * 1024) W >>= 1;   // default dynamic-LDS limit
-  if (bwd) blocks = std::min((p->rows + W - 1) / W, AVSR_LN_BLOCKS);
+  if (bwd) blocks = std::min((p->rows + W - 1) / W, ln_bwd_blocks());
   const size_t red = (size_t)W * p->N * sizeof(float);
 #define LNB(V, W_, R_) hipLaunchKernelGGL((ln_bwd_kernel<T, V, W_, R_>), dim3(blocks), dim3(64 * W_), red, st, a)
 #define LNL(V)                                                                                   \
@@ -198,7 +205,8 @@ int ln_launch(const avsr_layernorm_params* p, bool bwd, hipStream_t st) {
     if (bwd) {                                                                                   \
       if (W == 16) { if (R == 2) LNB(V, 16, 2); else LNB(V, 16, 1); }                            \
       else if (W == 8) { if (R == 2) LNB(V, 8, 2); else LNB(V, 8, 1); }                          \
-      else { if (R == 2) LNB(V, 4, 2); else LNB(V, 4, 1); }                                      \
+      else if (W == 4) { if (R == 2) LNB(V, 4, 2); else LNB(V, 4, 1); }                          \
+      else { if (R == 2) LNB(V, 2, 2); else LNB(V, 2, 1); }                                      \
       if (p->dgamma) {                                                                           \
         AVSR_CHECK_LAUNCH();                                                                     \
         return colsum_launch((const float*)p->ws, blocks, (int64_t)2 * p->N, 2 * p->N, p->dgamma, \

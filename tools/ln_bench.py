@@ -21,7 +21,7 @@ for rows, N in ((6000, 1024), (656, 512), (6000, 2048)):
     db = torch.zeros(N, device=dev)
     line = f"rows {rows} N {N}:"
     ref = None
-    for shape in ("4,1", "4,2", "8,1", "8,2", "16,1", "16,2"):
+    for shape in ("4,1", "2,1", "2,2", "4,2", "8,1", "8,2", "16,1", "16,2"):
         os.environ["AVSR_LN_BWD"] = shape
         dg.zero_(); db.zero_()
         dx = ops.layernorm_bwd(dy, x, g, mean, rstd, dres=dres, dgamma=dg, dbeta=db)
