@@ -162,7 +162,8 @@ __global__ __launch_bounds__(64 * W) void ln_bwd_kernel(LnArgs a) {
 
 // LayerNorm backward launch shape: AVSR_LN_BWD = "W,R" (waves per block, rows in flight per
 // wave) for experiments. Default 4,1: in isolation (tools/ln_bench.py) 6000 x 1024 takes
-// 18.6-20.4 us under every shape, and 8-16 waves lose 2x at N = 2048
+// 18.3-20.1 us with 4-8 waves (2 waves: 26 us; 16 waves: 38 us), 8-16 waves lose 2x at N = 2048,
+// and in the step 4,1 beats 2,x and 8,x by 0.5-1 % (profiles/r02_ln_bwd_shape_ab.txt)
 static void ln_bwd_shape(int& W, int& R) {
   W = 4; R = 1;
   const char* e = getenv("AVSR_LN_BWD");
