@@ -40,6 +40,7 @@ class GemmParams(ctypes.Structure):
         ("ws", _c_p),
         ("db", _c_p),
         ("db_ws", _c_p),
+        ("stamp", _c_p),
     ]
 
 
@@ -271,7 +272,7 @@ SYMBOLS = {
     "avsr_audio_pack": ([_i, _i, _i, _i, _c_p, _c_p, _c_p], _i),
     "avsr_weightnorm_fwd": ([_i, _i, _i, _i, _c_p, _c_p, _c_p, _c_p, _c_p], _i),
     "avsr_weightnorm_bwd": ([_i, _i, _i, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p], _i),
-    "avsr_sumsq": ([_c_p, _i64, _c_p, _c_p], _i),
+    "avsr_sumsq": ([_c_p, _i64, _c_p, _c_p, _c_p], _i),
     "avsr_adamw": ([ctypes.POINTER(AdamWParams), _c_p], _i),
     "avsr_log_softmax_rows": ([_i, _i, _i, _c_p, _i64, _c_p, _i64, _c_p], _i),
     "avsr_dec_attn": ([ctypes.POINTER(DecAttnParams), _c_p], _i),

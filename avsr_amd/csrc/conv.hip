@@ -72,7 +72,8 @@ __global__ __launch_bounds__(NT) void conv_kernel(ConvArgs a) {
     mainloop<T, WM, WN>(la, lb, m0, n0, kbeg, kend, acc, smem);
   }
   Epi e = a.e;
-  e.C = (OutT*)e.C + (int64_t)grp * a.c_gstride;
+  if (KIND == K_WGRAD && a.ws) e.C = a.ws + ((int64_t)grp * a.splits + sp) * a.M * a.N;
+  else e.C = (OutT*)e.C + (int64_t)grp * a.c_gstride;
   if (e.res) e.res = (const T*)e.res + (int64_t)grp * a.c_gstride;
   if (e.preact) e.preact = (T*)e.preact + (int64_t)grp * a.c_gstride;
   if (e.bias) e.bias += (int64_t)grp * a.c_gstride;
@@ -509,7 +510,7 @@ static WgradPlan wgrad_plan(const avsr_conv_params* p, bool glds, bool with_ws) 
   WgradPlan w;
   const int kq = glds ? GBK : BKE;
   long splits = p->splitk;
-  w.slab = glds && with_ws;
+  w.slab = with_ws;   // deterministic: per-split slabs + an ordered reduce (no fp32 atomics)
   if (splits <= 0) {
     // slab: ~2 full rounds of 512 block slots (2 per CU), rounded DOWN so the last round is
     // not a 1-block tail (513 blocks cost 2 rounds: measured 812 -> ~550 us on stage 1)
@@ -526,22 +527,29 @@ static WgradPlan wgrad_plan(const avsr_conv_params* p, bool glds, bool with_ws) 
   return w;
 }
 
-// dw[g] += sum over a chunk of splits of ws[g][s]; chunks > 1 combine with fp32 atomics
-// (chunks x M x N of them, a few hundred thousand at most)
-__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* ws, int splits, int chunks, int64_t mn,
+// dw[g] += sum over the splits of ws[g][s], in split order (deterministic). With chunks > 1
+// (few output elements, many splits) a first pass folds each chunk of splits into its first
+// slab (in place), and a second pass (chunks == -nchunks) sums those chunk heads in order.
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(float* ws, int splits, int chunks, int64_t mn,
                                                            float* dw, int64_t dw_gstride) {
   const int g = blockIdx.y, c = blockIdx.z;
-  const int s0 = (int)((int64_t)splits * c / chunks), s1 = (int)((int64_t)splits * (c + 1) / chunks);
-  const float* w = ws + (int64_t)g * splits * mn;
+  float* w = ws + (int64_t)g * splits * mn;
   float* d = dw + (int64_t)g * dw_gstride;
+  const int nch = chunks < 0 ? -chunks : chunks;
   for (int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4; i < mn; i += (int64_t)gridDim.x * 1024) {
     f32x4 s = {0.f, 0.f, 0.f, 0.f};
-    for (int q = s0; q < s1; ++q) s += *(const f32x4*)(w + (int64_t)q * mn + i);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {       // dw is a view into the parameter arena: 4-byte aligned only
-      if (chunks == 1) d[i + r] += s[r];
-      else atomicAdd(d + i + r, s[r]);
+    if (chunks < 0) {            // pass 2: the chunk heads
+      for (int q = 0; q < nch; ++q) s += *(const f32x4*)(w + (int64_t)((int64_t)splits * q / nch) * mn + i);
+    } else {
+      const int s0 = (int)((int64_t)splits * c / chunks), s1 = (int)((int64_t)splits * (c + 1) / chunks);
+      for (int q = s0; q < s1; ++q) s += *(const f32x4*)(w + (int64_t)q * mn + i);
+      if (chunks > 1) {          // pass 1: fold into the chunk's first slab
+        *(f32x4*)(w + (int64_t)s0 * mn + i) = s;
+        continue;
+      }
     }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) d[i + r] += s[r];   // dw is a view into the parameter arena: 4-byte aligned only
   }
 }
 
@@ -725,10 +733,9 @@ extern "C" int avsr_conv_bwd_weight(const avsr_conv_params* p, void* stream) {
   else if (w.splits == 1) { a.e.beta = 1.f; }          // dw += wgrad, one writer per element
   else { a.e.atomic = 1; }
   hipStream_t st = (hipStream_t)stream;
-  if (p->dtype == AVSR_F32) return by_tile<float, float, K_WGRAD>(a, p->groups, st);
-  if (p->dtype != AVSR_BF16) return AVSR_E_DTYPE;
-  if (!glds) return by_tile<bf16, float, K_WGRAD>(a, p->groups, st);
-  rc = glds_by_tile<float, K_WGRAD>(a, p->groups, st);
+  if (p->dtype == AVSR_F32) rc = by_tile<float, float, K_WGRAD>(a, p->groups, st);
+  else if (p->dtype != AVSR_BF16) return AVSR_E_DTYPE;
+  else rc = !glds ? by_tile<bf16, float, K_WGRAD>(a, p->groups, st) : glds_by_tile<float, K_WGRAD>(a, p->groups, st);
   if (rc || !w.slab) return rc;
   const int64_t mn = (int64_t)a.M * a.N;
   const int xb = avsr_grid(mn / 4, 256, 1024);
@@ -736,14 +743,19 @@ extern "C" int avsr_conv_bwd_weight(const avsr_conv_params* p, void* stream) {
   if (chunks > w.splits) chunks = w.splits;
   if (chunks < 1) chunks = 1;
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)xb, (unsigned)p->groups, (unsigned)chunks), dim3(256), 0, st,
-                     (const float*)p->ws, w.splits, chunks, mn, p->dw, a.c_gstride);
+                     p->ws, w.splits, chunks, mn, p->dw, a.c_gstride);
   AVSR_CHECK_LAUNCH();
+  if (chunks > 1) {
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)xb, (unsigned)p->groups, 1u), dim3(256), 0, st,
+                       p->ws, w.splits, -chunks, mn, p->dw, a.c_gstride);
+    AVSR_CHECK_LAUNCH();
+  }
   return 0;
 }
 
 extern "C" int64_t avsr_conv_wgrad_ws(const avsr_conv_params* p) {
-  if (!p || p->dtype != AVSR_BF16 || !conv_glds_enabled()) return 0;
-  const WgradPlan w = wgrad_plan(p, true, true);
+  if (!p || (p->dtype != AVSR_BF16 && p->dtype != AVSR_F32)) return 0;
+  const WgradPlan w = wgrad_plan(p, p->dtype == AVSR_BF16 && conv_glds_enabled(), true);
   if (!w.slab) return 0;
   return (int64_t)p->groups * w.splits * p->cout * ((int64_t)p->kh * p->kw * p->cin);
 }

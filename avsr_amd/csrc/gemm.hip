@@ -18,6 +18,7 @@ struct DenseArgs {
   const void* B; int64_t ldb, sB;
   int64_t sC, sR;
   Epi e;
+  unsigned long long* stamp;   // diagnostic {min start, max end} (avsr_gemm_params.stamp) or null
 };
 
 template <typename T, typename OutT, int WM, int WN, bool AK, bool BK>
@@ -46,6 +47,7 @@ __global__ __launch_bounds__(NT) void dense_kernel(DenseArgs a) {
 template <typename OutT, bool AK, bool BK, class CF>
 __global__ __launch_bounds__(CF::NTH, CF::MINB) void dense_glds_kernel(DenseArgs a, int tiles_m, int tiles_n) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  if (a.stamp != nullptr && threadIdx.x == 0) atomicMin(a.stamp, (unsigned long long)__builtin_amdgcn_s_memrealtime());
   const int id = gemmg::xcd_remap(blockIdx.x, gridDim.x);
   int tm, tn, z;
   gemmg::tile_of(id, tiles_m, tiles_n, tm, tn, z);
@@ -75,6 +77,10 @@ __global__ __launch_bounds__(CF::NTH, CF::MINB) void dense_glds_kernel(DenseArgs
   if (e.gate) e.gate = (const bf16*)e.gate + (int64_t)bz * a.sC;
   e.drop_base = (uint64_t)bz * (uint64_t)a.M * (uint64_t)a.N;
   gemmg::epilogue_g<bf16, OutT, CF>(e, m0, n0, acc, smem);
+  if (a.stamp != nullptr) {   // uniform: every wave's stores issued before the end stamp
+    __syncthreads();
+    if (threadIdx.x == 0) atomicMax(a.stamp + 1, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+  }
 }
 
 // 256x256 ping-pong core (gemm_pp.h)
@@ -302,6 +308,7 @@ extern "C" int avsr_gemm(const avsr_gemm_params* p, void* stream) {
   }
   a.B = p->B; a.ldb = p->ldb; a.sB = p->strideB;
   a.sC = p->strideC; a.sR = p->strideR;
+  a.stamp = p->stamp;
   Epi& e = a.e;
   e.M = p->M; e.N = p->N; e.C = p->C; e.ldc = p->ldc;
   e.alpha = p->alpha; e.beta = p->beta; e.bias = p->bias;

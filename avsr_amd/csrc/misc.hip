@@ -106,16 +106,45 @@ __global__ __launch_bounds__(256) void embed_kernel(avsr_embed_params p, int bwd
         o[j] = v;
       }
       stv((T*)p.y + (int64_t)r * p.D + d0, o);
-    } else {
+    }
+  }
+}
+
+// embedding backward without atomics (deterministic): block r owns the table row of token
+// tok[r] iff r is that token's first occurrence; it adds the row gradients of every occurrence
+// in row order. Other blocks exit.
+template <typename T>
+__global__ __launch_bounds__(256) void embed_bwd_kernel(avsr_embed_params p) {
+  constexpr int VE = VecW<T>::VE;
+  const int r = blockIdx.x;
+  const int tok = p.tok[r];
+  __shared__ int seen;
+  if (threadIdx.x == 0) seen = 0;
+  __syncthreads();
+  for (int q = threadIdx.x; q < r; q += 256)
+    if (p.tok[q] == tok) seen = 1;
+  __syncthreads();
+  if (seen) return;
+  const int nv = p.D / VE;
+  for (int c = threadIdx.x; c < nv; c += 256) {
+    const int d0 = c * VE;
+    float acc[VE];
+#pragma unroll
+    for (int j = 0; j < VE; ++j) acc[j] = 0.f;
+    for (int q = r; q < p.rows; ++q) {
+      if (p.tok[q] != tok) continue;
       float g[VE];
-      ldv((const T*)p.dy + (int64_t)r * p.D + d0, g);
+      ldv((const T*)p.dy + (int64_t)q * p.D + d0, g);
 #pragma unroll
       for (int j = 0; j < VE; ++j) {
         float v = g[j] * p.scale;
-        if (p.drop_p > 0.f) v *= drop_scale(p.drop_p, p.seed, (uint64_t)r * p.D + d0 + j);
-        atomicAdd(p.dtable + (int64_t)tok * p.D + d0 + j, v);
+        if (p.drop_p > 0.f) v *= drop_scale(p.drop_p, p.seed, (uint64_t)q * p.D + d0 + j);
+        acc[j] += v;
       }
     }
+    float* dt = p.dtable + (int64_t)tok * p.D + d0;
+#pragma unroll
+    for (int j = 0; j < VE; ++j) dt[j] += acc[j];
   }
 }
 
@@ -293,7 +322,9 @@ __global__ void wn_dg_kernel(int K, const float* s, const float* norm, float* dg
   if (k < K) dg[k] += s[k] / norm[k];
 }
 
-__global__ __launch_bounds__(256) void sumsq_kernel(const float* x, int64_t n, float* out) {
+// sum of squares in two deterministic passes: per-block partials -> ws, then one block sums
+// them in a fixed order and adds the total to *out
+__global__ __launch_bounds__(256) void sumsq_kernel(const float* x, int64_t n, float* ws) {
   float s = 0.f;
   const int64_t n4 = n / 4;
   for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
@@ -306,7 +337,17 @@ __global__ __launch_bounds__(256) void sumsq_kernel(const float* x, int64_t n, f
   __shared__ float sh[4];
   if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = s;
   __syncthreads();
-  if (threadIdx.x == 0) atomicAdd(out, sh[0] + sh[1] + sh[2] + sh[3]);
+  if (threadIdx.x == 0) ws[blockIdx.x] = (sh[0] + sh[1]) + (sh[2] + sh[3]);
+}
+
+__global__ __launch_bounds__(256) void sumsq_final_kernel(const float* ws, int nb, float* out) {
+  float s = 0.f;
+  for (int i = threadIdx.x; i < nb; i += 256) s += ws[i];
+  s = wave_sum(s);
+  __shared__ float sh[4];
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) *out += (sh[0] + sh[1]) + (sh[2] + sh[3]);
 }
 
 struct AdamCoef { float coef, step, rbc2, decay; };
@@ -489,6 +530,13 @@ extern "C" int avsr_mask_rows(int dtype, int B, int T, int N, void* x, int64_t l
 static int embed_launch(const avsr_embed_params* p, int bwd, hipStream_t st) {
   const int ve = p->dtype == AVSR_BF16 ? 8 : 4;
   if (p->D % ve) return AVSR_E_SHAPE;
+  if (p->rows <= 0) return 0;
+  if (bwd) {
+    if (p->dtype == AVSR_BF16) hipLaunchKernelGGL(embed_bwd_kernel<bf16>, dim3(p->rows), dim3(256), 0, st, *p);
+    else hipLaunchKernelGGL(embed_bwd_kernel<float>, dim3(p->rows), dim3(256), 0, st, *p);
+    AVSR_CHECK_LAUNCH();
+    return 0;
+  }
   const int g = avsr_grid((int64_t)p->rows * p->D / ve);
   if (p->dtype == AVSR_BF16) hipLaunchKernelGGL(embed_kernel<bf16>, dim3(g), dim3(256), 0, st, *p, bwd);
   else hipLaunchKernelGGL(embed_kernel<float>, dim3(g), dim3(256), 0, st, *p, bwd);
@@ -597,9 +645,13 @@ extern "C" int avsr_weightnorm_bwd(int O, int K, int C, const float* v, const fl
   return 0;
 }
 
-extern "C" int avsr_sumsq(const float* x, int64_t n, float* out, void* stream) {
+extern "C" int avsr_sumsq(const float* x, int64_t n, float* out, float* ws, void* stream) {
   if (!avsr_aligned16(x)) return AVSR_E_ALIGN;
-  hipLaunchKernelGGL(sumsq_kernel, dim3(avsr_grid(n / 4 + 1, 256, 1024)), dim3(256), 0, (hipStream_t)stream, x, n, out);
+  if (!out || !ws) return AVSR_E_ARG;
+  const int nb = avsr_grid(n / 4 + 1, 256, AVSR_SUMSQ_WS);
+  hipLaunchKernelGGL(sumsq_kernel, dim3(nb), dim3(256), 0, (hipStream_t)stream, x, n, ws);
+  AVSR_CHECK_LAUNCH();
+  hipLaunchKernelGGL(sumsq_final_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, (const float*)ws, nb, out);
   AVSR_CHECK_LAUNCH();
   return 0;
 }

@@ -58,6 +58,12 @@ def prioritize_step_stream(device):
     s = _STEP_STREAMS.get(idx)
     if s is None:
         s = _STEP_STREAMS[idx] = torch.cuda.Stream(device=idx, priority=-1)
+    # work already queued on the stream that was current (engine setup: arena copies, the
+    # bf16 shadow cast) must finish before the step stream reads it: side streams created by
+    # torch are non-blocking w.r.t. the legacy default stream
+    prev = torch.cuda.current_stream(idx)
+    if prev != s:
+        s.wait_stream(prev)
     torch.cuda.set_stream(s)
     return s
 
@@ -359,6 +365,8 @@ class Engine:
         """index tensors of a batch (labels / lengths are host data in the collator layout; a
         device tensor is read back once). All of them reach the device in ONE asynchronous copy."""
         B, _, T = videos.shape[:3]
+        if video_lengths.is_cuda and (labels is None or labels.is_cuda):
+            return self._prepare_device(B, T, video_lengths, labels)
         lens = video_lengths.detach().cpu().to(torch.int64)
         b = {"B": B, "T": T, "lens_host": lens, "full": bool((lens == T).all())}
         parts = [lens.to(torch.int32)]
@@ -386,6 +394,39 @@ class Engine:
         b["lens"] = views[0]
         if labels is not None:
             b.update(L1=L1, ys_in=views[1], ys_out=views[2], ctc_lab=views[3].view(B, Lmax), ctc_len=views[4])
+        return b
+
+    def _prepare_device(self, B, T, video_lengths, labels):
+        """prepare() for lengths / labels already on the device (HF Trainer moves the whole
+        batch there): every index tensor is built by device ops, nothing is read back, so the
+        host keeps issuing ahead of the GPU. Shapes come from the padded label width Lw
+        (= the collator's max label count, avhubert_dataset.py:302-311): the decoder runs
+        L1 = Lw + 1 positions. Columns past a row's labels are eos inputs with ignored (-1)
+        targets behind a causal mask, so losses and gradients equal those of L1 = max len + 1."""
+        dev = self.device
+        b = {"B": B, "T": T, "lens_host": None, "full": False,
+             "lens": video_lengths.detach().to(dev, torch.int32)}
+        if labels is None:
+            return b
+        lab = labels.detach().to(dev)
+        Lw = lab.shape[1]
+        eos = self.V - 1
+        valid = lab != -1
+        ylen = valid.sum(1)
+        # compaction of the non-(-1) labels of each row (the reference's ys = [y[y != ignore_id]])
+        pos = torch.where(valid, torch.cumsum(valid, 1) - 1, torch.full_like(ylen[:, None], Lw))
+        comp = torch.full((B, Lw + 1), -1, dtype=torch.int32, device=dev)
+        comp.scatter_(1, pos, lab.to(torch.int32))
+        comp = comp[:, :Lw].contiguous()
+        ar = torch.arange(Lw + 1, device=dev)[None]
+        ys_out = torch.full((B, Lw + 1), -1, dtype=torch.int32, device=dev)
+        ys_out[:, :Lw] = comp
+        ys_out = torch.where(ar == ylen[:, None], torch.full_like(ys_out, eos), ys_out)
+        ys_in = torch.full((B, Lw + 1), eos, dtype=torch.int32, device=dev)
+        ys_in[:, 1:] = torch.where(comp >= 0, comp, torch.full_like(comp, eos))
+        ctc_lab = comp if Lw > 0 else torch.full((B, 1), -1, dtype=torch.int32, device=dev)
+        b.update(L1=Lw + 1, ys_in=ys_in.reshape(-1), ys_out=ys_out.reshape(-1), ctc_lab=ctc_lab,
+                 ctc_len=ylen.to(torch.int32))
         return b
 
     # ===================================================================== video frontend
@@ -950,6 +991,21 @@ class Engine:
         prev = ops.colsum_defer(_COLSUM_DEFER)
         try:
             self._backward(ctx, d_ctc, d_att)
+            ops.colsum_flush()
+        finally:
+            ops.colsum_defer(prev)
+        if self.after_backward is not None:
+            self.after_backward()
+        self.join_side()
+
+    def encoder_backward(self, ectx, denc):
+        """encoder-only backward (the reference call form model.encoder(...) trained alone,
+        surface._EncoderStep) with backward()'s data-parallel hooks and finalise batching"""
+        if self.before_backward is not None:
+            self.before_backward()
+        prev = ops.colsum_defer(_COLSUM_DEFER)
+        try:
+            self.encoder_bwd(ectx, denc)
             ops.colsum_flush()
         finally:
             ops.colsum_defer(prev)

@@ -13,7 +13,9 @@ from . import _lib as L
 _DT = {torch.float32: L.AVSR_F32, torch.bfloat16: L.AVSR_BF16}
 
 # optional launch probes (bench.py): {"gemm": {"match": fn(M, N, K, ak, bk, dtype) -> bool,
-# "events": [(start, end), ...]}} — HIP events recorded on the launching (current) stream
+# "stamps": int64 device tensor [2 * max launches] initialised to {-1, 0} pairs (the kernel's
+# in-kernel first-start / last-end s_memrealtime stamps, 100 MHz), "events": [(start, end)]}}
+# — HIP events recorded on the launching (current) stream beside them
 PROBE = {}
 
 SLAB_PAD = 1088   # AVSR_GEMM_SLAB_PAD
@@ -77,6 +79,12 @@ def gemm(A, B, C, *, M, N, K, a_kmajor, b_kmajor, lda, ldb, ldc, batch=1,
         p.db, p.db_ws = db.data_ptr(), db_ws.data_ptr()
     probe = PROBE.get("gemm")
     if probe is not None and probe["match"](M, N, K, a_kmajor, b_kmajor, dt):
+        # in-kernel {first start, last end} stamps of this launch (s_memrealtime, 100 MHz) in
+        # a preallocated int64 buffer; plus HIP events on the launching stream for comparison
+        i = len(probe["events"])
+        st = probe["stamps"]
+        assert 2 * i + 2 <= st.numel(), "probe stamp buffer full"
+        p.stamp = st[2 * i:].data_ptr()
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         s.record()
         L.check(lib.avsr_gemm(ctypes.byref(p), L.stream_ptr()), "avsr_gemm")
@@ -515,6 +523,8 @@ def colsum_defer(on):
     prev = _COLSUM["on"]
     L.load().avsr_colsum_defer(int(bool(on)))
     _COLSUM["on"] = bool(on)
+    if not on:      # the C side drops passes still queued (an aborted step): so do we
+        _COLSUM["keep"].clear()
     return prev
 
 
@@ -628,8 +638,16 @@ def weightnorm_bwd(v, g, norm, dw, dv, dg, scratch):
             "avsr_weightnorm_bwd")
 
 
-def sumsq(x, out):
-    L.check(L.load().avsr_sumsq(x.data_ptr(), x.numel(), out.data_ptr(), L.stream_ptr()), "avsr_sumsq")
+SUMSQ_WS = 1024   # AVSR_SUMSQ_WS
+
+
+def sumsq(x, out, ws=None):
+    """out += sum(x^2) in a fixed summation order (two passes through ws, no atomics)"""
+    if ws is None:
+        ws = torch.empty(SUMSQ_WS, device=x.device)
+    assert ws.dtype == torch.float32 and ws.numel() >= SUMSQ_WS
+    L.check(L.load().avsr_sumsq(x.data_ptr(), x.numel(), out.data_ptr(), ws.data_ptr(), L.stream_ptr()),
+            "avsr_sumsq")
     return out
 
 

@@ -28,6 +28,7 @@ class FusedAdamW:
         self.schedule = schedule
         self.step_count = 0
         self._sumsq = torch.zeros(1, device=arena.device)
+        self._sumsq_ws = torch.empty(ops.SUMSQ_WS, device=arena.device)
 
     def grad_sumsq(self):
         """sum of squared gradients over the trainable segments (device scalar, no sync)"""
@@ -35,7 +36,7 @@ class FusedAdamW:
         d0, _ = a.segments["decay"]
         _, n1 = a.segments["no_decay"]
         self._sumsq.zero_()
-        ops.sumsq(a.grad[d0:n1], self._sumsq)
+        ops.sumsq(a.grad[d0:n1], self._sumsq, self._sumsq_ws)
         return self._sumsq
 
     def step(self, grad_scale=1.0, sumsq_ready=False):

@@ -80,6 +80,11 @@ class GradReducer:
         self._works = []
         self.enabled = True          # False inside ArenaDDP.no_sync(): gradients accumulate locally
         self.extra_streams = []      # other streams that produce gradients (the engine's side stream)
+        # optional timing (bench.py): per reduced step, HIP events (comm start, comm end) on
+        # the comm stream and (backward end, join) on the compute stream — join - backward
+        # end is the all-reduce time the step could not hide
+        self.timing = None           # list to enable
+        self._t0 = None
 
     def _reduce(self, a, b):
         w = dist.all_reduce(self.flat[a:b], op=dist.ReduceOp.SUM, group=self.group, async_op=self.stream is not None)
@@ -98,12 +103,16 @@ class GradReducer:
         for s in self.extra_streams:             # ... including those computed on side streams
             self.stream.wait_stream(s)
         with torch.cuda.stream(self.stream):
+            if self.timing is not None and self._t0 is None:
+                self._t0 = torch.cuda.Event(enable_timing=True)
+                self._t0.record()
             for a, b in ranges:
                 self._reduce(a, b)
 
     def begin(self):
         self._next = 0
         self._works = []
+        self._t0 = None
 
     def ready(self, offset):
         """the decay segment is final from `offset` on: reduce every bucket inside it"""
@@ -126,7 +135,19 @@ class GradReducer:
                     w.wait()
                 if average:
                     self.flat.mul_(1.0 / self.world)
-            torch.cuda.current_stream(self.flat.device).wait_stream(self.stream)
+                if self.timing is not None:
+                    t1 = torch.cuda.Event(enable_timing=True)
+                    t1.record()
+            cur = torch.cuda.current_stream(self.flat.device)
+            if self.timing is not None:
+                j0, j1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                for s in self.extra_streams:      # the backward ends when its side streams do
+                    cur.wait_stream(s)
+                j0.record(cur)
+            cur.wait_stream(self.stream)
+            if self.timing is not None:
+                j1.record(cur)
+                self.timing.append((self._t0, t1, j0, j1))
         elif average:
             self.flat.mul_(1.0 / self.world)
         self._works = []

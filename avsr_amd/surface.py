@@ -62,6 +62,8 @@ class _EncoderStep(torch.autograd.Function):
 
     @staticmethod
     def forward(fctx, anchor, eng, audios, videos, bt, seeds, modality):
+        if eng.before_forward is not None:      # DDP buffer broadcast (parallel.ArenaDDP)
+            eng.before_forward()
         x, ctx = eng.encoder_fwd(audios, videos, bt, True, True, seeds, modality)
         fctx.eng, fctx.ctx = eng, ctx
         B, T = bt["B"], bt["T"]
@@ -75,7 +77,7 @@ class _EncoderStep(torch.autograd.Function):
         eng.arena.attach_grads()
         B, T, D = dout.shape
         d = to_engine(eng, dout.reshape(B * T, D), eng.dtype)
-        eng.encoder_bwd(fctx.ctx, d)
+        eng.encoder_backward(fctx.ctx, d)     # with the DDP reducer's begin / buckets / finish
         fctx.ctx = None
         return (None,) * 7
 

@@ -20,8 +20,11 @@ resume) drives the engine instead:
 """
 import copy
 import gc
+import os
+import warnings
 
 import torch
+import torch.distributed as dist
 from transformers import Trainer
 
 from .engine import prioritize_step_stream
@@ -36,6 +39,13 @@ class AVSRTrainer(Trainer):
                  preprocess_logits_for_metrics=None):
         if model is None or not hasattr(model, "setup_engine"):
             raise TypeError("AVSRTrainer trains an avsr_amd AVHubertAVSR")
+        # RCCL's internal streams at high priority like the step stream (parallel.init_from_env);
+        # must be set before the process group exists, i.e. before args.device is first read
+        if not dist.is_initialized():
+            os.environ.setdefault("TORCH_NCCL_HIGH_PRIORITY", "1")
+        elif dist.get_world_size() > 1 and os.environ.get("TORCH_NCCL_HIGH_PRIORITY") != "1":
+            warnings.warn("process group created without TORCH_NCCL_HIGH_PRIORITY=1: gradient all-reduces "
+                          "queue behind the high-priority step stream")
         args = copy.copy(args)
         self.engine_dtype = torch.bfloat16 if (args.fp16 or args.bf16) else torch.float32
         args.fp16 = args.bf16 = False          # precision is the engine's: no autocast / GradScaler
@@ -53,10 +63,6 @@ class AVSRTrainer(Trainer):
         super().__init__(**kw)
         self.valid_data_collator = valid_data_collator
         self.ddp = ArenaDDP(self.model, average=True)
-        # the import-time heap (torch, transformers) moves to the collector's permanent
-        # generation: a full collection during a step otherwise stalls the host for ~0.1 s
-        gc.collect()
-        gc.freeze()
         # keep accelerate from wrapping the engine model in DistributedDataParallel
         prepare_model = self.accelerator.prepare_model
 
@@ -67,6 +73,17 @@ class AVSRTrainer(Trainer):
 
         self.accelerator.prepare_model = _prepare_model
         self._arena_opt = None
+
+    def train(self, *args, **kwargs):
+        """HF Trainer.train with the heap alive at its start in the collector's permanent
+        generation for the duration of training (a full collection inside a step stalls the
+        host for ~0.1 s, profiles/r02_gc_stall_ab.txt); unfrozen again when training ends."""
+        gc.collect()
+        gc.freeze()
+        try:
+            return super().train(*args, **kwargs)
+        finally:
+            gc.unfreeze()
 
     # ---------------------------------------------------------------- optimizer / clipping
     def create_optimizer(self, model=None):

@@ -7,18 +7,28 @@ L = 40 labels), train mode (dropouts on), bf16 compute / fp32 master weights.
 Inputs are resident in HBM before the timed region (SURVEY.md §8(d) d1 recipe).
 
   python bench.py [--gpus N --steps K --warmup W]
-  (N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N)
+
+With N > 1 and no torch.distributed.run environment (WORLD_SIZE unset) this process is only
+a launcher: it never touches the GPU, starts N child ranks of itself with RANK / WORLD_SIZE /
+LOCAL_RANK / MASTER_ADDR=127.0.0.1 / MASTER_PORT set, relays rank 0's JSON line and exits
+non-zero if any rank fails (reference: torchrun over script/train.py:23,259-308). Under
+`python -m torch.distributed.run ... bench.py --gpus N` the ranks run directly.
 
 Prints ONE JSON line (rank 0). `roofline` is measured live on the probe kernel (the encoder
-FFN up-projection GEMM, 6000x4096x1024 bf16, 24 launches per step) with HIP events on the
-stream it is launched on; `cpu_baseline` times the repo's CPU restatement of the same model
-(oracle/, "port") on the host cores on a bounded sample.
+FFN up-projection GEMM, 6000x4096x1024 bf16, 24 launches per step) from in-kernel
+s_memrealtime stamps (first workgroup start to last workgroup end of each launch);
+`cpu_baseline` times the repo's CPU restatement of the same model (oracle/, "port") on the
+host cores on a bounded sample. `--cpu-selftest` (no GPU, gloo) exercises the launcher and the
+bucketed all-reduce only — it measures nothing and is what the CPU test suite runs.
 """
 import argparse
 import gc
 import json
 import os
+import socket
+import subprocess
 import sys
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -31,8 +41,66 @@ import torch.distributed as dist  # noqa: E402
 METRIC = "AV-frames/sec/GPU (fwd+bwd) on 15s clips; WER parity on LRS2 test"
 BF16_PEAK_TFLOPS = 2500.0     # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 HBM_PEAK_GBS = 8000.0
+# modality dropout (avhubert.py:476-482): p(drop a modality) = 0.5, then audio w.p. 0.5
+MODALITY_P = {"none": 0.5, "audio_off": 0.25, "video_off": 0.25}
 
 
+# ============================================================================ launcher
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n, argv):
+    """Spawn n ranks of this script (the parent never initialises HIP: it only imports torch).
+    Rank 0's stdout is relayed; returns the exit code (first failing rank's, 0 if all pass,
+    1 if rank 0 printed no JSON line)."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(n), LOCAL_RANK=str(r), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__)] + argv, env=env,
+                                      stdout=subprocess.PIPE if r == 0 else None, text=True))
+    last_json = []
+
+    def pump():
+        for line in procs[0].stdout:
+            sys.stdout.write(line)
+            sys.stdout.flush()
+            if line.startswith("{"):
+                last_json.append(line)
+    th = threading.Thread(target=pump, daemon=True)
+    th.start()
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                sys.stderr.write(f"[bench] rank {procs.index(p)} exited with {code}; stopping the others\n")
+                for q in live:
+                    q.terminate()
+                deadline = time.time() + 30
+                for q in live:
+                    try:
+                        q.wait(timeout=max(1.0, deadline - time.time()))
+                    except subprocess.TimeoutExpired:
+                        q.kill()
+        time.sleep(0.2)
+    th.join(timeout=10)
+    if rc == 0 and not last_json:
+        sys.stderr.write("[bench] rank 0 printed no result line\n")
+        rc = 1
+    return rc
+
+
+# ========================================================================= inputs, FLOPs
 def synthetic_batch(B, T, L, seed=1234):
     """SURVEY.md §8(d) d1: uint8 96x96 lip frames -> crop 88 -> /255 -> (x-0.421)/0.165;
     standard-normal 104-dim 'mel' frames with per-frame LayerNorm; labels U[1, 5047]."""
@@ -73,15 +141,33 @@ def model_flops_per_frame(cfg, T, L):
     return 3 * fwd - stem
 
 
+def expected_step_ms(variant_ms, world):
+    """E[step time] when every rank draws its modality independently with the reference's
+    probabilities and a step lasts as long as its slowest rank (the all-reduce joins them)."""
+    lv = sorted((variant_ms[k], MODALITY_P[k]) for k in MODALITY_P)
+    e, cum_prev = 0.0, 0.0
+    for ms, p in lv:
+        cum = cum_prev + p
+        e += ms * (cum ** world - cum_prev ** world)
+        cum_prev = cum
+    return e
+
+
+# ===================================================================== CPU baselines
+def _oracle_cfg(model_cfg):
+    from oracle import avsr_oracle as O
+    return O.OracleConfig.from_dict(dict(odim=model_cfg.odim, hidden_size=model_cfg.hidden_size,
+                                         num_attention_heads=model_cfg.num_attention_heads,
+                                         intermediate_size=model_cfg.intermediate_size,
+                                         num_hidden_layers=model_cfg.num_hidden_layers, ddim=model_cfg.ddim,
+                                         dheads=model_cfg.dheads, dunits=model_cfg.dunits, dlayers=model_cfg.dlayers))
+
+
 def cpu_baseline(model_cfg, state, T, threads):
     """Time the repo's CPU restatement (oracle/avsr_oracle.py) fwd+bwd on 1 x 15 s clip."""
     from oracle import avsr_oracle as O
     torch.set_num_threads(threads)
-    cfg = O.OracleConfig.from_dict(dict(odim=model_cfg.odim, hidden_size=model_cfg.hidden_size,
-                                        num_attention_heads=model_cfg.num_attention_heads,
-                                        intermediate_size=model_cfg.intermediate_size,
-                                        num_hidden_layers=model_cfg.num_hidden_layers, ddim=model_cfg.ddim,
-                                        dheads=model_cfg.dheads, dunits=model_cfg.dunits, dlayers=model_cfg.dlayers))
+    cfg = _oracle_cfg(model_cfg)
     sd = {k: v.detach().float().cpu().clone() for k, v in state.items()}
     for k, v in sd.items():
         if v.is_floating_point() and not (k.endswith("running_mean") or k.endswith("running_var")):
@@ -94,6 +180,28 @@ def cpu_baseline(model_cfg, state, T, threads):
     return T / dt, dt
 
 
+def decode_cpu_baseline(model_cfg, state, T, beam, threads, steps=8):
+    """oracle/decode_oracle.py beam search (the reference's BatchBeamSearch restated) on ONE
+    utterance of T frames, first `steps` output steps: utterances/s extrapolated to the T steps
+    a random-weight search takes (each step scores the full T-frame CTC prefix)."""
+    from oracle import decode_oracle as D
+    torch.set_num_threads(threads)
+    cfg = _oracle_cfg(model_cfg)
+    sd = {k: v.detach().float().cpu() for k, v in state.items()}
+    W, b = sd["avsr.ctc.ctc_lo.weight"], sd["avsr.ctc.ctc_lo.bias"]
+    x = torch.randn(T, model_cfg.hidden_size, generator=torch.Generator().manual_seed(5)) * 0.5
+    t0 = time.perf_counter()
+    with torch.no_grad():
+        lp = torch.log_softmax(x @ W.t() + b, -1)
+        D.beam_search(sd, cfg, x, lp, beam, ctc_weight=0.1, maxlenratio=-steps)
+    dt = time.perf_counter() - t0
+    per_step = dt / steps
+    return {"value": round(1.0 / (per_step * T), 4), "unit": "utt/s", "cores": threads, "kind": "port",
+            "sample": f"1 utterance, T={T}, beam {beam}, fp32: {steps} of {T} decode steps in {dt:.1f} s, "
+                      f"extrapolated to {T} steps"}
+
+
+# ======================================================================= side measurements
 def frontend_timing(B, T, dev, reps=5):
     """Device front end on one C2 batch -- 16 x 240000-sample waveforms -> log-fbank /
     stack / LN, 16 x T x 96 x 96 uint8 frames -> crop / normalise. Reported beside the metric,
@@ -146,20 +254,98 @@ def encoder_gemm_table(dev, M, D, F):
             "note": "isolated launches, plain epilogue (tools/gemm_table.py); the in-step probe is `roofline`"}
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=16, help="clips per GPU")
-    ap.add_argument("--seq", type=int, default=375, help="AV-frames per clip (15 s at 25 fps)")
-    ap.add_argument("--labels", type=int, default=40)
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--layers", type=int, default=None, help="debug only: fewer encoder layers (INVALID for the metric)")
-    ap.add_argument("--seed", type=int, default=1234, help="seeds the inputs, dropout streams and the "
-                    "modality-dropout draws (numpy global RNG, as the reference draws them)")
-    args = ap.parse_args()
+def decode_throughput(dev, state_cpu, model_cfg, cpu_threads):
+    """C1 (8 x 1 s, greedy), C4 (LRS2-length 4 s utterances, beam 3) and C5 (15 s chunks,
+    beam 5) decode on the HIP engine, fp32 like the reference's evaluation
+    (script/evaluation.py:89-108): random-init weights, so every search runs to maxlen = T.
+    Batched over 8 utterances (decode_batch) and, for C1 / C4, the reference's one-utterance
+    call form. cpu_baseline: the oracle's beam search on one utterance (bounded)."""
+    from avsr_amd.avhubert_avsr_model import AVHubertAVSR, get_beam_search_decoder
+    from avsr_amd.configuration_avhubert_avsr import AVHubertAVSRConfig
+    torch.manual_seed(0)
+    model = AVHubertAVSR(AVHubertAVSRConfig(odim=5049)).eval()
+    if state_cpu is not None:
+        model.load_state_dict(state_cpu, strict=True)
+    model.setup_engine(dev, torch.float32)
+    tokens = ["<blank>"] + [f"u{i}" for i in range(1, 5048)] + ["<eos>"]
+    out = []
+    for name, T, beam, seq in (("C1 greedy", 25, 1, True), ("C4 beam 3", 100, 3, True), ("C5 beam 5", 375, 5, False)):
+        bs = get_beam_search_decoder(model.avsr, tokens, ctc_weight=0.1, beam_size=beam)
+        g = torch.Generator().manual_seed(5)
+        xs = [(torch.randn(T, 1024, generator=g) * 0.5).to(dev) for _ in range(8)]
+        bs.decode_batch(xs[:2])
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        bat = bs.decode_batch(xs)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        rec = {"config": name, "utterances": 8, "frames_per_utt": T, "beam": beam, "dtype": "fp32",
+               "batched_utt_per_s": round(8 / (t1 - t0), 2)}
+        if seq:
+            t0 = time.perf_counter()
+            one = [bs(x) for x in xs]
+            torch.cuda.synchronize()
+            rec["sequential_utt_per_s"] = round(8 / (time.perf_counter() - t0), 2)
+            rec["batched_equals_sequential"] = all(
+                [h.asdict()["yseq"] for h in a] == [h.asdict()["yseq"] for h in b] for a, b in zip(one, bat))
+        if state_cpu is not None:
+            rec["cpu_baseline"] = decode_cpu_baseline(model_cfg, state_cpu, T, beam, cpu_threads,
+                                                      steps=4 if T > 100 else 8)
+        out.append(rec)
+    del model
+    torch.cuda.empty_cache()
+    return out
 
+
+# ===================================================================== CPU self-test
+def cpu_selftest(args):
+    """No GPU: the launcher, rendezvous, barrier + max-over-ranks timing and the bucketed
+    all-reduce of a flat fp32 gradient arena (parallel.GradReducer over gloo, readiness
+    watermarks like the engine's backward) are exercised and checked. Not a measurement."""
+    from avsr_amd import parallel
+    if os.environ.get("AVSR_BENCH_SELFTEST_FAIL_RANK") == os.environ.get("RANK", "0"):
+        sys.exit(7)            # test hook: a rank dying before the rendezvous (tests/test_bench_launcher.py)
+    rank, world, _ = parallel.init_from_env(backend="gloo")
+    assert world == args.gpus, f"--gpus {args.gpus} but WORLD_SIZE {world}"
+    n = 3_000_001
+    flat = torch.zeros(n)
+    seg = (1000, 2_500_000)
+    red = parallel.GradReducer(flat, bucket_bytes=4 << 18, segment=seg, use_stream=False)
+    ok = True
+    for _ in range(args.warmup):
+        flat.fill_(rank + 1.0)
+        red.begin()
+        red.finish(average=True)
+    dist.barrier()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        flat.copy_(torch.arange(n, dtype=torch.float32) * (rank + 1 + i))
+        red.begin()
+        for off in (2_000_000, 1_200_000, 400_000, seg[0]):     # layers finishing back to front
+            red.ready(off)
+        red.finish(average=True)
+        want = torch.arange(n, dtype=torch.float32) * (sum(range(1, world + 1)) / world + i)
+        ok = ok and torch.allclose(flat, want, rtol=1e-6)
+    dist.barrier()
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    okt = torch.tensor([1 if ok else 0])
+    dist.all_reduce(okt, op=dist.ReduceOp.MIN)
+    res = {"metric": "cpu-selftest (launcher + bucketed all-reduce; not a measurement)", "value": None,
+           "unit": None, "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+           "ms_per_step": round(t.item() / max(1, args.steps) * 1e3, 3), "data": "synthetic",
+           "allreduce": {"backend": dist.get_backend(), "ranks": dist.get_world_size(),
+                         "buckets": len(red.buckets) + len(red.tail), "elements": n,
+                         "mean_ok": bool(okt.item())}}
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    dist.destroy_process_group()
+    return 0 if okt.item() else 3
+
+
+# ============================================================================ GPU bench
+def gpu_bench(args):
     from avsr_amd import parallel
     rank, world, local = parallel.init_from_env()
     assert world == args.gpus, f"--gpus {args.gpus} but WORLD_SIZE {world}"
@@ -232,8 +418,13 @@ def main():
     torch.cuda.synchronize()
     # probe: encoder FFN up-projection (M = B*T, N = F, K = D), forward, bf16
     M, N_, K_ = B * T, cfg.intermediate_size, cfg.hidden_size
+    nprobe = args.steps * cfg.num_hidden_layers + 8
+    stamps = torch.zeros(nprobe, 2, dtype=torch.int64, device=dev)
+    stamps[:, 0] = -1                                   # {~0ull, 0}: min-start / max-end identities
     ops.PROBE["gemm"] = {"match": lambda m, n, k, ak, bk, dt: (m, n, k, ak, bk) == (M, N_, K_, True, True),
-                         "events": []}
+                         "events": [], "stamps": stamps.view(-1)}
+    red = ddp.reducer
+    red.timing = [] if world > 1 else None
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -254,57 +445,91 @@ def main():
     elapsed = time.perf_counter() - t0
     ms1 = torch.cuda.memory_stats(dev)
     timed_drops = list(drops)
-    probe_ev = ops.PROBE.pop("gemm")["events"]
+    probe = ops.PROBE.pop("gemm")
+    ar_timing, red.timing = red.timing, None
     if world > 1:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
-    # diagnostic (outside the timed region): host time to issue one step vs its device time
-    issue, dev_ms = [], []
-    for _ in range(3):
-        torch.cuda.synchronize()
-        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        ev0.record()
-        h0 = time.perf_counter()
-        step()
-        issue.append((time.perf_counter() - h0) * 1e3)
-        ev1.record()
-        torch.cuda.synchronize()
-        dev_ms.append(ev0.elapsed_time(ev1))
     losses = out4.cpu().tolist()
     frames = args.steps * B * T * world
     value = frames / elapsed
-    kern_ms = [s.elapsed_time(e) for s, e in probe_ev]
-    avg_ms = sum(kern_ms) / max(1, len(kern_ms))
+    # probe kernel duration from its in-kernel stamps (100 MHz ticks), events beside it
+    nl = len(probe["events"])
+    st = stamps[:nl].cpu()
+    kern_ms = [(int(e) - int(s)) * 1e-5 for s, e in st.tolist()]
+    kern_ms_sorted = sorted(kern_ms)
+    avg_ms = sum(kern_ms) / max(1, nl)
+    med_ms = kern_ms_sorted[nl // 2] if nl else 0.0
+    ev_ms = [s.elapsed_time(e) for s, e in probe["events"]]
+    ev_avg = sum(ev_ms) / max(1, len(ev_ms))
     flops = 2.0 * M * N_ * K_
     achieved = flops / (avg_ms * 1e-3) / 1e12 if avg_ms > 0 else 0.0
     fpf = model_flops_per_frame(cfg, T, L)
     traffic = None      # HBM bytes per launch from the committed PMC passes (tools/pmc_traffic.py)
-    tp = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "pmc_traffic.json")
+    tp = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(tp):
         rec = json.load(open(tp))
         if rec.get("shape") == [M, N_, K_]:
             traffic = rec["traffic_bytes"]
+
+    # per-modality-variant step time (outside the timed region; every rank forced alike)
+    variant_ms = {}
+    for name, forced in (("none", None), ("audio_off", "audio_off"), ("video_off", "video_off")):
+        eng.force_modality = (forced,)
+        per = []
+        for _ in range(3):
+            if world > 1:
+                dist.barrier()
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            step()
+            e1.record()
+            torch.cuda.synchronize()
+            per.append(e0.elapsed_time(e1))
+        variant_ms[name] = round(sorted(per)[1], 2)
+    eng.force_modality = None
+    exp_ms = expected_step_ms(variant_ms, world)
+    allreduce = None
+    if world > 1:
+        exposed = [j0.elapsed_time(j1) for (c0, c1, j0, j1) in ar_timing]
+        comm = [c0.elapsed_time(c1) for (c0, c1, j0, j1) in ar_timing if c0 is not None]
+        allreduce = {"backend": dist.get_backend(), "ranks": dist.get_world_size(),
+                     "buckets": len(red.buckets) + len(red.tail), "bucket_mib": parallel.BUCKET_BYTES >> 20,
+                     "bytes_per_step": arena.grad.numel() * 4,
+                     "exposed_ms_per_step": round(sum(exposed) / max(1, len(exposed)), 3),
+                     "comm_ms_per_step": round(sum(comm) / max(1, len(comm)), 3),
+                     "note": "exposed = compute-stream wait for the comm stream after the backward (rank 0); "
+                             "comm = first bucket launch to last completion"}
     result = {
         "metric": METRIC, "value": round(value, 2), "unit": "AV-frames/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup,
-        "warmup_note": "plus one untimed fwd+bwd per modality variant (none / video_off / audio_off) before the warm-up steps", "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "warmup_note": "plus one untimed fwd+bwd per modality variant (none / video_off / audio_off) before the warm-up steps",
+        "ms_per_step": round(elapsed / args.steps * 1e3, 3),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
         "data": "synthetic (SURVEY d1 recipe: uint8 lip frames, normal+LN 104-d audio, U[1,5047] labels)",
         "config": {"workload": f"C2/C3: AVHubertAVSR fwd+bwd+AdamW, {B}x{T / 25:.0f}s clips per GPU "
                                f"(T={T}, L={L}), train mode, dropouts on",
                    "global_batch": B * world, "seq_len": T, "parallelism": f"dp{world}",
                    "encoder_layers": cfg.num_hidden_layers},
-        "roofline": {"bound": "mfma", "kernel": f"dense_kernel bf16 (encoder FFN1 {M}x{N_}x{K_})",
+        "roofline": {"bound": "mfma", "kernel": f"dense_glds_kernel bf16 (encoder FFN1 fwd {M}x{N_}x{K_})",
                      "achieved": round(achieved, 1), "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": round(achieved / BF16_PEAK_TFLOPS, 4), "traffic": traffic,
                      "traffic_unit": "bytes/launch (rocprofv3 FETCH_SIZEx2+WRITE_SIZE, profiles/pmc_traffic.json)",
-                     "launches": len(kern_ms), "avg_launch_ms": round(avg_ms, 4)},
+                     "algorithmic_flops_per_launch": flops, "launches": nl,
+                     "avg_launch_ms": round(avg_ms, 4), "median_launch_ms": round(med_ms, 4),
+                     "timing": "in-kernel s_memrealtime stamps (first workgroup start -> last workgroup end)",
+                     "event_avg_launch_ms": round(ev_avg, 4)},
         "model_tflops_per_s": round(value * fpf / world / 1e12, 1),
         "model_mfu": round(value * fpf / world / 1e12 / BF16_PEAK_TFLOPS, 4),
+        "modality_variants": {"step_ms": variant_ms, "p": MODALITY_P,
+                              "expected_ms_per_step": round(exp_ms, 3),
+                              "value_expected": round(B * T * world / exp_ms * 1e3, 2),
+                              "note": "median of 3 forced steps per variant; value_expected weights them with "
+                                      "the reference's draw probabilities (avhubert.py:476-482), slowest rank "
+                                      "bounding a step for N > 1"},
         "loss": [round(x, 4) for x in losses],
-        "host_issue_ms_per_step": round(sum(issue) / len(issue), 2),
-        "device_ms_per_step_synced": round(sum(dev_ms) / len(dev_ms), 2),
         "host_ms_per_step_timed": round(sum(host_t) / len(host_t) * 1e3, 2),
         "host_ms_steps": [round(t * 1e3, 1) for t in host_t],
         "stream_ms_steps": [round(step_ev[i].elapsed_time(step_ev[i + 1]), 1) for i in range(args.steps)],
@@ -314,22 +539,53 @@ def main():
                            "audio_off": timed_drops.count("audio_off"), "none": timed_drops.count(None),
                            "note": "rank 0's timed steps; video_off skips the ResNet backward "
                                    "(its gradient is exactly zero, avhubert.py:480)"},
+        "allreduce": allreduce,
     }
-    result["frontend"] = frontend_timing(B, T, dev)
-    if args.layers is None:
-        result["encoder_gemms"] = encoder_gemm_table(dev, B * T, cfg.hidden_size, cfg.intermediate_size)
-        result["roofline"]["worst_encoder_gemm"] = result["encoder_gemms"]["worst"]
+    if rank == 0 and not args.quick:
+        result["frontend"] = frontend_timing(B, T, dev)
+        if args.layers is None:
+            result["encoder_gemms"] = encoder_gemm_table(dev, B * T, cfg.hidden_size, cfg.intermediate_size)
+            result["roofline"]["worst_encoder_gemm"] = result["encoder_gemms"]["worst"]
+    threads = min(16, os.cpu_count() or 1)
     if state_cpu is not None:
-        threads = min(16, os.cpu_count() or 1)
         fps, dt = cpu_baseline(cfg, state_cpu, T, threads)
         result["cpu_baseline"] = {"value": round(fps, 2), "unit": "AV-frames/s", "cores": threads, "kind": "port",
                                   "sample": f"1x15s clip (T={T}, L=40) fwd+bwd, oracle/avsr_oracle.py fp32, "
                                             f"{dt:.1f} s"}
+    if rank == 0 and world == 1 and args.layers is None and not args.quick and not args.no_decode:
+        del eng, arena, opt, ddp, model
+        gc.collect()
+        torch.cuda.empty_cache()
+        result["decode"] = decode_throughput(dev, state_cpu, cfg, threads)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    return 0
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=16, help="clips per GPU")
+    ap.add_argument("--seq", type=int, default=375, help="AV-frames per clip (15 s at 25 fps)")
+    ap.add_argument("--labels", type=int, default=40)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-decode", action="store_true", help="skip the C1/C4/C5 decode throughput section")
+    ap.add_argument("--quick", action="store_true", help="only the step measurement (profiling runs)")
+    ap.add_argument("--layers", type=int, default=None, help="debug only: fewer encoder layers (INVALID for the metric)")
+    ap.add_argument("--seed", type=int, default=1234, help="seeds the inputs, dropout streams and the "
+                    "modality-dropout draws (numpy global RNG, as the reference draws them)")
+    ap.add_argument("--cpu-selftest", action="store_true", help="no GPU: launcher + gloo all-reduce check only")
+    args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return launch_ranks(args.gpus, sys.argv[1:])
+    if args.cpu_selftest:
+        return cpu_selftest(args)
+    return gpu_bench(args)
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

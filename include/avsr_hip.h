@@ -79,6 +79,10 @@ typedef struct {
                                 bias gradient of the layer whose output gradient C is, e.g.
                                 FFN1's bias from the FFN2 data-grad); bf16, N % 8 == 0, no split */
   float* db_ws;              /* its row-tile partials, AVSR_GEMM_COLSUM_WS(M, N) fp32 */
+  unsigned long long* stamp; /* optional diagnostic (bench.py roofline probe; bf16 LDS-DMA path):
+                                {min start, max end} in s_memrealtime ticks (100 MHz) — every
+                                workgroup folds its first / last instant in by vector atomics.
+                                Caller initialises {~0ull, 0}. No output depends on it. */
 } avsr_gemm_params;
 #define AVSR_GEMM_COLSUM_WS(M, N) ((int64_t)(((M) + 63) / 64) * (N))
 /* slabs are AVSR_GEMM_SLAB_PAD floats apart beyond M*N: power-of-two slab strides put the
@@ -350,8 +354,8 @@ int avsr_loss_finalize(int B, const float* nll, int rows, const float* row_loss,
  *                  ctc.py:27,98, encoder dropout after pos-conv avhubert.py:704)
  * avsr_mask_rows:  x[b*T + t][:] = 0 for t >= len[b]   (avhubert.py:683-686)
  * avsr_embed_fwd:  y[r] = dropout(table[tok[r]] * scale + pe[r % L])  (decoder embed +
- *                  PositionalEncoding, decoder.py:89-93, embedding.py:80-87); bwd: fp32
- *                  atomics into dtable
+ *                  PositionalEncoding, decoder.py:89-93, embedding.py:80-87); bwd: dtable
+ *                  += per-token sums of the row gradients in row order (no atomics)
  * avsr_cast:       dst = alpha * src + beta * dst over a [rows][cols] strided view
  * avsr_cast_flat:  dst = src over n contiguous elements (fp32 -> bf16 vectorised: the arena's
  *                  master -> compute-shadow refresh after load_state_dict / optimizer steps)
@@ -414,7 +418,9 @@ int avsr_weightnorm_fwd(int dtype, int O, int K, int C, const float* v, const fl
 int avsr_weightnorm_bwd(int O, int K, int C, const float* v, const float* g, const float* norm,
                         const float* dw, float* dv, float* dg, float* scratch, void* stream);
 
-int avsr_sumsq(const float* x, int64_t n, float* out, void* stream);
+/* *out += sum x^2 in a fixed summation order (deterministic); ws: AVSR_SUMSQ_WS floats */
+#define AVSR_SUMSQ_WS 1024
+int avsr_sumsq(const float* x, int64_t n, float* out, float* ws, void* stream);
 typedef struct {
   int64_t n;
   float* param; const float* grad; float* exp_avg; float* exp_avg_sq;

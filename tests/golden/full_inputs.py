@@ -8,3 +8,5 @@ ENC_ROWS = (0, 1, 74, 150, 299, 300, 374)          # frames whose full encoder r
 DEC_ROWS = (0, 1, 20, 31, 40)                      # decoder positions whose logits are kept
 
 
+# early-ending beam searches (make_golden_endbeam.py): <eos> logit bias offsets, beams, C1 clips
+ENDBEAM = dict(offsets=(4.0, 6.0, 8.0), beams=(3, 5), clips=(0, 3, 6))

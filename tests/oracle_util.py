@@ -81,3 +81,31 @@ def zero_grad_by_symmetry(key):
     to adding q.b to every score): reference and engine both return round-off there, so their
     norms are compared against an absolute floor instead of relatively."""
     return key.endswith("k_proj.bias") or key.endswith("linear_k.bias")
+
+
+GOLDEN_ENDBEAM = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "avsr_endbeam.npz")
+
+
+def load_golden_endbeam():
+    return dict(np.load(GOLDEN_ENDBEAM, allow_pickle=False))
+
+
+def endbeam_case(ge, off, beam, clip):
+    """the reference's ended hypotheses (best first) of one early-ending search
+    (tests/golden/make_golden_endbeam.py): list of (yseq, score, decoder score, ctc score)"""
+    key = f"eb_{off:g}_b{beam}_{clip}"
+    lens, flat = ge[key + "_len"], ge[key + "_yseq"]
+    out, o = [], 0
+    for i, n in enumerate(lens):
+        out.append((flat[o:o + n].tolist(), float(ge[key + "_score"][i]), float(ge[key + "_dec"][i]),
+                    float(ge[key + "_ctc"][i])))
+        o += n
+    return out
+
+
+def endbeam_state(g, off):
+    """recipe weights with the <eos> logit bias raised by `off` (make_golden_endbeam.py)"""
+    st = full_state(g)
+    st["avsr.decoder.output_layer.bias"] = st["avsr.decoder.output_layer.bias"].copy()
+    st["avsr.decoder.output_layer.bias"][5048] += np.float32(off)
+    return st

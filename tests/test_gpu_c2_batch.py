@@ -1,0 +1,149 @@
+"""The production bf16 path at C2's real batch: B = 16 clips x T = 375
+AV-frames, 40 labels each, full-size model (recipe weights), dropouts 0, train mode.
+
+At this shape the bf16 engine runs the kernels the bench runs and the B = 2 golden tests do
+not reach: the 192-row GEMM / conv tiles (M = 6000 encoder GEMMs with N >= 3072, ResNet stages
+2-3), the fused BN-backward (BNR) data-grad epilogues, the resident-K/V `res::` attention
+kernels, the M = 6000 weight-gradient split-K policies and BatchNorm statistics over 6,000
+frames. Its results are compared with the engine's fp32 parity path on the same inputs — which
+is pinned to the reference's own output at B = 2 (tests/test_gpu_fullsize_golden.py) — at the
+bf16 tolerances used there (relative, ||a - b||_inf / ||b||_inf):
+losses 3e-2, encoder / CTC / decoder logit rows 8e-2, every gradient norm 1.2e-1, BN running
+statistics 5e-2. Two bf16 steps on the same inputs must give bit-identical gradients (no
+atomics on the training path).
+
+Also: a batch whose lengths / labels already live on the device (HF Trainer's layout) takes
+the sync-free device preparation (Engine._prepare_device) and equals the host-prepared batch,
+including a label matrix with an extra all-padding column."""
+import numpy as np
+import pytest
+import torch
+
+from avsr_amd import _lib as L
+from avsr_amd import ops
+from avsr_amd.avhubert_avsr_model import AVHubertAVSR
+from avsr_amd.configuration_avhubert_avsr import AVHubertAVSRConfig
+from oracle.weights import NO_DROPOUT, TINY_CONFIG
+from tests.oracle_util import full_state, golden_batch, golden_state, load_golden, load_golden_full, rel, \
+    zero_grad_by_symmetry
+
+pytestmark = pytest.mark.gpu
+
+B, T, NL = 16, 375, 40
+TOL = dict(loss=3e-2, rows=8e-2, grad=1.2e-1, bn=5e-2)
+ENC_ROWS = (0, 1, 187, 374)
+DEC_ROWS = (0, 20, 40)
+
+
+def _c2_batch():
+    """SURVEY d1 synthetic inputs (bench.synthetic_batch), every clip 15 s long"""
+    import bench
+    v, a, lens, lab = bench.synthetic_batch(B, T, NL, seed=1234)
+    return {"videos": v, "audios": a, "labels": lab, "video_lengths": lens, "audio_lengths": lens.clone(),
+            "label_lengths": torch.full((B,), NL, dtype=torch.int64)}
+
+
+def _run(m, dtype, batch, state):
+    m.setup_engine("cuda", dtype)
+    m.load_state_dict(state, strict=True)
+    m.train()
+    m.zero_grad()
+    eng = m.avsr.engine()
+    eng.capture = {}
+    out = m(**{k: v.cuda() for k, v in batch.items()})
+    out.loss.backward()
+    torch.cuda.synchronize()
+    ctx, eng.capture = eng.capture, None
+    L1 = ctx["bt"]["L1"]
+    res = {"loss": [float(out.loss), float(out.loss_ctc), float(out.loss_att)],
+           "enc": ctx["enc"].float().view(B, T, -1)[:, list(ENC_ROWS)].cpu(),
+           "ctc": ctx["clog"].float().view(B, T, -1)[:, list(ENC_ROWS), :5049].cpu(),
+           "dec": ctx["dlog"].float().view(B, L1, -1)[:, list(DEC_ROWS), :5049].cpu(),
+           "grad": {k: p.grad.double().norm().item() for k, p in m.named_parameters() if p.grad is not None},
+           "gflat": eng.arena.grad.clone(),
+           "bn": {k: v.detach().float().cpu().clone() for k, v in m.state_dict().items()
+                  if k.endswith("running_mean") or k.endswith("running_var")}}
+    del ctx
+    return res
+
+
+@pytest.fixture(scope="module")
+def runs():
+    g = load_golden_full()
+    state = {k: torch.from_numpy(v) for k, v in full_state(g).items()}
+    m = AVHubertAVSR(AVHubertAVSRConfig(odim=5049, **NO_DROPOUT))
+    batch = _c2_batch()
+    out = {}
+    for key, dtype in (("f32", torch.float32), ("bf16", torch.bfloat16), ("bf16_again", torch.bfloat16)):
+        out[key] = _run(m, dtype, batch, state)
+        torch.cuda.empty_cache()
+    return out
+
+
+def test_c2_shape_selects_production_tiles():
+    """the bf16 conv forward of ResNet stage 2 at C2 launches 192-row tiles (its BN partials
+    are counted per tile); fp32 keeps 128 rows"""
+    geo = ops.ConvGeom(B * T, 11, 11, 128, 128, 3, 3, (1, 1), (1, 1))
+    M = B * T * 121
+    assert ops.conv_stat_tiles(geo, L.AVSR_BF16) == -(-M // 192)
+    assert ops.conv_stat_tiles(geo, L.AVSR_F32) == -(-M // 128)
+
+
+def test_c2_bf16_matches_fp32_parity_path(runs):
+    ref, got = runs["f32"], runs["bf16"]
+    e_loss = max(abs(a - b) / abs(b) for a, b in zip(got["loss"], ref["loss"]))
+    e_rows = max(rel(got[k], ref[k]) for k in ("enc", "ctc", "dec"))
+    bad, worst = [], 0.0
+    for k, n in ref["grad"].items():
+        gv = got["grad"][k]
+        if zero_grad_by_symmetry(k):
+            continue
+        if n > 1e-3:
+            worst = max(worst, abs(gv - n) / n)
+        if abs(gv - n) > TOL["grad"] * abs(n) + 1e-6:
+            bad.append((k, gv, n))
+    e_bn = max(float((got["bn"][k] - v).abs().max() / v.abs().max().clamp_min(1e-6)) for k, v in ref["bn"].items())
+    print(f"C2 bf16 vs fp32: loss {e_loss:.2e} rows {e_rows:.2e} grad-norm worst {worst:.2e} bn {e_bn:.2e}")
+    assert e_loss < TOL["loss"]
+    assert e_rows < TOL["rows"]
+    assert not bad, bad[:8]
+    assert e_bn < TOL["bn"]
+    assert len(ref["grad"]) == len(got["grad"]) > 600
+
+
+def test_c2_bf16_step_is_deterministic(runs):
+    a, b = runs["bf16"], runs["bf16_again"]
+    assert a["loss"] == b["loss"]
+    assert torch.equal(a["gflat"], b["gflat"])
+
+
+# ------------------------------------------------------------------ device-side prepare
+def test_device_prepared_batch_equals_host_batch():
+    """lengths / labels on the device (no read-back) give the host path's losses and
+    gradients (fp32 parity mode, tiny model, padded row); a label matrix with an extra
+    all -1 column runs one more (ignored, causally masked) decoder position and still does"""
+    g = load_golden()
+    cfg = AVHubertAVSRConfig(**TINY_CONFIG, **NO_DROPOUT)
+    m = AVHubertAVSR(cfg)
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in golden_state(g).items()}, strict=True)
+    m.setup_engine("cuda", torch.float32)
+    m.train()
+    b = {k: torch.from_numpy(v) for k, v in golden_batch(g).items()}
+    results = []
+    for variant in ("host", "device", "device_wide"):
+        bb = dict(b)
+        if variant == "device_wide":
+            lab = bb["labels"]
+            bb["labels"] = torch.cat([lab, torch.full((lab.shape[0], 1), -1, dtype=lab.dtype)], 1)
+        if variant != "host":
+            bb = {k: v.cuda() for k, v in bb.items()}
+        m.zero_grad()
+        out = m(**bb)
+        out.loss.backward()
+        torch.cuda.synchronize()
+        results.append(([float(out.loss), float(out.loss_ctc), float(out.loss_att), float(out.acc)],
+                        m.avsr.engine().arena.grad.clone()))
+    (l0, g0) = results[0]
+    for li, gi in results[1:]:
+        np.testing.assert_allclose(li, l0, rtol=2e-6)
+        assert (gi - g0).abs().max().item() <= 1e-5 * g0.abs().max().item()

@@ -157,3 +157,38 @@ def test_stride2_dgrad_parity_classes_match_full(dev, case, beta, monkeypatch):
         outs.append(dx)
     torch.cuda.synchronize()
     assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_conv_stats_at_192_eligible_shape(dev, dtype):
+    """the s3h fault's regression on the device: a stage-2 conv with enough rows for the
+    192-row bf16 tile (M = 900 x 11 x 11 = 108,900), BN partials sized by conv_stat_tiles for
+    the dtype, statistics combining to the batch moments; a buffer sized for the other
+    dtype's tile count is refused before launch."""
+    n, h, c = 900, 11, 128
+    geom = ops.ConvGeom(n, h, h, c, c, 3, 3, (1, 1), (1, 1))
+    tiles = ops.conv_stat_tiles(geom, ops.dtype_code(torch.empty(0, dtype=dtype)))
+    other = ops.conv_stat_tiles(geom, ops.dtype_code(torch.empty(0, dtype=torch.bfloat16 if dtype == torch.float32
+                                                                   else torch.float32)))
+    M = n * h * h
+    assert tiles == -(-M // (192 if dtype == torch.bfloat16 else 128)) and tiles != other
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(n, h, h, c, generator=g).to(dev, dtype)
+    w = (torch.randn(c, 3, 3, c, generator=g) * (9 * c) ** -0.5).to(dev, dtype)
+    y = torch.empty(n, h, h, c, device=dev, dtype=dtype)
+    if other < tiles:
+        with pytest.raises(ValueError):
+            ops.conv_fwd(geom, x, w, y, torch.empty(c, other, 3, device=dev))
+    guard = torch.full((c * tiles * 3 + 4096,), 12345.0, device=dev)
+    stats = guard[:c * tiles * 3].view(c, tiles, 3)
+    ops.conv_fwd(geom, x, w, y, stats)
+    torch.cuda.synchronize()
+    assert bool((guard[c * tiles * 3:] == 12345.0).all()), "statistics written past the buffer"
+    cnt, mean, m2 = stats[..., 0].double(), stats[..., 1].double(), stats[..., 2].double()
+    assert torch.allclose(cnt.sum(1), torch.full((c,), float(M), device=dev, dtype=torch.float64))
+    tot = cnt.sum(1, keepdim=True)
+    gm = (cnt * mean).sum(1, keepdim=True) / tot
+    var = ((m2 + cnt * (mean - gm) ** 2).sum(1, keepdim=True) / tot).flatten()
+    yf = y.double().reshape(-1, c)
+    assert _rel(gm.flatten(), yf.mean(0)) < 1e-3 or (gm.flatten() - yf.mean(0)).abs().max() < 1e-4
+    assert _rel(var, yf.var(0, unbiased=False)) < 1e-3

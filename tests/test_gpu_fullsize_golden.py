@@ -224,3 +224,33 @@ def test_train_step_t375(g, model, state, dtype):
     assert not bad, bad[:8]
     assert e_bn < tol["bn"]
     assert len(params) and len(g["grad_keys"]) == sum(1 for p in m.parameters() if p.grad is not None)
+
+
+# ------------------------------------------------------------- searches ending early
+@pytest.mark.parametrize("off", [4.0, 6.0, 8.0])
+@pytest.mark.parametrize("beam", [3, 5])
+def test_early_ending_beam_search(g, model, state, off, beam):
+    """tests/golden/avsr_endbeam.npz: the reference's searches with a raised <eos> bias stop
+    before maxlen (end_detect, e2e_asr_common.py:18-48) and return hypotheses that ended at
+    different lengths (beam_search.py:330-406). The engine's one-utterance search AND the
+    batched search return the same ended list: token sequences identical, total / decoder /
+    CTC scores within 1e-4 (fp32)."""
+    from tests.golden.full_inputs import ENDBEAM
+    from tests.oracle_util import endbeam_case, endbeam_state, load_golden_endbeam
+    ge = load_golden_endbeam()
+    st = {k: torch.from_numpy(v) for k, v in endbeam_state(g, off).items()}
+    m = _fresh(model, st, torch.float32).eval()
+    bs = get_beam_search_decoder(m.avsr, TOKENS, ctc_weight=0.1, beam_size=beam)
+    xs = [torch.from_numpy(g["c1_enc"][c]).cuda() for c in ENDBEAM["clips"]]
+    batched = bs.decode_batch(xs)
+    worst = 0.0
+    for c, x, hb in zip(ENDBEAM["clips"], xs, batched):
+        ref = endbeam_case(ge, off, beam, c)
+        for hyps in (bs(x), hb):
+            got = [h.asdict() for h in hyps]
+            assert [h["yseq"] for h in got] == [r[0] for r in ref], (c, [len(h["yseq"]) for h in got])
+            for h, r in zip(got, ref):
+                for a, b in ((h["score"], r[1]), (h["scores"]["decoder"], r[2]), (h["scores"]["ctc"], r[3])):
+                    worst = max(worst, abs(a - b) / max(abs(b), 1e-3))
+    _report(f"endbeam_{off:g}_b{beam}", worst)
+    assert worst <= 1e-4

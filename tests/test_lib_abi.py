@@ -39,3 +39,21 @@ def test_struct_sizes_match_c_layout():
     # int fields then 8-byte aligned pointers/int64: ctypes follows the C ABI
     assert ctypes.sizeof(L.GemmParams) % 8 == 0
     assert ctypes.sizeof(L.ConvParams) % 8 == 0
+
+
+def test_conv_stat_tiles_per_dtype():
+    """regression of the round-2 s3h fault: the BN partial-statistics buffer of a conv forward
+    is sized by avsr_conv_stat_tiles, whose tile height must be the one the dtype's path
+    launches — 192-row tiles on the bf16 LDS-DMA path where they pay (ResNet stage 2 at C2,
+    M = 6000 x 11 x 11), the 128-row register-staged tile for fp32. Host-side query, no GPU."""
+    from avsr_amd import ops
+    g = ops.ConvGeom(6000, 11, 11, 128, 128, 3, 3, (1, 1), (1, 1))
+    M = 6000 * 11 * 11
+    assert ops.conv_stat_tiles(g, L.AVSR_BF16) == -(-M // 192)
+    assert ops.conv_stat_tiles(g, L.AVSR_F32) == -(-M // 128)
+    # a shape below the 192 rule stays on 128 rows for both
+    g2 = ops.ConvGeom(8, 11, 11, 128, 128, 3, 3, (1, 1), (1, 1))
+    assert ops.conv_stat_tiles(g2, L.AVSR_BF16) == ops.conv_stat_tiles(g2, L.AVSR_F32) == -(-8 * 121 // 128)
+    # N <= 64 (stage 1): 256-row tiles on both paths
+    g3 = ops.ConvGeom(6000, 22, 22, 64, 64, 3, 3, (1, 1), (1, 1))
+    assert ops.conv_stat_tiles(g3, L.AVSR_BF16) == ops.conv_stat_tiles(g3, L.AVSR_F32) == -(-6000 * 484 // 256)

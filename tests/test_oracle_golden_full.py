@@ -79,3 +79,25 @@ def test_train_step_t375(g):
     for k, row in zip(g["bn_keys"], g["bn_after"]):
         got = sdg[k].detach().flatten()[:8].numpy()
         np.testing.assert_allclose(got, row[:len(got)], rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("off", [4.0, 6.0, 8.0])
+@pytest.mark.parametrize("beam", [3, 5])
+def test_early_ending_beams(g, off, beam):
+    """searches that end before maxlen (raised <eos> bias): end_detect and the ranking of
+    hypotheses ended at different lengths reproduce the reference's full ended list"""
+    from tests.golden.full_inputs import ENDBEAM
+    from tests.oracle_util import endbeam_case, endbeam_state, load_golden_endbeam
+    ge = load_golden_endbeam()
+    torch.set_num_threads(8)
+    sdb = O.to_torch_state(endbeam_state(g, off))
+    cfg = O.OracleConfig()
+    W, bias = sdb["avsr.ctc.ctc_lo.weight"], sdb["avsr.ctc.ctc_lo.bias"]
+    c = ENDBEAM["clips"][-1]
+    x = torch.from_numpy(g["c1_enc"][c])
+    hyps = D.beam_search(sdb, cfg, x, torch.log_softmax(x @ W.t() + bias, -1), beam, ctc_weight=0.1)
+    ref = endbeam_case(ge, off, beam, c)
+    assert len(hyps) == len(ref)
+    for h, r in zip(hyps, ref):
+        assert h.yseq == r[0]
+        assert abs(h.score - r[1]) <= 1e-4 * abs(r[1])
