@@ -585,6 +585,176 @@ static bool s2_phase(const avsr_conv_params* p) {
   return t.a_bytes != 0;
 }
 
+// ---------------------------------------------------------------- patch-resident 3x3 / stride 1
+// 3x3 / stride 1 / pad 1 convolutions with 64 channels on both sides (ResNet stage 1 at 22 x 22:
+// layer1 conv1 / conv2 forward and data-grad). The general kernel builds each of the 9 tap
+// K-tiles by re-gathering the block's pixels, so a block streams its input 9x through L2 — at
+// N = 64 that made stage 1 L2-bandwidth bound (21 % of MFMA peak). Here a block of 256 output
+// pixels DMAs the input patch around them into LDS ONCE, in padded coordinates ((H+2) x (W+2)
+// per image; border and out-of-range positions come from the buffer's out-of-range zeros), and
+// every tap of every pixel is a row offset into that image: no per-fragment masking, 9x fewer
+// input bytes per block. The weight K-tiles (one tap x 64 channels, 8 KiB) stream through a
+// 3-stage LDS ring as in gemm_glds.h; epilogues (BN statistics, fused BN-backward reduction)
+// are gemm_glds.h's, unchanged. Forward reads x at p + (kh-1, kw-1); the data-grad reads dy at
+// p - (kh-1, kw-1) against the weight viewed (ci, (kh, kw, co)).
+struct PatchGeom {
+  int nimg, H, W, Wp, PP;        // Wp = W + 2, PP = (H + 2) * Wp
+  FastDiv f_pp, f_wp, f_hw, f_w;
+  int sign;                      // +1 forward, -1 data-grad
+};
+constexpr int PATCH_ROWS = 384;                        // padded pixels of 64 channels (128 B) per block
+constexpr int PATCH_BYTES = PATCH_ROWS * 128;
+using PCfg = gemmg::GCfg<4, 1, 2, 2, 3>;               // 256 x 64, 4 waves of 64 x 64, 3-stage weight ring
+constexpr int PATCH_SB = PCfg::BN * GBK * 2;           // one weight K-tile
+constexpr int PATCH_LDS = PATCH_BYTES + PCfg::S * PATCH_SB;   // 72 KiB: two blocks per CU
+static_assert(PCfg::EP_BYTES <= PATCH_LDS && PCfg::NTH * 33 * 4 <= PATCH_LDS, "epilogue staging exceeds LDS");
+
+AVSR_DEV int patch_pos(int p, const PatchGeom& pg) {   // output pixel -> padded position
+  const uint32_t n = fdiv((uint32_t)p, pg.f_hw), rem = (uint32_t)p - n * pg.f_hw.d;
+  const uint32_t y = fdiv(rem, pg.f_w), x = rem - y * pg.f_w.d;
+  return (int)(n * pg.PP + (y + 1) * pg.Wp + x + 1);
+}
+
+// the patch image [PATCH_ROWS][64] (k-major row swizzle of gemm_glds.h on the patch row)
+template <int NW> struct PatchLoad {
+  static constexpr int PIECES = PATCH_ROWS * 8 / 64 / NW;
+  __amdgpu_buffer_rsrc_t rs;
+  uint32_t vo[PIECES];
+  AVSR_DEV void init(const bf16* base, uint32_t bytes, const PatchGeom& pg, int qmin, int wave, int lane) {
+    rs = make_rsrc(base, bytes);
+#pragma unroll
+    for (int i = 0; i < PIECES; ++i) {
+      const int pr = (i * NW + wave) * 8 + (lane >> 3);
+      const int c = (lane & 7) ^ ((pr >> 1) & 7);
+      const uint32_t q = (uint32_t)(qmin + pr);
+      const uint32_t n = fdiv(q, pg.f_pp), rem = q - n * (uint32_t)pg.PP;
+      const uint32_t yy = fdiv(rem, pg.f_wp), xx = rem - yy * (uint32_t)pg.Wp;
+      const bool ok = n < (uint32_t)pg.nimg && yy - 1u < (uint32_t)pg.H && xx - 1u < (uint32_t)pg.W;
+      vo[i] = ok ? (((n * pg.H + yy - 1) * pg.W + xx - 1) * 64u + c * 8u) * 2u : OOB;
+    }
+  }
+  AVSR_DEV void issue(char* img, int wave) const {
+#pragma unroll
+    for (int i = 0; i < PIECES; ++i) bglds16(rs, vo[i], 0u, img + (i * NW + wave) * 1024);
+  }
+};
+
+template <class LB>
+struct PatchFrags {
+  bf16x8 a[PCfg::TM], b[PCfg::TN];
+  AVSR_DEV void load(const char* patch, const int (&row)[PCfg::TM], int toff, const char* wstage, int s, int lane) {
+#pragma unroll
+    for (int i = 0; i < PCfg::TM; ++i) {
+      const int r = row[i] + toff;
+      const int c = (4 * s + (lane >> 4)) ^ ((r >> 1) & 7);
+      a[i] = *(const bf16x8*)(patch + r * 128 + c * 16);
+    }
+#pragma unroll
+    for (int j = 0; j < PCfg::TN; ++j) b[j] = gemmg::gfrag<PCfg::BN, LB::KMAJ>(wstage, j * 16, s, lane);
+  }
+  AVSR_DEV void mma(f32x4 (&acc)[PCfg::TM][PCfg::TN]) const {
+#pragma unroll
+    for (int i = 0; i < PCfg::TM; ++i)
+#pragma unroll
+      for (int j = 0; j < PCfg::TN; ++j) acc[i][j] = mfma16(a[i], b[j], acc[i][j]);
+  }
+};
+
+template <int KIND>
+__global__ __launch_bounds__(PCfg::NTH, 2) void conv_patch_kernel(ConvArgs a, PatchGeom pg) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int S = PCfg::S, NK = 9, KS = GBK / 32, GLB = PATCH_SB / 1024 / PCfg::NW;
+  const int m0 = gemmg::xcd_remap(blockIdx.x, gridDim.x) * PCfg::BM;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int qmin = patch_pos(m0, pg) - pg.Wp - 1;
+  char* patch = smem;
+  char* ring = smem + PATCH_BYTES;
+  PatchLoad<PCfg::NW> lp;
+  lp.init((const bf16*)a.a, a.a_bytes, pg, qmin, wave, lane);
+  using LB = typename std::conditional<KIND == K_FWD, gemmg::BDenseK<PCfg::BN, PCfg::NW>,
+                                       BWgtR<PCfg::BN, PCfg::NW>>::type;
+  LB lb;
+  if constexpr (KIND == K_FWD) lb.init((const bf16*)a.b, a.b_bytes, a.K, 0, a.N, a.K, wave, lane);
+  else lb.init((const bf16*)a.b, a.b_bytes, a.g, 0, a.N, wave, lane);
+  int row[PCfg::TM];                 // patch row of this lane's output pixel in each 16-row block
+#pragma unroll
+  for (int i = 0; i < PCfg::TM; ++i) {
+    const int p = min(m0 + wave * 64 + i * 16 + (lane & 15), a.M - 1);
+    row[i] = patch_pos(p, pg) - qmin;
+  }
+  f32x4 acc[PCfg::TM][PCfg::TN];
+#pragma unroll
+  for (int i = 0; i < PCfg::TM; ++i)
+#pragma unroll
+    for (int j = 0; j < PCfg::TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  lp.issue(patch, wave);
+#pragma unroll
+  for (int p = 0; p < S; ++p) lb.issue(ring + p * PATCH_SB, p * GBK, wave);
+  gemmg::wait_vmcnt<GLB * (S - 1)>();      // the patch and weight tile 0 have landed
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  auto toff = [&](int kt) {                 // row offset of tap kt = (kh, kw) in the padded patch
+    const int kh = kt / 3, kw = kt - 3 * kh;
+    return pg.sign * ((kh - 1) * pg.Wp + (kw - 1));
+  };
+  PatchFrags<LB> cur, nxt;
+  cur.load(patch, row, toff(0), ring, 0, lane);
+  int cs = 0;
+  for (int kt = 0; kt < NK; ++kt) {
+    const int ns = cs + 1 == S ? 0 : cs + 1;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      if (s + 1 < KS) {
+        nxt.load(patch, row, toff(kt), ring + cs * PATCH_SB, s + 1, lane);
+      } else if (kt + 1 < NK) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (kt + S - 1 < NK) gemmg::wait_vmcnt<GLB * (S - 2)>();
+        else gemmg::wait_vmcnt<0>();
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (kt + S < NK) lb.issue(ring + cs * PATCH_SB, (kt + S) * GBK, wave);
+        nxt.load(patch, row, toff(kt + 1), ring + ns * PATCH_SB, 0, lane);
+      }
+      cur.mma(acc);
+      cur = nxt;
+    }
+    cs = ns;
+  }
+  __syncthreads();
+  if constexpr (KIND >= K_DGRAD_BNR) {
+    gemmg::epilogue_bnr<PCfg, KIND - K_DGRAD_BNR>(a.e, a.bnr, m0, 0, acc, smem);
+  } else {
+    gemmg::epilogue_g<bf16, bf16, PCfg>(a.e, m0, 0, acc, smem);
+  }
+}
+
+// AVSR_CONV_PATCH=0 keeps the general kernel (A/B comparisons)
+static bool patch_ok(const avsr_conv_params* p, const ConvArgs& a) {
+  const char* env = getenv("AVSR_CONV_PATCH");
+  if ((env && env[0] == '0') || p->dtype != AVSR_BF16 || !conv_glds_enabled() || !a.a_bytes || p->groups != 1) return false;
+  if (p->kh != 3 || p->kw != 3 || p->sh != 1 || p->sw != 1 || p->ph != 1 || p->pw != 1) return false;
+  if (p->cin != 64 || p->cout != 64 || p->ldx != 64 || p->ldy != 64) return false;
+  if (p->hin != p->hout || p->win != p->wout) return false;
+  // worst-case padded span of 256 consecutive output pixels, plus the tap halo on both sides
+  const int64_t W = p->win, HW = (int64_t)p->hin * p->win, Wp = W + 2;
+  const int64_t span = (PCfg::BM - 1) + 2 * ((PCfg::BM - 1) / W + 1) + 2 * Wp * ((PCfg::BM - 1) / HW + 1) + 2 * (Wp + 1) + 1;
+  return span <= PATCH_ROWS;
+}
+
+template <int KIND>
+static int patch_launch(const ConvArgs& a, const avsr_conv_params* p, int sign, hipStream_t st) {
+  PatchGeom pg;
+  pg.nimg = p->nimg; pg.H = p->hin; pg.W = p->win; pg.Wp = p->win + 2; pg.PP = (p->hin + 2) * (p->win + 2);
+  pg.f_pp = make_fastdiv((uint32_t)pg.PP); pg.f_wp = make_fastdiv((uint32_t)pg.Wp);
+  pg.f_hw = make_fastdiv((uint32_t)(p->hin * p->win)); pg.f_w = make_fastdiv((uint32_t)p->win);
+  pg.sign = sign;
+  const int tm = (a.M + PCfg::BM - 1) / PCfg::BM;
+  if (a.e.stats && a.e.stats_tiles != tm) return AVSR_E_SHAPE;
+  hipLaunchKernelGGL((conv_patch_kernel<KIND>), dim3((unsigned)tm), dim3(PCfg::NTH), PATCH_LDS, st, a, pg);
+  AVSR_CHECK_LAUNCH();
+  return 0;
+}
+
 template <int KIND>
 static int s2_launch(const ConvArgs& a0, const avsr_conv_params* p, hipStream_t st) {
   S2Class cl[4];
@@ -658,6 +828,8 @@ extern "C" int avsr_conv_fwd(const avsr_conv_params* p, void* stream) {
   if (a.M == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
   if (p->dtype == AVSR_F32) return by_tile<float, float, K_FWD>(a, p->groups, st);
+  if (p->dtype == AVSR_BF16 && !p->bias && !p->act && !p->res && !p->preact && patch_ok(p, a))
+    return patch_launch<K_FWD>(a, p, 1, st);
   if (p->dtype == AVSR_BF16)
     return conv_glds_enabled() ? glds_by_tile<bf16, K_FWD>(a, p->groups, st) : by_tile<bf16, bf16, K_FWD>(a, p->groups, st);
   return AVSR_E_DTYPE;
@@ -696,6 +868,11 @@ extern "C" int avsr_conv_bwd_data(const avsr_conv_params* p, void* stream) {
       if (p->bnr_res) return s2_launch<K_DGRAD_BNR + 1>(a, p, st);
       return s2_launch<K_DGRAD_BNR>(a, p, st);
     }
+    if (patch_ok(p, a)) {
+      if (p->bnr_scale2) return patch_launch<K_DGRAD_BNR + 2>(a, p, -1, st);
+      if (p->bnr_res) return patch_launch<K_DGRAD_BNR + 1>(a, p, -1, st);
+      return patch_launch<K_DGRAD_BNR>(a, p, -1, st);
+    }
     if (p->bnr_scale2) return glds_by_tile<bf16, K_DGRAD_BNR + 2>(a, 1, st);
     if (p->bnr_res) return glds_by_tile<bf16, K_DGRAD_BNR + 1>(a, 1, st);
     return glds_by_tile<bf16, K_DGRAD_BNR>(a, 1, st);
@@ -704,6 +881,7 @@ extern "C" int avsr_conv_bwd_data(const avsr_conv_params* p, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   if (p->dtype == AVSR_F32) return by_tile<float, float, K_DGRAD>(a, p->groups, st);
   if (s2_phase(p)) return s2_launch<K_DGRAD>(a, p, st);
+  if (p->dtype == AVSR_BF16 && patch_ok(p, a)) return patch_launch<K_DGRAD>(a, p, -1, st);
   if (p->dtype == AVSR_BF16)
     return conv_glds_enabled() ? glds_by_tile<bf16, K_DGRAD>(a, p->groups, st)
                                : by_tile<bf16, bf16, K_DGRAD>(a, p->groups, st);

@@ -42,6 +42,8 @@ _COLSUM_DEFER = os.environ.get("AVSR_COLSUM_DEFER", "1") == "1"
 _SIDE_BIAS = os.environ.get("AVSR_SIDE_BIAS", "1") == "1"
 # the CTC branch of the forward runs on the side stream beside the decoder forward
 _CTC_SIDE = os.environ.get("AVSR_CTC_SIDE", "1") == "1"
+# bf16 stem conv straight from the video (stem.hip) instead of pack + general implicit GEMM
+_STEM_DIRECT = os.environ.get("AVSR_STEM_DIRECT", "0") == "1"
 
 
 _STEP_STREAMS = {}
@@ -454,23 +456,32 @@ class Engine:
         N = B * T
         R = "encoder.feature_extractor_video.resnet."
         ctx = {"N": N}
-        xp = self._e(N, 88, 88, 8)
-        ops.stem_pack(videos.contiguous(), xp)
-        wp = self._e(64, 7, 7, 8)
-        ops.stem_wpack(self.arena.master(R + "frontend3D.0.weight"), wp)
         gs = ops.ConvGeom(N, 88, 88, 8, 64, 7, 7, (2, 2), (3, 3))
-        # stem conv uses the packed weight (not an arena view)
         h0 = self._e(N * 44 * 44, 64)
         bn, gam, bet = self._bn(R + "frontend3D.1")
         st0 = ops.BnState(64, self.device)
-        if train:
-            part = self._e(64, ops.conv_stat_tiles(gs, ops.dtype_code(xp)), 3, dtype=torch.float32)
+        vid = videos.contiguous()
+        direct = self.dtype == torch.bfloat16 and _STEM_DIRECT
+        # the packed 8-channel input: the general conv's operand, and the stem weight-grad's
+        xp = None
+        if not direct or save:
+            xp = self._e(N, 88, 88, 8)
+            ops.stem_pack(vid, xp)
+        if direct:      # bf16: the stem conv reads the video itself (stem.hip, K = 288 instead of 392)
+            wk = self._e(64, ops.STEM_K)
+            ops.stem_wpack2(self.arena.master(R + "frontend3D.0.weight"), wk)
+            part = self._e(64, ops.stem_conv_tiles(N), 3, dtype=torch.float32) if train else None
+            ops.stem_conv_fwd(vid, wk, h0, part)
+        else:
+            wp = self._e(64, 7, 7, 8)        # the packed weight (not an arena view)
+            ops.stem_wpack(self.arena.master(R + "frontend3D.0.weight"), wp)
+            part = self._e(64, ops.conv_stat_tiles(gs, ops.dtype_code(xp)), 3, dtype=torch.float32) if train else None
             ops.conv_fwd(gs, xp, wp, h0, part)
+        if train:
             ops.bn_finalize(st0, gam, bet, bn.running_mean, bn.running_var, partials=part, training=True,
                             momentum=bn.momentum, eps=bn.eps)
             bn.num_batches_tracked.add_(1)
         else:
-            ops.conv_fwd(gs, xp, wp, h0)
             ops.bn_finalize(st0, gam, bet, bn.running_mean, bn.running_var, training=False, eps=bn.eps)
         x = self._e(N * 22 * 22, 64)
         am = self._e(N * 22 * 22, 64, dtype=torch.uint8)

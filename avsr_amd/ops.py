@@ -613,6 +613,35 @@ def stem_wpack(w, wp):
     return wp
 
 
+STEM_K = 288     # packed stem weight row (avsr_stem_wpack2)
+
+
+def stem_wpack2(w, wk):
+    """Conv3d stem weight (64,1,5,7,7) fp32 -> [64][288] bf16 (k = (dt*7 + kh)*8 + kw)"""
+    assert w.dtype == torch.float32 and w.numel() == 64 * 245 and w.is_contiguous()
+    assert wk.dtype == torch.bfloat16 and wk.numel() == 64 * STEM_K
+    L.check(L.load().avsr_stem_wpack2(w.data_ptr(), wk.data_ptr(), L.stream_ptr()), "avsr_stem_wpack2")
+    return wk
+
+
+def stem_conv_tiles(nimg):
+    return L.load().avsr_stem_conv_tiles(int(nimg))
+
+
+def stem_conv_fwd(videos, wk, h, stats=None):
+    """stem Conv3d straight from the videos (B,1,T,88,88) fp32 -> h [B*T*44*44][64] bf16 (+ BN
+    partial statistics [64][stem_conv_tiles(B*T)][3])"""
+    B, _, T = videos.shape[:3]
+    assert videos.dtype == torch.float32 and videos.is_contiguous() and tuple(videos.shape[3:]) == (88, 88)
+    assert h.dtype == torch.bfloat16 and h.numel() == B * T * 44 * 44 * 64 and h.is_contiguous()
+    if stats is not None:
+        assert stats.dtype == torch.float32 and stats.numel() >= 64 * stem_conv_tiles(B * T) * 3
+    L.check(L.load().avsr_stem_conv_fwd(B, T, videos.data_ptr(), wk.data_ptr(), h.data_ptr(),
+                                        None if stats is None else stats.data_ptr(), L.stream_ptr()),
+            "avsr_stem_conv_fwd")
+    return h
+
+
 def stem_wgrad_unpack(gp, gw):
     L.check(L.load().avsr_stem_wgrad_unpack(gp.data_ptr(), gw.data_ptr(), L.stream_ptr()), "avsr_stem_wgrad_unpack")
 

@@ -162,10 +162,10 @@ def test_stride2_dgrad_parity_classes_match_full(dev, case, beta, monkeypatch):
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_conv_stats_at_192_eligible_shape(dev, dtype):
     """the s3h fault's regression on the device: a stage-2 conv with enough rows for the
-    192-row bf16 tile (M = 900 x 11 x 11 = 108,900), BN partials sized by conv_stat_tiles for
+    192-row bf16 tile (M = 3000 x 11 x 11 = 363,000), BN partials sized by conv_stat_tiles for
     the dtype, statistics combining to the batch moments; a buffer sized for the other
     dtype's tile count is refused before launch."""
-    n, h, c = 900, 11, 128
+    n, h, c = 3000, 11, 128
     geom = ops.ConvGeom(n, h, h, c, c, 3, 3, (1, 1), (1, 1))
     tiles = ops.conv_stat_tiles(geom, ops.dtype_code(torch.empty(0, dtype=dtype)))
     other = ops.conv_stat_tiles(geom, ops.dtype_code(torch.empty(0, dtype=torch.bfloat16 if dtype == torch.float32
@@ -192,3 +192,35 @@ def test_conv_stats_at_192_eligible_shape(dev, dtype):
     yf = y.double().reshape(-1, c)
     assert _rel(gm.flatten(), yf.mean(0)) < 1e-3 or (gm.flatten() - yf.mean(0)).abs().max() < 1e-4
     assert _rel(var, yf.var(0, unbiased=False)) < 1e-3
+
+
+def test_stem_conv_direct(dev):
+    """stem Conv3d (k 5x7x7, stride 1x2x2, pad 2x3x3) straight from the fp32 video
+    (stem.hip, K = 288 grouped (frame, row) x 8 columns) vs fp64 conv3d on the same
+    bf16-rounded operands; BN partial statistics combine to the batch moments. T = 7 so
+    that frames outside the clip (time padding) are hit at both ends."""
+    B, T = 2, 7
+    g = torch.Generator().manual_seed(11)
+    video = torch.randn(B, 1, T, 88, 88, generator=g)
+    w = torch.randn(64, 1, 5, 7, 7, generator=g) * 0.05
+    ref = F.conv3d(video.bfloat16().double(), w.bfloat16().double(), stride=(1, 2, 2), padding=(2, 3, 3))
+    ref = ref.permute(0, 2, 3, 4, 1).reshape(B * T * 44 * 44, 64)
+    wk = torch.empty(64, ops.STEM_K, device=dev, dtype=torch.bfloat16)
+    ops.stem_wpack2(w.to(dev), wk)
+    tiles = ops.stem_conv_tiles(B * T)
+    h = torch.empty(B * T * 44 * 44, 64, device=dev, dtype=torch.bfloat16)
+    stats = torch.empty(64, tiles, 3, device=dev)
+    ops.stem_conv_fwd(video.to(dev), wk, h, stats)
+    torch.cuda.synchronize()
+    assert _rel(h, ref) < 8e-3
+    cnt, mean, m2 = stats[..., 0].double(), stats[..., 1].double(), stats[..., 2].double()
+    assert torch.all(cnt.sum(1) == B * T * 44 * 44)
+    tot = cnt.sum(1, keepdim=True)
+    gm = (cnt * mean).sum(1, keepdim=True) / tot
+    var = ((m2 + cnt * (mean - gm) ** 2).sum(1, keepdim=True) / tot).flatten()
+    assert (gm.flatten().cpu() - ref.mean(0)).abs().max() < 1e-3 * ref.abs().max()
+    assert _rel(var, ref.var(0, unbiased=False)) < 2e-3
+    h2 = torch.empty_like(h)
+    ops.stem_conv_fwd(video.to(dev), wk, h2)          # statistics optional (eval)
+    torch.cuda.synchronize()
+    assert torch.equal(h, h2)

@@ -294,3 +294,48 @@ def test_conv_192_tiles_match_128(dev, monkeypatch, case):
     assert torch.equal(o0[0], o1[0]) and torch.equal(o0[3], o1[3])
     assert _rel(o1[1], o0[1]) < 1e-5 and _rel(o1[2], o0[2]) < 1e-5
     assert _rel(o1[4], o0[4]) < 1e-5
+
+
+@pytest.mark.parametrize("case", [(40, 22, 64, 64, 3, 1, 1, "identity"), (33, 22, 64, 64, 3, 1, 1, "plain")])
+def test_conv_patch_matches_general(dev, monkeypatch, case):
+    """the patch-resident 3x3 stride-1 kernel (AVSR_CONV_PATCH, ResNet stage 1: one LDS image of
+    the padded input patch per 256-pixel block) against the general implicit-GEMM kernel:
+    same tiles, same K order -> bit-identical forward outputs, BN partial statistics, data-grads
+    with the fused BN-backward epilogue and their column sums, and plain data-grads
+    accumulated into an existing dx (beta = 1). Ragged last tile (M % 256 != 0)."""
+    n, hw, cin, cout, k, s, p, mode = case
+    g = torch.Generator().manual_seed(n + hw + 7)
+    geom = ops.ConvGeom(n, hw, hw, cin, cout, k, k, (s, s), (p, p))
+    M = n * hw * hw
+    assert M % 256
+    bf = torch.bfloat16
+    x = torch.randn(M, cin, generator=g).to(dev, bf)
+    w = (torch.randn(cout, k, k, cin, generator=g) * (cin * k * k) ** -0.5).to(dev, bf)
+    dy = torch.randn(geom.out_pixels, cout, generator=g).to(dev, bf)
+    h = (torch.randn(M, cin, generator=g) * 1.3 + 0.2).to(dev, bf)
+    r = (torch.randn(M, cin, generator=g) * 0.8 - 0.1).to(dev, bf)
+    dx0 = (torch.randn(M, cin, generator=g) * 0.3).to(dev, bf)
+    st = ops.BnState(cin, dev)
+    st.mean.copy_(0.1 * torch.randn(cin, generator=g)); st.invstd.copy_(0.5 + torch.rand(cin, generator=g))
+    st.scale.copy_(1 + 0.2 * torch.randn(cin, generator=g)); st.shift.copy_(0.2 * torch.randn(cin, generator=g))
+    a = (0.25 + 0.05 * torch.randn(cin, generator=g)).to(dev)
+    out = {}
+    for flag in ("0", "1"):
+        monkeypatch.setenv("AVSR_CONV_PATCH", flag)
+        y = torch.empty(geom.out_pixels, cout, device=dev, dtype=bf)
+        part = torch.empty(cout, ops.conv_stat_tiles(geom, ops.dtype_code(x)), 3, device=dev)
+        ops.conv_fwd(geom, x, w, y, stats=part)
+        dx = dx0.clone()
+        ws, tiles = ops.conv_bwd_data_bnr(geom, dy, w, dx, h, st, a, res=None if mode == "plain" else r,
+                                          beta=1.0)
+        dxp = dx0.clone()
+        ops.conv_bwd_data(geom, dy, w, dxp, beta=1.0)
+        torch.cuda.synchronize()
+        out[flag] = (y, part.clone(), dx, ws[:tiles * 4 * cin].clone(), dxp)
+    for t0, t1 in zip(out["0"], out["1"]):
+        assert torch.equal(t0, t1)
+    # and the forward is a convolution (fp64 reference)
+    xr = x.double().view(n, hw, hw, cin).permute(0, 3, 1, 2)
+    wr = w.double().permute(0, 3, 1, 2)
+    ref = torch.nn.functional.conv2d(xr, wr, padding=1).permute(0, 2, 3, 1).reshape(M, cout)
+    assert _rel(out["1"][0], ref) < 2e-2

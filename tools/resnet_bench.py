@@ -43,12 +43,16 @@ def once(fuse):
 mode = sys.argv[2] if len(sys.argv) > 2 else "fuse"
 variants = [("fuse=1", True, "1"), ("fuse=0", False, "1")] if mode == "fuse" else \
     [("c192=1", True, "1", "1"), ("c192=0", True, "1", "0")] if mode == "c192" else \
+    [("patch=1", True, "1", "1", "1"), ("patch=0", True, "1", "1", "0")] if mode == "patch" else \
+    [("new", True, "1", "1", "1", True), ("old", True, "1", "1", "0", False)] if mode == "new" else \
     [("s2phase=1", True, "1"), ("s2phase=0", True, "0")]
 
 
 def run(var):
     os.environ["AVSR_CONV_S2PHASE"] = var[2]
     os.environ["AVSR_CONV_192"] = var[3] if len(var) > 3 else "1"
+    os.environ["AVSR_CONV_PATCH"] = var[4] if len(var) > 4 else "1"
+    E._STEM_DIRECT = var[5] if len(var) > 5 else True
     return once(var[1])
 
 
