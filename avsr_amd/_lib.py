@@ -268,7 +268,7 @@ SYMBOLS = {
     "avsr_cast_flat": ([_i, _i, _i64, _c_p, _c_p, _c_p], _i),
     "avsr_stem_pack": ([_i, _i, _i, _c_p, _c_p, _c_p], _i),
     "avsr_stem_wpack": ([_i, _c_p, _c_p, _c_p], _i),
-    "avsr_stem_conv_tiles": ([_i], _i),
+    "avsr_stem_conv_tiles": ([_i, _i], _i),
     "avsr_stem_wpack2": ([_c_p, _c_p, _c_p], _i),
     "avsr_stem_conv_fwd": ([_i, _i, _c_p, _c_p, _c_p, _c_p, _c_p], _i),
     "avsr_stem_wgrad_unpack": ([_c_p, _c_p, _c_p], _i),

@@ -11,24 +11,23 @@
 // 4 output rows needs (fp32 video -> bf16) in two copies shifted by one pixel pair, so every
 // window starts 8-byte aligned in one of them: an A fragment is two ds_read_b64 per lane, no
 // gather, no packed tensor. The 64 x 288 weight sits in LDS with padded rows (conflict-free
-// ds_read_b128). The epilogue writes the NHWC output through an LDS staging tile and the BN
-// partial statistics (count, mean, M2) of the block (the general conv epilogue's format).
+// ds_read_b128). The epilogue writes the NHWC output and BN partial statistics (count, mean,
+// M2) in the general conv epilogue's format.
 #include "common.h"
 
 namespace {
 
-constexpr int SC_R = 4;                    // output rows per block (44 = 11 bands)
+constexpr int SC_R = 4;                    // output rows per band (44 = 11 bands)
 constexpr int SC_BANDS = 44 / SC_R;
 constexpr int SC_VW = 48;                  // virtual output width (columns 44..47 computed and dropped)
-constexpr int SC_PX = SC_R * SC_VW;        // 192 pixels per block
 constexpr int SC_ROWS = 2 * SC_R + 5;      // input rows per band
 constexpr int SC_CW = 96;                  // elements per staged copy of an input row
-constexpr int SC_IMG = 5 * SC_ROWS * 2 * SC_CW * 2;      // 24,960 B
-constexpr int SC_K = 288, SC_WROW = SC_K + 8;            // weight row: 592 B (conflict-free)
-constexpr int SC_WB = 64 * SC_WROW * 2;                  // 37,888 B
-constexpr int SC_LDS = SC_IMG + SC_WB;                   // 62,848 B: two blocks per CU
-constexpr int SC_SROW = 64 + 8;                          // staging row (bf16), 144 B
-static_assert(SC_PX * SC_SROW * 2 + 2 * 64 * 3 * 4 <= SC_LDS, "epilogue staging exceeds LDS");
+constexpr int SC_ND = SC_CW / 2 + 1;       // pixel pairs staged per input row (49)
+constexpr int SC_K = 288;
+constexpr int SC_ROWB = 2 * SC_CW * 2;     // one staged input row, both copies (384 B)
+constexpr int SC_SLOT = SC_ROWS * SC_ROWB; // one frame's band (4,992 B)
+constexpr int SC_LDS = 5 * SC_SLOT;        // ring of the 5 frames a step reads (24,960 B)
+constexpr int SC_BLOCKS_PER_CU = 2;
 
 AVSR_DEV uint32_t pack_bf16(float a, float b) {
   union { bf16 h[2]; uint32_t u; } v;
@@ -36,171 +35,223 @@ AVSR_DEV uint32_t pack_bf16(float a, float b) {
   return v.u;
 }
 
-// XCD-aware block order (gemm_glds.h xcd_remap): consecutive bands / frames share input rows
-AVSR_DEV int sc_remap(int orig, int nwg) {
-  const int xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
-  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+// Stage input frame tt of clip b (rows ir0 .. ir0 + 12 of the band) into ring slot tt mod 5:
+// pair k of a row is D_k = (x[2k - 3], x[2k - 2]); copy A dword d = D_d (an even ow's window
+// starts at element 2ow), copy B dword d = D_(d+1) (an odd ow's starts at 2ow - 2). Frames,
+// rows and columns outside the clip come back as zeros from the buffer's range check (the
+// conv padding). Split in two so the loads of the next frame fly during a step's MFMAs.
+constexpr int SC_NT = 256;
+constexpr int SC_NI = (SC_ROWS * SC_ND + SC_NT - 1) / SC_NT;
+struct StageRegs { float xa[SC_NI], xb[SC_NI]; };
+
+AVSR_DEV void stem_stage_load(StageRegs& g, __amdgpu_buffer_rsrc_t rs, int b, int T, int tt, int ir0, int tid) {
+  constexpr uint32_t OOB = 0x80000000u;
+  const bool fok = tt >= 0 && tt < T;
+#pragma unroll
+  for (int u = 0; u < SC_NI; ++u) {
+    const int i = tid + u * SC_NT;
+    const int r = i / SC_ND, k = i - r * SC_ND;
+    const int ir = ir0 + r, c0 = 2 * k - 3;
+    const bool rok = fok && i < SC_ROWS * SC_ND && ir >= 0 && ir < 88;
+    const uint32_t row = (uint32_t)(((b * T + tt) * 88 + ir) * 88);
+    const uint32_t oa = rok && c0 >= 0 && c0 < 88 ? (row + c0) * 4u : OOB;
+    const uint32_t ob = rok && c0 + 1 >= 0 && c0 + 1 < 88 ? (row + c0 + 1) * 4u : OOB;
+    g.xa[u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, oa, 0, 0));
+    g.xb[u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, ob, 0, 0));
+  }
 }
 
-__global__ __launch_bounds__(256, 2) void stem_conv_kernel(int B, int T, const float* __restrict__ video,
-                                                           const bf16* __restrict__ wk, bf16* __restrict__ h,
-                                                           float* __restrict__ stats, int tiles) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* img = smem;
-  char* wl = smem + SC_IMG;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int blk = sc_remap(blockIdx.x, gridDim.x);
-  const int n = blk / SC_BANDS, band = blk - n * SC_BANDS;
-  const int b = n / T, t = n - b * T;
-  const int oh0 = band * SC_R, ir0 = 2 * oh0 - 3;
-  // weights -> LDS (16-B pieces of the [64][288] packed weight into 592-B rows) and the input
-  // band -> LDS: every global load of the block is issued before any LDS write (a loop that
-  // waits for each load in turn made this prologue latency-bound: 1.7 ms at C2)
-  constexpr int WP = 64 * SC_K / 8 / 256;                  // 9 weight pieces per thread
-  constexpr int ND = SC_CW / 2 + 1;                        // 49 pixel pairs per input row
-  constexpr int NI = (5 * SC_ROWS * ND + 255) / 256;       // 13 pairs per thread
-  uint4 wv[WP];
+AVSR_DEV void stem_stage_store(const StageRegs& g, char* ring, int tt, int tid) {
+  char* slot = ring + ((tt + 10) % 5) * SC_SLOT;
 #pragma unroll
-  for (int u = 0; u < WP; ++u) {
-    const int i = tid + u * 256, co = i / (SC_K / 8), c = i - co * (SC_K / 8);
-    wv[u] = *(const uint4*)(wk + co * SC_K + c * 8);
-  }
-  // pair k of staged row rr: D_k = (x[2k - 3], x[2k - 2]); copy A dword d = D_d (an even ow's
-  // window starts at element 2ow), copy B dword d = D_(d+1) (an odd ow's starts at 2ow - 2);
-  // frames / rows / columns outside the clip read as zero (the conv padding)
-  float xa[NI], xb[NI];
-#pragma unroll
-  for (int u = 0; u < NI; ++u) {
-    const int i = tid + u * 256;
-    const int rr = i / ND, k = i - rr * ND;
-    const int r = rr % SC_ROWS, dt = rr / SC_ROWS;
-    const int tt = t + dt - 2, ir = ir0 + r, c0 = 2 * k - 3;
-    const bool rowok = i < 5 * SC_ROWS * ND && tt >= 0 && tt < T && ir >= 0 && ir < 88;
-    const float* row = video + (((int64_t)b * T + (rowok ? tt : 0)) * 88 + (rowok ? ir : 0)) * 88;
-    xa[u] = (rowok && c0 >= 0 && c0 < 88) ? row[c0] : 0.f;
-    xb[u] = (rowok && c0 + 1 >= 0 && c0 + 1 < 88) ? row[c0 + 1] : 0.f;
-  }
-#pragma unroll
-  for (int u = 0; u < WP; ++u) {
-    const int i = tid + u * 256, co = i / (SC_K / 8), c = i - co * (SC_K / 8);
-    *(uint4*)(wl + co * SC_WROW * 2 + c * 16) = wv[u];
-  }
-#pragma unroll
-  for (int u = 0; u < NI; ++u) {
-    const int i = tid + u * 256;
-    if (i < 5 * SC_ROWS * ND) {
-      const int rr = i / ND, k = i - rr * ND;
-      const uint32_t dk = pack_bf16(xa[u], xb[u]);
-      char* base = img + (rr * 2) * (SC_CW * 2);
-      if (k < ND - 1) *(uint32_t*)(base + k * 4) = dk;                    // copy A
+  for (int u = 0; u < SC_NI; ++u) {
+    const int i = tid + u * SC_NT;
+    if (i < SC_ROWS * SC_ND) {
+      const int r = i / SC_ND, k = i - r * SC_ND;
+      const uint32_t dk = pack_bf16(g.xa[u], g.xb[u]);
+      char* base = slot + r * SC_ROWB;
+      if (k < SC_ND - 1) *(uint32_t*)(base + k * 4) = dk;                  // copy A
       if (k > 0) *(uint32_t*)(base + SC_CW * 2 + (k - 1) * 4) = dk;       // copy B
     }
   }
-  __syncthreads();
-  // wave tile: 96 pixels (wm) x 32 output channels (wn); 16x16x32 MFMA, K-step = 4 groups
+}
+
+// Persistent blocks, one per (clip, band of 4 output rows, run of frames): consecutive frames
+// of a band share 4 of their 5 input frames, so each step stages ONE new frame into a 5-slot
+// ring (13 rows x 2 copies) instead of five. 4 waves: wave (wm, wn) = 96 pixels x 32 output
+// channels. The MFMA computes C[co][px] (A = weights, held in registers for the whole run: the
+// wave's 32 channels x 288 k; B = the input windows from the ring), so a lane's accumulator is
+// 4 consecutive channels of one pixel -> 8-byte NHWC stores, no staging. BN statistics (count,
+// mean, M2) per channel are merged over the block's whole run (Chan), one partial per block.
+__global__ __launch_bounds__(256, SC_BLOCKS_PER_CU) void stem_conv_kernel(
+    int B, int T, int chunks, int fpc, const float* __restrict__ video, uint32_t vbytes, const bf16* __restrict__ wk,
+    bf16* __restrict__ h, float* __restrict__ stats, int tiles) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  __shared__ float red[2][64][3];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
-  int abase[6];
+  const int blk = blockIdx.x;
+  const int stream = blk / chunks, chunk = blk - stream * chunks;
+  const int b = stream / SC_BANDS, band = stream - b * SC_BANDS;
+  const int t0 = chunk * fpc, t1 = min(T, t0 + fpc);
+  const int oh0 = band * SC_R, ir0 = 2 * oh0 - 3;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(video), (short)0,
+                                                                        (int)vbytes, 0x00020000);
+  // this wave's weights: rows co = 32wn + 16j + (lane & 15), k-chunk (lane >> 4) of each step
+  bf16x8 wr[SC_K / 32][2];
+#pragma unroll
+  for (int ks = 0; ks < SC_K / 32; ++ks)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      wr[ks][j] = *(const bf16x8*)(wk + (wn * 32 + j * 16 + (lane & 15)) * SC_K + ks * 32 + (lane >> 4) * 8);
+  // this lane's pixel (B column) in each of the wave's 6 pixel fragments
+  int pbase[6];
+  bool pvalid[6];
 #pragma unroll
   for (int i = 0; i < 6; ++i) {
     const int v = wm * 96 + i * 16 + (lane & 15);
-    const int ob = v / SC_VW, ow = min(v - ob * SC_VW, 43);
-    const int cp = ow & 1, j0 = 2 * ow - 2 * cp;
-    abase[i] = (2 * ob * 2 + cp) * (SC_CW * 2) + j0 * 2;    // row 2*ob of frame 0; + (dt*13 + kh) rows below
+    const int ob = v / SC_VW, ow = v - ob * SC_VW;
+    const int owc = min(ow, 43), cp = owc & 1, j0 = 2 * owc - 2 * cp;
+    pvalid[i] = ow < 44;
+    pbase[i] = 2 * ob * SC_ROWB + cp * (SC_CW * 2) + j0 * 2;
   }
-  f32x4 acc[6][2];
+  float rn = 0.f, rmean[8], rm2[8];                       // running stats of this lane's 8 channels
 #pragma unroll
-  for (int i = 0; i < 6; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int q = 0; q < 8; ++q) rmean[q] = rm2[q] = 0.f;
+  if (t0 < t1) {
+    for (int f = t0 - 2; f <= t0 + 2; ++f) {
+      StageRegs g;
+      stem_stage_load(g, rs, b, T, f, ir0, tid);
+      stem_stage_store(g, smem, f, tid);
+    }
+  }
+  __syncthreads();
   const int g0 = lane >> 4;
-#pragma unroll 1
-  for (int ks = 0; ks < SC_K / 32; ++ks) {
-    const int g = 4 * ks + g0;                              // (dt, kh) group of this lane's 8 k
-    const int dt = g < 35 ? g / 7 : 0, kh = g < 35 ? g - 7 * (g / 7) : 0;
-    const int roff = (dt * SC_ROWS + kh) * 2 * (SC_CW * 2);
-    bf16x8 a[6], bw[2];
+  for (int t = t0; t < t1; ++t) {
+    StageRegs nxt;                                        // frame t + 3: loads in flight during the MFMAs
+    if (t + 1 < t1) stem_stage_load(nxt, rs, b, T, t + 3, ir0, tid);
+    f32x4 acc[6][2];
+#pragma unroll
+    for (int i = 0; i < 6; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // B fragments of K-step ks (the lane's 8 k = group 4ks + g0 of its pixel), double-buffered:
+    // step ks + 1's reads are issued before step ks's MFMAs
+    auto rdB = [&](int ks, bf16x8 (&xb)[6]) {
+      const int g = 4 * ks + g0;
+      const int dt = g < 35 ? g / 7 : 0, kh = g < 35 ? g - 7 * (g / 7) : 0;
+      const int roff = ((t + dt - 2 + 10) % 5) * SC_SLOT + kh * SC_ROWB;
+#pragma unroll
+      for (int i = 0; i < 6; ++i) {
+        const int o1 = pbase[i] + roff;
+        int o2 = o1 + 8;
+        asm volatile("" : "+v"(o2));                      // two ds_read_b64 (2 cycles each), not one ds_read2_b64 (8)
+        union { uint2 u[2]; bf16x8 hh; } x;
+        x.u[0] = *(const uint2*)(smem + o1);
+        x.u[1] = *(const uint2*)(smem + o2);
+        xb[i] = x.hh;
+      }
+    };
+    bf16x8 bcur[6], bnx[6];
+    rdB(0, bcur);
+#pragma unroll
+    for (int ks = 0; ks < SC_K / 32; ++ks) {
+      if (ks + 1 < SC_K / 32) rdB(ks + 1, bnx);
+#pragma unroll
+      for (int i = 0; i < 6; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = mfma16(wr[ks][j], bcur[i], acc[i][j]);
+#pragma unroll
+      for (int i = 0; i < 6; ++i) bcur[i] = bnx[i];
+    }
+    // output: lane holds channels co0 .. co0+3 of pixel (ob, ow) in tile (i, j)
+    const int n = b * T + t;
+    bf16* out = h + ((int64_t)n * 44 * 44 + (int64_t)oh0 * 44) * 64;
 #pragma unroll
     for (int i = 0; i < 6; ++i) {
-      const char* p = img + abase[i] + roff;
-      union { uint2 u[2]; bf16x8 h; } x;
-      x.u[0] = *(const uint2*)p;
-      x.u[1] = *(const uint2*)(p + 8);
-      a[i] = x.h;
-    }
+      if (!pvalid[i]) continue;
+      const int v = wm * 96 + i * 16 + (lane & 15);
+      const int ob = v / SC_VW, ow = v - ob * SC_VW;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int co = wn * 32 + j * 16 + (lane & 15);
-      bw[j] = *(const bf16x8*)(wl + co * SC_WROW * 2 + (4 * ks + g0) * 16);
-    }
-#pragma unroll
-    for (int i = 0; i < 6; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) acc[i][j] = mfma16(a[i], bw[j], acc[i][j]);
-  }
-  __syncthreads();
-  // ---- epilogue 1: BN partial statistics of the block's 176 valid pixels, per channel
-  float* red = (float*)(smem + SC_PX * SC_SROW * 2);       // [2 (wm)][64][3]
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    float s = 0.f, c = 0.f;
-#pragma unroll
-    for (int i = 0; i < 6; ++i)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int v = wm * 96 + i * 16 + 4 * (lane >> 4) + r;
-        const bool ok = v % SC_VW < 44;
-        s += ok ? acc[i][j][r] : 0.f;
-        c += ok ? 1.f : 0.f;
+      for (int j = 0; j < 2; ++j) {
+        const int co0 = wn * 32 + j * 16 + 4 * g0;
+        union { bf16x4 v4; uint2 u; } o;
+        o.v4 = bf16x4{(bf16)acc[i][j][0], (bf16)acc[i][j][1], (bf16)acc[i][j][2], (bf16)acc[i][j][3]};
+        *(uint2*)(out + (ob * 44 + ow) * 64 + co0) = o.u;
       }
-    s += __shfl_xor(s, 16, 64); s += __shfl_xor(s, 32, 64);
-    c += __shfl_xor(c, 16, 64); c += __shfl_xor(c, 32, 64);
-    const float mean = s / c;
-    float m2 = 0.f;
+    }
+    if (stats != nullptr) {   // this step's (count, mean, M2) per channel over the wave's 88 pixels
+      float s[8], m2[8];
 #pragma unroll
-    for (int i = 0; i < 6; ++i)
+      for (int q = 0; q < 8; ++q) {
+        const int j = q >> 2, r = q & 3;
+        float a = 0.f;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int v = wm * 96 + i * 16 + 4 * (lane >> 4) + r;
-        const float dd = acc[i][j][r] - mean;
-        m2 += v % SC_VW < 44 ? dd * dd : 0.f;
+        for (int i = 0; i < 6; ++i) a += pvalid[i] ? acc[i][j][r] : 0.f;
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) a += __shfl_xor(a, o, 64);
+        s[q] = a * (1.f / 88.f);
+        float d2 = 0.f;
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+          const float d = acc[i][j][r] - s[q];
+          d2 += pvalid[i] ? d * d : 0.f;
+        }
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) d2 += __shfl_xor(d2, o, 64);
+        m2[q] = d2;
       }
-    m2 += __shfl_xor(m2, 16, 64); m2 += __shfl_xor(m2, 32, 64);
-    if (lane < 16) {
-      const int co = wn * 32 + j * 16 + lane;
-      red[(wm * 64 + co) * 3 + 0] = c;
-      red[(wm * 64 + co) * 3 + 1] = mean;
-      red[(wm * 64 + co) * 3 + 2] = m2;
+      const float nb = 88.f, nn = rn + nb;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {                       // Chan: merge (88, s, m2) into the run
+        const float d = s[q] - rmean[q];
+        rmean[q] += d * nb / nn;
+        rm2[q] += m2[q] + d * d * rn * nb / nn;
+      }
+      rn = nn;
+    }
+    __syncthreads();                                      // every wave is done with frame t - 2's slot
+    if (t + 1 < t1) {
+      stem_stage_store(nxt, smem, t + 3, tid);
+      __syncthreads();
     }
   }
-  // ---- epilogue 2: bf16 tile -> LDS staging [192 px][64 co]
-  bf16* stg = (bf16*)smem;
+  if (stats != nullptr) {     // merge the two pixel halves (wm) and write the block's partial
+    if ((lane & 15) == 0) {
 #pragma unroll
-  for (int i = 0; i < 6; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int v = wm * 96 + i * 16 + 4 * (lane >> 4) + r;
-        stg[v * SC_SROW + wn * 32 + j * 16 + (lane & 15)] = (bf16)acc[i][j][r];
+      for (int q = 0; q < 8; ++q) {
+        const int co = wn * 32 + (q >> 2) * 16 + 4 * g0 + (q & 3);
+        red[wm][co][0] = rn; red[wm][co][1] = rmean[q]; red[wm][co][2] = rm2[q];
       }
-  __syncthreads();
-  if (stats != nullptr && tid < 64) {                      // Chan's merge of the two pixel halves
-    const float n0 = red[tid * 3], m0 = red[tid * 3 + 1], q0 = red[(tid) * 3 + 2];
-    const float n1 = red[(64 + tid) * 3], m1 = red[(64 + tid) * 3 + 1], q1 = red[(64 + tid) * 3 + 2];
-    const float nn = n0 + n1, dd = m1 - m0;
-    float* o = stats + ((int64_t)tid * tiles + blk) * 3;
-    o[0] = nn;
-    o[1] = m0 + dd * n1 / nn;
-    o[2] = q0 + q1 + dd * dd * n0 * n1 / nn;
+    }
+    __syncthreads();
+    if (tid < 64) {
+      const float n0 = red[0][tid][0], m0 = red[0][tid][1], q0 = red[0][tid][2];
+      const float n1 = red[1][tid][0], m1 = red[1][tid][1], q1 = red[1][tid][2];
+      const float nn = n0 + n1;
+      float* o = stats + ((int64_t)tid * tiles + blk) * 3;
+      if (nn > 0.f) {
+        const float dd = m1 - m0;
+        o[0] = nn; o[1] = m0 + dd * n1 / nn; o[2] = q0 + q1 + dd * dd * n0 * n1 / nn;
+      } else {
+        o[0] = 0.f; o[1] = 0.f; o[2] = 0.f;
+      }
+    }
   }
-  // ---- 16-byte stores of the 176 valid pixel rows (NHWC, 128 B each)
-  bf16* out = h + ((int64_t)n * 44 * 44 + (int64_t)oh0 * 44) * 64;
-  for (int i = tid; i < SC_R * 44 * 8; i += 256) {
-    const int c = i & 7, pxi = i >> 3;                     // pixel (ob, ow) with ow < 44
-    const int ob = pxi / 44, ow = pxi - ob * 44;
-    const uint4 v = *(const uint4*)(stg + (ob * SC_VW + ow) * SC_SROW + c * 8);
-    *(uint4*)(out + (int64_t)pxi * 64 + c * 8) = v;
-  }
+}
+
+// grid: (clip, band) streams split into runs of >= 16 frames, about 8 blocks per block slot
+// (256 CUs x 2) so that the last round's tail stays small
+static void stem_grid(int B, int T, int& chunks, int& fpc, int& nblk) {
+  const int streams = B * SC_BANDS;
+  const long target = 8L * 256 * SC_BLOCKS_PER_CU;
+  chunks = (int)((target + streams - 1) / streams);
+  const int maxc = T / 16 > 0 ? T / 16 : 1;
+  if (chunks > maxc) chunks = maxc;
+  if (chunks < 1) chunks = 1;
+  fpc = (T + chunks - 1) / chunks;
+  chunks = (T + fpc - 1) / fpc;
+  nblk = streams * chunks;
 }
 
 // Conv3d weight (64, 1, 5, 7, 7) fp32 -> [64][36 groups][8] bf16, group = dt*7 + kh, entry kw
@@ -215,7 +266,11 @@ __global__ void stem_wpack2_kernel(const float* w, bf16* wk) {
 
 }  // namespace
 
-extern "C" int avsr_stem_conv_tiles(int nimg) { return nimg * SC_BANDS; }
+extern "C" int avsr_stem_conv_tiles(int B, int T) {
+  int chunks, fpc, nblk;
+  stem_grid(B, T, chunks, fpc, nblk);
+  return nblk;
+}
 
 extern "C" int avsr_stem_wpack2(const float* w, void* wk, void* stream) {
   if (!w || !wk || !avsr_aligned16(wk)) return AVSR_E_ARG;
@@ -230,10 +285,12 @@ extern "C" int avsr_stem_conv_fwd(int B, int T, const float* video, const void* 
   if (B <= 0 || T <= 0) return B == 0 || T == 0 ? 0 : AVSR_E_SHAPE;
   if (!video || !wk || !h) return AVSR_E_ARG;
   if (!avsr_aligned16(wk) || !avsr_aligned16(h) || !avsr_aligned16(video)) return AVSR_E_ALIGN;
-  const int64_t nblk = (int64_t)B * T * SC_BANDS;
-  if (nblk > 0x7fffffff) return AVSR_E_SHAPE;
-  hipLaunchKernelGGL(stem_conv_kernel, dim3((unsigned)nblk), dim3(256), SC_LDS, (hipStream_t)stream, B, T, video,
-                     (const bf16*)wk, (bf16*)h, stats, (int)nblk);
+  const int64_t vbytes = (int64_t)B * T * 88 * 88 * 4;
+  if (vbytes >= 0x7fffffffLL) return AVSR_E_SHAPE;
+  int chunks, fpc, nblk;
+  stem_grid(B, T, chunks, fpc, nblk);
+  hipLaunchKernelGGL(stem_conv_kernel, dim3((unsigned)nblk), dim3(256), SC_LDS, (hipStream_t)stream, B, T, chunks, fpc,
+                     video, (uint32_t)vbytes, (const bf16*)wk, (bf16*)h, stats, nblk);
   AVSR_CHECK_LAUNCH();
   return 0;
 }

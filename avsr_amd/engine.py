@@ -43,7 +43,7 @@ _SIDE_BIAS = os.environ.get("AVSR_SIDE_BIAS", "1") == "1"
 # the CTC branch of the forward runs on the side stream beside the decoder forward
 _CTC_SIDE = os.environ.get("AVSR_CTC_SIDE", "1") == "1"
 # bf16 stem conv straight from the video (stem.hip) instead of pack + general implicit GEMM
-_STEM_DIRECT = os.environ.get("AVSR_STEM_DIRECT", "0") == "1"
+_STEM_DIRECT = os.environ.get("AVSR_STEM_DIRECT", "1") == "1"
 
 
 _STEP_STREAMS = {}
@@ -470,7 +470,7 @@ class Engine:
         if direct:      # bf16: the stem conv reads the video itself (stem.hip, K = 288 instead of 392)
             wk = self._e(64, ops.STEM_K)
             ops.stem_wpack2(self.arena.master(R + "frontend3D.0.weight"), wk)
-            part = self._e(64, ops.stem_conv_tiles(N), 3, dtype=torch.float32) if train else None
+            part = self._e(64, ops.stem_conv_tiles(B, T), 3, dtype=torch.float32) if train else None
             ops.stem_conv_fwd(vid, wk, h0, part)
         else:
             wp = self._e(64, 7, 7, 8)        # the packed weight (not an arena view)

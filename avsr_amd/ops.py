@@ -624,8 +624,9 @@ def stem_wpack2(w, wk):
     return wk
 
 
-def stem_conv_tiles(nimg):
-    return L.load().avsr_stem_conv_tiles(int(nimg))
+def stem_conv_tiles(B, T):
+    """BN partial-statistics tiles of stem_conv_fwd (one per persistent block)"""
+    return L.load().avsr_stem_conv_tiles(int(B), int(T))
 
 
 def stem_conv_fwd(videos, wk, h, stats=None):
@@ -635,7 +636,7 @@ def stem_conv_fwd(videos, wk, h, stats=None):
     assert videos.dtype == torch.float32 and videos.is_contiguous() and tuple(videos.shape[3:]) == (88, 88)
     assert h.dtype == torch.bfloat16 and h.numel() == B * T * 44 * 44 * 64 and h.is_contiguous()
     if stats is not None:
-        assert stats.dtype == torch.float32 and stats.numel() >= 64 * stem_conv_tiles(B * T) * 3
+        assert stats.dtype == torch.float32 and stats.numel() >= 64 * stem_conv_tiles(B, T) * 3
     L.check(L.load().avsr_stem_conv_fwd(B, T, videos.data_ptr(), wk.data_ptr(), h.data_ptr(),
                                         None if stats is None else stats.data_ptr(), L.stream_ptr()),
             "avsr_stem_conv_fwd")

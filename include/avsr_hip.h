@@ -412,10 +412,10 @@ int avsr_stem_pack(int dtype, int B, int T, const float* video, void* out, void*
 int avsr_stem_wpack(int dtype, const float* w, void* wp, void* stream);
 /* avsr_stem_conv_fwd (bf16): the stem Conv3d (resnet.py:132) read straight from videos
  *                  (B,1,T,88,88) fp32 (zero frames outside the clip) -> h [B*T][44][44][64] bf16,
- *                  and (stats != NULL) BN partials stats[64][avsr_stem_conv_tiles(B*T)][3]
+ *                  and (stats != NULL) BN partials stats[64][avsr_stem_conv_tiles(B, T)][3]
  *                  (count, mean, M2) as avsr_conv_fwd writes them; wk from avsr_stem_wpack2:
  *                  [64][288] bf16, k = (dt*7 + kh)*8 + kw (kw = 7 and k >= 280 zero) */
-int avsr_stem_conv_tiles(int nimg);
+int avsr_stem_conv_tiles(int B, int T);
 int avsr_stem_wpack2(const float* w, void* wk, void* stream);
 int avsr_stem_conv_fwd(int B, int T, const float* video, const void* wk, void* h, float* stats, void* stream);
 int avsr_stem_wgrad_unpack(const float* gp, float* gw, void* stream);

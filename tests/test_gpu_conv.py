@@ -207,7 +207,7 @@ def test_stem_conv_direct(dev):
     ref = ref.permute(0, 2, 3, 4, 1).reshape(B * T * 44 * 44, 64)
     wk = torch.empty(64, ops.STEM_K, device=dev, dtype=torch.bfloat16)
     ops.stem_wpack2(w.to(dev), wk)
-    tiles = ops.stem_conv_tiles(B * T)
+    tiles = ops.stem_conv_tiles(B, T)
     h = torch.empty(B * T * 44 * 44, 64, device=dev, dtype=torch.bfloat16)
     stats = torch.empty(64, tiles, 3, device=dev)
     ops.stem_conv_fwd(video.to(dev), wk, h, stats)

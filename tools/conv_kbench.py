@@ -51,7 +51,7 @@ def stem_old():
 
 wk = torch.empty(64, ops.STEM_K, device=dev, dtype=bf)
 ops.stem_wpack2(w5, wk)
-part2 = torch.empty(64, ops.stem_conv_tiles(N), 3, device=dev)
+part2 = torch.empty(64, ops.stem_conv_tiles(B, T), 3, device=dev)
 res["stem_pack"] = timed(lambda: ops.stem_pack(video, xp))
 res["stem_conv_general"] = timed(lambda: ops.conv_fwd(gs, xp, wp, h0, part))
 res["stem_conv_direct"] = timed(lambda: ops.stem_conv_fwd(video, wk, h0, part2))
