@@ -115,9 +115,12 @@ __global__ __launch_bounds__(256, SC_BLOCKS_PER_CU) void stem_conv_kernel(
     pvalid[i] = ow < 44;
     pbase[i] = 2 * ob * SC_ROWB + cp * (SC_CW * 2) + j0 * 2;
   }
-  float rn = 0.f, rmean[8], rm2[8];                       // running stats of this lane's 8 channels
+  float shift[8], s1[8], s2[8], cnt = 0.f;               // this lane's 8 channels: shifted sums
+  float pv_count = 0.f;
 #pragma unroll
-  for (int q = 0; q < 8; ++q) rmean[q] = rm2[q] = 0.f;
+  for (int i = 0; i < 6; ++i) pv_count += pvalid[i] ? 1.f : 0.f;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) shift[q] = s1[q] = s2[q] = 0.f;
   if (t0 < t1) {
     for (int f = t0 - 2; f <= t0 + 2; ++f) {
       StageRegs g;
@@ -180,35 +183,20 @@ __global__ __launch_bounds__(256, SC_BLOCKS_PER_CU) void stem_conv_kernel(
         *(uint2*)(out + (ob * 44 + ow) * 64 + co0) = o.u;
       }
     }
-    if (stats != nullptr) {   // this step's (count, mean, M2) per channel over the wave's 88 pixels
-      float s[8], m2[8];
+    if (stats != nullptr) {   // per-lane shifted sums of the lane's 8 channels (no cross-lane work per step)
+      if (t == t0) {
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const int j = q >> 2, r = q & 3;
-        float a = 0.f;
+        for (int q = 0; q < 8; ++q) shift[q] = acc[0][q >> 2][q & 3];   // pixel fragment 0 is always valid
+      }
 #pragma unroll
-        for (int i = 0; i < 6; ++i) a += pvalid[i] ? acc[i][j][r] : 0.f;
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1) a += __shfl_xor(a, o, 64);
-        s[q] = a * (1.f / 88.f);
-        float d2 = 0.f;
+      for (int q = 0; q < 8; ++q)
 #pragma unroll
         for (int i = 0; i < 6; ++i) {
-          const float d = acc[i][j][r] - s[q];
-          d2 += pvalid[i] ? d * d : 0.f;
+          const float x = pvalid[i] ? acc[i][q >> 2][q & 3] - shift[q] : 0.f;
+          s1[q] += x;
+          s2[q] = fmaf(x, x, s2[q]);
         }
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1) d2 += __shfl_xor(d2, o, 64);
-        m2[q] = d2;
-      }
-      const float nb = 88.f, nn = rn + nb;
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {                       // Chan: merge (88, s, m2) into the run
-        const float d = s[q] - rmean[q];
-        rmean[q] += d * nb / nn;
-        rm2[q] += m2[q] + d * d * rn * nb / nn;
-      }
-      rn = nn;
+      cnt += pv_count;
     }
     __syncthreads();                                      // every wave is done with frame t - 2's slot
     if (t + 1 < t1) {
@@ -216,12 +204,37 @@ __global__ __launch_bounds__(256, SC_BLOCKS_PER_CU) void stem_conv_kernel(
       __syncthreads();
     }
   }
-  if (stats != nullptr) {     // merge the two pixel halves (wm) and write the block's partial
+  if (stats != nullptr) {
+    // per lane (count, mean, M2) from the shifted sums, Chan-merged over the 16 pixel lanes of
+    // the lane group (fixed butterfly: every lane ends with the same bits), then over the two
+    // pixel halves (wm) in LDS: the block's partial per channel
+    float rn[8], rmean[8], rm2[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      rn[q] = cnt;
+      rmean[q] = cnt > 0.f ? shift[q] + s1[q] / cnt : 0.f;
+      rm2[q] = cnt > 0.f ? fmaxf(s2[q] - s1[q] * s1[q] / cnt, 0.f) : 0.f;
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) {
+        const float nb = __shfl_xor(rn[q], o, 64), mb = __shfl_xor(rmean[q], o, 64), qb = __shfl_xor(rm2[q], o, 64);
+        // symmetric merge (a, b) -> same bits on both lanes: order the pair by lane bit
+        const bool lo = (lane & o) == 0;
+        const float na = lo ? rn[q] : nb, ma = lo ? rmean[q] : mb, qa = lo ? rm2[q] : qb;
+        const float nc = lo ? nb : rn[q], mc = lo ? mb : rmean[q], qc = lo ? qb : rm2[q];
+        const float nn = na + nc;
+        if (nn > 0.f) {
+          const float d = mc - ma;
+          rmean[q] = ma + d * nc / nn;
+          rm2[q] = qa + qc + d * d * na * nc / nn;
+        }
+        rn[q] = nn;
+      }
+    }
     if ((lane & 15) == 0) {
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
         const int co = wn * 32 + (q >> 2) * 16 + 4 * g0 + (q & 3);
-        red[wm][co][0] = rn; red[wm][co][1] = rmean[q]; red[wm][co][2] = rm2[q];
+        red[wm][co][0] = rn[q]; red[wm][co][1] = rmean[q]; red[wm][co][2] = rm2[q];
       }
     }
     __syncthreads();
@@ -240,8 +253,6 @@ __global__ __launch_bounds__(256, SC_BLOCKS_PER_CU) void stem_conv_kernel(
   }
 }
 
-// grid: (clip, band) streams split into runs of >= 16 frames, about 8 blocks per block slot
-// (256 CUs x 2) so that the last round's tail stays small
 static void stem_grid(int B, int T, int& chunks, int& fpc, int& nblk) {
   const int streams = B * SC_BANDS;
   const long target = 8L * 256 * SC_BLOCKS_PER_CU;

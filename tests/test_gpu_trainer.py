@@ -56,14 +56,29 @@ class SeqTrainer(AVSRTrainer):
         return SequentialSampler(self.train_dataset)
 
 
+class StopAfter(TrainerCallback):
+    def __init__(self, n):
+        self.n = n
+
+    def on_step_end(self, args, state, control, **kw):
+        if state.global_step >= self.n:
+            control.should_save = True
+            control.should_training_stop = True
+        return control
+
+
 class Capture(TrainerCallback):
     def __init__(self, model):
-        self.model, self.grads, self.before, self.after = model, [], [], []
+        self.model, self.grads, self.before, self.after, self.lrs = model, [], [], [], []
 
     def on_pre_optimizer_step(self, args, state, control, **kw):
         a = self.model.avsr.engine().arena
         self.grads.append(a.grad.clone())
         self.before.append(a.data.clone())
+        opt = kw.get("optimizer")
+        if opt is not None:
+            inner = getattr(opt, "optimizer", opt)
+            self.lrs.append((float(inner.param_groups[0]["lr"]), int(inner.fused.step_count)))
 
     def on_optimizer_step(self, args, state, control, **kw):
         self.after.append(self.model.avsr.engine().arena.data.clone())
@@ -136,8 +151,10 @@ def test_trainer_checkpoint_resume(g, tmp_path):
     SeqTrainer(model=m1, args=_args(tmp_path / "a", 2), data_collator=collate, train_dataset=ds,
                callbacks=[cap1]).train()
     m2 = _model(g)
-    SeqTrainer(model=m2, args=_args(tmp_path / "b", 1, save_strategy="steps", save_steps=1), data_collator=collate,
-               train_dataset=ds).train()
+    # the same 2-step schedule, stopped after step 1 with its checkpoint saved (a max_steps=1 run
+    # would checkpoint the LR of a 1-step schedule, 0, and the resumed step would use it)
+    SeqTrainer(model=m2, args=_args(tmp_path / "b", 2, save_strategy="steps", save_steps=1), data_collator=collate,
+               train_dataset=ds, callbacks=[StopAfter(1)]).train()
     m3 = _model(g)
     cap3 = Capture(m3)
     tr3 = SeqTrainer(model=m3, args=_args(tmp_path / "b", 2, save_strategy="no"), data_collator=collate,
@@ -153,6 +170,6 @@ def test_trainer_checkpoint_resume(g, tmp_path):
     assert e_g == 0.0, (e_g, e_w)
     a1, a3 = m1.avsr.engine().arena, m3.avsr.engine().arena
     assert torch.equal(a1.exp_avg, a3.exp_avg) and torch.equal(a1.exp_avg_sq, a3.exp_avg_sq)   # AdamW moments
-    # the resumed step's update uses the LR the restored scheduler recomputes: equal to fp32 rounding
-    assert (a1.data - a3.data).abs().max().item() <= 1e-6 * a1.data.abs().max().item()
+    assert cap3.lrs[-1] == cap1.lrs[-1], (cap1.lrs, cap3.lrs)    # same LR and AdamW step count
+    assert torch.equal(a1.data, a3.data)                            # so the same update, bit for bit
     assert tr3.state.global_step == 2
