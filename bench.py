@@ -404,7 +404,12 @@ def gpu_bench(args):
     drops = []
     step_seed = [args.seed * 1000003 + rank]
 
-    def step():
+    forced_all = None if args.force_modality is None else (
+        (None if args.force_modality == "none" else args.force_modality),)
+
+    def step(variant=False):
+        if forced_all is not None and not variant:
+            eng.force_modality = forced_all
         arena.zero_grad()
         step_seed[0] += 1
         out4, ctx = eng.forward(v, a, lens, lab, train=True, need_grad=True, seed=step_seed[0])
@@ -484,7 +489,7 @@ def gpu_bench(args):
             torch.cuda.synchronize()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-            step()
+            step(variant=True)
             e1.record()
             torch.cuda.synchronize()
             per.append(e0.elapsed_time(e1))
@@ -541,6 +546,8 @@ def gpu_bench(args):
                                    "(its gradient is exactly zero, avhubert.py:480)"},
         "allreduce": allreduce,
     }
+    if forced_all is not None:
+        result["forced_modality"] = f"every timed step forced to {args.force_modality} (profiling run, not the metric)"
     if rank == 0 and not args.quick:
         result["frontend"] = frontend_timing(B, T, dev)
         if args.layers is None:
@@ -578,6 +585,8 @@ def main():
     ap.add_argument("--layers", type=int, default=None, help="debug only: fewer encoder layers (INVALID for the metric)")
     ap.add_argument("--seed", type=int, default=1234, help="seeds the inputs, dropout streams and the "
                     "modality-dropout draws (numpy global RNG, as the reference draws them)")
+    ap.add_argument("--force-modality", choices=["none", "audio_off", "video_off"], default=None,
+                    help="profiling only: every step uses this modality variant (the value is then not the metric)")
     ap.add_argument("--cpu-selftest", action="store_true", help="no GPU: launcher + gloo all-reduce check only")
     args = ap.parse_args()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
