@@ -105,8 +105,19 @@ constexpr uint32_t OOB = 0x80000000u;
 AVSR_DEV __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
 }
+// buffer_load_dwordx4 ... lds as inline asm. The compiler then does not know that the
+// instruction writes LDS: with __builtin_amdgcn_raw_ptr_buffer_load_lds its waitcnt pass puts
+// an s_waitcnt vmcnt(0) in front of every later ds_read_b64_tr_b16 (an LDS read it cannot
+// disambiguate from the pending DMA), which drained the prefetch of the NEXT K-tile before the
+// current one was computed in every kernel with a transposed operand (data-grads,
+// weight-grads). Callers order the DMAs against their LDS reads with explicit vmcnt waits and
+// barriers (mainloop_glds, the conv patch kernels). M0 is set here; no kernel of this library
+// keeps a compiler value live in M0 (the LDS-DMA builtins set it right before each use).
 AVSR_DEV void bglds16(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff, char* lds_wave_base) {
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void_t*)lds_wave_base, 16, voff, soff, 0, 0);
+  const uint32_t m = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_void_t*)lds_wave_base);
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds" ::"s"(m), "v"(voff), "s"(r),
+               "s"(soff)
+               : "memory");
 }
 
 // k-major: elem(r, k) = base[r*ld + k]

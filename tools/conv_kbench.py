@@ -77,7 +77,12 @@ for flag in ("0", "1"):
     res[f"s1_dgrad_bnr_patch{flag}"] = timed(lambda: ops.conv_bwd_data_bnr(geom, dy, w, dx, hh, st, a, beta=0.0))
     res[f"s1_dgrad_bnr_id_patch{flag}"] = timed(lambda: ops.conv_bwd_data_bnr(geom, dy, w, dx, hh, st, a, res=x,
                                                                              beta=1.0))
-res["s1_wgrad"] = timed(lambda: ops.conv_bwd_weight(geom, x, dy, dw))
+for flag in ("0", "1"):
+    os.environ["AVSR_CONV_WPATCH"] = flag
+    res[f"s1_wgrad_wpatch{flag}"] = timed(lambda: ops.conv_bwd_weight(geom, x, dy, dw))
+os.environ["AVSR_CONV_WHALF"] = "0"       # general-position patch kernel instead of half-image tiles
+res["s1_wgrad_wpatch1_whalf0"] = timed(lambda: ops.conv_bwd_weight(geom, x, dy, dw))
+os.environ["AVSR_CONV_WHALF"] = "1"
 fl = 2.0 * M * 64 * 576
 res["s1_gflop"] = round(fl / 1e9, 1)
 res["stem_gflop_direct_k288"] = round(2.0 * N * 1936 * 64 * 288 / 1e9, 1)
