@@ -216,23 +216,101 @@ __global__ __launch_bounds__(64) void ctc_prefix_kernel(avsr_ctc_prefix_params p
   if (j == 0) p.psi[h * (p.P + 1) + p.P] = rsum_last;
 }
 
+// The same recursion with its inputs staged in LDS first: the P scored tokens' and the blank's
+// log-probs over all T frames ([T][P + 1], gathered once by the whole block) and r_prev
+// ([T][2]). The sequential loop then reads LDS only (independent of the global r_new stores,
+// so the reads of later frames issue ahead), instead of a dependent ~L2-latency global
+// gather per frame (130 us per step at T = 375 -> the lse chain).
+__global__ __launch_bounds__(64) void ctc_prefix_lds_kernel(avsr_ctc_prefix_params p) {
+  extern __shared__ float sm[];
+  const int h = blockIdx.x, j = threadIdx.x;
+  const int V = p.V, P = p.P, W = P + 1;
+  const int u = p.uidx ? p.uidx[h] : 0;
+  const int T = p.uidx ? p.tlen[u] : p.T;
+  const int TS = p.T;
+  const float* __restrict__ logp = p.logp + (p.uidx ? (int64_t)u * p.logp_ustride : 0);
+  float* xs = sm;                           // [T][W]: ids then blank
+  float* rps = sm + (int64_t)TS * W;        // [T][2]
+  const int* __restrict__ ids = p.ids + h * P;
+  for (int idx = j; idx < T * W; idx += 64) {
+    const int t = idx / W, c = idx - t * W;
+    xs[idx] = logp[(int64_t)t * V + (c < P ? ids[c] : p.blank)];
+  }
+  const float* __restrict__ rp = p.r_prev ? p.r_prev + (int64_t)h * TS * 2 : nullptr;
+  if (rp)
+    for (int idx = j; idx < T * 2; idx += 64) rps[idx] = rp[idx];
+  __syncthreads();
+  const bool act = j < P;
+  const int id = act ? ids[j] : 0;
+  const bool same = act && id == p.last[h];
+  float* __restrict__ rn = act ? p.r_new + ((int64_t)h * P + j) * TS * 2 : nullptr;
+  const int jj = act ? j : 0;
+  auto rprev = [&](int t, int q, float cum) -> float { return rp ? rps[t * 2 + q] : (q == 0 ? LOGZERO : cum); };
+  const int start = max(p.out_len, 1);
+  float r0 = LOGZERO, r1 = LOGZERO;
+  float cum = 0.f;
+  for (int t = 0; t < start; ++t) {
+    const float xb = xs[t * W + P];
+    cum += xb;
+    float a0 = LOGZERO;
+    if (t == 0 && p.out_len == 0) a0 = act ? xs[jj] : LOGZERO;
+    if (act) { rn[t * 2 + 0] = a0; rn[t * 2 + 1] = LOGZERO; }
+    if (t == start - 1) { r0 = a0; r1 = LOGZERO; }
+  }
+  float pm = r0;
+  float ps = 1.f;
+  float prev_r0 = rprev(start - 1, 0, 0.f);
+  float prev_r1 = rprev(start - 1, 1, cum);
+  float cur_cum = cum;
+  for (int t = start; t < T; ++t) {
+    const float rsum_prev = lse2(prev_r0, prev_r1);
+    const float phi = same ? prev_r1 : rsum_prev;
+    const float x0 = act ? xs[t * W + jj] : LOGZERO;
+    const float xb = xs[t * W + P];
+    const float n0 = lse2(r0, phi) + x0;
+    const float n1 = lse2(r0, r1) + xb;
+    r0 = n0; r1 = n1;
+    if (act) { rn[t * 2 + 0] = r0; rn[t * 2 + 1] = r1; }
+    const float term = phi + x0;
+    if (term > pm) { ps = ps * expf(pm - term) + 1.f; pm = term; }
+    else ps += expf(term - pm);
+    cur_cum += xb;
+    prev_r0 = rprev(t, 0, 0.f);
+    prev_r1 = rprev(t, 1, cur_cum);
+  }
+  const float rsum_last = lse2(prev_r0, prev_r1);
+  float psi = pm + logf(ps);
+  if (act) {
+    if (id == p.blank) psi = LOGZERO;
+    if (id == p.eos) psi = rsum_last;
+    p.psi[h * (P + 1) + j] = psi;
+  }
+  if (j == 0) p.psi[h * (P + 1) + P] = rsum_last;
+}
+
 // ---------------------------------------------------------------- beam selection
 // weighted[h][v] = w_dec * dec[h][v] + w_ctc * (psi[h][v] - s_prev[h]) + score[h]
 // (psi = LOGZERO for tokens outside the pre-beam, r_sum[T-1] for eos; batch_beam_search.py
 // :228-260), flat top-`beam` over h*V + v; ties -> smaller flat index.
+// Tokens outside a row's pre-beam have psi = LOGZERO, i.e. a weighted score below
+// w_ctc * (LOGZERO - s_prev[h]) + score[h] (dec <= 0). The selection first runs over the
+// candidates only (each row's P pre-beam tokens and eos: <= 256 per segment) and keeps that
+// result when its beam-th score is above that bound for every row of the segment — then no
+// other token can enter the top beam and the result equals the full scan; otherwise (fewer
+// than `beam` finite candidates) it scans all rows x V as before.
 __global__ __launch_bounds__(256) void beam_select_kernel(avsr_beam_select_params p) {
   __shared__ float shv[4];
   __shared__ int shi[4];
+  __shared__ int use_full;
   float tv[KMAX];
   int ti[KMAX];
-#pragma unroll
-  for (int k = 0; k < KMAX; ++k) { tv[k] = -INFINITY; ti[k] = 0x7fffffff; }
   // segment (utterance) of this block: rows [r0, r0 + nrow); flat ids are segment-local
   const int u = blockIdx.x;
   const int r0 = p.nseg ? p.seg[u] : 0, nrow = p.nseg ? p.seg[u + 1] - r0 : p.n;
   const int beam = min(p.beam, nrow * p.V);
   const int total = nrow * p.V;
-  for (int f = threadIdx.x; f < total; f += 256) {
+  const int W = p.P + 1;
+  auto weighted = [&](int f) -> float {
     const int h = r0 + f / p.V, v = f - (f / p.V) * p.V;
     float psi = LOGZERO;
     if (v == p.eos) psi = p.psi[h * (p.P + 1) + p.P];
@@ -243,8 +321,9 @@ __global__ __launch_bounds__(256) void beam_select_kernel(avsr_beam_select_param
     w += p.w_dec * (p.dec[(int64_t)h * p.ld + v]);
     w += p.w_ctc * (psi - p.s_prev[h]);
     w += p.score[h];
-    float val = w;
-    int id = f;
+    return w;
+  };
+  auto insert = [&](float val, int id) {
 #pragma unroll
     for (int k = 0; k < KMAX; ++k) {
       if (k < beam && (val > tv[k] || (val == tv[k] && id < ti[k]))) {
@@ -252,32 +331,70 @@ __global__ __launch_bounds__(256) void beam_select_kernel(avsr_beam_select_param
         tv[k] = val; ti[k] = id; val = t; id = w;
       }
     }
-  }
-  int head = 0;
-  for (int r = 0; r < beam; ++r) {
-    float v = -INFINITY; int id = 0x7fffffff;
+  };
+  // top-beam of the block's per-thread lists (written to out_*); returns the beam-th score
+  auto select = [&]() -> float {
+    int head = 0;
+    float last = INFINITY;
+    for (int r = 0; r < beam; ++r) {
+      float v = -INFINITY; int id = 0x7fffffff;
 #pragma unroll
-    for (int k = 0; k < KMAX; ++k) if (k == head) { v = tv[k]; id = ti[k]; }
-    const int mine = id;
-    block_argmax256(v, id, shv, shi);
-    if (mine == id && id != 0x7fffffff) ++head;
-    if (threadIdx.x == 0) {
-      const int h = r0 + id / p.V, tok = id - (id / p.V) * p.V;
-      int col = p.P - 1;                       // scoring_idmap == -1 -> python index -1
-      for (int c = 0; c < p.P; ++c)
-        if (p.ids[h * p.P + c] == tok) { col = c; break; }
-      float psi = LOGZERO;
-      if (tok == p.eos) psi = p.psi[h * (p.P + 1) + p.P];
-      else if (tok != p.blank && p.ids[h * p.P + col] == tok) psi = p.psi[h * (p.P + 1) + col];
-      const int o = u * p.beam + r;
-      p.out_prev[o] = h;
-      p.out_tok[o] = tok;
-      p.out_col[o] = col;
-      p.out_score[o] = v;
-      p.out_dec[o] = p.dec[(int64_t)h * p.ld + tok];
-      p.out_ctc[o] = psi - p.s_prev[h];
-      p.out_s[o] = psi;
+      for (int k = 0; k < KMAX; ++k) if (k == head) { v = tv[k]; id = ti[k]; }
+      const int mine = id;
+      block_argmax256(v, id, shv, shi);
+      if (mine == id && id != 0x7fffffff) ++head;
+      last = v;
+      if (threadIdx.x == 0 && id != 0x7fffffff) {     // (fewer candidates than beam: left to the full scan)
+        const int h = r0 + id / p.V, tok = id - (id / p.V) * p.V;
+        int col = p.P - 1;                       // scoring_idmap == -1 -> python index -1
+        for (int c = 0; c < p.P; ++c)
+          if (p.ids[h * p.P + c] == tok) { col = c; break; }
+        float psi = LOGZERO;
+        if (tok == p.eos) psi = p.psi[h * (p.P + 1) + p.P];
+        else if (tok != p.blank && p.ids[h * p.P + col] == tok) psi = p.psi[h * (p.P + 1) + col];
+        const int o = u * p.beam + r;
+        p.out_prev[o] = h;
+        p.out_tok[o] = tok;
+        p.out_col[o] = col;
+        p.out_score[o] = v;
+        p.out_dec[o] = p.dec[(int64_t)h * p.ld + tok];
+        p.out_ctc[o] = psi - p.s_prev[h];
+        p.out_s[o] = psi;
+      }
     }
+    return last;
+  };
+  auto reset = [&]() {
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) { tv[k] = -INFINITY; ti[k] = 0x7fffffff; }
+  };
+  bool full = !(nrow * W <= 256 && p.w_ctc > 0.f);     // block-uniform
+  if (!full) {
+    reset();
+    const int c = threadIdx.x;
+    if (c < nrow * W) {
+      const int hl = c / W, k = c - hl * W, h = r0 + hl;
+      const int v = k < p.P ? p.ids[h * p.P + k] : p.eos;
+      // eos once per row: as the extra candidate, not again as a pre-beam id
+      if (!(k < p.P && v == p.eos)) insert(weighted(hl * p.V + v), hl * p.V + v);
+    }
+    const float last = select();
+    if (threadIdx.x == 0) {
+      // bound on any non-candidate's score (dec <= 0), with a relative margin for rounding
+      float bound = -INFINITY;
+      for (int hl = 0; hl < nrow; ++hl) {
+        const int h = r0 + hl;
+        bound = fmaxf(bound, p.w_ctc * (LOGZERO - p.s_prev[h]) + p.score[h]);
+      }
+      use_full = !(last > bound + 1e-3f * fabsf(bound));
+    }
+    __syncthreads();
+    full = use_full != 0;
+  }
+  if (full) {
+    reset();
+    for (int f = threadIdx.x; f < total; f += 256) insert(weighted(f), f);
+    select();
   }
 }
 
@@ -332,7 +449,12 @@ extern "C" int avsr_row_topk(const avsr_topk_params* p, void* stream) {
 extern "C" int avsr_ctc_prefix(const avsr_ctc_prefix_params* p, void* stream) {
   if (!p || p->n <= 0) return AVSR_E_ARG;
   if (p->P < 1 || p->P > 64 || p->T < 1) return AVSR_E_SHAPE;
-  hipLaunchKernelGGL(ctc_prefix_kernel, dim3(p->n), dim3(64), 0, (hipStream_t)stream, *p);
+  const size_t lds = (size_t)p->T * (p->P + 1 + 2) * sizeof(float);
+  static const bool nolds = getenv("AVSR_CTC_PREFIX_NOLDS") && getenv("AVSR_CTC_PREFIX_NOLDS")[0] == '1';
+  if (lds <= 64 * 1024 && !nolds)
+    hipLaunchKernelGGL(ctc_prefix_lds_kernel, dim3(p->n), dim3(64), lds, (hipStream_t)stream, *p);
+  else
+    hipLaunchKernelGGL(ctc_prefix_kernel, dim3(p->n), dim3(64), 0, (hipStream_t)stream, *p);
   AVSR_CHECK_LAUNCH();
   return 0;
 }

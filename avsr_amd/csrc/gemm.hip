@@ -261,6 +261,133 @@ int by_tile(const avsr_gemm_params* p, const DenseArgs& a, hipStream_t st) {
   return by_layout<T, OutT, 2, 2>(p, a, st);
 }
 
+// ---------------------------------------------------------------- skinny (M <= 64) linears
+// The decoder's per-step linears during beam search have n = utterances x beam rows (<= 40 at
+// C5). The tiled cores put one 64 x 256 tile per 256 columns on them (4 workgroups for
+// N = 1024, each streaming a 1 MiB weight slab; 63 us per call in fp32 parity mode). Here the
+// work is spread over N / 16 workgroups and done with fp32 FMAs on the vector ALUs (exact
+// fp32 products and sums, fixed order): a workgroup stages the A rows of a 256-wide K chunk in
+// LDS (as fp32), thread (column pair cg, K lane kl) keeps partial sums of 2 columns for every
+// row over k = 4kl + 128j .. +3 (one 16-byte weight load per column and k group, 4 FMAs per
+// row), then the 32 K lanes are reduced (shuffles within a wave, LDS across the 4 waves) and
+// the usual elementwise epilogue (bias / activation / residual / beta) writes the tile.
+constexpr int SK_NB = 16;
+
+template <typename T> AVSR_DEV f32x4 ld4f(const T* p) {
+  if constexpr (sizeof(T) == 2) {
+    const bf16x4 v = *(const bf16x4*)p;
+    return f32x4{(float)v[0], (float)v[1], (float)v[2], (float)v[3]};
+  } else {
+    return *(const f32x4*)p;
+  }
+}
+
+template <typename T, typename OutT, int MR>
+__global__ __launch_bounds__(256) void skinny_kernel(DenseArgs a) {
+  constexpr int SK_KC = MR <= 32 ? 256 : 128;        // K chunk staged per pass (<= 33 KiB of LDS)
+  constexpr int XPT = MR * SK_KC / 4 / 256;           // A vectors per thread per chunk
+  constexpr int WJ = SK_KC / 128;                     // k groups per thread per chunk
+  __shared__ __attribute__((aligned(16))) float xs[MR][SK_KC + 4];
+  static_assert(4 * MR * (SK_NB + 1) <= MR * (SK_KC + 4), "reduction slab reuses the staging buffer");
+  float (*red)[MR][SK_NB + 1] = (float (*)[MR][SK_NB + 1])&xs[0][0];
+  const int tid = threadIdx.x, cg = tid & 7, kl = tid >> 3, lane = tid & 63, wave = tid >> 6;
+  const int n0 = blockIdx.x * SK_NB, c0 = n0 + 2 * cg, c1 = c0 + 1;
+  const T* A = (const T*)a.A;
+  const T* B0 = (const T*)a.B + (int64_t)min(c0, a.N - 1) * a.ldb;
+  const T* B1 = (const T*)a.B + (int64_t)min(c1, a.N - 1) * a.ldb;
+  const bool ok0 = c0 < a.N, ok1 = c1 < a.N;
+  float acc0[MR], acc1[MR];
+#pragma unroll
+  for (int m = 0; m < MR; ++m) acc0[m] = acc1[m] = 0.f;
+  // the next chunk's A rows and weights are loaded into registers while this chunk computes
+  f32x4 xr[XPT], w0[WJ], w1[WJ];
+  auto load = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < XPT; ++i) {
+      const int idx = tid + 256 * i, m = idx / (SK_KC / 4), q = idx - m * (SK_KC / 4), k = k0 + 4 * q;
+      xr[i] = (m < a.M && k < a.K) ? ld4f(A + (int64_t)m * a.lda + k) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int j = 0; j < WJ; ++j) {
+      const int k = k0 + 4 * (kl + 32 * j);
+      w0[j] = (ok0 && k < a.K) ? ld4f(B0 + k) : f32x4{0.f, 0.f, 0.f, 0.f};
+      w1[j] = (ok1 && k < a.K) ? ld4f(B1 + k) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  load(0);
+  for (int k0 = 0; k0 < a.K; k0 += SK_KC) {
+    __syncthreads();                                // the previous chunk's reads of xs are done
+#pragma unroll
+    for (int i = 0; i < XPT; ++i) {
+      const int idx = tid + 256 * i, m = idx / (SK_KC / 4), q = idx - m * (SK_KC / 4);
+      *(f32x4*)&xs[m][4 * q] = xr[i];
+    }
+    f32x4 wc0[WJ], wc1[WJ];
+#pragma unroll
+    for (int j = 0; j < WJ; ++j) { wc0[j] = w0[j]; wc1[j] = w1[j]; }
+    __syncthreads();
+    if (k0 + SK_KC < a.K) load(k0 + SK_KC);
+#pragma unroll
+    for (int j = 0; j < WJ; ++j) {
+      const int g = kl + 32 * j;
+#pragma unroll
+      for (int m = 0; m < MR; ++m) {
+        const f32x4 x = *(const f32x4*)&xs[m][4 * g];
+        acc0[m] = fmaf(x[0], wc0[j][0], acc0[m]); acc0[m] = fmaf(x[1], wc0[j][1], acc0[m]);
+        acc0[m] = fmaf(x[2], wc0[j][2], acc0[m]); acc0[m] = fmaf(x[3], wc0[j][3], acc0[m]);
+        acc1[m] = fmaf(x[0], wc1[j][0], acc1[m]); acc1[m] = fmaf(x[1], wc1[j][1], acc1[m]);
+        acc1[m] = fmaf(x[2], wc1[j][2], acc1[m]); acc1[m] = fmaf(x[3], wc1[j][3], acc1[m]);
+      }
+    }
+  }
+  // sum over the 8 K lanes of a wave (lane bits 3-5), then over the 4 waves
+#pragma unroll
+  for (int m = 0; m < MR; ++m) {
+#pragma unroll
+    for (int o = 8; o < 64; o <<= 1) {
+      acc0[m] += __shfl_xor(acc0[m], o, 64);
+      acc1[m] += __shfl_xor(acc1[m], o, 64);
+    }
+  }
+  __syncthreads();                                  // staging buffer -> reduction slab
+  if (lane < 8) {
+#pragma unroll
+    for (int m = 0; m < MR; ++m) { red[wave][m][2 * cg] = acc0[m]; red[wave][m][2 * cg + 1] = acc1[m]; }
+  }
+  __syncthreads();
+  for (int o = tid; o < MR * SK_NB; o += 256) {
+    const int m = o / SK_NB, c = o - m * SK_NB, col = n0 + c;
+    if (m < a.M && col < a.N) {
+      const float v = (red[0][m][c] + red[1][m][c]) + (red[2][m][c] + red[3][m][c]);
+      epi_elems<T, OutT, 1>(a.e, m, col, &v);
+    }
+  }
+}
+
+template <typename T, typename OutT>
+int skinny_launch(const DenseArgs& a, hipStream_t st) {
+  const dim3 g((unsigned)((a.N + SK_NB - 1) / SK_NB));
+  if (a.M <= 8) hipLaunchKernelGGL((skinny_kernel<T, OutT, 8>), g, dim3(256), 0, st, a);
+  else if (a.M <= 16) hipLaunchKernelGGL((skinny_kernel<T, OutT, 16>), g, dim3(256), 0, st, a);
+  else if (a.M <= 24) hipLaunchKernelGGL((skinny_kernel<T, OutT, 24>), g, dim3(256), 0, st, a);
+  else if (a.M <= 32) hipLaunchKernelGGL((skinny_kernel<T, OutT, 32>), g, dim3(256), 0, st, a);
+  else if (a.M <= 40) hipLaunchKernelGGL((skinny_kernel<T, OutT, 40>), g, dim3(256), 0, st, a);
+  else if (a.M <= 48) hipLaunchKernelGGL((skinny_kernel<T, OutT, 48>), g, dim3(256), 0, st, a);
+  else hipLaunchKernelGGL((skinny_kernel<T, OutT, 64>), g, dim3(256), 0, st, a);
+  AVSR_CHECK_LAUNCH();
+  return 0;
+}
+
+// forward linears with few rows (AVSR_GEMM_NOSKINNY=1 keeps the tiled cores: A/B comparisons)
+bool skinny_ok(const avsr_gemm_params* p, int splits) {
+  static int off = -1;
+  if (off < 0) { const char* e = getenv("AVSR_GEMM_NOSKINNY"); off = (e && e[0] == '1') ? 1 : 0; }
+  const int esz = p->dtype == AVSR_BF16 ? 2 : 4;
+  return !off && p->M <= 64 && p->a_kmajor && p->b_kmajor && p->batch == 1 && splits == 1 && !p->epi_bwd && !p->db &&
+         (p->K % 4) == 0 && (p->lda % 4) == 0 && (p->ldb % 4) == 0 && ((uintptr_t)p->A % (4 * esz)) == 0 &&
+         ((uintptr_t)p->B % (4 * esz)) == 0;
+}
+
 bool getenv_flag(const char* name) {
   const char* e = getenv(name);
   return e && e[0] == '1';
@@ -335,6 +462,10 @@ extern "C" int avsr_gemm(const avsr_gemm_params* p, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   if (p->K == 0) return AVSR_E_SHAPE;
   int rc;
+  if (!glds && !slab && skinny_ok(p, splits)) {
+    if (p->dtype == AVSR_F32) return skinny_launch<float, float>(a, st);
+    return p->c_f32 ? skinny_launch<bf16, float>(a, st) : skinny_launch<bf16, bf16>(a, st);
+  }
   if (glds) rc = p->c_f32 ? glds_by_layout<float>(p, a, st) : glds_by_layout<bf16>(p, a, st);
   else if (p->dtype == AVSR_F32) rc = by_tile<float, float>(p, a, st);
   else if (p->c_f32) rc = by_tile<bf16, float>(p, a, st);

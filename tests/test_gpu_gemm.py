@@ -200,3 +200,22 @@ def test_tile_configs_bit_identical(dev, monkeypatch, tile):
     # the bias gradient sums per-row-tile partials: a different row-tile height re-associates
     assert _rel(got[3], ref[3]) < 1e-5
 
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("M,N,K", [(1, 1024, 1024), (5, 3072, 1024), (40, 5049, 1024), (17, 1024, 3072),
+                                   (64, 100, 264), (33, 17, 8), (47, 256, 512), (12, 300, 3072)])
+def test_skinny_linear(dev, dtype, M, N, K):
+    """Few-row linears (beam-search decoder steps) on the vector-ALU skinny kernel: vs fp64 with
+    the bias / ReLU / residual epilogue; run-to-run bit-identical."""
+    g = torch.Generator(device="cpu").manual_seed(M * 13 + N + K)
+    x = torch.randn(M, K, generator=g).to(dev, dtype)
+    W = (torch.randn(N, K, generator=g) * K ** -0.5).to(dev, dtype)
+    b = torch.randn(N, generator=g).to(dev)
+    r = torch.randn(M, N, generator=g).to(dev, dtype)
+    y = ops.linear_fwd(x, W, b, act=L.ACT_RELU, res=r)
+    ref = torch.relu(x.double() @ W.double().t() + b.double()) + r.double()
+    tol = 1e-6 if dtype == torch.float32 else 1e-2
+    assert _rel(y, ref) < tol
+    y2 = ops.linear_fwd(x, W, b, act=L.ACT_RELU, res=r)
+    assert torch.equal(y, y2)

@@ -1,0 +1,10 @@
+# GEMM + decode parity tests, then decode throughput (C1 / C4 / C5)
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+O=gpurun_out/${1:-dec}; mkdir -p $O
+timeout -k 10 600 python -u -m pytest tests/test_gpu_gemm.py tests/test_gpu_decode.py tests/test_gpu_fullsize_golden.py -x -q --timeout 300 --timeout-method thread > $O/tests.log 2>&1 || { echo tests failed; tail -30 $O/tests.log; exit 1; }
+tail -1 $O/tests.log
+timeout -k 10 300 python -u tools/decode_bench.py > $O/dec.json 2> $O/dec.err || { echo dec failed; tail -20 $O/dec.err; exit 1; }
+cat $O/dec.json
+echo rc=0

@@ -1,0 +1,8 @@
+# rocprof kernel trace of the decode throughput run
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+O=gpurun_out/${1:-decp}; mkdir -p $O
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/p -o run -- python3 tools/decode_bench.py > $O/dec.log 2>&1 || { echo dec failed; tail -20 $O/dec.log; exit 1; }
+grep config $O/dec.log
+echo rc=0
