@@ -729,157 +729,48 @@ __global__ __launch_bounds__(PCfg::NTH, 2) void conv_patch_kernel(ConvArgs a, Pa
 }
 
 // ---------------------------------------------------------------- patch-resident weight-grad
-// dW[co][(kh, kw, ci)] = sum_p dy[p][co] * x[p + (kh-1, kw-1)][ci] for the same 3x3 / stride 1 /
-// 64-channel convolutions. The general weight-grad re-gathers x for every tap (9 passes of the
-// input through L2, 64 x 256 tiles of which the last of three is 3/4 padding: 17 % of MFMA
-// peak). Here persistent blocks (one per CU) walk contiguous 256-pixel tiles; per tile the dy
-// rows (32 KiB) and the padded x patch around them (48 KiB) are DMA'd into LDS once, double
-// buffered (2 x 80 KiB), and all 9 taps read the patch at row offsets. The whole 64 x 576
-// gradient stays in registers: wave w owns columns [144w, 144w + 144) = 9 column tiles of 16
-// (36 accumulators of 16 x 16). Both operands are pixel-major, so both fragments are transposed
-// LDS reads (ds_read_b64_tr_b16); the B fragment's rows are the patch rows of its 8 pixels (a
-// per-lane row table, 16 entries per tile). Each block writes its fp32 partial once to a slab
-// [block][64][576]; wgrad_reduce_kernel sums the slabs in block order (deterministic).
-constexpr int WP_TILE = 256;                               // pixels per tile
-constexpr int WP_DY = WP_TILE * 128;                       // dy rows: 32 KiB
-constexpr int WP_BUF = WP_DY + PATCH_BYTES;                // one buffer: 80 KiB
-constexpr int WP_LDS = 2 * WP_BUF;                         // 160 KiB: one block per CU
-constexpr int WP_N = 576, WP_CT = WP_N / 16 / 4;           // 9 column tiles per wave
-constexpr int WP_BLOCKS = 256;
-
-AVSR_DEV int rswz8(int k) { return gemmg::rswz<8>(k); }
-
-// transposed 16x16x32 fragment of a [row][64] image whose rows for k = 0..7 of this lane are
-// rowa (k 0..3) / rowb (k 4..7), columns col..col+3 (col = 16-block + 4 * (lane & 3))
-AVSR_DEV bf16x8 trfrag(const char* img, int rowa, int rowb, int col) {
-  const char* pa = img + rowa * 128 + (((col >> 3) ^ rswz8(rowa)) << 4) + (col & 7) * 2;
-  const char* pb = img + rowb * 128 + (((col >> 3) ^ rswz8(rowb)) << 4) + (col & 7) * 2;
-  const v4i16 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)pa);
-  const v4i16 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)pb);
-  union { v4i16 s4[2]; bf16x8 h; } u;
-  u.s4[0] = a; u.s4[1] = b;
-  return u.h;
-}
-
-__global__ __launch_bounds__(256, 1) void conv_wgrad_patch_kernel(const bf16* __restrict__ x, uint32_t x_bytes,
-                                                                  const bf16* __restrict__ dy, uint32_t dy_bytes,
-                                                                  int M, PatchGeom pg, float* __restrict__ ws, int dbg) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int ntiles = (M + WP_TILE - 1) / WP_TILE;
-  const int blk = blockIdx.x, nblk = gridDim.x;
-  const int ta = (int)((int64_t)ntiles * blk / nblk), tb = (int)((int64_t)ntiles * (blk + 1) / nblk);
-  const __amdgpu_buffer_rsrc_t rx = make_rsrc(x, x_bytes), rdy = make_rsrc(dy, dy_bytes);
-  const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
-  // this wave's column tiles: tap and channel block of global column tile 9 * wave + j
-  int toffj[WP_CT], colj[WP_CT];
-#pragma unroll
-  for (int j = 0; j < WP_CT; ++j) {
-    const int jj = WP_CT * wave + j, tap = jj >> 2, kh = tap / 3, kw = tap - 3 * kh;
-    toffj[j] = (kh - 1) * pg.Wp + (kw - 1);
-    colj[j] = (jj & 3) * 16 + 4 * pp;
-  }
-  f32x4 acc[4][WP_CT];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < WP_CT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // DMA of tile t into buffer buf: dy rows (8 pieces per wave: rows 8 * (wave + 4i) ..), patch
-  // rows (12 pieces per wave); the patch starts one padded row + one column before the tile
-  auto issue = [&](int t, char* buf) {
-    const int m0 = t * WP_TILE;
-    const int qmin = patch_pos(m0, pg) - pg.Wp - 1;
-#pragma unroll
-    for (int i = 0; i < WP_TILE / 8 / 4; ++i) {
-      const int row = (wave + 4 * i) * 8 + (lane >> 3);
-      const int c = (lane & 7) ^ rswz8(row);
-      const uint32_t vo = m0 + row < M ? ((uint32_t)(m0 + row) * 64u + c * 8u) * 2u : gemmg::OOB;
-      gemmg::bglds16(rdy, vo, 0u, buf + (wave + 4 * i) * 1024);
-    }
-#pragma unroll
-    for (int i = 0; i < PATCH_ROWS / 8 / 4; ++i) {
-      const int pr = (wave + 4 * i) * 8 + (lane >> 3);
-      const int c = (lane & 7) ^ rswz8(pr);
-      const uint32_t qq = (uint32_t)(qmin + pr);
-      const uint32_t n = fdiv(qq, pg.f_pp), rem = qq - n * (uint32_t)pg.PP;
-      const uint32_t yy = fdiv(rem, pg.f_wp), xx = rem - yy * (uint32_t)pg.Wp;
-      const bool ok = n < (uint32_t)pg.nimg && yy - 1u < (uint32_t)pg.H && xx - 1u < (uint32_t)pg.W;
-      const uint32_t vo = ok ? (((n * pg.H + yy - 1) * pg.W + xx - 1) * 64u + c * 8u) * 2u : gemmg::OOB;
-      gemmg::bglds16(rx, vo, 0u, buf + WP_DY + (wave + 4 * i) * 1024);
-    }
-  };
-  if (ta < tb && dbg != 2) issue(ta, smem);
-  for (int t = ta; t < tb; ++t) {
-    char* buf = smem + ((t - ta) & 1) * WP_BUF;
-    const int m0 = t * WP_TILE;
-    const int qmin = patch_pos(m0, pg) - pg.Wp - 1;
-    // patch rows of this lane's fragment pixels: k-step kb reads pixels 32kb + 8g + q (+4)
-    int pra[8], prb[8];
-#pragma unroll
-    for (int kb = 0; kb < 8; ++kb) {
-      const int p = m0 + 32 * kb + 8 * g + q;
-      pra[kb] = patch_pos(min(p, M - 1), pg) - qmin;
-      prb[kb] = patch_pos(min(p + 4, M - 1), pg) - qmin;
-    }
-    gemmg::wait_vmcnt<0>();                 // tile t has landed (only its DMAs are outstanding)
-    __builtin_amdgcn_s_barrier();           // ... for every wave; every wave is done with tile t-1
-    asm volatile("" ::: "memory");
-    if (t + 1 < tb && dbg != 2) issue(t + 1, smem + ((t + 1 - ta) & 1) * WP_BUF);
-    if (dbg == 1) continue;
-    const char* dimg = buf;
-    const char* patch = buf + WP_DY;
-#pragma unroll
-    for (int kb = 0; kb < 8; ++kb) {
-      bf16x8 a[4], b[WP_CT];
-      const int ka = 32 * kb + 8 * g + q;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) a[i] = trfrag(dimg, ka, ka + 4, 16 * i + 4 * pp);
-#pragma unroll
-      for (int j = 0; j < WP_CT; ++j) b[j] = trfrag(patch, pra[kb] + toffj[j], prb[kb] + toffj[j], colj[j]);
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < WP_CT; ++j) acc[i][j] = mfma16(a[i], b[j], acc[i][j]);
-    }
-  }
-  // partial -> ws[blk][co][576]: accumulator (i, j) register r = row 16i + 4g + r, column
-  // 144 * wave + 16j + (lane & 15)
-  float* o = ws + (int64_t)blk * 64 * WP_N;
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < WP_CT; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        o[(16 * i + 4 * g + r) * WP_N + 144 * wave + 16 * j + (lane & 15)] = acc[i][j][r];
-}
-
-// Half-image tiles for the 22 x 22 images of ResNet stage 1 (88 x 88 lip crops): the same
-// gradient, but every tile has the same geometry (11 image rows = 242 pixels, a 13 x 24 padded
-// patch), so every LDS address of the main loop is a per-lane base fixed for the whole kernel
-// plus a compile-time offset (the general-position kernel above spends ~8 VALU per fragment
-// address and is VALU-bound at 3x the MFMA time). Wave w owns input channels [16w, 16w + 16)
-// of all 9 taps; a tap is an immediate row offset into the patch. The MFMA k order within a
-// fragment is permuted (k bits 2 and 3 swapped), so each half-wave transposed read covers 8
-// consecutive pixels: the dy image (128-byte rows) is conflict-free with a chunk XOR on pixel
-// bits 1-2, the patch (144-byte rows, no XOR) is conflict-free except where 8 pixels straddle an
-// image row. DMAs of the next tile are spread over the k-steps (2-3 per step, ~60 issue
-// cycles each).
-constexpr int WH_W = 22, WH_R = 11, WH_PX = WH_R * WH_W;          // 242 pixels per tile
-constexpr int WH_WP = WH_W + 2, WH_PROWS = (WH_R + 2) * WH_WP;    // 312 padded positions
-constexpr int WH_PST = 144;                                        // patch row stride: 128 B + 16 B
-constexpr int WH_PPIECE = (WH_PROWS * 9 + 255) / 256;              // 11 patch DMA pieces per wave
-constexpr int WH_PBYTES = WH_PPIECE * 4 * 1024;                    // 45,056 (2,816 16-byte slots)
-constexpr int WH_DY = 256 * 128;                                   // dy rows (>= 242: zero)
-constexpr int WH_BUF = WH_DY + WH_PBYTES;
-constexpr int WH_LDS = 2 * WH_BUF;                                 // 155,648: one block per CU
+// dW[co][(kh, kw, ci)] = sum_p dy[p][co] * x[p + (kh-1, kw-1)][ci] for the 3x3 / stride 1 /
+// pad 1 convolutions of ResNet stages 1 (22 x 22 x 64) and 2 (11 x 11 x 128). The general
+// weight-grad re-gathers x for every tap (9 passes of the input through L2; at stage 1 its
+// 64 x 256 tiles are 1/4 padding). Here persistent blocks (one per CU) walk tiles of TR whole
+// image rows; a block owns a 64 x 64 (co, ci) block of every tap. Per tile the block's dy
+// channels and the zero-padded (TR+2) x (W+2) patch of its x channels are DMA'd into LDS once,
+// double buffered, and all 9 taps read the patch at row offsets. Every tile has the same
+// geometry, so each LDS address of the main loop is a per-lane base fixed for the kernel plus a
+// compile-time offset. The 64 x 576 gradient block stays in registers: wave w owns input
+// channels [16w, 16w + 16) of all 9 taps (36 accumulators of 16 x 16). Both operands are
+// pixel-major, so both fragments are transposed LDS reads (ds_read_b64_tr_b16); the MFMA k
+// order within a fragment is permuted (k bits 2 and 3 swapped) so that each half-wave read
+// covers 8 consecutive pixels: the dy image (128-byte rows) is conflict-free with a chunk XOR
+// on pixel bits 1-2, the patch (padded rows, no XOR) is (nearly) conflict-free. The
+// DMAs of the next tile are spread over the k-steps. With several (co, ci) blocks (stage 2:
+// 2 x 2), the blocks that share an XCD (ids b, b+8, ...) take the blocks of the same tile range,
+// so x and dy come from that XCD's L2 after the first read. Each block writes its fp32 partial
+// once to a slab [block][64][576]; wpatch_reduce_kernel sums them in block order (deterministic).
+template <int W_, int TR_, int TPI_, int NBUF_, int PST_>
+struct WPGeo {
+  static constexpr int W = W_, TR = TR_, TPI = TPI_, H = TR * TPI, NBUF = NBUF_, PST = PST_;
+  static constexpr int PX = TR * W;                  // pixels per tile
+  static constexpr int KS = (PX + 31) / 32;          // k-steps of 32 pixels
+  static constexpr int DYR = KS * 32;                // dy image rows (>= PX: zero)
+  static constexpr int WP = W + 2, PROWS = (TR + 2) * WP;
+  static constexpr int SLOTS = PST / 16;             // 16-byte slots per patch row (8 data + pad)
+  static constexpr int PPIECE = (PROWS * SLOTS + 255) / 256;   // patch DMA pieces per wave
+  static constexpr int PBYTES = PPIECE * 4 * 1024;
+  static constexpr int DYPIECE = DYR * 128 / 4096;   // dy DMA pieces per wave
+  static constexpr int DYB = DYR * 128;
+  static constexpr int BUF = DYB + PBYTES;
+  static constexpr int LDS = NBUF * BUF;
+  static constexpr int NP = DYPIECE + PPIECE;        // DMAs per wave per tile
+  static_assert(LDS <= 160 * 1024, "the tile buffers must fit the CU's LDS");
+};
+// patch row stride 144 B: one 2-way overlap among 8 consecutive rows' 32-byte windows; 160 B:
+// none (what the LDS allows)
+using WPStage1 = WPGeo<22, 11, 2, 2, 144>;   // half images: 242 pixels, 13 x 24 patch, double buffered
+using WPStage2 = WPGeo<11, 11, 1, 3, 160>;   // whole images: 121 pixels, 13 x 13 patch, 3 buffers (short tiles)
+constexpr int WP_BLOCKS = 256, WP_COLS = 576;
 
 AVSR_DEV int whswz(int row) { return ((row >> 1) & 3) << 1; }
-AVSR_DEV int whprow(int px) {                                     // tile pixel -> patch row
-  px = min(px, WH_PX - 1);
-  const int y = px / WH_W, x = px - y * WH_W;
-  return (y + 1) * WH_WP + x + 1;
-}
 AVSR_DEV bf16x8 trpair(const char* pa, const char* pb) {
   const v4i16 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)pa);
   const v4i16 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)pb);
@@ -888,157 +779,206 @@ AVSR_DEV bf16x8 trpair(const char* pa, const char* pb) {
   return u.h;
 }
 
-__global__ __launch_bounds__(256, 1) void conv_wgrad_half_kernel(const bf16* __restrict__ x, const bf16* __restrict__ dy,
-                                                                 uint32_t bytes, int nimg, float* __restrict__ ws) {
+// (co, ci) block q and tile range r of block b: the nq blocks with the same range sit at
+// ids b, b+8, ... (one XCD under round-robin placement); ranges per block kind = 256 / nq
+AVSR_DEV void wp_block(int b, int nq, int& q, int& r) {
+  q = (b >> 3) % nq;
+  r = ((b >> 3) / nq) * 8 + (b & 7);
+}
+
+template <class G>
+__global__ __launch_bounds__(256, 1) void conv_wgrad_patch_kernel(const bf16* __restrict__ x, const bf16* __restrict__ dy,
+                                                                  uint32_t x_bytes, uint32_t dy_bytes, int nimg,
+                                                                  int cin, int cout, float* __restrict__ ws) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int IMG = G::H * G::W;
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int ntiles = 2 * nimg;
-  const int blk = blockIdx.x, nblk = gridDim.x;
-  const int ta = (int)((int64_t)ntiles * blk / nblk), tb = (int)((int64_t)ntiles * (blk + 1) / nblk);
-  const __amdgpu_buffer_rsrc_t rx = make_rsrc(x, bytes), rdy = make_rsrc(dy, bytes);
-  // DMA pieces of a tile, relative to its first pixel (img * 484 + 11 * half) * 128 bytes
-  int dyrel[8], prel[WH_PPIECE];
-  uint32_t vtop = 0u, vbot = 0u;          // patch piece validity for the top / bottom half
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
+  const int ncih = cin / 64, nq = (cout / 64) * ncih, bpq = gridDim.x / nq;
+  int q, rng;
+  wp_block(blockIdx.x, nq, q, rng);
+  const int coh = q / ncih, cih = q - coh * ncih;
+  const int ntiles = nimg * G::TPI;
+  const int ta = (int)((int64_t)ntiles * rng / bpq), tb = (int)((int64_t)ntiles * (rng + 1) / bpq);
+  const __amdgpu_buffer_rsrc_t rx = make_rsrc(x, x_bytes), rdy = make_rsrc(dy, dy_bytes);
+  // DMA pieces of a tile (offsets recomputed per issue: compile-time divisors, no registers held)
+  auto tile_px = [&](int t) { return (t / G::TPI) * IMG + (t % G::TPI) * G::PX; };
+  auto issue_dy = [&](int i, int t, char* buf) {
     const int s = (wave + 4 * i) * 64 + lane, row = s >> 3;
     const int c = (s & 7) ^ whswz(row);
-    dyrel[i] = row < WH_PX ? row * 128 + c * 16 : -1;
-  }
-#pragma unroll
-  for (int i = 0; i < WH_PPIECE; ++i) {
-    const int s = (wave + 4 * i) * 64 + lane, row = s / 9, ch = s - row * 9;
-    const int py = row / WH_WP, pxp = row - py * WH_WP;
-    const bool ok = ch < 8 && row < WH_PROWS && pxp >= 1 && pxp <= WH_W;
-    prel[i] = ((py - 1) * WH_W + pxp - 1) * 128 + ch * 16;
-    vtop |= (ok && py >= 1 && py <= WH_R + 1 ? 1u : 0u) << i;
-    vbot |= (ok && py <= WH_R ? 1u : 0u) << i;
-  }
-  auto issue_dy = [&](int i, int t, char* buf) {
-    const uint32_t base = (uint32_t)((t >> 1) * (WH_W * WH_W) + (t & 1) * WH_PX) * 128u;
-    gemmg::bglds16(rdy, dyrel[i] >= 0 ? base + (uint32_t)dyrel[i] : gemmg::OOB, 0u, buf + (wave + 4 * i) * 1024);
+    const uint32_t vo = row < G::PX ? (uint32_t)(tile_px(t) + row) * (uint32_t)(cout * 2) + coh * 128 + c * 16 : gemmg::OOB;
+    gemmg::bglds16(rdy, vo, 0u, buf + (wave + 4 * i) * 1024);
   };
   auto issue_patch = [&](int i, int t, char* buf) {
-    const uint32_t base = (uint32_t)((t >> 1) * (WH_W * WH_W) + (t & 1) * WH_PX) * 128u;
-    const bool ok = (((t & 1) ? vbot : vtop) >> i) & 1u;
-    gemmg::bglds16(rx, ok ? base + (uint32_t)prel[i] : gemmg::OOB, 0u, buf + WH_DY + (wave + 4 * i) * 1024);
+    const int s = (wave + 4 * i) * 64 + lane, row = s / G::SLOTS, ch = s - row * G::SLOTS;
+    const int py = row / G::WP, pxp = row - py * G::WP;
+    const int y = (t % G::TPI) * G::TR + py - 1;       // image row of this slot's patch row
+    const bool ok = ch < 8 && row < G::PROWS && pxp >= 1 && pxp <= G::W && y >= 0 && y < G::H;
+    const uint32_t vo = ok ? (uint32_t)(tile_px(t) + (py - 1) * G::W + pxp - 1) * (uint32_t)(cin * 2) + cih * 128 + ch * 16
+                           : gemmg::OOB;
+    gemmg::bglds16(rx, vo, 0u, buf + G::DYB + (wave + 4 * i) * 1024);
   };
   // fragment bases: lane group g holds k = 8g + j <-> pixel 32kb + 16(g >> 1) + 4(g & 1) + (j & 3) + 8(j >> 2)
-  const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
-  const int pxa = 16 * (g >> 1) + 4 * (g & 1) + q;
+  const int g = lane >> 4, qq = (lane & 15) >> 2, pp = lane & 3;
+  const int pxa = 16 * (g >> 1) + 4 * (g & 1) + qq;
   const int sw = whswz(pxa);
   int dA[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) dA[i] = pxa * 128 + (((2 * i + (pp >> 1)) ^ sw) << 4) + 8 * (pp & 1);
-  int pA[8], pB[8];                       // patch byte bases (tap (0, 0) = offset 0) per k-step
+  auto prow = [&](int px) {                        // tile pixel -> patch row
+    px = min(px, G::PX - 1);
+    const int yy = px / G::W, xx = px - yy * G::W;
+    return (yy + 1) * G::WP + xx + 1;
+  };
+  int pA[G::KS], pB[G::KS];               // patch byte bases (tap (0, 0) = offset 0) per k-step
 #pragma unroll
-  for (int kb = 0; kb < 8; ++kb) {
-    pA[kb] = (whprow(32 * kb + pxa) - WH_WP - 1) * WH_PST + 32 * wave + 8 * pp;
-    pB[kb] = (whprow(32 * kb + pxa + 8) - WH_WP - 1) * WH_PST + 32 * wave + 8 * pp;
+  for (int kb = 0; kb < G::KS; ++kb) {
+    pA[kb] = (prow(32 * kb + pxa) - G::WP - 1) * G::PST + 32 * wave + 8 * pp;
+    pB[kb] = (prow(32 * kb + pxa + 8) - G::WP - 1) * G::PST + 32 * wave + 8 * pp;
   }
   f32x4 acc[4][9];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int t = 0; t < 9; ++t) acc[i][t] = f32x4{0.f, 0.f, 0.f, 0.f};
-  if (ta < tb) {
+  constexpr int PD = G::NBUF - 1;          // tiles in flight ahead of the one computed
 #pragma unroll
-    for (int i = 0; i < 8; ++i) issue_dy(i, ta, smem);
+  for (int d = 0; d < PD; ++d)
+    if (ta + d < tb) {
 #pragma unroll
-    for (int i = 0; i < WH_PPIECE; ++i) issue_patch(i, ta, smem);
-  }
+      for (int i = 0; i < G::DYPIECE; ++i) issue_dy(i, ta + d, smem + d * G::BUF);
+#pragma unroll
+      for (int i = 0; i < G::PPIECE; ++i) issue_patch(i, ta + d, smem + d * G::BUF);
+    }
+  constexpr int PER = (G::DYPIECE + G::PPIECE + G::KS - 1) / G::KS;   // DMAs per k-step
   for (int t = ta; t < tb; ++t) {
-    const char* buf = smem + ((t - ta) & 1) * WH_BUF;
-    char* nbuf = smem + ((t + 1 - ta) & 1) * WH_BUF;
-    const bool more = t + 1 < tb;
-    gemmg::wait_vmcnt<0>();               // tile t has landed (only its DMAs are outstanding)
+    const char* buf = smem + ((t - ta) % G::NBUF) * G::BUF;
+    char* nbuf = smem + ((t + PD - ta) % G::NBUF) * G::BUF;
+    const bool more = t + PD < tb;
+    // tile t has landed: the DMAs of the (up to PD - 1) later tiles already issued may still fly
+    if constexpr (PD == 2) {
+      if (t + 1 < tb) gemmg::wait_vmcnt<G::NP>();
+      else gemmg::wait_vmcnt<0>();
+    } else {
+      gemmg::wait_vmcnt<0>();
+    }
     __builtin_amdgcn_s_barrier();         // ... for every wave; every wave is done with tile t-1
     asm volatile("" ::: "memory");
-    const char* patch = buf + WH_DY;
+    const char* patch = buf + G::DYB;
+    // fragments of k-step kb: 4 dy (A) and 9 tap (B) transposed reads; the reads of step kb+1
+    // are issued before the MFMAs of step kb (one wave per SIMD: nothing else hides their
+    // latency), the next tile's DMAs after them (the asm DMA is a compiler memory barrier)
+    struct Fr { bf16x8 a[4], b[9]; };
+    auto load = [&](Fr& f, int kb) {
 #pragma unroll
-    for (int kb = 0; kb < 8; ++kb) {
-      if (more) {
-        issue_dy(kb, t + 1, nbuf);
-        issue_patch(kb, t + 1, nbuf);
-        if (kb + 8 < WH_PPIECE) issue_patch(kb + 8, t + 1, nbuf);
-      }
-      bf16x8 a[4], b[9];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) a[i] = trpair(buf + dA[i] + kb * 4096, buf + dA[i] + kb * 4096 + 1024);
+      for (int i = 0; i < 4; ++i) f.a[i] = trpair(buf + dA[i] + kb * 4096, buf + dA[i] + kb * 4096 + 1024);
 #pragma unroll
       for (int tp = 0; tp < 9; ++tp) {
-        const int off = ((tp / 3) * WH_WP + tp % 3) * WH_PST;
-        b[tp] = trpair(patch + pA[kb] + off, patch + pB[kb] + off);
+        const int off = ((tp / 3) * G::WP + tp % 3) * G::PST;
+        f.b[tp] = trpair(patch + pA[kb] + off, patch + pB[kb] + off);
+      }
+    };
+    Fr cur, nxt;
+    load(cur, 0);
+#pragma unroll
+    for (int kb = 0; kb < G::KS; ++kb) {
+      if (kb + 1 < G::KS) load(nxt, kb + 1);
+      if (more) {
+#pragma unroll
+        for (int d = 0; d < PER; ++d) {
+          const int pc = kb * PER + d;
+          if (pc < G::DYPIECE) issue_dy(pc, t + PD, nbuf);
+          else if (pc < G::DYPIECE + G::PPIECE) issue_patch(pc - G::DYPIECE, t + PD, nbuf);
+        }
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int tp = 0; tp < 9; ++tp) acc[i][tp] = mfma16(a[i], b[tp], acc[i][tp]);
+        for (int tp = 0; tp < 9; ++tp) acc[i][tp] = mfma16(cur.a[i], cur.b[tp], acc[i][tp]);
+      if (kb + 1 < G::KS) cur = nxt;
     }
   }
-  // partial -> ws[blk][co][576]: accumulator (i, tap) register r = co 16i + 4g + r, column
+  // partial -> ws[block][co 64][576]: accumulator (i, tap) register r = co 16i + 4g + r, column
   // tap * 64 + 16 * wave + (lane & 15)
-  float* o = ws + (int64_t)blk * 64 * WP_N;
+  float* o = ws + (int64_t)blockIdx.x * 64 * WP_COLS;
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int tp = 0; tp < 9; ++tp)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) o[(16 * i + 4 * g + r) * WP_N + tp * 64 + 16 * wave + (lane & 15)] = acc[i][tp][r];
+      for (int r = 0; r < 4; ++r) o[(16 * i + 4 * g + r) * WP_COLS + tp * 64 + 16 * wave + (lane & 15)] = acc[i][tp][r];
+}
+
+AVSR_DEV int wp_bid(int q, int r, int nq) { return ((((r >> 3) * nq) + q) << 3) + (r & 7); }   // inverse of wp_block
+
+// dw[co][tap][ci] += sum over the tile ranges r of block kind q of ws[wp_bid(q, r)][co % 64][tap * 64 + ci % 64],
+// in range order (deterministic), in two passes: chunk c of WPR_CHUNKS folds its ranges into the
+// slab of its first range (in place); pass 2 (chunk < 0) adds the chunk heads in order to dw.
+// 4 consecutive ci per thread.
+constexpr int WPR_CHUNKS = 8;
+__global__ __launch_bounds__(256) void wpatch_reduce_kernel(float* __restrict__ ws, int bpq, int cin, int cout,
+                                                            float* dw, int pass2) {
+  const int ncih = cin / 64, nq = (cout / 64) * ncih;
+  const int e = (blockIdx.x * 256 + threadIdx.x) * 4;      // element of the 64 x 576 block
+  const int q = blockIdx.y, c = blockIdx.z;
+  if (e >= 64 * WP_COLS) return;
+  f32x4 s = {0.f, 0.f, 0.f, 0.f};
+  if (!pass2) {
+    const int r0 = bpq * c / WPR_CHUNKS, r1 = bpq * (c + 1) / WPR_CHUNKS;
+    for (int r = r0; r < r1; ++r) s += *(const f32x4*)(ws + (int64_t)wp_bid(q, r, nq) * 64 * WP_COLS + e);
+    if (r1 > r0) *(f32x4*)(ws + (int64_t)wp_bid(q, r0, nq) * 64 * WP_COLS + e) = s;
+    return;
+  }
+  for (int k = 0; k < WPR_CHUNKS; ++k) {
+    const int r0 = bpq * k / WPR_CHUNKS, r1 = bpq * (k + 1) / WPR_CHUNKS;
+    if (r1 > r0) s += *(const f32x4*)(ws + (int64_t)wp_bid(q, r0, nq) * 64 * WP_COLS + e);
+  }
+  const int r = e / WP_COLS, col = e - r * WP_COLS, tap = col >> 6, ci = col & 63;
+  const int coh = q / ncih, cih = q - coh * ncih;
+  float* d = dw + ((int64_t)(coh * 64 + r) * 9 + tap) * cin + cih * 64 + ci;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) d[k] += s[k];     // dw is a view into the parameter arena: 4-byte aligned only
 }
 
 // the patch-resident weight-grad applies: bf16, slab workspace, automatic split, 3x3 / stride 1
-// / pad 1, 64 -> 64 channels, one group, tiles whose padded span fits the patch;
+// / pad 1, one group, the stage-1 (22 x 22, 64 -> 64) or stage-2 (11 x 11, 128 -> 128) geometry;
 // AVSR_CONV_WPATCH=0 keeps the general kernel (A/B comparisons)
 static bool wpatch_ok(const avsr_conv_params* p) {
   const char* env = getenv("AVSR_CONV_WPATCH");
   if ((env && env[0] == '0') || p->dtype != AVSR_BF16 || !conv_glds_enabled() || p->groups != 1 || p->splitk > 0)
     return false;
   if (p->kh != 3 || p->kw != 3 || p->sh != 1 || p->sw != 1 || p->ph != 1 || p->pw != 1) return false;
-  if (p->cin != 64 || p->cout != 64 || p->ldx != 64 || p->ldy != 64) return false;
-  if (p->hin != p->hout || p->win != p->wout) return false;
-  const int64_t M = (int64_t)p->nimg * p->hin * p->win;
-  if (M <= 0 || M * 128 >= (int64_t)gemmg::OOB - (1 << 20)) return false;
-  const int64_t W = p->win, HW = (int64_t)p->hin * p->win, Wp = W + 2;
-  const int64_t span = (WP_TILE - 1) + 2 * ((WP_TILE - 1) / W + 1) + 2 * Wp * ((WP_TILE - 1) / HW + 1) + 2 * (Wp + 1) + 1;
-  return span <= PATCH_ROWS;
+  if (p->cin != p->cout || p->ldx != p->cin || p->ldy != p->cout || p->hin != p->hout || p->win != p->wout) return false;
+  if (p->hin != p->win) return false;
+  const int64_t bytes = (int64_t)p->nimg * p->hin * p->win * p->cin * 2;
+  if (bytes <= 0 || bytes >= (int64_t)gemmg::OOB - (1 << 20)) return false;
+  return (p->cin == 64 && p->hin == 22) || (p->cin == 128 && p->hin == 11);
 }
 
-// diagnostic (AVSR_WPATCH_DBG): 1 = DMAs only, 2 = MFMAs only (results invalid)
-static int wpatch_dbg() {
-  const char* e = getenv("AVSR_WPATCH_DBG");
-  return e ? atoi(e) : 0;
+template <class G>
+static int wpatch_launch_g(const avsr_conv_params* p, hipStream_t st) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)conv_wgrad_patch_kernel<G>, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS);
+    attr = true;
+  }
+  const uint32_t bytes = (uint32_t)((int64_t)p->nimg * p->hin * p->win * p->cin * 2);
+  hipLaunchKernelGGL((conv_wgrad_patch_kernel<G>), dim3(WP_BLOCKS), dim3(256), G::LDS, st, (const bf16*)p->x,
+                     (const bf16*)p->dy, bytes, bytes, p->nimg, p->cin, p->cout, p->ws);
+  AVSR_CHECK_LAUNCH();
+  const int nq = (p->cout / 64) * (p->cin / 64), bpq = WP_BLOCKS / nq;
+  const unsigned gx = (64 * WP_COLS / 4 + 255) / 256;
+  hipLaunchKernelGGL(wpatch_reduce_kernel, dim3(gx, (unsigned)nq, (unsigned)WPR_CHUNKS), dim3(256), 0, st, p->ws, bpq,
+                     p->cin, p->cout, p->dw, 0);
+  AVSR_CHECK_LAUNCH();
+  hipLaunchKernelGGL(wpatch_reduce_kernel, dim3(gx, (unsigned)nq, 1u), dim3(256), 0, st, p->ws, bpq, p->cin, p->cout,
+                     p->dw, 1);
+  AVSR_CHECK_LAUNCH();
+  return 0;
 }
 
 static int wpatch_launch(const avsr_conv_params* p, hipStream_t st) {
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)conv_wgrad_patch_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, WP_LDS);
-    attr = true;
-  }
-  PatchGeom pg;
-  pg.nimg = p->nimg; pg.H = p->hin; pg.W = p->win; pg.Wp = p->win + 2; pg.PP = (p->hin + 2) * (p->win + 2);
-  pg.f_pp = make_fastdiv((uint32_t)pg.PP); pg.f_wp = make_fastdiv((uint32_t)pg.Wp);
-  pg.f_hw = make_fastdiv((uint32_t)(p->hin * p->win)); pg.f_w = make_fastdiv((uint32_t)p->win);
-  pg.sign = 1;
-  const int M = p->nimg * p->hin * p->win;
-  const uint32_t bytes = (uint32_t)((int64_t)M * 128);
-  const char* half = getenv("AVSR_CONV_WHALF");
-  if (p->hin == WH_W && p->win == WH_W && !(half && half[0] == '0')) {
-    static bool attr2 = false;
-    if (!attr2) {
-      (void)hipFuncSetAttribute((const void*)conv_wgrad_half_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, WH_LDS);
-      attr2 = true;
-    }
-    hipLaunchKernelGGL(conv_wgrad_half_kernel, dim3(WP_BLOCKS), dim3(256), WH_LDS, st, (const bf16*)p->x,
-                       (const bf16*)p->dy, bytes, p->nimg, p->ws);
-    AVSR_CHECK_LAUNCH();
-    return 0;
-  }
-  hipLaunchKernelGGL(conv_wgrad_patch_kernel, dim3(WP_BLOCKS), dim3(256), WP_LDS, st, (const bf16*)p->x, bytes,
-                     (const bf16*)p->dy, bytes, M, pg, p->ws, wpatch_dbg());
-  AVSR_CHECK_LAUNCH();
-  return 0;
+  if (p->cin == 64) return wpatch_launch_g<WPStage1>(p, st);
+  return wpatch_launch_g<WPStage2>(p, st);
 }
 
 // AVSR_CONV_PATCH=0 keeps the general kernel (A/B comparisons)
@@ -1212,20 +1152,7 @@ extern "C" int avsr_conv_bwd_weight(const avsr_conv_params* p, void* stream) {
   a.a_gstride = p->cout; a.b_gstride = p->cin; a.c_gstride = p->cout * ktot;
   a.M = p->cout; a.N = (int)ktot; a.K = p->nimg * p->hout * p->wout;
   if (a.K == 0) return 0;
-  if (p->ws && wpatch_ok(p)) {     // patch-resident: one slab per persistent block, ordered reduce
-    rc = wpatch_launch(p, (hipStream_t)stream);
-    if (rc) return rc;
-    const int64_t mn = 64 * WP_N;
-    const int xb = avsr_grid(mn / 4, 256, 1024);
-    const int chunks = 16;
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)xb, 1u, (unsigned)chunks), dim3(256), 0, (hipStream_t)stream,
-                       p->ws, WP_BLOCKS, chunks, mn, p->dw, a.c_gstride);
-    AVSR_CHECK_LAUNCH();
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)xb, 1u, 1u), dim3(256), 0, (hipStream_t)stream, p->ws,
-                       WP_BLOCKS, -chunks, mn, p->dw, a.c_gstride);
-    AVSR_CHECK_LAUNCH();
-    return 0;
-  }
+  if (p->ws && wpatch_ok(p)) return wpatch_launch(p, (hipStream_t)stream);   // patch-resident, ordered slab reduce
   set_extents(a, p, true, ((int64_t)p->nimg * p->hout * p->wout - 1) * p->ldy + p->cout,
               ((int64_t)p->nimg * p->hin * p->win - 1) * p->ldx + p->cin);
   const bool glds = p->dtype == AVSR_BF16 && conv_glds_enabled();
@@ -1260,7 +1187,7 @@ extern "C" int avsr_conv_bwd_weight(const avsr_conv_params* p, void* stream) {
 
 extern "C" int64_t avsr_conv_wgrad_ws(const avsr_conv_params* p) {
   if (!p || (p->dtype != AVSR_BF16 && p->dtype != AVSR_F32)) return 0;
-  if (wpatch_ok(p)) return (int64_t)WP_BLOCKS * 64 * WP_N;
+  if (wpatch_ok(p)) return (int64_t)WP_BLOCKS * 64 * WP_COLS;
   const WgradPlan w = wgrad_plan(p, p->dtype == AVSR_BF16 && conv_glds_enabled(), true);
   if (!w.slab) return 0;
   return (int64_t)p->groups * w.splits * p->cout * ((int64_t)p->kh * p->kw * p->cin);

@@ -226,18 +226,19 @@ def test_stem_conv_direct(dev):
     assert torch.equal(h, h2)
 
 
+@pytest.mark.parametrize("hw,c", [(22, 64), (11, 128)])
 @pytest.mark.parametrize("nimg", [1, 37, 600])
-def test_wgrad_patch_matches_general(dev, nimg, monkeypatch):
-    """Patch-resident stage-1 weight-grad (persistent blocks, per-block slabs, ordered reduce) vs
-    the general implicit-GEMM weight-grad and fp64 torch; ragged last tile, blocks without tiles
-    (nimg = 1: 2 tiles for 256 blocks), accumulation into a non-zero dw, run-to-run bit-identical."""
-    g = torch.Generator().manual_seed(nimg)
-    geom = ops.ConvGeom(nimg, 22, 22, 64, 64, 3, 3, (1, 1), (1, 1))
-    x = torch.randn(nimg, 64, 22, 22, generator=g)
-    dyt = torch.randn(nimg, 64, 22, 22, generator=g)
+def test_wgrad_patch_matches_general(dev, nimg, hw, c, monkeypatch):
+    """Patch-resident weight-grad of the stage-1 / stage-2 3x3 convolutions (persistent blocks,
+    per-block slabs, ordered reduce) vs the general implicit-GEMM weight-grad and fp64 torch;
+    blocks without tiles (nimg = 1), accumulation into a non-zero dw, run-to-run bit-identical."""
+    g = torch.Generator().manual_seed(nimg + c)
+    geom = ops.ConvGeom(nimg, hw, hw, c, c, 3, 3, (1, 1), (1, 1))
+    x = torch.randn(nimg, c, hw, hw, generator=g)
+    dyt = torch.randn(nimg, c, hw, hw, generator=g)
     xd = x.permute(0, 2, 3, 1).contiguous().to(dev, torch.bfloat16)
     dy = dyt.permute(0, 2, 3, 1).contiguous().to(dev, torch.bfloat16)
-    init = torch.randn(64, 3, 3, 64, generator=g).to(dev)
+    init = torch.randn(c, 3, 3, c, generator=g).to(dev)
     dw1 = init.clone()
     ops.conv_bwd_weight(geom, xd, dy, dw1)
     dw1b = init.clone()
@@ -248,6 +249,6 @@ def test_wgrad_patch_matches_general(dev, nimg, monkeypatch):
     ops.conv_bwd_weight(geom, xd, dy, dw2)
     assert _rel(dw1 - init, dw2 - init) < 1e-4
     xr = xd.double().cpu().permute(0, 3, 1, 2).requires_grad_()
-    wr = torch.zeros(64, 64, 3, 3, dtype=torch.float64, requires_grad=True)
+    wr = torch.zeros(c, c, 3, 3, dtype=torch.float64, requires_grad=True)
     F.conv2d(xr, wr, padding=1).backward(dy.double().cpu().permute(0, 3, 1, 2))
     assert _rel(dw1 - init, wr.grad.permute(0, 2, 3, 1)) < 1e-4

@@ -80,9 +80,15 @@ for flag in ("0", "1"):
 for flag in ("0", "1"):
     os.environ["AVSR_CONV_WPATCH"] = flag
     res[f"s1_wgrad_wpatch{flag}"] = timed(lambda: ops.conv_bwd_weight(geom, x, dy, dw))
-os.environ["AVSR_CONV_WHALF"] = "0"       # general-position patch kernel instead of half-image tiles
-res["s1_wgrad_wpatch1_whalf0"] = timed(lambda: ops.conv_bwd_weight(geom, x, dy, dw))
-os.environ["AVSR_CONV_WHALF"] = "1"
+# stage 2: 11 x 11 x 128, 3x3 stride 1
+geom2 = ops.ConvGeom(N, 11, 11, 128, 128, 3, 3, (1, 1), (1, 1))
+M2 = N * 121
+x2 = torch.randn(M2, 128, generator=g).to(dev, bf)
+dy2 = torch.randn(M2, 128, generator=g).to(dev, bf)
+dw2 = torch.zeros(128, 3, 3, 128, device=dev)
+for flag in ("0", "1"):
+    os.environ["AVSR_CONV_WPATCH"] = flag
+    res[f"s2_wgrad_wpatch{flag}"] = timed(lambda: ops.conv_bwd_weight(geom2, x2, dy2, dw2))
 fl = 2.0 * M * 64 * 576
 res["s1_gflop"] = round(fl / 1e9, 1)
 res["stem_gflop_direct_k288"] = round(2.0 * N * 1936 * 64 * 288 / 1e9, 1)

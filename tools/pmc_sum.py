@@ -17,6 +17,9 @@ def short(name):
     g = re.search(r"GCfg<([^>]*)>", name) or re.search(r"GCfgILi(\d)ELi(\d)ELi(\d)ELi(\d)", name)
     if g:
         k += "[" + ",".join(x.strip() for x in g.groups() if x) + "]" if g.lastindex and g.lastindex > 1 else "[" + g.group(1).replace(" ", "") + "]"
+    wp = re.search(r"WPGeoILi(\d+)E", name)
+    if wp:
+        k += f"<W{wp.group(1)}>"
     kind = re.search(r"conv_glds_kernelI(\w+?)Li(\d)E", name)
     if kind:
         k += f"<{kind.group(1)},{kind.group(2)}>"

@@ -6,9 +6,9 @@ import re
 import sys
 
 rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
-starts = [i for i, r in enumerate(rows) if "stem_conv_kernel" in r["Kernel_Name"] or "stem_pack" in r["Kernel_Name"]]
-# iterations alternate fuse=1 / fuse=0; the last complete fuse=1 one is the second-to-last start
-firsts = [s for j, s in enumerate(starts) if j == 0 or s != starts[j - 1] + 1]
+# every fwd+bwd iteration starts with the stem input pack; iterations alternate fuse=1 / fuse=0,
+# so the last complete fuse=1 one is the second-to-last start
+firsts = [i for i, r in enumerate(rows) if "stem_pack" in r["Kernel_Name"]]
 seg = rows[firsts[-2]:firsts[-1]]
 t0, t1 = int(seg[0]["Start_Timestamp"]), int(seg[-1]["End_Timestamp"])
 print(f"span {(t1 - t0) / 1e6:.2f} ms")
