@@ -144,6 +144,8 @@ using Cfg128x64 = gemmg::GCfg<4, 1, 1, 2, 2>;    // 128x64, 4 waves (32x64 each)
 using Cfg192 = gemmg::GCfg<2, 2, 3, 2, 2>;       // 192x128, 4 waves (96x64 each), 2 stages (80 KiB), 2 blocks/CU
 using Cfg192x256 = gemmg::GCfg<2, 4, 3, 2, 2>;   // 192x256, 8 waves (96x64 each), 2 stages (112 KiB)
 using Cfg192s3 = gemmg::GCfg<2, 2, 3, 2, 3>;     // 192x128, 4 waves, 3 stages (120 KiB)
+using Cfg192w8 = gemmg::GCfg<2, 4, 3, 1, 2>;     // 192x128, 8 waves (96x32 each), 2 stages (80 KiB)
+using Cfg192w8s3 = gemmg::GCfg<2, 4, 3, 1, 3>;   // 192x128, 8 waves, 3 stages (120 KiB)
 
 // tile choice: AVSR_GEMM_TILE=128|256|256x128|128x256 forces one (benchmarks); otherwise the
 // configuration with the fewest block rounds x per-tile work (wave quantisation over 256 CUs)
@@ -153,7 +155,8 @@ int tile_cfg(const avsr_gemm_params* p, int splits) {
                    : !strcmp(e, "128x256") ? 3 : !strcmp(e, "128s3") ? 4 : !strcmp(e, "128s4") ? 5
                    : !strcmp(e, "128w8s3") ? 6 : !strcmp(e, "128w8s4") ? 7 : !strcmp(e, "pp") ? 8
                    : !strcmp(e, "96") ? 9 : !strcmp(e, "128x64") ? 10 : !strcmp(e, "192") ? 11
-                   : !strcmp(e, "192x256") ? 12 : !strcmp(e, "192s3") ? 13 : -1;
+                   : !strcmp(e, "192x256") ? 12 : !strcmp(e, "192s3") ? 13 : !strcmp(e, "192w8") ? 14
+                   : !strcmp(e, "192w8s3") ? 15 : -1;
   if (forced >= 0) return forced;
   // 128x128 at two blocks per CU is the default (tools/gemm_table.py, profiles/r02_gemm_table.*:
   // the 256x256 ping-pong core loses 8-36 % at M = 6000, the 3-stage / 8-wave variants are
@@ -168,6 +171,10 @@ int tile_cfg(const avsr_gemm_params* p, int splits) {
     const long t192 = (long)((p->M + 191) / 192) * ((p->N + 127) / 128) * tiles_z;
     const long n128 = (t128 + 255) / 256, n192 = (t192 + 255) / 256;   // blocks on the busiest CU
     if (n192 >= 2 && 3 * n192 * 50 <= 2 * n128 * 51) return 11;      // 1.5 n192 <= 1.02 n128
+    // one round of 192-row tiles that fills at least half the chip (the M = 6000, N = 1024
+    // encoder GEMMs: 256 tiles): one block per CU, so 8 waves (two per SIMD, one's MFMAs cover
+    // the other's LDS-DMA issue) and 3 stages: -10..-15 % vs 128x128 (profiles/r03_gemm_table_192w8.txt)
+    if (t192 > 128 && t192 <= 256) return 15;
   }
   return 0;
 }
@@ -188,6 +195,8 @@ int cfg_bm(int cfg, bool ak) {
     case 11: return ak ? Cfg192::BM : Cfg128::BM;
     case 12: return ak ? Cfg192x256::BM : Cfg128::BM;
     case 13: return ak ? Cfg192s3::BM : Cfg128::BM;
+    case 14: return ak ? Cfg192w8::BM : Cfg128::BM;
+    case 15: return ak ? Cfg192w8s3::BM : Cfg128::BM;
     default: return Cfg128::BM;
   }
 }
@@ -215,6 +224,12 @@ int launch_cfg(int cfg, const DenseArgs& a, int batch, hipStream_t st) {
       else return launch_glds<OutT, AK, BK, Cfg128>(a, batch, st);
     case 13:
       if constexpr (AK) return launch_glds<OutT, AK, BK, Cfg192s3>(a, batch, st);
+      else return launch_glds<OutT, AK, BK, Cfg128>(a, batch, st);
+    case 14:
+      if constexpr (AK) return launch_glds<OutT, AK, BK, Cfg192w8>(a, batch, st);
+      else return launch_glds<OutT, AK, BK, Cfg128>(a, batch, st);
+    case 15:
+      if constexpr (AK) return launch_glds<OutT, AK, BK, Cfg192w8s3>(a, batch, st);
       else return launch_glds<OutT, AK, BK, Cfg128>(a, batch, st);
     default: return launch_glds<OutT, AK, BK, Cfg128>(a, batch, st);
   }
