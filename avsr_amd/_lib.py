@@ -72,6 +72,7 @@ class LayerNormParams(ctypes.Structure):
         ("gamma", _c_p), ("beta", _c_p), ("mean", _c_p), ("rstd", _c_p),
         ("dy", _c_p), ("lddy", _i64), ("dx", _c_p), ("lddx", _i64),
         ("dres", _c_p), ("lddres", _i64), ("dgamma", _c_p), ("dbeta", _c_p), ("ws", _c_p),
+        ("g", _c_p), ("ldg", _i64), ("drop_p", _f), ("seed", ctypes.c_uint64), ("db", _c_p),
     ]
 
 

@@ -17,6 +17,7 @@ struct LnArgs {
   const float* gamma; const float* beta; float* mean; float* rstd;
   const void* dy; int64_t lddy; void* dx; int64_t lddx; const void* dres; int64_t lddres;
   float* dgamma; float* dbeta; float* ws;
+  void* g; int64_t ldg; float drop_p; uint64_t seed; bool db;   // fused ew_bwd (see avsr_layernorm_params)
 };
 
 // one wave per row; lane owns vectors lane, lane+64, ... (VPL of them)
@@ -71,12 +72,14 @@ __global__ __launch_bounds__(64 * W) void ln_bwd_kernel(LnArgs a) {
   constexpr int VE = VecW<T>::VE;
   const int lane = threadIdx.x & 63;
   const int nw = gridDim.x * W;
-  float dg[VPL][VE], db[VPL][VE], gm[VPL][VE];
+  float dg[VPL][VE], db[VPL][VE], gm[VPL][VE], gb[VPL][VE];
 #pragma unroll
   for (int i = 0; i < VPL; ++i) {
     const int c = (lane + i * 64) * VE;
 #pragma unroll
-    for (int j = 0; j < VE; ++j) { dg[i][j] = 0.f; db[i][j] = 0.f; gm[i][j] = c < a.N ? a.gamma[c + j] : 0.f; }
+    for (int j = 0; j < VE; ++j) {
+      dg[i][j] = 0.f; db[i][j] = 0.f; gb[i][j] = 0.f; gm[i][j] = c < a.N ? a.gamma[c + j] : 0.f;
+    }
   }
   for (int row0 = blockIdx.x * W + (threadIdx.x >> 6); row0 < a.rows; row0 += R * nw) {
     float xv[R][VPL][VE], dv[R][VPL][VE], rv[R][VPL][VE];
@@ -131,31 +134,49 @@ __global__ __launch_bounds__(64 * W) void ln_bwd_kernel(LnArgs a) {
 #pragma unroll
             for (int j = 0; j < VE; ++j) o[j] = rv[u][i][j] + rstd[u] * (dv[u][i][j] - s1 - xv[u][i][j] * s2);
             stv(dx + c, o);
+            if (a.g) {
+              // the fused ew_bwd: dropout backward of dx AS STORED (rounded to T), same mask
+              // stream and column sums as ew_bwd_kernel
+              float d[VE];
+#pragma unroll
+              for (int j = 0; j < VE; ++j) d[j] = to_f(from_f<T>(o[j]));
+              if (a.drop_p > 0.f) {
+                const uint64_t i0 = (uint64_t)(row0 + u * nw) * a.N + c;
+                if constexpr (VE == 8) drop8(a.drop_p, a.seed, i0, d);
+                else {
+#pragma unroll
+                  for (int j = 0; j < VE; ++j) d[j] *= drop_scale(a.drop_p, a.seed, i0 + j);
+                }
+              }
+#pragma unroll
+              for (int j = 0; j < VE; ++j) gb[i][j] += d[j];
+              stv((T*)a.g + (int64_t)(row0 + u * nw) * a.ldg + c, d);
+            }
           }
         }
       }
     }
   }
   if (!a.dgamma) return;
-  // per-block column partials (the block's waves summed in LDS) -> ws[block][2][N]
+  // per-block column partials (the block's waves summed in LDS) -> ws[block][2 or 3][N]
   extern __shared__ float red[];                 // [W][N]
   const int w = threadIdx.x >> 6;
-#pragma unroll
-  for (int q = 0; q < 2; ++q) {
+  const int nq = a.db ? 3 : 2;
+  for (int q = 0; q < nq; ++q) {
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < VPL; ++i) {
       const int c = (lane + i * 64) * VE;
       if (c < a.N)
 #pragma unroll
-        for (int j = 0; j < VE; ++j) red[w * a.N + c + j] = q == 0 ? dg[i][j] : db[i][j];
+        for (int j = 0; j < VE; ++j) red[w * a.N + c + j] = q == 0 ? dg[i][j] : (q == 1 ? db[i][j] : gb[i][j]);
     }
     __syncthreads();
     for (int c = threadIdx.x; c < a.N; c += 64 * W) {
       float t = 0.f;
 #pragma unroll
       for (int v = 0; v < W; ++v) t += red[v * a.N + c];
-      a.ws[((int64_t)blockIdx.x * 2 + q) * a.N + c] = t;
+      a.ws[((int64_t)blockIdx.x * nq + q) * a.N + c] = t;
     }
   }
 }
@@ -188,6 +209,8 @@ int ln_launch(const avsr_layernorm_params* p, bool bwd, hipStream_t st) {
   a.x = p->x; a.ldx = p->ldx; a.y = p->y; a.ldy = p->ldy; a.gamma = p->gamma; a.beta = p->beta;
   a.mean = p->mean; a.rstd = p->rstd; a.dy = p->dy; a.lddy = p->lddy; a.dx = p->dx; a.lddx = p->lddx;
   a.dres = p->dres; a.lddres = p->lddres; a.dgamma = p->dgamma; a.dbeta = p->dbeta; a.ws = p->ws;
+  a.g = bwd ? p->g : nullptr; a.ldg = p->ldg; a.drop_p = p->drop_p; a.seed = p->seed; a.db = bwd && p->db != nullptr;
+  if (a.db && (!a.g || !p->dgamma)) return AVSR_E_ARG;     // the bias partials ride on the dgamma workspace
   const int vpl = (p->N / VE + 63) / 64;
   int blocks = (p->rows + 3) / 4;
   int W = 4, R = 1;
@@ -210,8 +233,12 @@ int ln_launch(const avsr_layernorm_params* p, bool bwd, hipStream_t st) {
       else { if (R == 2) LNB(V, 2, 2); else LNB(V, 2, 1); }                                      \
       if (p->dgamma) {                                                                           \
         AVSR_CHECK_LAUNCH();                                                                     \
-        return colsum_launch((const float*)p->ws, blocks, (int64_t)2 * p->N, 2 * p->N, p->dgamma, \
-                             p->N, p->dbeta, st);                                                \
+        const int nq = a.db ? 3 : 2;                                                             \
+        const int rc = colsum_launch((const float*)p->ws, blocks, (int64_t)nq * p->N, 2 * p->N,   \
+                                     p->dgamma, p->N, p->dbeta, st);                             \
+        if (rc || !a.db) return rc;                                                              \
+        return colsum_launch((const float*)p->ws + 2 * p->N, blocks, (int64_t)3 * p->N, p->N,    \
+                             p->db, 0, nullptr, st);                                             \
       }                                                                                          \
     } else {                                                                                     \
       hipLaunchKernelGGL((ln_fwd_kernel<T, V>), dim3(blocks), dim3(256), 0, st, a);              \
@@ -495,23 +522,39 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(BnArgs a) {
     }
   }
   const bool acc = a.beta_acc != 0.f;
-  for (int64_t v = t0; v < nv; v += stride) {
-    float dz[VE], h[VE], o[VE];
-    ldv((const T*)a.dz + v * VE, dz);
-    ldv((const T*)a.h + v * VE, h);
-    if (acc) ldv((const T*)a.dh + v * VE, o);
+  // U grid-stride vectors per iteration with every load issued first (memory-level
+  // parallelism: one vector in flight per thread left this pass at ~65 % of HBM bandwidth)
+  constexpr int U = 4;
+  for (int64_t v0 = t0; v0 < nv; v0 += U * stride) {
+    float dz[U][VE], h[U][VE], o[U][VE], r[U][VE];
+    bool ok[U];
 #pragma unroll
-    for (int j = 0; j < VE; ++j) {
-      const float g = ka[j] * dz[j] + kb[j] * (h[j] - km[j]) + kc[j];
-      o[j] = acc ? a.beta_acc * o[j] + g : g;
+    for (int u = 0; u < U; ++u) {
+      const int64_t v = v0 + u * stride;
+      ok[u] = v < nv;
+      const int64_t vv = ok[u] ? v : v0;
+      ldv((const T*)a.dz + vv * VE, dz[u]);
+      ldv((const T*)a.h + vv * VE, h[u]);
+      if (acc) ldv((const T*)a.dh + vv * VE, o[u]);
+      if (a.dh2) ldv((const T*)a.res + vv * VE, r[u]);
     }
-    stv((T*)a.dh + v * VE, o);
-    if (a.dh2) {
-      float r[VE], o2[VE];
-      ldv((const T*)a.res + v * VE, r);
 #pragma unroll
-      for (int j = 0; j < VE; ++j) o2[j] = ka2[j] * dz[j] + kb2[j] * (r[j] - km2[j]) + kc2[j];
-      stv((T*)a.dh2 + v * VE, o2);
+    for (int u = 0; u < U; ++u) {
+      if (!ok[u]) break;
+      const int64_t v = v0 + u * stride;
+      float g[VE];
+#pragma unroll
+      for (int j = 0; j < VE; ++j) {
+        const float gg = ka[j] * dz[u][j] + kb[j] * (h[u][j] - km[j]) + kc[j];
+        g[j] = acc ? a.beta_acc * o[u][j] + gg : gg;
+      }
+      stv((T*)a.dh + v * VE, g);
+      if (a.dh2) {
+        float o2[VE];
+#pragma unroll
+        for (int j = 0; j < VE; ++j) o2[j] = ka2[j] * dz[u][j] + kb2[j] * (r[u][j] - km2[j]) + kc2[j];
+        stv((T*)a.dh2 + v * VE, o2);
+      }
     }
   }
 }

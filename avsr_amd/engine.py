@@ -44,6 +44,9 @@ _SIDE_BIAS = os.environ.get("AVSR_SIDE_BIAS", "1") == "1"
 _CTC_SIDE = os.environ.get("AVSR_CTC_SIDE", "1") == "1"
 # bf16 stem conv straight from the video (stem.hip) instead of pack + general implicit GEMM
 _STEM_DIRECT = os.environ.get("AVSR_STEM_DIRECT", "1") == "1"
+# encoder residual-branch dropout backward (+ bias gradient) fused into the LayerNorm backward
+# that produces its input gradient; 0 = separate ew_bwd passes (A/B)
+_LN_EW_FUSE = os.environ.get("AVSR_LN_EW_FUSE", "1") == "1"
 
 
 _STEP_STREAMS = {}
@@ -605,9 +608,21 @@ class Engine:
         y, mean, rstd = ops.layernorm_fwd(x, self.arena.master(name + ".weight"), self.arena.master(name + ".bias"), eps)
         return y, mean, rstd
 
-    def _ln_bwd(self, dy, x, name, mean, rstd, dres=None, dx=None):
-        return ops.layernorm_bwd(dy, x, self.arena.master(name + ".weight"), mean, rstd, dx=dx, dres=dres,
-                                 dgamma=self.g(name + ".weight"), dbeta=self.g(name + ".bias"))
+    def _ln_bwd(self, dy, x, name, mean, rstd, dres=None, dx=None, ew=None):
+        """LayerNorm backward; ew = (g_out, drop_p, seed, db name): the dropout backward of the
+        sublayer whose output was added to this LayerNorm's input, fused in (ew_bwd(dx, out=g_out,
+        drop_p, seed, db)): dx is the residual gradient of that sublayer's output"""
+        if ew is not None and _LN_EW_FUSE:
+            g, p, seed, dbn = ew
+            return ops.layernorm_bwd(dy, x, self.arena.master(name + ".weight"), mean, rstd, dx=dx, dres=dres,
+                                     dgamma=self.g(name + ".weight"), dbeta=self.g(name + ".bias"), g=g, drop_p=p,
+                                     seed=seed, db=self.g(dbn))
+        out = ops.layernorm_bwd(dy, x, self.arena.master(name + ".weight"), mean, rstd, dx=dx, dres=dres,
+                                dgamma=self.g(name + ".weight"), dbeta=self.g(name + ".bias"))
+        if ew is not None:
+            g, p, seed, dbn = ew
+            ops.ew_bwd(out, out=g, drop_p=p, seed=seed, db=self.g(dbn))
+        return out
 
     def encoder_fwd(self, audios, videos, bt, train, save, seeds, modality=None):
         """AVHubertModel.forward_gen(features_only=True) — returns (x (M, D), ctx)."""
@@ -706,26 +721,35 @@ class Engine:
                       x1=x1, ln2=ln2, m2=m2, r2=r2, h=h, act=act, sd_a=sd_a, p_a=p_a, sd_f=sd_f)
         return x2, lc
 
-    def _enc_layer_bwd(self, i, lc, dx2, B, T, klen):
-        """returns d(layer input); dx2 is consumed (may be reused)."""
+    def _ew_next(self, i, lc, M):
+        """the FFN output dropout backward of layer i (x2 = x1 + drop(act W2^T + b2)), fused into
+        the LayerNorm backward that produces dx2: (g2 buffer, p, seed, bias-gradient name)"""
+        return (self._e(M, self.D), lc["p_h"], lc["sd_f"], f"encoder.encoder.layers.{i}.feed_forward.output_dense.bias")
+
+    def _enc_layer_bwd(self, i, lc, dx2, B, T, klen, g2=None, lc_prev=None):
+        """returns (d(layer input), g2 of layer i-1 or None); dx2 is consumed (may be reused).
+        g2: this layer's FFN-output dropout backward of dx2, already computed by the LayerNorm
+        backward that produced dx2 (else computed here); lc_prev: layer i-1's context, whose g2
+        this layer's input LayerNorm backward computes."""
         D, H = self.D, self.H
         M = B * T
         p = f"encoder.encoder.layers.{i}."
         a = p + "attention."
         ff = p + "feed_forward."
         # x2 = x1 + drop(act W2^T + b2)
-        g2 = self._e(M, D)
-        ops.ew_bwd(dx2, out=g2, drop_p=lc["p_h"], seed=lc["sd_f"], db=self.g(ff + "output_dense.bias"))
+        if g2 is None:
+            g2 = self._e(M, D)
+            ops.ew_bwd(dx2, out=g2, drop_p=lc["p_h"], seed=lc["sd_f"], db=self.g(ff + "output_dense.bias"))
         self._wgrad(g2, lc["act"], self.g(ff + "output_dense.weight"))
         dh = ops.linear_dgrad(g2, self.w(ff + "output_dense.weight"), gate=lc["h"], act=GELU, drop_p=lc["p_a"],
                               seed=lc["sd_a"], db=self._fused_db(ff + "intermediate_dense.bias"))
         self._bias_grad(dh, self.g(ff + "intermediate_dense.bias"), fused=True)
         self._wgrad(dh, lc["ln2"], self.g(ff + "intermediate_dense.weight"))
         dln2 = ops.linear_dgrad(dh, self.w(ff + "intermediate_dense.weight"))
-        dx1 = self._ln_bwd(dln2, lc["x1"], p + "final_layer_norm", lc["m2"], lc["r2"], dres=dx2, dx=dx2)
-        # x1 = x + drop(o Wo^T + bo)
+        # x1 = x + drop(o Wo^T + bo): the out-proj dropout backward rides on this LN backward
         go = self._e(M, D)              # fresh: g2 may still be read by the side stream
-        ops.ew_bwd(dx1, out=go, drop_p=lc["p_h"], seed=lc["sd_o"], db=self.g(a + "out_proj.bias"))
+        dx1 = self._ln_bwd(dln2, lc["x1"], p + "final_layer_norm", lc["m2"], lc["r2"], dres=dx2, dx=dx2,
+                           ew=(go, lc["p_h"], lc["sd_o"], a + "out_proj.bias"))
         self._wgrad(go, lc["o"], self.g(a + "out_proj.weight"))
         do = ops.linear_dgrad(go, self.w(a + "out_proj.weight"))
         # attention
@@ -743,7 +767,9 @@ class Engine:
         self._bias_grad_side(dqkv, self.arena.span(names_b, buf="g"))
         self._wgrad(dqkv, lc["ln1"], self.arena.span(names_w, buf="g"))
         dln1 = ops.linear_dgrad(dqkv, self.arena.span(names_w))
-        return self._ln_bwd(dln1, lc["x"], p + "layer_norm", lc["m1"], lc["r1"], dres=dx1, dx=dx1)
+        ew = self._ew_next(i - 1, lc_prev, M) if lc_prev is not None else None
+        dx = self._ln_bwd(dln1, lc["x"], p + "layer_norm", lc["m1"], lc["r1"], dres=dx1, dx=dx1, ew=ew)
+        return dx, (ew[0] if ew is not None else None)
 
     def encoder_bwd(self, ctx, dout):
         cfg = self.cfg
@@ -751,9 +777,13 @@ class Engine:
         M, D = B * T, self.D
         EN = "encoder."
         E = "encoder.encoder."
-        dx = self._ln_bwd(dout, ctx["x_last"], E + "layer_norm", ctx["mf"], ctx["rf"])
+        layers = ctx["layers"]
+        ew = self._ew_next(self.nl - 1, layers[-1], M) if self.nl else None
+        dx = self._ln_bwd(dout, ctx["x_last"], E + "layer_norm", ctx["mf"], ctx["rf"], ew=ew)
+        g2 = ew[0] if ew is not None else None
         for i in reversed(range(self.nl)):
-            dx = self._enc_layer_bwd(i, ctx["layers"][i], dx, B, T, ctx["klen"])
+            dx, g2 = self._enc_layer_bwd(i, layers[i], dx, B, T, ctx["klen"], g2=g2,
+                                         lc_prev=layers[i - 1] if i > 0 else None)
             ops.colsum_flush()                      # this layer's bias / LayerNorm gradients
             if self.on_grad_ready is not None:      # layers >= i (and everything after them) final
                 self.on_grad_ready(self._layer_decay_off[i])   # (the reducer also waits for the side stream)

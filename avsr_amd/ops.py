@@ -283,16 +283,22 @@ def layernorm_fwd(x, gamma, beta, eps, y=None, mean=None, rstd=None):
     return y, mean, rstd
 
 
-def layernorm_bwd(dy, x, gamma, mean, rstd, dx=None, dres=None, dgamma=None, dbeta=None):
-    """dx = dres + LN-backward(dy); dgamma/dbeta (fp32) accumulate."""
+def layernorm_bwd(dy, x, gamma, mean, rstd, dx=None, dres=None, dgamma=None, dbeta=None, g=None, drop_p=0.0, seed=0,
+                  db=None):
+    """dx = dres + LN-backward(dy); dgamma/dbeta (fp32) accumulate. With g: the following
+    ew_bwd(dx, out=g, drop_p, seed, db) fused in (g = dropout-backward of dx as stored,
+    db += column sums of g)."""
     rows, N = x.shape
     dx = torch.empty_like(x) if dx is None else dx
-    ws = None if dgamma is None else _colsum_ws(256 * 2 * N, x.device)   # AVSR_LN_WS
+    if db is not None:
+        assert g is not None and dgamma is not None
+    ws = None if dgamma is None else _colsum_ws(256 * (3 if db is not None else 2) * N, x.device)   # AVSR_LN_WS(3)
     _call("avsr_layernorm_bwd", L.fill(L.LayerNormParams, dtype=dtype_code(x), rows=rows, N=N, eps=0.0,
                                         x=x, ldx=x.stride(0), ldy=N, gamma=gamma, mean=mean, rstd=rstd,
                                         dy=dy, lddy=dy.stride(0), dx=dx, lddx=dx.stride(0),
                                         dres=dres, lddres=0 if dres is None else dres.stride(0),
-                                        dgamma=dgamma, dbeta=dbeta, ws=ws))
+                                        dgamma=dgamma, dbeta=dbeta, ws=ws, g=g, ldg=0 if g is None else g.stride(0),
+                                        drop_p=float(drop_p), seed=int(seed) & (2 ** 64 - 1), db=db))
     return dx
 
 

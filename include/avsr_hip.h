@@ -169,9 +169,16 @@ typedef struct {
   const void* dres; int64_t lddres;         /* bwd: residual gradient added to dx (may alias dx) */
   float* dgamma; float* dbeta;              /* bwd: fp32 accumulators [N] or NULL */
   float* ws;                                /* bwd with dgamma: workspace >= AVSR_LN_WS(N) floats */
+  /* bwd, optional: the next elementwise backward of the chain fused in (avsr_ew_bwd with out,
+   * drop_p, seed, db): g = dropout-backward(dx as stored) and db += column sums of g. The
+   * reference applies dropout to the sublayer output that is added to this LayerNorm's input
+   * (HF Wav2Vec2EncoderLayer), so its gradient is the residual gradient dx masked. With db the
+   * workspace needs AVSR_LN_WS3(N) floats. */
+  void* g; int64_t ldg; float drop_p; uint64_t seed; float* db;
 } avsr_layernorm_params;
 #define AVSR_LN_BLOCKS 256
 #define AVSR_LN_WS(N) (AVSR_LN_BLOCKS * 2 * (N))
+#define AVSR_LN_WS3(N) (AVSR_LN_BLOCKS * 3 * (N))
 int avsr_layernorm_fwd(const avsr_layernorm_params* p, void* stream);
 int avsr_layernorm_bwd(const avsr_layernorm_params* p, void* stream);
 

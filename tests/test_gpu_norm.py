@@ -40,6 +40,36 @@ def test_layernorm(dev, dtype, N, eps):
     assert _rel(db, br.grad) < _tol(dtype, 1e-5)
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_layernorm_bwd_fused_dropout_bias(dev, dtype, p):
+    """The residual-branch dropout backward + bias gradient fused into the LayerNorm backward
+    (engine._ln_bwd ew=...) equals LayerNorm backward followed by ew_bwd, bit for bit."""
+    g = torch.Generator().manual_seed(11)
+    rows, N = 613, 1024
+    x = (torch.randn(rows, N, generator=g) * 2 + 0.5).to(dev, dtype)
+    gam = (1 + 0.1 * torch.randn(N, generator=g)).to(dev)
+    bet = (0.1 * torch.randn(N, generator=g)).to(dev)
+    dy = torch.randn(rows, N, generator=g).to(dev, dtype)
+    dres = torch.randn(rows, N, generator=g).to(dev, dtype)
+    _, mean, rstd = ops.layernorm_fwd(x, gam, bet, 1e-5)
+    outs = []
+    for fused in (True, False):
+        dg = torch.zeros(N, device=dev); dbt = torch.zeros(N, device=dev); dbias = torch.full((N,), 0.5, device=dev)
+        gout = torch.empty(rows, N, device=dev, dtype=dtype)
+        if fused:
+            dx = ops.layernorm_bwd(dy, x, gam, mean, rstd, dres=dres, dgamma=dg, dbeta=dbt, g=gout, drop_p=p,
+                                   seed=1234, db=dbias)
+        else:
+            dx = ops.layernorm_bwd(dy, x, gam, mean, rstd, dres=dres, dgamma=dg, dbeta=dbt)
+            ops.ew_bwd(dx, out=gout, drop_p=p, seed=1234, db=dbias)
+        torch.cuda.synchronize()
+        outs.append((dx.clone(), gout.clone(), dg.clone(), dbt.clone(), dbias.clone()))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b) or _rel(a, b) < 1e-6
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+
+
 def _partials(h, chunks=7):
     """(count, mean, M2) per channel per row-chunk, layout [C][tiles][3]."""
     parts = []

@@ -1,11 +1,9 @@
-# full GPU suite + bench + per-kernel step profile. Usage: gpurun -- bash tools/gpu_stepprof.sh TAG
+# rocprof kernel trace of video-on training steps (bench --force-modality none)
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 O=gpurun_out/${1:-sp}; mkdir -p $O
-timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/tests.log 2>&1 || { echo tests failed; tail -30 $O/tests.log; exit 1; }
-tail -1 $O/tests.log
-timeout -k 10 400 python -u bench.py > $O/bench.log 2>&1 || { echo bench failed; exit 1; }
-timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 bench.py --steps 4 --warmup 2 --no-cpu-baseline > $O/prof.log 2>&1 || { echo prof failed; exit 1; }
-timeout -k 10 60 python tools/profsum.py $O/prof/run_kernel_trace.csv 3 45 > $O/steps.txt 2>&1 || { echo profsum failed; exit 1; }
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 bench.py --steps 3 --warmup 2 --quick --no-cpu-baseline --force-modality none > $O/prof.log 2>&1 || { echo prof failed; tail -20 $O/prof.log; exit 1; }
+python tools/profsum.py $O/prof/run_kernel_trace.csv 3 45 > $O/sum.txt
+cat $O/sum.txt
 echo rc=0

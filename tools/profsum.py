@@ -1,6 +1,6 @@
 """Summarise a rocprofv3 kernel trace per training step.
 
-  python tools/profsum.py <run_kernel_trace.csv> [last_steps] [top]
+  python tools/profsum.py <run_kernel_trace.csv> [last_steps] [top] [--grid] [--skip S]
 
 Steps are delimited by the optimizer launches (adamw_kernel closes each step); only the last
 `last_steps` steps are counted so setup work (initial shadow cast, warm-up) is excluded.
@@ -29,6 +29,11 @@ rows = sorted(load_rows(path), key=lambda r: int(r["Start_Timestamp"]))
 ends = [i for i, r in enumerate(rows) if "adamw_kernel" in r["Kernel_Name"]]
 # two adamw launches (decay / no-decay segments) per step
 ends = ends[1::2]
+# --skip S: leave out the last S steps (bench --quick appends 9 per-variant steps: none x3,
+# audio_off x3, video_off x3; the forced timed steps are the 3 before them)
+skip = int(sys.argv[sys.argv.index("--skip") + 1]) if "--skip" in sys.argv else 0
+if skip:
+    ends = ends[:-skip]
 if len(ends) > last:
     rows = rows[ends[-last - 1] + 1: ends[-1] + 1]
     steps = last
