@@ -640,7 +640,10 @@ class Engine:
         else:
             ops.linear_fwd(ain, self.w(EN + "feature_extractor_audio.proj.weight"),
                            self.arena.master(EN + "feature_extractor_audio.proj.bias"), out=fcat[:, :D])
-        feat, vctx = self.video_fwd(videos, train, save)
+        # video_off: the ResNet gradient is exactly zero (avhubert.py:480), so nothing of its
+        # forward is kept for a backward (no packed stem input, no pooled-grid argmax values);
+        # the forward itself still runs for the BatchNorm running statistics, as in the reference
+        feat, vctx = self.video_fwd(videos, train, save and modality != "video_off")
         if modality == "video_off":
             fcat[:, D:].zero_()
         else:
