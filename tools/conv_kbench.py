@@ -89,6 +89,19 @@ dw2 = torch.zeros(128, 3, 3, 128, device=dev)
 for flag in ("0", "1"):
     os.environ["AVSR_CONV_WPATCH"] = flag
     res[f"s2_wgrad_wpatch{flag}"] = timed(lambda: ops.conv_bwd_weight(geom2, x2, dy2, dw2))
+# stage-2 forward / data-grad (general implicit-GEMM kernels), for the fwd vs dgrad gap
+w2 = (torch.randn(128, 3, 3, 128, generator=g) * 0.03).to(dev, bf)
+y2 = torch.empty(M2, 128, device=dev, dtype=bf)
+dx2 = torch.zeros(M2, 128, device=dev, dtype=bf)
+hh2 = torch.randn(M2, 128, generator=g).to(dev, bf)
+st2 = ops.BnState(128, dev)
+st2.mean.zero_(); st2.invstd.fill_(1.0); st2.scale.fill_(1.0); st2.shift.zero_()
+a2 = torch.full((128,), 0.25, device=dev)
+p2 = torch.empty(128, ops.conv_stat_tiles(geom2, ops.dtype_code(x2)), 3, device=dev)
+res["s2_fwd"] = timed(lambda: ops.conv_fwd(geom2, x2, w2, y2, p2))
+res["s2_dgrad"] = timed(lambda: ops.conv_bwd_data(geom2, dy2, w2, dx2))
+res["s2_dgrad_bnr"] = timed(lambda: ops.conv_bwd_data_bnr(geom2, dy2, w2, dx2, hh2, st2, a2, beta=0.0))
+res["s2_gflop"] = round(2.0 * M2 * 128 * 1152 / 1e9, 1)
 fl = 2.0 * M * 64 * 576
 res["s1_gflop"] = round(fl / 1e9, 1)
 res["stem_gflop_direct_k288"] = round(2.0 * N * 1936 * 64 * 288 / 1e9, 1)
