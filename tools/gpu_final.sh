@@ -10,5 +10,5 @@ tail -1 $O/smoke.log
 timeout -k 10 600 python -u bench.py > $O/bench.log 2>&1 || { echo bench failed; tail -20 $O/bench.log; exit 1; }
 tail -1 $O/bench.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['ms_per_step'], d['roofline']['frac'], d['cpu_baseline'], d['modality_drops']['video_off'])"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 bench.py --steps 4 --warmup 2 --no-cpu-baseline > $O/prof.log 2>&1 || { echo prof failed; exit 1; }
-timeout -k 10 60 python tools/profsum.py $O/prof/run_kernel_trace.csv 3 45 > $O/steps.txt 2>&1 || { echo profsum failed; exit 1; }
+timeout -k 10 60 python tools/profsum.py $O/prof/run_kernel_trace.csv 3 60 --skip 9 > $O/steps.txt 2>&1 || { echo profsum failed; exit 1; }
 echo rc=0
