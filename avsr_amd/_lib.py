@@ -289,6 +289,8 @@ SYMBOLS = {
     "avsr_time_mask": ([ctypes.POINTER(TimeMaskParams), _c_p], _i),
     "avsr_add_noise": ([ctypes.POINTER(AddNoiseParams), _c_p], _i),
     "avsr_rgb_to_gray": ([_c_p, _c_p, _i64, _c_p], _i),
+    "avsr_stream_create_cumask": ([_c_p, _i, ctypes.POINTER(_c_p)], _i),
+    "avsr_stream_destroy": ([_c_p], _i),
 }
 
 _lib = None

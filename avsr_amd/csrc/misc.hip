@@ -4,6 +4,7 @@
 // packing, pos-conv weight norm, and the fused clip-grad-norm + AdamW step.
 // All HBM-bound: 16-byte vectors where the layout allows, grid-stride loops.
 #include "common.h"
+#include <hip/hip_ext.h>
 #include <vector>
 
 namespace {
@@ -674,4 +675,17 @@ extern "C" int avsr_adamw(const avsr_adamw_params* p, void* stream) {
   else hipLaunchKernelGGL(adamw_kernel<bf16>, dim3(g), dim3(256), 0, (hipStream_t)stream, *p, head, nv);
   AVSR_CHECK_LAUNCH();
   return 0;
+}
+
+extern "C" int avsr_stream_create_cumask(const uint32_t* mask, int nwords, void** stream) {
+  if (!mask || nwords <= 0 || !stream) return AVSR_E_ARG;
+  hipStream_t s = nullptr;
+  const hipError_t e = hipExtStreamCreateWithCUMask(&s, (uint32_t)nwords, mask);
+  if (e != hipSuccess) return (int)e;
+  *stream = (void*)s;
+  return 0;
+}
+
+extern "C" int avsr_stream_destroy(void* stream) {
+  return (int)hipStreamDestroy((hipStream_t)stream);
 }

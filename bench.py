@@ -372,7 +372,12 @@ def gpu_bench(args):
     # statistics broadcast, bucketed RCCL all-reduce overlapped with the backward; the 1/world
     # average is folded into the AdamW kernel (average=False, grad_scale below)
     ddp = parallel.ArenaDDP(model, average=False)
-    opt = FusedAdamW(arena, lr=1e-4, weight_decay=0.005, max_grad_norm=1.0)
+    # the AdamW update of the later layers overlaps the next step's frontend forward (each forward
+    # stage waits only for the chunk of the update it reads; optim.ParamGate) with --opt-overlap; off by
+    # default: no wall-clock gain on MI355X
+    overlap = args.opt_overlap
+    opt = FusedAdamW(arena, lr=1e-4, weight_decay=0.005, max_grad_norm=1.0, overlap=overlap,
+                     stage_bounds=eng.param_stage_bounds())
 
     B, T, L = args.batch, args.seq, args.labels
     v, a, lens, lab = synthetic_batch(B, T, L, seed=args.seed + rank)
@@ -410,12 +415,13 @@ def gpu_bench(args):
     def step(variant=False):
         if forced_all is not None and not variant:
             eng.force_modality = forced_all
-        arena.zero_grad()
+        if not overlap:
+            arena.zero_grad()                   # overlapped: cleared behind the previous update
         step_seed[0] += 1
         out4, ctx = eng.forward(v, a, lens, lab, train=True, need_grad=True, seed=step_seed[0])
         drops.append(eng.last_modality)
         eng.backward(ctx, d_ctc, d_att)
-        opt.step(grad_scale=1.0 / world)
+        opt.step(grad_scale=1.0 / world, zero_grad=overlap)
         return out4
 
     for _ in range(args.warmup):
@@ -490,6 +496,7 @@ def gpu_bench(args):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             step(variant=True)
+            opt.sync()                          # an overlapped update belongs to the step
             e1.record()
             torch.cuda.synchronize()
             per.append(e0.elapsed_time(e1))
@@ -517,7 +524,9 @@ def gpu_bench(args):
         "config": {"workload": f"C2/C3: AVHubertAVSR fwd+bwd+AdamW, {B}x{T / 25:.0f}s clips per GPU "
                                f"(T={T}, L={L}), train mode, dropouts on",
                    "global_batch": B * world, "seq_len": T, "parallelism": f"dp{world}",
-                   "encoder_layers": cfg.num_hidden_layers},
+                   "encoder_layers": cfg.num_hidden_layers,
+                   "optimizer": "fused clip+AdamW, " + ("update overlapped with the next forward (per-stage readiness "
+                                                        "events, optim.ParamGate)" if overlap else "serial")},
         "roofline": {"bound": "mfma", "kernel": f"dense_glds_kernel bf16 (encoder FFN1 fwd {M}x{N_}x{K_})",
                      "achieved": round(achieved, 1), "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": round(achieved / BF16_PEAK_TFLOPS, 4), "traffic": traffic,
@@ -580,6 +589,8 @@ def main():
     ap.add_argument("--seq", type=int, default=375, help="AV-frames per clip (15 s at 25 fps)")
     ap.add_argument("--labels", type=int, default=40)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--opt-overlap", action="store_true",
+                    help="run the AdamW update beside the next step's forward (measured: no wall-clock gain, DESIGN §9)")
     ap.add_argument("--no-decode", action="store_true", help="skip the C1/C4/C5 decode throughput section")
     ap.add_argument("--quick", action="store_true", help="only the step measurement (profiling runs)")
     ap.add_argument("--layers", type=int, default=None, help="debug only: fewer encoder layers (INVALID for the metric)")

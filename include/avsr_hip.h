@@ -608,6 +608,16 @@ int avsr_add_noise(const avsr_add_noise_params* p, void* stream);
 
 int avsr_rgb_to_gray(const uint8_t* rgb, uint8_t* gray, int64_t n, void* stream);
 
+/* ------------------------------------------------------------------------------------
+ * Runtime helper (no reference counterpart: the reference has one CUDA stream).
+ * avsr_stream_create_cumask: a HIP stream whose kernels may only occupy the CUs whose bits
+ *   are set in mask[0..nwords) (hipExtStreamCreateWithCUMask); used for the weight-gradient
+ *   side stream so that the data-gradient chain always finds free CUs. *stream receives the
+ *   hipStream_t; avsr_stream_destroy releases it. Both return 0 or the hipError_t.
+ * ------------------------------------------------------------------------------------ */
+int avsr_stream_create_cumask(const uint32_t* mask, int nwords, void** stream);
+int avsr_stream_destroy(void* stream);
+
 #ifdef __cplusplus
 }
 #endif

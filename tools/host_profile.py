@@ -38,6 +38,17 @@ def step(i):
 for i in range(3):
     step(i)
 torch.cuda.synchronize()
+# enqueue time of one step with the GPU idle at its start (no profiler) vs its completion
+import time  # noqa: E402
+for i in range(6):
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    step(20 + i)
+    t1 = time.perf_counter()
+    torch.cuda.synchronize()
+    t2 = time.perf_counter()
+    print(f"step {i} ({eng.last_modality}): host enqueue {1e3 * (t1 - t0):.1f} ms, GPU done at {1e3 * (t2 - t0):.1f} ms",
+          flush=True)
 pr = cProfile.Profile()
 pr.enable()
 for i in range(4):
