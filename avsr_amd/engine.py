@@ -42,6 +42,9 @@ _COLSUM_DEFER = os.environ.get("AVSR_COLSUM_DEFER", "1") == "1"
 _SIDE_BIAS = os.environ.get("AVSR_SIDE_BIAS", "1") == "1"
 # the CTC branch of the forward runs on the side stream beside the decoder forward
 _CTC_SIDE = os.environ.get("AVSR_CTC_SIDE", "1") == "1"
+# weight-gradient handoffs of one transformer layer's backward batched into ONE event record +
+# wait (every record/wait pair cost the step stream a stall; AVSR_SIDE_BATCH=0: one per handoff)
+_SIDE_BATCH = os.environ.get("AVSR_SIDE_BATCH", "1") == "1"
 # bf16 stem conv straight from the video (stem.hip) instead of pack + general implicit GEMM
 _STEM_DIRECT = os.environ.get("AVSR_STEM_DIRECT", "1") == "1"
 # encoder residual-branch dropout backward (+ bias gradient) fused into the LayerNorm backward
@@ -183,6 +186,7 @@ class Engine:
         # operands the side stream reads stay referenced until join_side() (instead of
         # record_stream, whose deferred frees keep the caching allocator growing for steps)
         self._side_keep = [] if os.environ.get("AVSR_SIDE_KEEP", "1") == "1" else None
+        self._side_defer = None      # list while a layer's handoffs are batched (_side_layer)
         E = "encoder.encoder.layers"
         groups = []
         for i in range(self.nl):
@@ -329,6 +333,9 @@ class Engine:
         side = self.side
         if side is None:
             return fn()
+        if self._side_defer is not None:        # batched: issued by _flush_side after one wait
+            self._side_defer.append((fn, keep))
+            return None
         # order the side stream after the work queued so far on the current stream: one raw
         # event record + wait (torch's wait_stream builds Stream / Event objects per call)
         if self._side_ev:
@@ -347,8 +354,37 @@ class Engine:
                 t.record_stream(side)
         return r
 
+    def _side_layer(self, on):
+        """start (on) / end a batch of side-stream handoffs: the layer's weight-gradient work is
+        queued and issued at the end of its data-gradient chain behind ONE event wait, so the
+        step stream records one event per layer instead of one per weight-gradient (the side
+        stream then trails by at most one layer; its operands are never overwritten)"""
+        if self.side is None or not _SIDE_BATCH:
+            return
+        if on:
+            self._flush_side()
+            self._side_defer = []
+        else:
+            self._flush_side()
+            self._side_defer = None
+
+    def _flush_side(self):
+        q = self._side_defer
+        if not q:
+            return
+        self._side_defer = None
+        keep = [t for _, k in q for t in k]
+
+        def run_all():
+            for fn, _ in q:
+                fn()
+        self._on_side(run_all, *keep)
+        self._side_defer = []
+
     def join_side(self):
         """make the current stream wait for every weight gradient issued so far"""
+        self._flush_side()
+        self._side_defer = None
         if self.side is not None:
             torch.cuda.current_stream(self.device).wait_stream(self.side)
             if self._side_keep:
@@ -837,8 +873,10 @@ class Engine:
         dx = self._ln_bwd(dout, ctx["x_last"], E + "layer_norm", ctx["mf"], ctx["rf"], ew=ew)
         g2 = ew[0] if ew is not None else None
         for i in reversed(range(self.nl)):
+            self._side_layer(True)
             dx, g2 = self._enc_layer_bwd(i, layers[i], dx, B, T, ctx["klen"], g2=g2,
                                          lc_prev=layers[i - 1] if i > 0 else None)
+            self._side_layer(False)
             ops.colsum_flush()                      # this layer's bias / LayerNorm gradients
             if self.on_grad_ready is not None:      # layers >= i (and everything after them) final
                 self.on_grad_ready(self._layer_decay_off[i])   # (the reducer also waits for the side stream)
@@ -953,6 +991,7 @@ class Engine:
         dy = ops.layernorm_bwd(dyn, ctx["y_last"], self.arena.master("decoder.after_norm.weight"), ctx["mf"], ctx["rf"],
                                dgamma=self.g("decoder.after_norm.weight"), dbeta=self.g("decoder.after_norm.bias"))
         for i in reversed(range(self.dl)):
+            self._side_layer(True)              # flushes the previous layer's batch first
             lc = ctx["layers"][i]
             p = f"decoder.decoders.{i}."
             sa, ca, ff = p + "self_attn.", p + "src_attn.", p + "feed_forward."
@@ -1011,6 +1050,7 @@ class Engine:
             dn1 = ops.linear_dgrad(dqkv, self.arena.span(nw))
             dy = ops.layernorm_bwd(dn1, lc["y"], self.arena.master(p + "norm1.weight"), lc["m1"], lc["r1"], dx=dy, dres=dy,
                                    dgamma=self.g(p + "norm1.weight"), dbeta=self.g(p + "norm1.bias"))
+        self._side_layer(False)
         ops.embed_bwd(bt["ys_in"], dy, math.sqrt(D), self.g("decoder.embed.0.weight"), L1, drop_p=p_d, seed=ctx["sd_e"])
 
     # ======================================================================== full model
