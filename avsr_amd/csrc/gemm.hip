@@ -4,6 +4,7 @@
 #include "gemm_core.h"
 #include "gemm_glds.h"
 #include "gemm_pp.h"
+#include <algorithm>
 #include <cstring>
 
 using namespace gemmcore;
@@ -297,8 +298,11 @@ template <typename T> AVSR_DEV f32x4 ld4f(const T* p) {
   }
 }
 
+// K split (part != nullptr): block row blockIdx.y sums k in [y * kchunk, (y + 1) * kchunk) and
+// writes the raw sums to part[y][m][n]; skinny_reduce_kernel adds the S partials in a fixed
+// order and runs the epilogue (N / 16 workgroups alone leave most CUs idle at N = 1024)
 template <typename T, typename OutT, int MR>
-__global__ __launch_bounds__(256) void skinny_kernel(DenseArgs a) {
+__global__ __launch_bounds__(256) void skinny_kernel(DenseArgs a, float* part, int kchunk) {
   constexpr int SK_KC = MR <= 32 ? 256 : 128;        // K chunk staged per pass (<= 33 KiB of LDS)
   constexpr int XPT = MR * SK_KC / 4 / 256;           // A vectors per thread per chunk
   constexpr int WJ = SK_KC / 128;                     // k groups per thread per chunk
@@ -314,23 +318,25 @@ __global__ __launch_bounds__(256) void skinny_kernel(DenseArgs a) {
   float acc0[MR], acc1[MR];
 #pragma unroll
   for (int m = 0; m < MR; ++m) acc0[m] = acc1[m] = 0.f;
+  const int kbeg = part ? blockIdx.y * kchunk : 0;
+  const int kend = part ? min(a.K, kbeg + kchunk) : a.K;
   // the next chunk's A rows and weights are loaded into registers while this chunk computes
   f32x4 xr[XPT], w0[WJ], w1[WJ];
   auto load = [&](int k0) {
 #pragma unroll
     for (int i = 0; i < XPT; ++i) {
       const int idx = tid + 256 * i, m = idx / (SK_KC / 4), q = idx - m * (SK_KC / 4), k = k0 + 4 * q;
-      xr[i] = (m < a.M && k < a.K) ? ld4f(A + (int64_t)m * a.lda + k) : f32x4{0.f, 0.f, 0.f, 0.f};
+      xr[i] = (m < a.M && k < kend) ? ld4f(A + (int64_t)m * a.lda + k) : f32x4{0.f, 0.f, 0.f, 0.f};
     }
 #pragma unroll
     for (int j = 0; j < WJ; ++j) {
       const int k = k0 + 4 * (kl + 32 * j);
-      w0[j] = (ok0 && k < a.K) ? ld4f(B0 + k) : f32x4{0.f, 0.f, 0.f, 0.f};
-      w1[j] = (ok1 && k < a.K) ? ld4f(B1 + k) : f32x4{0.f, 0.f, 0.f, 0.f};
+      w0[j] = (ok0 && k < kend) ? ld4f(B0 + k) : f32x4{0.f, 0.f, 0.f, 0.f};
+      w1[j] = (ok1 && k < kend) ? ld4f(B1 + k) : f32x4{0.f, 0.f, 0.f, 0.f};
     }
   };
-  load(0);
-  for (int k0 = 0; k0 < a.K; k0 += SK_KC) {
+  load(kbeg);
+  for (int k0 = kbeg; k0 < kend; k0 += SK_KC) {
     __syncthreads();                                // the previous chunk's reads of xs are done
 #pragma unroll
     for (int i = 0; i < XPT; ++i) {
@@ -341,7 +347,7 @@ __global__ __launch_bounds__(256) void skinny_kernel(DenseArgs a) {
 #pragma unroll
     for (int j = 0; j < WJ; ++j) { wc0[j] = w0[j]; wc1[j] = w1[j]; }
     __syncthreads();
-    if (k0 + SK_KC < a.K) load(k0 + SK_KC);
+    if (k0 + SK_KC < kend) load(k0 + SK_KC);
 #pragma unroll
     for (int j = 0; j < WJ; ++j) {
       const int g = kl + 32 * j;
@@ -374,22 +380,58 @@ __global__ __launch_bounds__(256) void skinny_kernel(DenseArgs a) {
     const int m = o / SK_NB, c = o - m * SK_NB, col = n0 + c;
     if (m < a.M && col < a.N) {
       const float v = (red[0][m][c] + red[1][m][c]) + (red[2][m][c] + red[3][m][c]);
-      epi_elems<T, OutT, 1>(a.e, m, col, &v);
+      if (part) part[((int64_t)blockIdx.y * a.M + m) * a.N + col] = v;
+      else epi_elems<T, OutT, 1>(a.e, m, col, &v);
     }
   }
 }
 
 template <typename T, typename OutT>
-int skinny_launch(const DenseArgs& a, hipStream_t st) {
-  const dim3 g((unsigned)((a.N + SK_NB - 1) / SK_NB));
-  if (a.M <= 8) hipLaunchKernelGGL((skinny_kernel<T, OutT, 8>), g, dim3(256), 0, st, a);
-  else if (a.M <= 16) hipLaunchKernelGGL((skinny_kernel<T, OutT, 16>), g, dim3(256), 0, st, a);
-  else if (a.M <= 24) hipLaunchKernelGGL((skinny_kernel<T, OutT, 24>), g, dim3(256), 0, st, a);
-  else if (a.M <= 32) hipLaunchKernelGGL((skinny_kernel<T, OutT, 32>), g, dim3(256), 0, st, a);
-  else if (a.M <= 40) hipLaunchKernelGGL((skinny_kernel<T, OutT, 40>), g, dim3(256), 0, st, a);
-  else if (a.M <= 48) hipLaunchKernelGGL((skinny_kernel<T, OutT, 48>), g, dim3(256), 0, st, a);
-  else hipLaunchKernelGGL((skinny_kernel<T, OutT, 64>), g, dim3(256), 0, st, a);
+__global__ __launch_bounds__(256) void skinny_reduce_kernel(DenseArgs a, const float* part, int S) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x, MN = (int64_t)a.M * a.N;
+  if (i >= MN) return;
+  float v = part[i];
+  for (int s = 1; s < S; ++s) v += part[s * MN + i];
+  const int m = (int)(i / a.N), col = (int)(i - (int64_t)m * a.N);
+  epi_elems<T, OutT, 1>(a.e, m, col, &v);
+}
+
+// K split count: enough block rows for >= 512 workgroups, chunks of >= 256 k, and S * 64 * N
+// partials within AVSR_SKINNY_WS (S depends on N and K only, never on M: a row's result does
+// not depend on how many rows share the launch). AVSR_SKINNY_NOSPLIT=1: one block row.
+int skinny_splits(int N, int K, int& kchunk) {
+  static int off = -1;
+  if (off < 0) { const char* e = getenv("AVSR_SKINNY_NOSPLIT"); off = (e && e[0] == '1') ? 1 : 0; }
+  const int nb = (N + SK_NB - 1) / SK_NB;
+  int S = off ? 1 : (512 + nb - 1) / nb;
+  S = std::min(S, std::max(1, K / 256));
+  S = std::min(S, (int)std::max<int64_t>(1, AVSR_SKINNY_WS / (64 * (int64_t)N)));
+  kchunk = ((K + S - 1) / S + 255) / 256 * 256;
+  return (K + kchunk - 1) / kchunk;
+}
+
+template <typename T, typename OutT>
+int skinny_launch(const DenseArgs& a, float* ws, hipStream_t st) {
+  int kchunk = a.K;
+  const int S = ws ? skinny_splits(a.N, a.K, kchunk) : 1;
+  float* part = S > 1 ? ws : nullptr;
+  const dim3 g((unsigned)((a.N + SK_NB - 1) / SK_NB), (unsigned)S);
+#define SKL(R) hipLaunchKernelGGL((skinny_kernel<T, OutT, R>), g, dim3(256), 0, st, a, part, kchunk)
+  if (a.M <= 8) SKL(8);
+  else if (a.M <= 16) SKL(16);
+  else if (a.M <= 24) SKL(24);
+  else if (a.M <= 32) SKL(32);
+  else if (a.M <= 40) SKL(40);
+  else if (a.M <= 48) SKL(48);
+  else SKL(64);
+#undef SKL
   AVSR_CHECK_LAUNCH();
+  if (part) {
+    const int64_t MN = (int64_t)a.M * a.N;
+    hipLaunchKernelGGL((skinny_reduce_kernel<T, OutT>), dim3((unsigned)((MN + 255) / 256)), dim3(256), 0, st, a,
+                       (const float*)part, S);
+    AVSR_CHECK_LAUNCH();
+  }
   return 0;
 }
 
@@ -478,8 +520,9 @@ extern "C" int avsr_gemm(const avsr_gemm_params* p, void* stream) {
   if (p->K == 0) return AVSR_E_SHAPE;
   int rc;
   if (!glds && !slab && skinny_ok(p, splits)) {
-    if (p->dtype == AVSR_F32) return skinny_launch<float, float>(a, st);
-    return p->c_f32 ? skinny_launch<bf16, float>(a, st) : skinny_launch<bf16, bf16>(a, st);
+    float* sws = p->ws;                 // splitk == 1 here: ws, if given, holds the K-split partials
+    if (p->dtype == AVSR_F32) return skinny_launch<float, float>(a, sws, st);
+    return p->c_f32 ? skinny_launch<bf16, float>(a, sws, st) : skinny_launch<bf16, bf16>(a, sws, st);
   }
   if (glds) rc = p->c_f32 ? glds_by_layout<float>(p, a, st) : glds_by_layout<bf16>(p, a, st);
   else if (p->dtype == AVSR_F32) rc = by_tile<float, float>(p, a, st);

@@ -37,6 +37,21 @@ def _ptr(t):
     return None if t is None else ctypes.c_void_p(t.data_ptr())
 
 
+_SKINNY_WS = {}
+_SKINNY_SPLIT = os.environ.get("AVSR_SKINNY_SPLIT", "0") == "1"
+SKINNY_WS = 1 << 19        # AVSR_SKINNY_WS
+
+
+def _skinny_ws(device):
+    """per (device, stream) partial-sum workspace of the few-row GEMM path: launches on one
+    stream run in order, so one buffer per stream is never read and written at once"""
+    key = (device, L.stream_ptr().value)
+    ws = _SKINNY_WS.get(key)
+    if ws is None:
+        ws = _SKINNY_WS[key] = torch.empty(SKINNY_WS, device=device, dtype=torch.float32)
+    return ws
+
+
 def gemm(A, B, C, *, M, N, K, a_kmajor, b_kmajor, lda, ldb, ldc, batch=1,
          strideA=0, strideB=0, strideC=0, alpha=1.0, beta=0.0, bias=None, act=L.ACT_NONE,
          epi_bwd=False, preact=None, res=None, ldr=None, strideR=0, gate=None, drop_p=0.0, seed=0,
@@ -73,6 +88,8 @@ def gemm(A, B, C, *, M, N, K, a_kmajor, b_kmajor, lda, ldb, ldc, batch=1,
     if ws is not None:
         assert ws.dtype == torch.float32 and ws.numel() >= slab_ws(batch, splitk, M, N)
         p.ws = ws.data_ptr()
+    elif _SKINNY_SPLIT and M <= 64 and splitk == 1 and batch == 1 and a_kmajor and b_kmajor and not epi_bwd and db is None:
+        p.ws = _skinny_ws(A.device).data_ptr()      # K-split partials of the few-row vector-ALU path
     if db is not None:
         assert db.dtype == torch.float32 and db.numel() >= N and db_ws is not None and db_ws.dtype == torch.float32
         assert db_ws.numel() >= ((M + 63) // 64) * N

@@ -74,7 +74,10 @@ typedef struct {
   float* ws;                 /* split-K slab workspace, AVSR_GEMM_SLAB_WS(batch, splitk, M, N) fp32:
                                 each split stores its partial tile, a reduce pass writes
                                 C = alpha*sum + beta*C (plain epilogue only). NULL: C += alpha*acc
-                                by fp32 atomics */
+                                by fp32 atomics. With splitk == 1 and M <= 64 (the vector-ALU
+                                path for decoder steps) a ws of >= AVSR_SKINNY_WS floats lets
+                                the launch split K over more workgroups (fp32 partials, ordered
+                                reduce + epilogue); NULL: one workgroup row */
   float* db;                 /* optional: db[n] += sum_m C[m][n] of the stored tile values (the
                                 bias gradient of the layer whose output gradient C is, e.g.
                                 FFN1's bias from the FFN2 data-grad); bf16, N % 8 == 0, no split */
@@ -89,6 +92,7 @@ typedef struct {
  * reduce pass's split-many reads of one vector on the same HBM channels (measured 0.55 TB/s for
  * 8 slabs of 4 MiB) */
 #define AVSR_GEMM_SLAB_PAD 1088
+#define AVSR_SKINNY_WS (1 << 19)
 #define AVSR_GEMM_SLAB_WS(batch, splitk, M, N) ((int64_t)(batch) * (splitk) * ((int64_t)(M) * (N) + AVSR_GEMM_SLAB_PAD))
 
 int avsr_gemm(const avsr_gemm_params* p, void* stream);

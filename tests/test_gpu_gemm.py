@@ -219,3 +219,18 @@ def test_skinny_linear(dev, dtype, M, N, K):
     assert _rel(y, ref) < tol
     y2 = ops.linear_fwd(x, W, b, act=L.ACT_RELU, res=r)
     assert torch.equal(y, y2)
+
+
+@pytest.mark.parametrize("N,K", [(1024, 4096), (1024, 1024), (4096, 1024), (5056, 1024)])
+def test_skinny_k_split_rows_independent(dev, N, K):
+    """The few-row path splits K over more workgroups (partials reduced in a fixed order) with a
+    split count that depends on N and K only: every row equals the same row launched alone, bit
+    for bit (batched beam search == per-utterance search relies on it), and matches fp64."""
+    g = torch.Generator(device="cpu").manual_seed(N + K)
+    x = torch.randn(40, K, generator=g).to(dev)
+    W = (torch.randn(N, K, generator=g) * K ** -0.5).to(dev)
+    b = torch.randn(N, generator=g).to(dev)
+    y = ops.linear_fwd(x, W, b)
+    for m in (0, 7, 39):
+        assert torch.equal(ops.linear_fwd(x[m:m + 1].contiguous(), W, b)[0], y[m]), m
+    assert _rel(y, x.double() @ W.double().t() + b.double()) < 1e-6
