@@ -41,6 +41,7 @@ class GemmParams(ctypes.Structure):
         ("db", _c_p),
         ("db_ws", _c_p),
         ("stamp", _c_p),
+        ("skinny_ws", _c_p),
     ]
 
 
@@ -230,6 +231,7 @@ class VideoNormParams(ctypes.Structure):
 SYMBOLS = {
     "avsr_version": ([], ctypes.c_char_p),
     "avsr_gemm": ([ctypes.POINTER(GemmParams), _c_p], _i),
+    "avsr_gemm_skinny_splits": ([_i, _i], _i),
     "avsr_conv_fwd": ([ctypes.POINTER(ConvParams), _c_p], _i),
     "avsr_conv_bwd_data": ([ctypes.POINTER(ConvParams), _c_p], _i),
     "avsr_conv_bwd_weight": ([ctypes.POINTER(ConvParams), _c_p], _i),
@@ -289,8 +291,6 @@ SYMBOLS = {
     "avsr_time_mask": ([ctypes.POINTER(TimeMaskParams), _c_p], _i),
     "avsr_add_noise": ([ctypes.POINTER(AddNoiseParams), _c_p], _i),
     "avsr_rgb_to_gray": ([_c_p, _c_p, _i64, _c_p], _i),
-    "avsr_stream_create_cumask": ([_c_p, _i, ctypes.POINTER(_c_p)], _i),
-    "avsr_stream_destroy": ([_c_p], _i),
 }
 
 _lib = None

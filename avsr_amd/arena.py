@@ -100,9 +100,6 @@ class Arena:
         # (the frozen ones — mask_emb, label_embs_concat — get no gradient, as in the reference)
         self.params = {}
         self._frozen = frozen
-        # optim.ParamGate of an overlapped optimizer step (FusedAdamW(overlap=True)): readers of
-        # the parameters / writers of the gradients wait on its events; None when not overlapped
-        self.gate = None
         for n in self.order:
             m = self.meta[n]
             old = params[n]
@@ -210,8 +207,6 @@ class Arena:
         if not missing:
             return
         if zero:
-            if self.gate is not None:
-                self.gate.wait_all()
             if len(missing) == len(self.grad_views):
                 self.grad.zero_()
             else:
@@ -222,8 +217,6 @@ class Arena:
             self.params[n].grad = self.grad_views[n]
 
     def zero_grad(self):
-        if self.gate is not None:              # an overlapped optimizer step may still read them
-            self.gate.wait_all()
         self.grad.zero_()
         self.attach_grads(zero=False)
 

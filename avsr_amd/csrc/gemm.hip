@@ -398,12 +398,10 @@ __global__ __launch_bounds__(256) void skinny_reduce_kernel(DenseArgs a, const f
 
 // K split count: enough block rows for >= 512 workgroups, chunks of >= 256 k, and S * 64 * N
 // partials within AVSR_SKINNY_WS (S depends on N and K only, never on M: a row's result does
-// not depend on how many rows share the launch). AVSR_SKINNY_NOSPLIT=1: one block row.
+// not depend on how many rows share the launch).
 int skinny_splits(int N, int K, int& kchunk) {
-  static int off = -1;
-  if (off < 0) { const char* e = getenv("AVSR_SKINNY_NOSPLIT"); off = (e && e[0] == '1') ? 1 : 0; }
   const int nb = (N + SK_NB - 1) / SK_NB;
-  int S = off ? 1 : (512 + nb - 1) / nb;
+  int S = (512 + nb - 1) / nb;
   S = std::min(S, std::max(1, K / 256));
   S = std::min(S, (int)std::max<int64_t>(1, AVSR_SKINNY_WS / (64 * (int64_t)N)));
   kchunk = ((K + S - 1) / S + 255) / 256 * 256;
@@ -520,7 +518,7 @@ extern "C" int avsr_gemm(const avsr_gemm_params* p, void* stream) {
   if (p->K == 0) return AVSR_E_SHAPE;
   int rc;
   if (!glds && !slab && skinny_ok(p, splits)) {
-    float* sws = p->ws;                 // splitk == 1 here: ws, if given, holds the K-split partials
+    float* sws = p->skinny_ws;          // optional K-split partials (AVSR_SKINNY_WS floats)
     if (p->dtype == AVSR_F32) return skinny_launch<float, float>(a, sws, st);
     return p->c_f32 ? skinny_launch<bf16, float>(a, sws, st) : skinny_launch<bf16, bf16>(a, sws, st);
   }
@@ -542,4 +540,10 @@ extern "C" int avsr_gemm(const avsr_gemm_params* p, void* stream) {
                      (int64_t)p->M * p->N + AVSR_GEMM_SLAB_PAD, (float*)p->C, p->ldc, p->strideC, p->alpha, p->beta);
   AVSR_CHECK_LAUNCH();
   return 0;
+}
+
+extern "C" int avsr_gemm_skinny_splits(int N, int K) {
+  if (N <= 0 || K <= 0) return 1;
+  int kchunk;
+  return skinny_splits(N, K, kchunk);
 }

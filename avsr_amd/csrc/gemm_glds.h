@@ -111,13 +111,13 @@ AVSR_DEV __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
 // disambiguate from the pending DMA), which drained the prefetch of the NEXT K-tile before the
 // current one was computed in every kernel with a transposed operand (data-grads,
 // weight-grads). Callers order the DMAs against their LDS reads with explicit vmcnt waits and
-// barriers (mainloop_glds, the conv patch kernels). M0 is set here; no kernel of this library
-// keeps a compiler value live in M0 (the LDS-DMA builtins set it right before each use).
+// barriers (mainloop_glds, the conv patch kernels). M0 is written here and listed as clobbered,
+// so the compiler re-materialises any value it keeps in M0 (LDS-DMA builtins, readlane, DS ops).
 AVSR_DEV void bglds16(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff, char* lds_wave_base) {
   const uint32_t m = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_void_t*)lds_wave_base);
   asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds" ::"s"(m), "v"(voff), "s"(r),
                "s"(soff)
-               : "memory");
+               : "memory", "m0");
 }
 
 // k-major: elem(r, k) = base[r*ld + k]

@@ -182,6 +182,17 @@ __global__ __launch_bounds__(256) void cast_flat_f32_bf16_kernel(int64_t n8, con
   }
 }
 
+// bf16 -> fp32 over 8-element vectors (the compressed gradient all-reduce's decompress,
+// parallel.GradReducer(compress="bf16"))
+__global__ __launch_bounds__(256) void cast_flat_bf16_f32_kernel(int64_t n8, const bf16x8* __restrict__ src,
+                                                                 float4* __restrict__ dst) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n8; i += (int64_t)gridDim.x * 256) {
+    const bf16x8 v = src[i];
+    dst[2 * i] = float4{(float)v[0], (float)v[1], (float)v[2], (float)v[3]};
+    dst[2 * i + 1] = float4{(float)v[4], (float)v[5], (float)v[6], (float)v[7]};
+  }
+}
+
 // grid (clip x chunk of PACK_TC frames, pixel blocks): a thread walks one pixel through a
 // chunk of output frames, loading each of the chunk's PACK_TC + 4 source frames once (all
 // loads issued first) instead of 5 loads per output (the source video is read ~1.25x, not 5x)
@@ -561,6 +572,14 @@ extern "C" int avsr_cast_flat(int sd, int dd, int64_t n, const void* src, void* 
     AVSR_CHECK_LAUNCH();
     return 0;
   }
+  if (sd == AVSR_BF16 && dd == AVSR_F32 && n % 8 == 0 && ((uintptr_t)src & 15) == 0 && ((uintptr_t)dst & 15) == 0) {
+    const int64_t n8 = n / 8;
+    int64_t g = (n8 + 255) / 256;
+    g = g > 256 * 32 ? 256 * 32 : g;
+    hipLaunchKernelGGL(cast_flat_bf16_f32_kernel, dim3((unsigned)g), dim3(256), 0, st, n8, (const bf16x8*)src, (float4*)dst);
+    AVSR_CHECK_LAUNCH();
+    return 0;
+  }
   // general case: a [rows][4096] view of the flat buffer plus a tail row
   const int64_t cols = 4096, rows = n / cols, tail = n - rows * cols;
   const size_t es = sd == AVSR_F32 ? 4 : 2, ed = dd == AVSR_F32 ? 4 : 2;
@@ -677,15 +696,3 @@ extern "C" int avsr_adamw(const avsr_adamw_params* p, void* stream) {
   return 0;
 }
 
-extern "C" int avsr_stream_create_cumask(const uint32_t* mask, int nwords, void** stream) {
-  if (!mask || nwords <= 0 || !stream) return AVSR_E_ARG;
-  hipStream_t s = nullptr;
-  const hipError_t e = hipExtStreamCreateWithCUMask(&s, (uint32_t)nwords, mask);
-  if (e != hipSuccess) return (int)e;
-  *stream = (void*)s;
-  return 0;
-}
-
-extern "C" int avsr_stream_destroy(void* stream) {
-  return (int)hipStreamDestroy((hipStream_t)stream);
-}

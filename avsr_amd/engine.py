@@ -42,9 +42,6 @@ _COLSUM_DEFER = os.environ.get("AVSR_COLSUM_DEFER", "1") == "1"
 _SIDE_BIAS = os.environ.get("AVSR_SIDE_BIAS", "1") == "1"
 # the CTC branch of the forward runs on the side stream beside the decoder forward
 _CTC_SIDE = os.environ.get("AVSR_CTC_SIDE", "1") == "1"
-# weight-gradient handoffs of one transformer layer's backward batched into ONE event record +
-# wait (every record/wait pair cost the step stream a stall; AVSR_SIDE_BATCH=0: one per handoff)
-_SIDE_BATCH = os.environ.get("AVSR_SIDE_BATCH", "1") == "1"
 # bf16 stem conv straight from the video (stem.hip) instead of pack + general implicit GEMM
 _STEM_DIRECT = os.environ.get("AVSR_STEM_DIRECT", "1") == "1"
 # encoder residual-branch dropout backward (+ bias gradient) fused into the LayerNorm backward
@@ -114,32 +111,6 @@ def positional_encoding(L_, d, device):
     return pe.to(device)
 
 
-def _side_stream(device):
-    """the weight-gradient side stream. AVSR_SIDE_CUS="k/n" confines its kernels to k of every
-    n CUs (hipExtStreamCreateWithCUMask through the C-ABI), so the data-gradient chain on the
-    step stream never waits for side-stream workgroups to retire before it gets a CU; unset:
-    an ordinary stream on every CU. The masked stream lives as long as the process."""
-    spec = os.environ.get("AVSR_SIDE_CUS", "")
-    if not spec:
-        return torch.cuda.Stream(device=device)
-    import ctypes
-    from . import _lib
-    k, n = (int(t) for t in spec.split("/"))
-    if not 0 < k <= n:
-        raise ValueError(f"AVSR_SIDE_CUS={spec!r}: need 0 < k <= n")
-    ncu = torch.cuda.get_device_properties(device).multi_processor_count
-    words = (ncu + 31) // 32
-    mask = [0] * words
-    for i in range(ncu):
-        if i % n < k:
-            mask[i // 32] |= 1 << (i % 32)
-    arr = (ctypes.c_uint32 * words)(*mask)
-    out = ctypes.c_void_p()
-    with torch.cuda.device(device):
-        _lib.check(_lib.load().avsr_stream_create_cumask(arr, words, ctypes.byref(out)), "avsr_stream_create_cumask")
-    return torch.cuda.ExternalStream(out.value, device=device)
-
-
 class Engine:
     RES_BLOCKS = [(1, 0, 64, 64, 1), (1, 1, 64, 64, 1), (2, 0, 64, 128, 2), (2, 1, 128, 128, 1),
                   (3, 0, 128, 256, 2), (3, 1, 256, 256, 1), (4, 0, 256, 512, 2), (4, 1, 512, 512, 1)]
@@ -177,15 +148,14 @@ class Engine:
         self._pinned = [(None, None)] * 4
         self._pin_next = 0
         import os
-        self.side = (_side_stream(self.device)
+        self.side = (torch.cuda.Stream(device=self.device)
                      if self.device.type == "cuda" and os.environ.get("AVSR_SIDE_STREAM", "1") == "1" else None)
         # reused events: a stream wait binds the record that precedes it
-        self._side_ev = [torch.cuda.Event() for _ in range(int(os.environ.get("AVSR_SIDE_EV", "8")))] \
-            if self.side is not None else []
+        self._side_ev = [torch.cuda.Event() for _ in range(8)] if self.side is not None else []
         self._side_i = 0
         # operands the side stream reads stay referenced until join_side() (instead of
         # record_stream, whose deferred frees keep the caching allocator growing for steps)
-        self._side_keep = [] if os.environ.get("AVSR_SIDE_KEEP", "1") == "1" else None
+        self._side_keep = []
         self._side_defer = None      # list while a layer's handoffs are batched (_side_layer)
         E = "encoder.encoder.layers"
         groups = []
@@ -245,15 +215,6 @@ class Engine:
             pre = f"encoder.encoder.layers.{i}."
             offs = [m["off"] for n, m in self.arena.meta.items() if n.startswith(pre) and d0 <= m["off"] < d1]
             self._layer_decay_off.append(min(offs) if offs else d1)
-        # forward stages -> arena offset each needs updated (overlapped optimizer, optim.ParamGate):
-        # [frontends + projections + pos-conv | layer 0 | ... | layer nl-1]; the no-decay segment
-        # is updated first, and the decoder / CTC head wait for everything
-        self._stage_end = []
-        if self.nl:
-            last = [m["off"] for n, m in self.arena.meta.items()
-                    if n.startswith(f"encoder.encoder.layers.{self.nl - 1}.") and d0 <= m["off"] < d1]
-            after = [m["off"] for m in self.arena.meta.values() if d0 <= m["off"] < d1 and last and m["off"] > max(last)]
-            self._stage_end = self._layer_decay_off + [min(after) if after else d1]
         self.shell = shell
         self.step_count = 0
         self._pe = positional_encoding(max(512, 64), self.dD, self.device)
@@ -299,20 +260,6 @@ class Engine:
         the backward writes dQ straight into the activation-dtype gradient buffer."""
         return self._z(rows, D, dtype=torch.float32) if self.dtype == torch.float32 else None
 
-    def param_stage_bounds(self):
-        """arena offsets at which the forward's stages begin (FusedAdamW(overlap=True) chunks)"""
-        return list(self._stage_end)
-
-    def _params_wait(self, stage=None):
-        """overlapped optimizer: the current stream waits until stage `stage`'s parameters are
-        updated (None: all of them)"""
-        g = self.arena.gate
-        if g is not None:
-            if stage is None or stage >= len(self._stage_end):
-                g.wait_params()
-            else:
-                g.wait(self._stage_end[stage])
-
     def w(self, n):
         return self.arena.w(n)
 
@@ -347,11 +294,7 @@ class Engine:
             side.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(side):
             r = fn()
-        if self._side_keep is not None:
-            self._side_keep.extend(keep)
-        else:
-            for t in keep:
-                t.record_stream(side)
+        self._side_keep.extend(keep)
         return r
 
     def _side_layer(self, on):
@@ -359,7 +302,7 @@ class Engine:
         queued and issued at the end of its data-gradient chain behind ONE event wait, so the
         step stream records one event per layer instead of one per weight-gradient (the side
         stream then trails by at most one layer; its operands are never overwritten)"""
-        if self.side is None or not _SIDE_BATCH:
+        if self.side is None:
             return
         if on:
             self._flush_side()
@@ -549,7 +492,10 @@ class Engine:
         bn, gam, bet = self._bn(R + "frontend3D.1")
         st0 = ops.BnState(64, self.device)
         vid = videos.contiguous()
-        direct = self.dtype == torch.bfloat16 and _STEM_DIRECT
+        # the direct kernel addresses the fp32 video with 32-bit buffer offsets (avsr_stem_conv_fwd
+        # returns AVSR_E_SHAPE from 2^31 bytes, ~69 k frames): larger batches take the packed conv
+        direct = (self.dtype == torch.bfloat16 and _STEM_DIRECT
+                  and vid.numel() * vid.element_size() < ops.STEM_DIRECT_MAX_BYTES)
         # the packed 8-channel input: the general conv's operand, and the stem weight-grad's
         xp = None
         if not direct or save:
@@ -716,7 +662,6 @@ class Engine:
         M, D = B * T, self.D
         EN = "encoder."
         ctx = {"B": B, "T": T, "modality": modality}
-        self._params_wait(0)
         # audio / video frontends -> concat buffer [M][2D] (audio | video)
         fcat = self._e(M, 2 * D)
         ain = self._e(M, cfg.audio_feat_dim)
@@ -765,11 +710,9 @@ class Engine:
         x = y
         layers = []
         for i in range(self.nl):
-            self._params_wait(i + 1)
             x, lc = self._enc_layer_fwd(i, x, B, T, klen, train, save, seeds)
             if save:
                 layers.append(lc)
-        self._params_wait()
         E = "encoder.encoder."
         out, mf, rf = self._ln(x, E + "layer_norm", 1e-5)
         if save:
@@ -1120,8 +1063,6 @@ class Engine:
         M = B * T
         d_ctc = d_ctc.reshape(1).to(torch.float32)
         d_att = d_att.reshape(1).to(torch.float32)
-        if self.arena.gate is not None:
-            self.arena.gate.wait_grads()
         if self.before_backward is not None:
             self.before_backward()
         # bias / LayerNorm parameter-gradient finalise passes are batched: one launch per
@@ -1139,8 +1080,6 @@ class Engine:
     def encoder_backward(self, ectx, denc):
         """encoder-only backward (the reference call form model.encoder(...) trained alone,
         surface._EncoderStep) with backward()'s data-parallel hooks and finalise batching"""
-        if self.arena.gate is not None:
-            self.arena.gate.wait_grads()
         if self.before_backward is not None:
             self.before_backward()
         prev = ops.colsum_defer(_COLSUM_DEFER)

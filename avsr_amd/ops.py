@@ -38,8 +38,14 @@ def _ptr(t):
 
 
 _SKINNY_WS = {}
-_SKINNY_SPLIT = os.environ.get("AVSR_SKINNY_SPLIT", "0") == "1"
 SKINNY_WS = 1 << 19        # AVSR_SKINNY_WS
+# few-row (decoder step) linears: split K over more workgroups (gemm(skinny_split=None) default)
+SKINNY_SPLIT = False
+
+
+def skinny_splits(N, K):
+    """the K-split count the few-row path uses for an (N, K) weight when split (avsr_hip.h)"""
+    return int(L.load().avsr_gemm_skinny_splits(int(N), int(K)))
 
 
 def _skinny_ws(device):
@@ -55,8 +61,10 @@ def _skinny_ws(device):
 def gemm(A, B, C, *, M, N, K, a_kmajor, b_kmajor, lda, ldb, ldc, batch=1,
          strideA=0, strideB=0, strideC=0, alpha=1.0, beta=0.0, bias=None, act=L.ACT_NONE,
          epi_bwd=False, preact=None, res=None, ldr=None, strideR=0, gate=None, drop_p=0.0, seed=0,
-         splitk=1, ws=None, db=None, db_ws=None):
-    """Raw GEMM launch: C[b,m,n] = epi(alpha * sum_k A(b,m,k) B(b,n,k)). See avsr_hip.h."""
+         splitk=1, ws=None, db=None, db_ws=None, skinny_split=None):
+    """Raw GEMM launch: C[b,m,n] = epi(alpha * sum_k A(b,m,k) B(b,n,k)). See avsr_hip.h.
+    skinny_split: few-row launches (M <= 64) split K over skinny_splits(N, K) workgroup rows
+    (None: the module default SKINNY_SPLIT)."""
     lib = L.load()
     assert A.is_cuda and B.is_cuda and C.is_cuda
     assert A.dtype == B.dtype, "A/B dtype mismatch"
@@ -88,8 +96,8 @@ def gemm(A, B, C, *, M, N, K, a_kmajor, b_kmajor, lda, ldb, ldc, batch=1,
     if ws is not None:
         assert ws.dtype == torch.float32 and ws.numel() >= slab_ws(batch, splitk, M, N)
         p.ws = ws.data_ptr()
-    elif _SKINNY_SPLIT and M <= 64 and splitk == 1 and batch == 1 and a_kmajor and b_kmajor and not epi_bwd and db is None:
-        p.ws = _skinny_ws(A.device).data_ptr()      # K-split partials of the few-row vector-ALU path
+    if (SKINNY_SPLIT if skinny_split is None else skinny_split) and M <= 64 and splitk <= 1:
+        p.skinny_ws = _skinny_ws(A.device).data_ptr()   # K-split partials of the few-row vector-ALU path
     if db is not None:
         assert db.dtype == torch.float32 and db.numel() >= N and db_ws is not None and db_ws.dtype == torch.float32
         assert db_ws.numel() >= ((M + 63) // 64) * N
@@ -116,7 +124,8 @@ def gemm(A, B, C, *, M, N, K, a_kmajor, b_kmajor, lda, ldb, ldc, batch=1,
 # Linear layer building blocks (x: (M, K) row-major, W: (N, K) = torch.nn.Linear.weight)
 # ---------------------------------------------------------------------------------------
 
-def linear_fwd(x, W, bias=None, *, act=L.ACT_NONE, preact=None, res=None, drop_p=0.0, seed=0, out=None):
+def linear_fwd(x, W, bias=None, *, act=L.ACT_NONE, preact=None, res=None, drop_p=0.0, seed=0, out=None,
+               skinny_split=None):
     """y = dropout(act(x W^T + b)) + res ; optionally stores h = x W^T + b into `preact`."""
     M, K = x.shape
     N = W.shape[0]
@@ -125,7 +134,7 @@ def linear_fwd(x, W, bias=None, *, act=L.ACT_NONE, preact=None, res=None, drop_p
         out = torch.empty(M, N, device=x.device, dtype=x.dtype)
     gemm(x, W, out, M=M, N=N, K=K, a_kmajor=True, b_kmajor=True, lda=x.stride(0), ldb=W.stride(0),
          ldc=out.stride(0), bias=bias, act=act, preact=preact, res=res,
-         ldr=None if res is None else res.stride(0), drop_p=drop_p, seed=seed)
+         ldr=None if res is None else res.stride(0), drop_p=drop_p, seed=seed, skinny_split=skinny_split)
     return out
 
 
@@ -637,6 +646,7 @@ def stem_wpack(w, wp):
 
 
 STEM_K = 288     # packed stem weight row (avsr_stem_wpack2)
+STEM_DIRECT_MAX_BYTES = 0x7fffffff   # avsr_stem_conv_fwd: fp32 video bytes must stay below this
 
 
 def stem_wpack2(w, wk):

@@ -19,60 +19,13 @@ class LinearWarmupDecay:
         return self.lr * max(0.0, (self.total - s) / max(1, self.total - self.warm))
 
 
-class ParamGate:
-    """Readiness events of an overlapped optimizer step. The update runs on its own stream in
-    chunks that follow the arena's (module = forward) order; `marks` holds (end offset, event)
-    per chunk, `zeroed` the event after the gradient arena was cleared behind the update.
-    A reader of parameters [.., end) waits for the first chunk reaching `end` (wait), the
-    backward for the cleared gradients (wait_grads); events are recorded on one stream, so
-    waiting on one implies every earlier chunk."""
-
-    def __init__(self, device):
-        self.stream = torch.cuda.Stream(device=device)     # default priority: below the step stream
-        self.marks = []
-        self.zeroed = None
-        self.final = None
-
-    def wait(self, end):
-        """current stream waits until every parameter below arena offset `end` is updated"""
-        if not self.marks:
-            return
-        cur = torch.cuda.current_stream(self.stream.device)
-        for i, (off, ev) in enumerate(self.marks):
-            if off >= end:
-                cur.wait_event(ev)
-                del self.marks[:i + 1]
-                return
-        self.wait_params()
-
-    def wait_params(self):
-        if self.marks:
-            torch.cuda.current_stream(self.stream.device).wait_event(self.marks[-1][1])
-            self.marks = []
-
-    def wait_grads(self):
-        if self.zeroed is not None:
-            torch.cuda.current_stream(self.stream.device).wait_event(self.zeroed)
-            self.zeroed = None
-
-    def wait_all(self):
-        """everything the overlapped step wrote (parameters, moments, cleared gradients)"""
-        if self.final is not None:
-            torch.cuda.current_stream(self.stream.device).wait_event(self.final)
-        self.marks, self.zeroed, self.final = [], None, None
-
-
 class FusedAdamW:
-    """overlap=True (with stage_bounds = sorted arena offsets inside the weight-decay segment,
-    Engine.param_stage_bounds()): step() computes the gradient norm on the current stream, then
-    runs the update on a side stream — no-decay segment first, then the decay segment chunk by
-    chunk in forward order — and clears the gradients there (step(zero_grad=True)); the next
-    forward waits per stage only for the chunk it reads (Engine.encoder_fwd), so the update of
-    the later layers runs beside the frontends' forward. Results are bit-identical to the
-    serial step (the update is elementwise). Readers outside Engine.forward call sync()."""
+    """step(): gradient norm, then one fused clip + AdamW launch per weight-decay segment, all
+    on the current stream (an update overlapped with the next forward measured no gain in
+    round 3, profiles/r03_opt_overlap_ab.txt, and was removed)."""
 
     def __init__(self, arena, lr=1e-4, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.005, max_grad_norm=1.0,
-                 schedule=None, overlap=False, stage_bounds=()):
+                 schedule=None):
         self.arena = arena
         arena.init_optimizer()
         self.lr, self.betas, self.eps, self.wd, self.max_norm = lr, betas, eps, weight_decay, max_grad_norm
@@ -80,17 +33,6 @@ class FusedAdamW:
         self.step_count = 0
         self._sumsq = torch.zeros(1, device=arena.device)
         self._sumsq_ws = torch.empty(ops.SUMSQ_WS, device=arena.device)
-        self.gate = None
-        if overlap:
-            d0, d1 = arena.segments["decay"]
-            self._bounds = sorted({b for b in stage_bounds if d0 < b < d1} | {d1})
-            self.gate = ParamGate(arena.device)
-            self._events = [torch.cuda.Event() for _ in range(len(self._bounds) + 2)]
-
-    def sync(self):
-        """make the current stream wait for an overlapped step's writes"""
-        if self.gate is not None:
-            self.gate.wait_all()
 
     def grad_sumsq(self):
         """sum of squared gradients over the trainable segments (device scalar, no sync)"""
@@ -105,15 +47,12 @@ class FusedAdamW:
         """one AdamW step; with max_grad_norm > 0 the gradients are clipped by the global norm
         inside the kernel (coef = min(1, max_norm / (norm + 1e-6)), torch.nn.utils.
         clip_grad_norm_); sumsq_ready: grad_sumsq() was already computed for this step;
-        zero_grad: clear the gradient arena after the update (on the update's stream when
-        overlapped: no separate zero_grad() before the next backward)."""
+        zero_grad: clear the gradient arena after the update."""
         a = self.arena
         self.step_count += 1
         lr = self.schedule(self.step_count) if self.schedule else self.lr
         d0, d1 = a.segments["decay"]
         n0, n1 = a.segments["no_decay"]
-        if self.gate is not None:
-            self.gate.wait_all()                  # a previous overlapped step (no forward between)
         if self.max_norm and self.max_norm > 0 and not sumsq_ready:
             self.grad_sumsq()
 
@@ -124,35 +63,11 @@ class FusedAdamW:
                       sumsq_buf=self._sumsq if self.max_norm else None, max_norm=self.max_norm or 1.0,
                       grad_scale=grad_scale)
 
-        if self.gate is None:
-            for (s, e), wd in (((d0, d1), self.wd), ((n0, n1), 0.0)):
-                if e > s:
-                    launch(s, e, wd)
-            if zero_grad:
-                a.zero_grad()
-            return lr
-        g, ev = self.gate, self._events
-        g.stream.wait_stream(torch.cuda.current_stream(a.device))
-        marks = []
-        with torch.cuda.stream(g.stream):
-            if n1 > n0:
-                launch(n0, n1, 0.0)               # biases / LayerNorm weights: every stage reads some
-            s = d0
-            for i, e in enumerate(self._bounds):
-                if e > s:
-                    launch(s, e, self.wd)
-                ev[i].record(g.stream)
-                marks.append((e, ev[i]))
-                s = e
-            if zero_grad:
-                a.grad.zero_()
-            ev[-1].record(g.stream)
-        g.marks = marks
-        g.zeroed = ev[-1] if zero_grad else None
-        g.final = ev[-1]
-        a.gate = g
+        for (s, e), wd in (((d0, d1), self.wd), ((n0, n1), 0.0)):
+            if e > s:
+                launch(s, e, wd)
         if zero_grad:
-            a.attach_grads(zero=False)
+            a.zero_grad()
         return lr
 
     # ------------------------------------------------------------------ checkpoint / resume

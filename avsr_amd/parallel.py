@@ -23,6 +23,17 @@ import torch
 import torch.distributed as dist
 
 BUCKET_BYTES = 64 << 20   # 64 MiB buckets: ~7 links x ~153 GB/s per GPU want big messages
+COMPRESS_MODES = (None, "bf16")
+
+
+def _cast(src, dst):
+    """flat dtype cast for the compressed exchange: the library's HIP kernel for device
+    tensors; CPU tensors exist only in the gloo-on-CPU tests of this module's logic"""
+    if src.is_cuda:
+        from . import ops
+        ops.cast_flat(src, dst)
+    else:
+        dst.copy_(src)
 
 
 def init_from_env(backend=None):
@@ -53,10 +64,20 @@ class GradReducer:
     and CTC head final). Every newly complete bucket is all-reduced right away on the comm
     stream, which first waits on an event of the compute stream; `finish()` reduces the
     rest and makes the compute stream wait for the comm stream. `allreduce()` = begin +
-    finish (no overlap)."""
+    finish (no overlap).
 
-    def __init__(self, flat_grad, bucket_bytes=BUCKET_BYTES, group=None, use_stream=True, segment=None):
+    compress="bf16" (off by default: fp32 keeps gradient parity with the reference's DDP)
+    halves the bytes on xGMI: a bucket is cast to bf16 on the comm stream, summed in bf16 by
+    RCCL and cast back into the fp32 arena (torch DDP's bf16_compress_hook, minus its
+    pre-division: the 1/world factor stays in the optimizer or finish(average=True))."""
+
+    def __init__(self, flat_grad, bucket_bytes=BUCKET_BYTES, group=None, use_stream=True, segment=None,
+                 compress=None):
+        if compress not in COMPRESS_MODES:
+            raise ValueError(f"compress={compress!r}: one of {COMPRESS_MODES}")
         self.flat = flat_grad
+        self.compress = compress
+        self.cbuf = None
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         n = flat_grad.numel()
@@ -87,9 +108,17 @@ class GradReducer:
         self._t0 = None
 
     def _reduce(self, a, b):
-        w = dist.all_reduce(self.flat[a:b], op=dist.ReduceOp.SUM, group=self.group, async_op=self.stream is not None)
+        buf = self.flat
+        if self.compress == "bf16":
+            if self.cbuf is None:
+                self.cbuf = torch.empty(self.flat.numel(), dtype=torch.bfloat16, device=self.flat.device)
+            _cast(self.flat[a:b], self.cbuf[a:b])
+            buf = self.cbuf
+        w = dist.all_reduce(buf[a:b], op=dist.ReduceOp.SUM, group=self.group, async_op=self.stream is not None)
         if w is not None:
-            self._works.append(w)
+            self._works.append((w, a, b))
+        elif buf is not self.flat:
+            _cast(self.cbuf[a:b], self.flat[a:b])
 
     def _launch(self, ranges):
         if not ranges:
@@ -131,8 +160,10 @@ class GradReducer:
         self._next = len(self.buckets)
         if self.stream is not None:
             with torch.cuda.stream(self.stream):
-                for w in self._works:
+                for w, a, b in self._works:
                     w.wait()
+                    if self.compress == "bf16":
+                        _cast(self.cbuf[a:b], self.flat[a:b])
                 if average:
                     self.flat.mul_(1.0 / self.world)
                 if self.timing is not None:
@@ -181,7 +212,7 @@ class ArenaDDP:
     the 1/world factor to FusedAdamW.step(grad_scale=1/world) and saves one pass."""
 
     def __init__(self, model, bucket_bytes=BUCKET_BYTES, broadcast_buffers=True, average=True, use_stream=True,
-                 group=None):
+                 group=None, compress=None):
         eng = model.avsr.engine()
         self.model, self.eng, self.group = model, eng, group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
@@ -190,7 +221,7 @@ class ArenaDDP:
         broadcast_state(arena.data, [eng.bn_flat] + int_buffers, group=group)
         arena.sync_shadow()
         self.reducer = GradReducer(arena.grad, bucket_bytes=bucket_bytes, group=group, use_stream=use_stream,
-                                   segment=arena.segments["decay"])
+                                   segment=arena.segments["decay"], compress=compress)
         if getattr(eng, "side", None) is not None:
             self.reducer.extra_streams.append(eng.side)
         self.average = average

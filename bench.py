@@ -116,8 +116,10 @@ def synthetic_batch(B, T, L, seed=1234):
             torch.full((B,), T, dtype=torch.int64), torch.from_numpy(lab))
 
 
-def model_flops_per_frame(cfg, T, L):
-    """algorithmic fwd+bwd FLOPs per AV-frame: 3x the forward MACs*2."""
+def model_flops_per_frame(cfg, T, L, variant="none"):
+    """algorithmic fwd+bwd FLOPs per AV-frame: 3x the forward MACs*2.
+    variant "video_off" runs the ResNet forward only (its backward is skipped: the gradient is
+    exactly zero, avhubert.py:480), so the ResNet's backward FLOPs are not counted for it."""
     D, F, nl = cfg.hidden_size, cfg.intermediate_size, cfg.num_hidden_layers
     enc = nl * (2 * (4 * D * D + 2 * D * F) + 4 * T * D)            # per frame, forward
     # ResNet-18 frontend forward per frame (conv MACs * 2), stem + 4 stages + 512->D proj
@@ -138,7 +140,19 @@ def model_flops_per_frame(cfg, T, L):
     dec = (dec_tok * L1 + dl * 2 * 2 * T * dD * dD) / T               # memory K/V projections per frame
     fwd = enc + front + posconv + ctc + dec
     # backward = 2x forward except the stem (no data-grad): stem counted fwd + wgrad only
-    return 3 * fwd - stem
+    total = 3 * fwd - stem
+    if variant == "video_off":
+        total -= 2 * res + stem
+    return total
+
+
+def stratified_variants(steps, rank):
+    """modality variant of each timed step: the reference draws it per forward (p = 0.5 none,
+    0.25 audio_off, 0.25 video_off; avhubert.py:476-482); the bench takes the same distribution
+    stratified (period 4: none, video_off, none, audio_off; rotated per rank so ranks differ
+    like independent draws), so `value` is the expected-mix throughput instead of one draw's"""
+    pat = [None, "video_off", None, "audio_off"]
+    return [pat[(i + rank) % 4] for i in range(steps)]
 
 
 def expected_step_ms(variant_ms, world):
@@ -310,7 +324,7 @@ def cpu_selftest(args):
     n = 3_000_001
     flat = torch.zeros(n)
     seg = (1000, 2_500_000)
-    red = parallel.GradReducer(flat, bucket_bytes=4 << 18, segment=seg, use_stream=False)
+    red = parallel.GradReducer(flat, bucket_bytes=4 << 18, segment=seg, use_stream=False, compress=args.grad_compress)
     ok = True
     for _ in range(args.warmup):
         flat.fill_(rank + 1.0)
@@ -325,7 +339,7 @@ def cpu_selftest(args):
             red.ready(off)
         red.finish(average=True)
         want = torch.arange(n, dtype=torch.float32) * (sum(range(1, world + 1)) / world + i)
-        ok = ok and torch.allclose(flat, want, rtol=1e-6)
+        ok = ok and torch.allclose(flat, want, rtol=1e-6 if args.grad_compress is None else 2 ** -7)
     dist.barrier()
     elapsed = time.perf_counter() - t0
     t = torch.tensor([elapsed], dtype=torch.float64)
@@ -337,6 +351,7 @@ def cpu_selftest(args):
            "ms_per_step": round(t.item() / max(1, args.steps) * 1e3, 3), "data": "synthetic",
            "allreduce": {"backend": dist.get_backend(), "ranks": dist.get_world_size(),
                          "buckets": len(red.buckets) + len(red.tail), "elements": n,
+                         "compress": args.grad_compress or "none (fp32)",
                          "mean_ok": bool(okt.item())}}
     if rank == 0:
         print(json.dumps(res), flush=True)
@@ -371,13 +386,8 @@ def gpu_bench(args):
     # DDP semantics on the arena: rank-0 broadcast of parameters + buffers, per-forward BN
     # statistics broadcast, bucketed RCCL all-reduce overlapped with the backward; the 1/world
     # average is folded into the AdamW kernel (average=False, grad_scale below)
-    ddp = parallel.ArenaDDP(model, average=False)
-    # the AdamW update of the later layers overlaps the next step's frontend forward (each forward
-    # stage waits only for the chunk of the update it reads; optim.ParamGate) with --opt-overlap; off by
-    # default: no wall-clock gain on MI355X
-    overlap = args.opt_overlap
-    opt = FusedAdamW(arena, lr=1e-4, weight_decay=0.005, max_grad_norm=1.0, overlap=overlap,
-                     stage_bounds=eng.param_stage_bounds())
+    ddp = parallel.ArenaDDP(model, average=False, compress=args.grad_compress)
+    opt = FusedAdamW(arena, lr=1e-4, weight_decay=0.005, max_grad_norm=1.0)
 
     B, T, L = args.batch, args.seq, args.labels
     v, a, lens, lab = synthetic_batch(B, T, L, seed=args.seed + rank)
@@ -411,21 +421,25 @@ def gpu_bench(args):
 
     forced_all = None if args.force_modality is None else (
         (None if args.force_modality == "none" else args.force_modality),)
+    # per-step variants: stratified (default), or the reference's own random draw (--modality-draws random)
+    strat = args.modality_draws == "stratified"
+    sched = stratified_variants(args.warmup + args.steps, rank)
 
-    def step(variant=False):
+    def step(i=None, variant=False):
         if forced_all is not None and not variant:
             eng.force_modality = forced_all
-        if not overlap:
-            arena.zero_grad()                   # overlapped: cleared behind the previous update
+        elif strat and not variant:
+            eng.force_modality = (sched[i],)
+        arena.zero_grad()
         step_seed[0] += 1
         out4, ctx = eng.forward(v, a, lens, lab, train=True, need_grad=True, seed=step_seed[0])
         drops.append(eng.last_modality)
         eng.backward(ctx, d_ctc, d_att)
-        opt.step(grad_scale=1.0 / world, zero_grad=overlap)
+        opt.step(grad_scale=1.0 / world)
         return out4
 
-    for _ in range(args.warmup):
-        out4 = step()
+    for i in range(args.warmup):
+        out4 = step(i)
     torch.cuda.synchronize()
     # probe: encoder FFN up-projection (M = B*T, N = F, K = D), forward, bf16
     M, N_, K_ = B * T, cfg.intermediate_size, cfg.hidden_size
@@ -447,7 +461,7 @@ def gpu_bench(args):
     step_ev[0].record()
     for i in range(args.steps):
         h0 = time.perf_counter()
-        out4 = step()
+        out4 = step(args.warmup + i)
         step_ev[i + 1].record()
         host_t.append(time.perf_counter() - h0)
     torch.cuda.synchronize()
@@ -476,7 +490,8 @@ def gpu_bench(args):
     ev_avg = sum(ev_ms) / max(1, len(ev_ms))
     flops = 2.0 * M * N_ * K_
     achieved = flops / (avg_ms * 1e-3) / 1e12 if avg_ms > 0 else 0.0
-    fpf = model_flops_per_frame(cfg, T, L)
+    # FLOPs the timed steps performed (video_off steps skip the ResNet backward)
+    fpf = sum(model_flops_per_frame(cfg, T, L, d or "none") for d in timed_drops) / max(1, len(timed_drops))
     traffic = None      # HBM bytes per launch from the committed PMC passes (tools/pmc_traffic.py)
     tp = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(tp):
@@ -496,18 +511,26 @@ def gpu_bench(args):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             step(variant=True)
-            opt.sync()                          # an overlapped update belongs to the step
             e1.record()
             torch.cuda.synchronize()
             per.append(e0.elapsed_time(e1))
         variant_ms[name] = round(sorted(per)[1], 2)
     eng.force_modality = None
     exp_ms = expected_step_ms(variant_ms, world)
+    # what one seeded draw of the reference's RNG would have given for the same K steps
+    # (per-variant medians; the timed region itself runs the stratified schedule)
+    rs = np.random.RandomState(args.seed + 7919 * rank)
+    raw = []
+    for _ in range(args.steps):
+        pm, pa = rs.random_sample(), rs.random_sample()
+        raw.append("none" if pm >= cfg.modality_dropout else ("audio_off" if pa < cfg.audio_dropout else "video_off"))
+    raw_ms = sum(variant_ms[k] for k in raw)
     allreduce = None
     if world > 1:
         exposed = [j0.elapsed_time(j1) for (c0, c1, j0, j1) in ar_timing]
         comm = [c0.elapsed_time(c1) for (c0, c1, j0, j1) in ar_timing if c0 is not None]
         allreduce = {"backend": dist.get_backend(), "ranks": dist.get_world_size(),
+                     "compress": args.grad_compress or "none (fp32)",
                      "buckets": len(red.buckets) + len(red.tail), "bucket_mib": parallel.BUCKET_BYTES >> 20,
                      "bytes_per_step": arena.grad.numel() * 4,
                      "exposed_ms_per_step": round(sum(exposed) / max(1, len(exposed)), 3),
@@ -525,8 +548,9 @@ def gpu_bench(args):
                                f"(T={T}, L={L}), train mode, dropouts on",
                    "global_batch": B * world, "seq_len": T, "parallelism": f"dp{world}",
                    "encoder_layers": cfg.num_hidden_layers,
-                   "optimizer": "fused clip+AdamW, " + ("update overlapped with the next forward (per-stage readiness "
-                                                        "events, optim.ParamGate)" if overlap else "serial")},
+                   "optimizer": "fused clip+AdamW",
+                   "modality_draws": ("stratified 0.5/0.25/0.25 (period 4, rotated per rank)" if strat and forced_all is None
+                                      else "reference RNG draws" if forced_all is None else "forced")},
         "roofline": {"bound": "mfma", "kernel": f"dense_glds_kernel bf16 (encoder FFN1 fwd {M}x{N_}x{K_})",
                      "achieved": round(achieved, 1), "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": round(achieved / BF16_PEAK_TFLOPS, 4), "traffic": traffic,
@@ -537,12 +561,16 @@ def gpu_bench(args):
                      "event_avg_launch_ms": round(ev_avg, 4)},
         "model_tflops_per_s": round(value * fpf / world / 1e12, 1),
         "model_mfu": round(value * fpf / world / 1e12 / BF16_PEAK_TFLOPS, 4),
+        "model_flops_note": "algorithmic FLOPs of the steps actually timed (video_off: no ResNet backward)",
         "modality_variants": {"step_ms": variant_ms, "p": MODALITY_P,
                               "expected_ms_per_step": round(exp_ms, 3),
                               "value_expected": round(B * T * world / exp_ms * 1e3, 2),
+                              "value_seeded_draw": round(args.steps * B * T * world / raw_ms * 1e3, 2),
+                              "seeded_draw_counts": {k: raw.count(k) for k in MODALITY_P},
                               "note": "median of 3 forced steps per variant; value_expected weights them with "
                                       "the reference's draw probabilities (avhubert.py:476-482), slowest rank "
-                                      "bounding a step for N > 1"},
+                                      "bounding a step for N > 1; value_seeded_draw: the same K steps under one "
+                                      "numpy draw (seed --seed) instead of the stratified schedule"},
         "loss": [round(x, 4) for x in losses],
         "host_ms_per_step_timed": round(sum(host_t) / len(host_t) * 1e3, 2),
         "host_ms_steps": [round(t * 1e3, 1) for t in host_t],
@@ -583,14 +611,17 @@ def gpu_bench(args):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=4)
     ap.add_argument("--batch", type=int, default=16, help="clips per GPU")
     ap.add_argument("--seq", type=int, default=375, help="AV-frames per clip (15 s at 25 fps)")
     ap.add_argument("--labels", type=int, default=40)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--opt-overlap", action="store_true",
-                    help="run the AdamW update beside the next step's forward (measured: no wall-clock gain, DESIGN §9)")
+    ap.add_argument("--modality-draws", choices=["stratified", "random"], default="stratified",
+                    help="timed steps' modality variants: stratified to the reference's probabilities (default), "
+                         "or drawn from numpy's global RNG per forward as the reference does")
+    ap.add_argument("--grad-compress", choices=["bf16"], default=None,
+                    help="N > 1: exchange gradients in bf16 (parallel.GradReducer; default fp32 for parity)")
     ap.add_argument("--no-decode", action="store_true", help="skip the C1/C4/C5 decode throughput section")
     ap.add_argument("--quick", action="store_true", help="only the step measurement (profiling runs)")
     ap.add_argument("--layers", type=int, default=None, help="debug only: fewer encoder layers (INVALID for the metric)")

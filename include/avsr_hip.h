@@ -74,10 +74,7 @@ typedef struct {
   float* ws;                 /* split-K slab workspace, AVSR_GEMM_SLAB_WS(batch, splitk, M, N) fp32:
                                 each split stores its partial tile, a reduce pass writes
                                 C = alpha*sum + beta*C (plain epilogue only). NULL: C += alpha*acc
-                                by fp32 atomics. With splitk == 1 and M <= 64 (the vector-ALU
-                                path for decoder steps) a ws of >= AVSR_SKINNY_WS floats lets
-                                the launch split K over more workgroups (fp32 partials, ordered
-                                reduce + epilogue); NULL: one workgroup row */
+                                by fp32 atomics. Ignored when splitk <= 1. */
   float* db;                 /* optional: db[n] += sum_m C[m][n] of the stored tile values (the
                                 bias gradient of the layer whose output gradient C is, e.g.
                                 FFN1's bias from the FFN2 data-grad); bf16, N % 8 == 0, no split */
@@ -86,6 +83,10 @@ typedef struct {
                                 {min start, max end} in s_memrealtime ticks (100 MHz) — every
                                 workgroup folds its first / last instant in by vector atomics.
                                 Caller initialises {~0ull, 0}. No output depends on it. */
+  float* skinny_ws;          /* optional, >= AVSR_SKINNY_WS fp32: with splitk <= 1 and M <= 64 (the
+                                vector-ALU path of decoder steps) the launch splits K over
+                                avsr_gemm_skinny_splits(N, K) workgroup rows (fp32 partials here,
+                                ordered reduce + epilogue). NULL: one workgroup row */
 } avsr_gemm_params;
 #define AVSR_GEMM_COLSUM_WS(M, N) ((int64_t)(((M) + 63) / 64) * (N))
 /* slabs are AVSR_GEMM_SLAB_PAD floats apart beyond M*N: power-of-two slab strides put the
@@ -96,6 +97,9 @@ typedef struct {
 #define AVSR_GEMM_SLAB_WS(batch, splitk, M, N) ((int64_t)(batch) * (splitk) * ((int64_t)(M) * (N) + AVSR_GEMM_SLAB_PAD))
 
 int avsr_gemm(const avsr_gemm_params* p, void* stream);
+/* K-split count the few-row path uses for an N x K weight when skinny_ws is given (depends on N
+ * and K only, never on M: a row's result does not depend on how many rows share the launch) */
+int avsr_gemm_skinny_splits(int N, int K);
 
 /* ------------------------------------------------------------------------------------
  * Implicit-GEMM convolution over NHWC activations (no im2col buffer), grouped.
@@ -368,8 +372,9 @@ int avsr_loss_finalize(int B, const float* nll, int rows, const float* row_loss,
  *                  PositionalEncoding, decoder.py:89-93, embedding.py:80-87); bwd: dtable
  *                  += per-token sums of the row gradients in row order (no atomics)
  * avsr_cast:       dst = alpha * src + beta * dst over a [rows][cols] strided view
- * avsr_cast_flat:  dst = src over n contiguous elements (fp32 -> bf16 vectorised: the arena's
- *                  master -> compute-shadow refresh after load_state_dict / optimizer steps)
+ * avsr_cast_flat:  dst = src over n contiguous elements (fp32 <-> bf16 vectorised: the arena's
+ *                  master -> compute-shadow refresh after load_state_dict / optimizer steps; the
+ *                  bf16-compressed gradient all-reduce's compress / decompress)
  * avsr_stem_pack:  videos (B,1,T,88,88) fp32 -> (B*T, 88, 88, 8): channel c = frame t+c-2
  *                  (c < 5, zero outside [0,T)), the Conv3d(k=5x7x7, pad 2x3x3) stem as a 2-D conv
  * avsr_stem_wpack / avsr_stem_wgrad_unpack: Conv3d weight (64,1,5,7,7) <-> [64][7][7][8]
@@ -611,16 +616,6 @@ typedef struct {
 int avsr_add_noise(const avsr_add_noise_params* p, void* stream);
 
 int avsr_rgb_to_gray(const uint8_t* rgb, uint8_t* gray, int64_t n, void* stream);
-
-/* ------------------------------------------------------------------------------------
- * Runtime helper (no reference counterpart: the reference has one CUDA stream).
- * avsr_stream_create_cumask: a HIP stream whose kernels may only occupy the CUs whose bits
- *   are set in mask[0..nwords) (hipExtStreamCreateWithCUMask); used for the weight-gradient
- *   side stream so that the data-gradient chain always finds free CUs. *stream receives the
- *   hipStream_t; avsr_stream_destroy releases it. Both return 0 or the hipError_t.
- * ------------------------------------------------------------------------------------ */
-int avsr_stream_create_cumask(const uint32_t* mask, int nwords, void** stream);
-int avsr_stream_destroy(void* stream);
 
 #ifdef __cplusplus
 }

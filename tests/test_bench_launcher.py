@@ -20,9 +20,12 @@ def _env(**extra):
     return env
 
 
-def test_bench_self_launch_world2():
+@pytest.mark.parametrize("compress", [None, "bf16"])
+def test_bench_self_launch_world2(compress):
+    extra = [] if compress is None else ["--grad-compress", compress]
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--cpu-selftest",
-                        "--steps", "2", "--warmup", "1"], env=_env(), capture_output=True, text=True, timeout=300)
+                        "--steps", "2", "--warmup", "1"] + extra, env=_env(), capture_output=True, text=True,
+                       timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout
@@ -31,6 +34,7 @@ def test_bench_self_launch_world2():
     ar = d["allreduce"]
     assert ar["ranks"] == 2 and ar["backend"] == "gloo" and ar["mean_ok"] is True
     assert ar["buckets"] >= 4
+    assert ar["compress"] == (compress or "none (fp32)")
 
 
 def test_bench_launcher_fails_when_a_rank_fails():
@@ -52,3 +56,16 @@ def test_expected_step_ms():
     e2 = bench.expected_step_ms(v, 2)
     p_vo, p_le_ao = 0.25 ** 2, 0.5 ** 2
     assert e2 == pytest.approx(39 * p_vo + 54 * (p_le_ao - p_vo) + 55 * (1 - p_le_ao))
+
+
+def test_stratified_variants_match_reference_probabilities():
+    """bench.py's timed steps take the reference's modality distribution stratified: every 4
+    consecutive steps hold 2 none, 1 video_off, 1 audio_off, on every rank; ranks are rotated"""
+    sys.path.insert(0, ROOT)
+    import bench
+    for rank in range(3):
+        s = bench.stratified_variants(20, rank)
+        for i in range(0, 20, 4):
+            blk = s[i:i + 4]
+            assert blk.count(None) == 2 and blk.count("video_off") == 1 and blk.count("audio_off") == 1
+    assert bench.stratified_variants(4, 0) != bench.stratified_variants(4, 1)

@@ -15,6 +15,9 @@ atomics on the training path).
 Also: a batch whose lengths / labels already live on the device (HF Trainer's layout) takes
 the sync-free device preparation (Engine._prepare_device) and equals the host-prepared batch,
 including a label matrix with an extra all-padding column."""
+import json
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -104,6 +107,15 @@ def test_c2_bf16_matches_fp32_parity_path(runs):
             bad.append((k, gv, n))
     e_bn = max(float((got["bn"][k] - v).abs().max() / v.abs().max().clamp_min(1e-6)) for k, v in ref["bn"].items())
     print(f"C2 bf16 vs fp32: loss {e_loss:.2e} rows {e_rows:.2e} grad-norm worst {worst:.2e} bn {e_bn:.2e}")
+    d = os.environ.get("AVSR_REPORT_DIR")     # the achieved errors, kept under profiles/ by the GPU runs
+    if d:
+        os.makedirs(d, exist_ok=True)
+        per_rows = {k: rel(got[k], ref[k]) for k in ("enc", "ctc", "dec")}
+        with open(os.path.join(d, "c2_bf16_vs_fp32.json"), "w") as f:
+            json.dump({"shape": {"B": B, "T": T, "labels": NL}, "tolerance": TOL,
+                       "loss_rel": e_loss, "losses_bf16": got["loss"], "losses_fp32": ref["loss"],
+                       "rows_rel": per_rows, "grad_norm_rel_worst": worst, "bn_rel": e_bn,
+                       "n_grads": len(ref["grad"])}, f, indent=1)
     assert e_loss < TOL["loss"]
     assert e_rows < TOL["rows"]
     assert not bad, bad[:8]

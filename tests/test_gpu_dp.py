@@ -9,7 +9,12 @@ per-layer readiness watermarks.
   * gradient accumulation 2 with no_sync() on the first micro-step: the result equals the mean
     over ranks of the accumulated micro-step gradients (no double reduction);
   * BatchNorm running statistics: rank 0's win at construction and are broadcast before a
-    forward that follows a synchronising backward (DDP broadcast_buffers=True)."""
+    forward that follows a synchronising backward (DDP broadcast_buffers=True);
+  * mixed modality draws: rank 0 draws video_off (its ResNet backward is skipped), rank 1 draws
+    none, in the same synchronising step — what every C3 step with modality dropout does
+    (avhubert.py:476-482); the averaged arena equals the mean of the per-shard gradients;
+  * the reference's module-level encoder call (model.avsr.encoder(input_features=, video=),
+    surface.py) trained under ArenaDDP: the same parity on its gradients."""
 import os
 import socket
 
@@ -40,10 +45,22 @@ def _shard(batch, r):
     return {k: v[r:r + 1].contiguous() for k, v in batch.items()}
 
 
-def _grads(m, shards, scale):
+def _grads(m, shards, scale, modality=None):
+    eng = m.avsr.engine()
+    eng.force_modality = None if modality is None else (modality,)
     m.zero_grad()
     for sh in shards:
         (m(**sh).loss * scale).backward()
+    torch.cuda.synchronize()
+    eng.force_modality = None
+    return eng.arena.grad.clone()
+
+
+def _enc_grads(m, sh, wout):
+    """the surface encoder call in train mode, loss = <encoder output, wout>"""
+    m.zero_grad()
+    out = m.avsr.encoder(input_features=sh["audios"], video=sh["videos"]).last_hidden_state
+    (out * wout[:out.shape[1]].to(out.device)).sum().backward()
     torch.cuda.synchronize()
     return m.avsr.engine().arena.grad.clone()
 
@@ -69,6 +86,14 @@ def _worker(rank, world, port, q):
         g0 = _grads(ref_m, [_shard(batch, 0)], 1.0)
         g1 = _grads(ref_m, [_shard(batch, 1)], 1.0)
         mean = (g0 + g1) / 2
+        mix = ("video_off", None)                       # rank 0 / rank 1 draws of the mixed step
+        gm = [_grads(ref_m, [_shard(batch, r)], 1.0, modality=mix[r]) for r in range(2)]
+        mean_mix = (gm[0] + gm[1]) / 2
+        wout = torch.randn(batch["videos"].shape[2], cfg_kw["hidden_size"],
+                           generator=torch.Generator().manual_seed(3))
+        ge = [_enc_grads(ref_m, _shard(batch, r), wout) for r in range(2)]
+        mean_enc = (ge[0] + ge[1]) / 2
+        del ref_m
         # DDP model: rank r trains on shard r
         m = _model(state, cfg_kw)
         eng = m.avsr.engine()
@@ -94,6 +119,17 @@ def _worker(rank, world, port, q):
         # BN statistics broadcasts (DDP rule): before the first forward and before the forward
         # that follows a synchronising backward; not after the no_sync micro-step
         res["broadcasts"] = ddp.buffer_broadcasts
+        # mixed modality step: the ResNet gradient of rank 0's shard is exactly zero
+        rn = [(mt["off"], mt["off"] + mt["numel"]) for n, mt in eng.arena.meta.items()
+              if ".resnet." in n and n in eng.arena.grad_views]
+        got = _grads(m, [_shard(batch, rank)], 1.0, modality=mix[rank])
+        res["mix_err"] = (got - mean_mix).abs().max().item() / mean_mix.abs().max().item()
+        res["mix_video_zero_r0"] = (len(rn) > 0 and all(gm[0][a:b].abs().max().item() == 0 for a, b in rn)
+                                    and any(gm[1][a:b].abs().max().item() > 0 for a, b in rn))
+        # surface encoder call under DDP (its forward broadcasts BN buffers, its backward reduces)
+        got = _enc_grads(m, _shard(batch, rank), wout)
+        res["enc_err"] = (got - mean_enc).abs().max().item() / mean_enc.abs().max().item()
+        res["enc_nonzero"] = bool(mean_enc.abs().max().item() > 0)
     except Exception as e:  # pragma: no cover - reported to the parent
         import traceback
         res["error"] = traceback.format_exc()
@@ -123,5 +159,7 @@ def test_dp_world2_gradient_parity():
         assert r["no_sync_local_err"] < 1e-5, r
         assert r["ga_err"] < 1e-5, r
         assert r["broadcasts"] == 2, r
+        assert r["mix_err"] < 1e-5 and r["mix_video_zero_r0"], r
+        assert r["enc_err"] < 1e-5 and r["enc_nonzero"], r
     for p in procs:
         assert p.exitcode == 0

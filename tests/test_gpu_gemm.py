@@ -221,16 +221,27 @@ def test_skinny_linear(dev, dtype, M, N, K):
     assert torch.equal(y, y2)
 
 
-@pytest.mark.parametrize("N,K", [(1024, 4096), (1024, 1024), (4096, 1024), (5056, 1024)])
-def test_skinny_k_split_rows_independent(dev, N, K):
-    """The few-row path splits K over more workgroups (partials reduced in a fixed order) with a
-    split count that depends on N and K only: every row equals the same row launched alone, bit
-    for bit (batched beam search == per-utterance search relies on it), and matches fp64."""
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("N,K", [(1024, 4096), (1024, 1024), (4096, 1024), (5056, 1024), (256, 2048)])
+def test_skinny_k_split_rows_independent(dev, N, K, dtype):
+    """The few-row path with its K split (skinny_ws given: S = avsr_gemm_skinny_splits(N, K) > 1
+    workgroup rows, fp32 partials reduced in a fixed order): S depends on N and K only, so every
+    row equals the same row launched alone, bit for bit (batched beam search == per-utterance
+    search relies on it); split and unsplit both match fp64."""
+    S = ops.skinny_splits(N, K)
+    assert S > 1, (N, K, S)
     g = torch.Generator(device="cpu").manual_seed(N + K)
-    x = torch.randn(40, K, generator=g).to(dev)
-    W = (torch.randn(N, K, generator=g) * K ** -0.5).to(dev)
+    x = torch.randn(40, K, generator=g).to(dev, dtype)
+    W = (torch.randn(N, K, generator=g) * K ** -0.5).to(dev, dtype)
     b = torch.randn(N, generator=g).to(dev)
-    y = ops.linear_fwd(x, W, b)
+    r = torch.randn(40, N, generator=g).to(dev, dtype)
+    y = ops.linear_fwd(x, W, b, act=L.ACT_RELU, res=r, skinny_split=True)
+    y1 = ops.linear_fwd(x, W, b, act=L.ACT_RELU, res=r, skinny_split=False)
     for m in (0, 7, 39):
-        assert torch.equal(ops.linear_fwd(x[m:m + 1].contiguous(), W, b)[0], y[m]), m
-    assert _rel(y, x.double() @ W.double().t() + b.double()) < 1e-6
+        one = ops.linear_fwd(x[m:m + 1].contiguous(), W, b, act=L.ACT_RELU, res=r[m:m + 1].contiguous(),
+                             skinny_split=True)
+        assert torch.equal(one[0], y[m]), m
+    ref = torch.relu(x.double() @ W.double().t() + b.double()) + r.double()
+    tol = 1e-6 if dtype == torch.float32 else 1e-2
+    assert _rel(y, ref) < tol and _rel(y1, ref) < tol
+    assert _rel(y, y1.double()) < (1e-6 if dtype == torch.float32 else 1e-2)

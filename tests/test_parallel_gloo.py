@@ -66,3 +66,52 @@ def test_grad_reducer_and_broadcast_world2():
         assert p.exitcode == 0
     for rank, ok_sum, ok_avg, ok_bc in res:
         assert ok_sum and ok_avg and ok_bc, (rank, ok_sum, ok_avg, ok_bc)
+
+
+def _worker_compress(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    try:
+        parallel.init_from_env(backend="gloo")
+        n = 300007
+        gen = torch.Generator().manual_seed(100 + rank)
+        base = torch.randn(n, generator=gen) * torch.logspace(-6, 2, n)    # gradients over 8 decades
+        exact = base.clone()
+        parallel.GradReducer(exact, bucket_bytes=4 * 40000).allreduce(average=True)
+        comp = base.clone()
+        red = parallel.GradReducer(comp, bucket_bytes=4 * 40000, segment=(7, 250000), compress="bf16")
+        red.begin()
+        for off in (200000, 100000, 7):
+            red.ready(off)
+        red.finish(average=True)
+        # bf16 keeps 8 significant bits: each rank's value is rounded once (2^-9 relative), the
+        # two-rank sum once more; relative to the larger of the two summands
+        scale = torch.maximum(base.abs(), (2 * exact - base).abs())
+        err = ((comp - exact).abs() / scale.clamp_min(1e-30)).max().item()
+        differs = not torch.equal(comp, exact)
+        q.put((rank, err, differs))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def test_grad_reducer_bf16_compression_world2():
+    """GradReducer(compress="bf16"): every bucket (decay segment by readiness watermarks, then
+    the tail) is exchanged in bf16 and decompressed into the fp32 arena; the result agrees with
+    the fp32 exchange to bf16 rounding (and is not silently the uncompressed path)."""
+    with pytest.raises(ValueError):
+        parallel.GradReducer(torch.zeros(8), compress="fp8")
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_compress, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, err, differs in res:
+        assert err < 2 ** -7, (rank, err)
+        assert differs, rank
