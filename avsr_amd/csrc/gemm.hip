@@ -84,6 +84,88 @@ __global__ __launch_bounds__(CF::NTH, CF::MINB) void dense_glds_kernel(DenseArgs
   }
 }
 
+// Weight-gradient GEMM (both operands r-contiguous, fp32 out, plain epilogue) with an in-block
+// K split: 8 waves = two groups of 4, each group a 128x128 Cfg tile over its own half of the
+// block's K range with its own LDS ring (2 x 2 x 32 KiB), both groups in lockstep. Group 0 stages
+// its accumulators in LDS, group 1 adds its own (fp32 addition commutes: fixed result), then all
+// 8 waves write the tile: C = alpha*sum + beta*C, or the raw partial into split `sp`'s slab when
+// the block grid also splits K (out-proj: 64 tiles x 4 splits). Two groups per block replace the
+// two-blocks-per-CU split-K of the plain core without a slab round trip through HBM.
+template <class CF>
+__global__ __launch_bounds__(2 * CF::NTH, 1) void wgrad_dual_kernel(DenseArgs a, int tiles_m, int tiles_n) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  static_assert(CF::BM * (CF::BN + 4) * 4 <= 2 * CF::S * CF::STAGE, "reduction tile exceeds the two rings");
+  if (a.stamp != nullptr && threadIdx.x == 0) atomicMin(a.stamp, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+  const int id = gemmg::xcd_remap(blockIdx.x, gridDim.x);
+  int tm, tn, sp;
+  gemmg::tile_of(id, tiles_m, tiles_n, tm, tn, sp);
+  const int m0 = tm * CF::BM, n0 = tn * CF::BN;
+  const int kbeg = sp * a.kchunk, kend = min(a.K, kbeg + a.kchunk);
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int grp = wv >> 2, wave = wv & 3;
+  const int ntile = (kend - kbeg + gemmg::GBK - 1) / gemmg::GBK;
+  const int nk = (ntile + 1) >> 1;                  // per group; group 1's last tile may be empty (zeros)
+  const int gbeg = kbeg + grp * nk * gemmg::GBK, gend = min(kend, gbeg + nk * gemmg::GBK);
+  f32x4 acc[CF::TM][CF::TN];
+  char* ring = smem + grp * (CF::S * CF::STAGE);
+  if (a.a_bytes) {
+    gemmg::BDenseR<CF::BM, CF::NW> la; la.init((const bf16*)a.A, a.a_bytes, a.lda, m0, a.M, gend, wave, lane);
+    gemmg::BDenseR<CF::BN, CF::NW> lb; lb.init((const bf16*)a.B, a.b_bytes, a.ldb, n0, a.N, gend, wave, lane);
+    gemmg::mainloop_glds<CF>(la, lb, gbeg, nk, acc, ring, wave);
+  } else {
+    gemmg::GDenseR<CF::BM, CF::NW> la; la.init((const bf16*)a.A, a.lda, m0, a.M, gend, wave, lane);
+    gemmg::GDenseR<CF::BN, CF::NW> lb; lb.init((const bf16*)a.B, a.ldb, n0, a.N, gend, wave, lane);
+    gemmg::mainloop_glds<CF>(la, lb, gbeg, nk, acc, ring, wave);
+  }
+  // (mainloop_glds ends with a barrier: both rings are free)
+  constexpr int LDR = CF::BN + 4;
+  float* st = (float*)smem;
+  const int wm = wave / CF::WN, wn = wave % CF::WN;
+#pragma unroll
+  for (int i = 0; i < CF::TM; ++i)
+#pragma unroll
+    for (int j = 0; j < CF::TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = wm * 32 * CF::FM + 16 * i + 4 * (lane >> 4) + r, col = wn * 32 * CF::FN + 16 * j + (lane & 15);
+        if (grp == 0) st[row * LDR + col] = acc[i][j][r];
+      }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < CF::TM; ++i)
+#pragma unroll
+    for (int j = 0; j < CF::TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = wm * 32 * CF::FM + 16 * i + 4 * (lane >> 4) + r, col = wn * 32 * CF::FN + 16 * j + (lane & 15);
+        if (grp == 1) st[row * LDR + col] += acc[i][j][r];
+      }
+  __syncthreads();
+  const bool slab = a.sSplit != 0;
+  float* C = slab ? (float*)a.e.C + sp * a.sSplit : (float*)a.e.C;
+  const int64_t ldc = a.e.ldc;
+  const float alpha = slab ? 1.f : a.e.alpha, beta = slab ? 0.f : a.e.beta;
+  constexpr int Q = CF::BN / 4;                      // float4 per tile row
+  for (int c = threadIdx.x; c < CF::BM * Q; c += 2 * CF::NTH) {
+    const int lr = c / Q, lc = (c % Q) * 4, row = m0 + lr, col = n0 + lc;
+    if (row >= a.M || col >= a.N) continue;
+    const f32x4 v = *(const f32x4*)(st + lr * LDR + lc);
+    float* o = C + (int64_t)row * ldc + col;
+    if (col + 4 <= a.N) {
+      f32x4 y = v * alpha;
+      if (beta != 0.f) y += *(const f32x4*)o * beta;
+      *(f32x4*)o = y;
+    } else {
+      for (int q = 0; q < a.N - col; ++q) o[q] = beta != 0.f ? alpha * v[q] + beta * o[q] : alpha * v[q];
+    }
+  }
+  if (a.stamp != nullptr) {
+    __syncthreads();
+    if (threadIdx.x == 0) atomicMax(a.stamp + 1, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+  }
+}
+
 // 256x256 ping-pong core (gemm_pp.h)
 template <typename OutT, bool AK, bool BK>
 __global__ __launch_bounds__(gemmpp::NTH, 1) void dense_pp_kernel(DenseArgs a, int tiles_m, int tiles_n) {
@@ -433,6 +515,28 @@ int skinny_launch(const DenseArgs& a, float* ws, hipStream_t st) {
   return 0;
 }
 
+using CfgDual = gemmg::GCfg<2, 2, 2, 2, 2>;       // per wave group of wgrad_dual_kernel (8 waves, 128 KiB)
+
+// weight-gradient shape (dy^T x: both operands r-contiguous, fp32 C, plain epilogue, one batch):
+// the in-block split-K kernel (AVSR_WGRAD_DUAL=0 keeps the 4-wave core: A/B runs)
+bool wgrad_dual_ok(const avsr_gemm_params* p, int splits, bool slab) {
+  const char* e = getenv("AVSR_WGRAD_DUAL");
+  const bool off = e && e[0] == '0';
+  return !off && !p->a_kmajor && !p->b_kmajor && p->c_f32 && p->batch == 1 && (splits == 1 || slab) && !p->bias &&
+         !p->act && !p->preact && !p->res && !p->gate && p->drop_p == 0.f && !p->epi_bwd && !p->db &&
+         (p->ldc % 4) == 0 && avsr_aligned16(p->C);
+}
+
+int launch_wgrad_dual(const DenseArgs& a, hipStream_t st) {
+  const int tm = (a.M + CfgDual::BM - 1) / CfgDual::BM, tn = (a.N + CfgDual::BN - 1) / CfgDual::BN;
+  const long nwg = (long)tm * tn * a.splits;
+  if (nwg > 0x7fffffffL) return AVSR_E_SHAPE;
+  hipLaunchKernelGGL((wgrad_dual_kernel<CfgDual>), dim3((unsigned)nwg), dim3(2 * CfgDual::NTH),
+                     2 * CfgDual::S * CfgDual::STAGE, st, a, tm, tn);
+  AVSR_CHECK_LAUNCH();
+  return 0;
+}
+
 // forward linears with few rows (AVSR_GEMM_NOSKINNY=1 keeps the tiled cores: A/B comparisons)
 bool skinny_ok(const avsr_gemm_params* p, int splits) {
   static int off = -1;
@@ -522,7 +626,8 @@ extern "C" int avsr_gemm(const avsr_gemm_params* p, void* stream) {
     if (p->dtype == AVSR_F32) return skinny_launch<float, float>(a, sws, st);
     return p->c_f32 ? skinny_launch<bf16, float>(a, sws, st) : skinny_launch<bf16, bf16>(a, sws, st);
   }
-  if (glds) rc = p->c_f32 ? glds_by_layout<float>(p, a, st) : glds_by_layout<bf16>(p, a, st);
+  if (glds && wgrad_dual_ok(p, splits, slab)) rc = launch_wgrad_dual(a, st);
+  else if (glds) rc = p->c_f32 ? glds_by_layout<float>(p, a, st) : glds_by_layout<bf16>(p, a, st);
   else if (p->dtype == AVSR_F32) rc = by_tile<float, float>(p, a, st);
   else if (p->c_f32) rc = by_tile<bf16, float>(p, a, st);
   else rc = by_tile<bf16, bf16>(p, a, st);

@@ -246,11 +246,14 @@ AVSR_DEV void wait_tiles_ahead(bool full) {   // tile t+1 retired: at most tiles
   else wait_vmcnt<0>();
 }
 
+// `wave` = the wave's index inside its CF group (0 .. CF::NW-1): one group of waves per
+// workgroup normally; the in-block split-K weight-gradient kernel runs two groups, each with its
+// own LDS ring at `smem`, in lockstep (the same tile count, so the same barriers)
 template <class CF, class LA, class LB>
-AVSR_DEV void mainloop_glds(const LA& la, const LB& lb, int kbeg, int nk, f32x4 (&acc)[CF::TM][CF::TN], char* smem) {
+AVSR_DEV void mainloop_glds(const LA& la, const LB& lb, int kbeg, int nk, f32x4 (&acc)[CF::TM][CF::TN], char* smem,
+                            int wave) {
   constexpr int S = CF::S, KS = GBK / 32;
   const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave / CF::WN, wn = wave % CF::WN;
 #pragma unroll
   for (int i = 0; i < CF::TM; ++i)
@@ -295,6 +298,11 @@ AVSR_DEV void mainloop_glds(const LA& la, const LB& lb, int kbeg, int nk, f32x4 
     cs = ns;
   }
   __syncthreads();
+}
+
+template <class CF, class LA, class LB>
+AVSR_DEV void mainloop_glds(const LA& la, const LB& lb, int kbeg, int nk, f32x4 (&acc)[CF::TM][CF::TN], char* smem) {
+  mainloop_glds<CF>(la, lb, kbeg, nk, acc, smem, __builtin_amdgcn_readfirstlane(threadIdx.x >> 6));
 }
 
 // Epilogue for a GCfg tile: (1) optional BN column statistics from the accumulators;

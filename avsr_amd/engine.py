@@ -74,15 +74,16 @@ def prioritize_step_stream(device):
 
 
 def wgrad_splitk(M, N, K):
-    """token-dimension split of a weight-gradient GEMM dW[N][K] += dy[M][N]^T x[M][K]: split
-    only when the 128x128 output grid is at or below one block per CU (slab workspace, no
-    atomics)."""
+    """token-dimension split of a weight-gradient GEMM dW[N][K] += dy[M][N]^T x[M][K] over
+    blocks. The library runs weight-gradients as 8-wave blocks that already split their K range
+    between two wave groups (gemm.hip wgrad_dual_kernel, one block per CU), so the block grid is
+    split only when the 128x128 tiles fill less than half the chip (out-proj 1024x1024: 64 tiles
+    x 4), through a slab workspace (no atomics). AVSR_WGRAD_DUAL=0 (A/B): the 4-wave core at two
+    blocks per CU with its 512-block target."""
     tiles = ((N + 127) // 128) * ((K + 127) // 128)
-    forced = os.environ.get("AVSR_WGRAD_SPLIT")          # experiments (tools/gemm_table.py)
-    if forced:
-        return max(1, min(int(forced), M // 256))
-    target = int(os.environ.get("AVSR_WGRAD_TARGET", "512"))   # block target (A/B experiments)
-    return 1 if tiles > target // 2 else max(1, min(16, target // max(tiles, 1), M // 512))
+    if os.environ.get("AVSR_WGRAD_DUAL", "1") == "0":
+        return 1 if tiles > 256 else max(1, min(16, 512 // max(tiles, 1), M // 512))
+    return 1 if tiles >= 128 else max(1, min(16, 256 // max(tiles, 1), M // 1024))
 
 
 def _pad8(n):

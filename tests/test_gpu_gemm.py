@@ -133,6 +133,34 @@ def test_gemm_layouts_bf16(dev, gemm_tile, a_kmajor, b_kmajor, M, N, K, splitk):
         assert err < 8e-3, err
 
 
+@pytest.mark.parametrize("M,N,K,splitk", [(1024, 1024, 6000, 4), (3072, 1024, 6000, 1), (256, 384, 1000, 1),
+                                           (136, 200, 328, 1), (1024, 1024, 1000, 3), (640, 512, 64, 1)])
+def test_wgrad_dual_kernel(dev, monkeypatch, M, N, K, splitk):
+    """Weight-gradient GEMM dW[M][N] = beta*dW + alpha * dy^T x (both operands r-contiguous, the
+    in-block split-K kernel: two wave groups per block over halves of the K range, one LDS
+    reduction; with splitk > 1 also split over blocks into slabs): vs fp64, ragged K (a group
+    whose last tile is empty), ragged M / N edges, beta accumulation; bit-identical run to run;
+    and within fp32 re-association of the 4-wave core (AVSR_WGRAD_DUAL=0)."""
+    g = torch.Generator().manual_seed(M + N + K)
+    dy = torch.randn(K, M, generator=g).to(dev, torch.bfloat16)
+    x = torch.randn(K, N, generator=g).to(dev, torch.bfloat16)
+    C0 = torch.randn(M, N, generator=g).to(dev)
+    ref = 0.5 * (dy.double().t() @ x.double()) + C0.double()
+
+    def run():
+        C = C0.clone()
+        ws = torch.full((ops.slab_ws(1, splitk, M, N),), float("nan"), device=dev) if splitk > 1 else None
+        ops.gemm(dy, x, C, M=M, N=N, K=K, a_kmajor=False, b_kmajor=False, lda=M, ldb=N, ldc=N,
+                 alpha=0.5, beta=1.0, splitk=splitk, ws=ws)
+        return C
+    a, b = run(), run()
+    assert torch.equal(a, b)
+    assert _rel(a, ref) < 1e-5 * (K ** 0.5)
+    monkeypatch.setenv("AVSR_WGRAD_DUAL", "0")
+    c = run()
+    assert _rel(a, c.double()) < 1e-5 * (K ** 0.5)
+
+
 @pytest.mark.gpu
 def test_gemm_batched_strided_bf16(dev, gemm_tile):
     """batch > 1 with operand / output strides (attention-style batched products)."""
