@@ -1182,6 +1182,12 @@ inline bool small_index(const avsr_attn_params* p) {
   return (uint64_t)p->B * p->H * p->Lq * (uint64_t)((p->Lk + 1) / 2) <= 0xFFFFFFFFull;
 }
 
+// XCD-aware block order (blocks b, b + 8 share an XCD): consecutive ids on one XCD
+AVSR_DEV int xcd_id(int orig, int nwg) {
+  const int xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+}
+
 template <typename F> void allow_lds(F* f) {
   static bool done = false;                     // once per kernel instantiation
   if (!done) {
@@ -1190,6 +1196,181 @@ template <typename F> void allow_lds(F* f) {
   }
 }
 }  // namespace res
+
+// =====================================================================================
+// Query-tiled kernels with K/V streamed through an LDS-DMA ring (bf16, non-causal, Lq >= 128:
+// the encoder's self-attention). One workgroup = 4 waves x 32 queries of one (batch, head);
+// grid = B*H x ceil(Lq / 128), the q-blocks of one head adjacent in the XCD-remapped order (they
+// share that head's K/V in one L2). 64-key tiles of K and V go HBM/L2 -> LDS by
+// buffer_load ... lds (no staging registers, no VALU) into a 3-stage ring of 16 KiB stages, two
+// tiles in flight: 48 KiB per workgroup, so three workgroups share a CU (12 waves) and one's
+// load / store phases run beside the others' compute — the resident kernels hold a whole head
+// (110 KiB) per CU and serialise load -> compute -> store.
+// LDS images are unpadded [64][64] bf16 (128-B rows), swizzled on the DMA's global side:
+//   K (mfma32 A fragment, key on the lane, ds_read_b128): chunk' = chunk ^ ((row >> 1) & 7);
+//   V (transposed fragment, ds_read_b64_tr_b16):         chunk' = chunk ^ (((row >> 1) & 1) << 2);
+// both conflict-free, and every lane's fragment offsets are loop-invariant (a tile base plus
+// compile-time row-block offsets).
+namespace sq {
+using namespace res;
+constexpr int KT = 64;                   // keys per tile
+constexpr int NS = 3;                    // ring stages
+constexpr int IMGB = KT * 128;           // bytes of one [64][64] bf16 image
+constexpr int STAGEB = 2 * IMGB;         // K image | V image
+constexpr int LDSB = NS * STAGEB;        // 48 KiB (>= the 4 waves' 32 x 65 fp32 store slabs)
+static_assert(4 * 32 * 65 * 4 <= LDSB, "store slabs exceed the ring");
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef short s4v __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s4v lds_s4v;
+
+AVSR_DEV __amdgpu_buffer_rsrc_t rsrc(const void* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+// one wave-instruction: 64 lanes x 16 B -> 1 KiB of LDS at lds_wave_base (see gemm_glds.h
+// bglds16: inline asm so the compiler's waitcnt pass does not drain the ring before each
+// transposed LDS read; the ring is ordered by the explicit vmcnt waits + barriers below)
+AVSR_DEV void dma16(__amdgpu_buffer_rsrc_t r, uint32_t voff, char* lds_wave_base) {
+  const uint32_t m = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_void_t*)lds_wave_base);
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" ::"s"(m), "v"(voff), "s"(r)
+               : "memory", "m0");
+}
+template <int N> AVSR_DEV void vmwait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+
+// the DMA pieces of one tile of one (b, h): wave w moves 8-row pieces 2w, 2w+1 of K and of V
+struct TileDma {
+  const bf16* kg; const bf16* vg; int64_t ldk, ldv; int Lk;
+  uint32_t ko[2], vo[2];                 // per-lane byte offsets inside a tile (row, swizzled chunk)
+  AVSR_DEV void init(const bf16* k, int64_t ldk_, const bf16* v, int64_t ldv_, int Lk_, int w, int l) {
+    kg = k; vg = v; ldk = ldk_; ldv = ldv_; Lk = Lk_;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int row = 8 * (2 * w + i) + (l >> 3), ch = l & 7;
+      ko[i] = (uint32_t)((row * ldk + ((ch ^ ((row >> 1) & 7)) * 8)) * 2);
+      vo[i] = (uint32_t)((row * ldv + ((ch ^ (((row >> 1) & 1) << 2)) * 8)) * 2);
+    }
+  }
+  // rows of tile t past Lk fall outside the buffer extent: the DMA writes zeros for them
+  AVSR_DEV void issue(char* stage, int t, int w) const {
+    const int r0 = t * KT, nr = min(KT, Lk - r0);
+    const __amdgpu_buffer_rsrc_t rk = rsrc(kg + (int64_t)r0 * ldk, (uint32_t)(((nr - 1) * ldk + DH) * 2));
+    const __amdgpu_buffer_rsrc_t rv = rsrc(vg + (int64_t)r0 * ldv, (uint32_t)(((nr - 1) * ldv + DH) * 2));
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      dma16(rk, ko[i], stage + (2 * w + i) * 1024);
+      dma16(rv, vo[i], stage + IMGB + (2 * w + i) * 1024);
+    }
+  }
+};
+
+__global__ __launch_bounds__(256, 3) void attn_fwd_kernel(AttnArgs a, int nqb) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int id = xcd_id(blockIdx.x, gridDim.x);
+  const int bh = id / nqb, qb = id - bh * nqb, b = bh / a.H, h = bh % a.H;
+  const int tid = threadIdx.x, w = __builtin_amdgcn_readfirstlane(tid >> 6), l = tid & 63, c = l & 31, hh = l >> 5;
+  const int q0 = qb * 128 + w * 32, qi = q0 + c;
+  TileDma dma;
+  dma.init((const bf16*)a.k + (int64_t)b * a.Lk * a.ldk + h * DH, a.ldk,
+           (const bf16*)a.v + (int64_t)b * a.Lk * a.ldv + h * DH, a.ldv, a.Lk, w, l);
+  const int klen = a.klen ? min(a.klen[b], a.Lk) : a.Lk;
+  const int nt = (klen + KT - 1) / KT;
+  // tile 0's DMA, then the Q fragments; an empty asm reading them makes the compiler's own
+  // wait for these loads (vmcnt(0), which also covers tile 0) happen here, once, instead of at
+  // their first use inside the tile loop, where it would drain the ring's prefetch every tile
+  if (nt > 0) dma.issue(smem, 0, w);
+  const bf16* Q = (const bf16*)a.q + (int64_t)b * a.Lq * a.ldq + h * DH;
+  bf16x8 qf[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) qf[s] = ldrow_sel(Q, a.ldq, qi, a.Lq, s * 16 + 8 * hh);
+#pragma unroll
+  for (int s = 0; s < 4; ++s) asm volatile("" ::"v"(qf[s]));
+  if (nt > 1) dma.issue(smem + STAGEB, 1, w);
+  // loop-invariant fragment offsets: K rows c (+32 for the second key block), d-chunk 2s + hh;
+  // V rows 4hh + (i >> 2) (+8, + the 16-key block), columns 16g + 4(i & 3) (+32 for d 32..63)
+  uint32_t kof[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) kof[s] = c * 128 + (((2 * s + hh) ^ ((c >> 1) & 7)) << 4);
+  const int vi = l & 15, vg = (l >> 4) & 1;
+  const int vcc = 2 * vg + ((vi & 3) >> 1), vf = ((vi >> 3) & 1) << 2;
+  const uint32_t vrow = (4 * hh + (vi >> 2)) * 128 + (vi & 1) * 8;
+  const uint32_t vof0 = vrow + ((vcc ^ vf) << 4), vof1 = vrow + ((vcc ^ 4 ^ vf) << 4);
+  const float sl2 = a.scale * LOG2E;
+  const AttnDrop drop(a.drop_p, a.seed, a.B, a.H, a.Lq, a.Lk);
+  const uint32_t rowG = ((uint32_t)bh * (uint32_t)a.Lq + (uint32_t)min(qi, a.Lq - 1)) * drop.npair * GOLD;
+  f32x16 o0, o1;
+  zacc(o0); zacc(o1);
+  float lsum = 0.f, mb = -INFINITY;          // lazy reference max, as res::attn_fwd_kernel
+  int cs = 0;                                // stage of tile t
+  for (int t = 0; t < nt; ++t) {
+    if (t + 1 < nt) vmwait<4>(); else vmwait<0>();
+    __builtin_amdgcn_s_barrier();            // tile t visible; every wave is done with tile t-1
+    asm volatile("" ::: "memory");
+    if (t + 2 < nt) dma.issue(smem + (cs == 0 ? 2 : cs - 1) * STAGEB, t + 2, w);
+    const char* Ks = smem + cs * STAGEB;
+    const char* Vs = Ks + IMGB;
+    f32x16 s0, s1;
+    zacc(s0); zacc(s1);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      s0 = mfma32(*(const bf16x8*)(Ks + kof[s]), qf[s], s0);
+      s1 = mfma32(*(const bf16x8*)(Ks + 4096 + kof[s]), qf[s], s1);
+    }
+    const int k0 = t * KT;
+    if (k0 + KT > klen) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        s0[r] = k0 + qrow(r, hh) < klen ? s0[r] : -INFINITY;
+        s1[r] = k0 + 32 + qrow(r, hh) < klen ? s1[r] : -INFINITY;
+      }
+    }
+    float mt = fmaxf(s0[0], s1[0]);
+#pragma unroll
+    for (int r = 1; r < 16; ++r) mt = fmaxf(mt, fmaxf(s0[r], s1[r]));
+    mt = fmaxf(mt, __shfl_xor(mt, 32, 64)) * sl2;
+    const bool grow = mt > mb + 8.f;
+    if (__any(grow)) {
+      const float alpha = grow ? (mb == -INFINITY ? 0.f : fexp2(mb - mt)) : 1.f;
+      mb = grow ? mt : mb;
+      lsum *= alpha;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) { o0[r] *= alpha; o1[r] *= alpha; }
+    }
+    const float mbu = mb == -INFINITY ? 0.f : mb;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      s0[r] = fexp2(fmaf(s0[r], sl2, -mbu));
+      s1[r] = fexp2(fmaf(s1[r], sl2, -mbu));
+      lsum += s0[r] + s1[r];
+    }
+    if (a.drop_p > 0.f) {
+      drop_tile_sel(s0, rowG + (uint32_t)(k0 >> 1) * GOLD, drop, hh);
+      drop_tile_sel(s1, rowG + (uint32_t)((k0 + 32) >> 1) * GOLD, drop, hh);
+    }
+    const bf16x8 p0a = accb(s0, 0), p0b = accb(s0, 1), p1a = accb(s1, 0), p1b = accb(s1, 1);
+    auto vt = [&](int r0, uint32_t vof) -> bf16x8 {      // rows r0 + {4hh + 0..3, +8}
+      union { s4v s[2]; bf16x8 x; } u;
+      u.s[0] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4v*)(Vs + r0 * 128 + vof));
+      u.s[1] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4v*)(Vs + r0 * 128 + 1024 + vof));
+      return u.x;
+    };
+    o0 = mfma32(vt(0, vof0), p0a, o0);
+    o1 = mfma32(vt(0, vof1), p0a, o1);
+    o0 = mfma32(vt(16, vof0), p0b, o0);
+    o1 = mfma32(vt(16, vof1), p0b, o1);
+    o0 = mfma32(vt(32, vof0), p1a, o0);
+    o1 = mfma32(vt(32, vof1), p1a, o1);
+    o0 = mfma32(vt(48, vof0), p1b, o0);
+    o1 = mfma32(vt(48, vof1), p1b, o1);
+    cs = cs + 1 == NS ? 0 : cs + 1;
+  }
+  lsum += __shfl_xor(lsum, 32, 64);
+  if (hh == 0 && qi < a.Lq) a.lse[(int64_t)bh * a.Lq + qi] = lsum > 0.f ? (mb + log2f(lsum)) * LN2 : -INFINITY;
+  __syncthreads();                           // the ring is free: reuse it as the store slabs
+  const float inv = lsum > 0.f ? (a.drop_p > 0.f ? drop.scale : 1.f) / lsum : 0.f;
+  bf16* O = (bf16*)a.o + ((int64_t)b * a.Lq + q0) * a.ldo + h * DH;
+  store_t<bf16>(o0, o1, inv, (float*)smem + w * 32 * 65, O, a.ldo, a.Lq - q0);
+}
+}  // namespace sq
 
 AttnArgs args(const avsr_attn_params* p) {
   AttnArgs a;
@@ -1217,11 +1398,27 @@ extern "C" int avsr_debug_attn_stamps(unsigned long long* buf) {
   return (int)hipMemcpyToSymbol(HIP_SYMBOL(res::g_stamps), &buf, sizeof(buf));
 }
 
+// query-tiled streamed kernels for the encoder's self-attention (AVSR_ATTN_SQ=0: the resident
+// kernels, A/B runs)
+static bool sq_enabled() {
+  const char* e = getenv("AVSR_ATTN_SQ");
+  return !(e && e[0] == '0');
+}
+
 extern "C" int avsr_attn_fwd(const avsr_attn_params* p, void* stream) {
   int rc = check(p);
   if (rc) return rc;
   if (p->B * p->H == 0 || p->Lq == 0) return 0;
   AttnArgs a = args(p);
+  if (p->dtype == AVSR_BF16 && !p->causal && p->Lq >= 128 && res::small_index(p) && sq_enabled() &&
+      (p->ldk % 8) == 0 && (p->ldv % 8) == 0) {
+    const int nqb = (p->Lq + 127) / 128;
+    const long nwg = (long)p->B * p->H * nqb;
+    if (nwg > 0x7fffffffL) return AVSR_E_SHAPE;
+    hipLaunchKernelGGL(sq::attn_fwd_kernel, dim3((unsigned)nwg), dim3(256), sq::LDSB, (hipStream_t)stream, a, nqb);
+    AVSR_CHECK_LAUNCH();
+    return 0;
+  }
   if (p->dtype == AVSR_BF16 && p->Lk <= res::MAXR && res::small_index(p)) {
     const int nw = res::nwaves(p->Lq);
     const size_t lds = std::max(res::img_lds(p->Lk), res::slab_lds(nw));

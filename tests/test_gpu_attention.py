@@ -38,6 +38,8 @@ CASES = [
     (2, 2, 41, 41, None, True),
     (3, 2, 41, 150, [150, 77, 129], False),
     (2, 16, 375, 375, [375, 301], False),
+    (1, 2, 520, 520, [517], False),          # Lk > 384: streamed kernels only
+    (2, 3, 200, 130, [130, 65], False),      # cross-shaped, two q-blocks, the last one partial
 ]
 
 
@@ -180,3 +182,30 @@ def test_attention_dropout_bf16(dev):
     ops.attn_bwd(db, qb, kb, vb, o, lse, None, dk, dv, delta, B=B, H=H, Lq=L, Lk=L, scale=0.125, drop_p=p,
                  seed=seed, dq=dqb)
     assert _rel(dqb, qr.grad) < 3e-2
+
+
+@pytest.mark.parametrize("B,H,L,klen", [(2, 16, 375, [375, 301]), (3, 2, 200, [200, 129, 64])])
+def test_attention_sq_matches_resident(dev, monkeypatch, B, H, L, klen):
+    """The query-tiled forward (K/V streamed through the LDS-DMA ring, sq::attn_fwd_kernel)
+    against the resident-K/V forward on the same bf16 inputs with dropout: the same dropout
+    mask (zero pattern of P' through one-hot V rows is covered by test_attention_dropout_bf16;
+    here every output row agrees to bf16 rounding of P) and the same log-sum-exp."""
+    D = H * 64
+    g = torch.Generator().manual_seed(L + H)
+    bf = torch.bfloat16
+    qkv = torch.randn(B * L, 3 * D, generator=g).to(dev, bf)
+    q, k, v = qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:]
+    kl = torch.tensor(klen, dtype=torch.int32, device=dev)
+
+    def run():
+        o = torch.empty(B * L, D, device=dev, dtype=bf)
+        lse = torch.empty(B, H, L, device=dev)
+        ops.attn_fwd(q, k, v, o, lse, B=B, H=H, Lq=L, Lk=L, klen=kl, scale=0.125, drop_p=0.1, seed=99)
+        return o, lse
+    o1, l1 = run()
+    o1b, l1b = run()
+    assert torch.equal(o1, o1b) and torch.equal(l1, l1b)
+    monkeypatch.setenv("AVSR_ATTN_SQ", "0")
+    o0, l0 = run()
+    assert _rel(o1, o0) < 1e-2
+    assert (l1 - l0).abs().max().item() < 1e-4
