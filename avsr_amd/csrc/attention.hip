@@ -1198,102 +1198,150 @@ template <typename F> void allow_lds(F* f) {
 }  // namespace res
 
 // =====================================================================================
-// Query-tiled kernels with K/V streamed through an LDS-DMA ring (bf16, non-causal, Lq >= 128:
-// the encoder's self-attention). One workgroup = 4 waves x 32 queries of one (batch, head);
-// grid = B*H x ceil(Lq / 128), the q-blocks of one head adjacent in the XCD-remapped order (they
-// share that head's K/V in one L2). 64-key tiles of K and V go HBM/L2 -> LDS by
-// buffer_load ... lds (no staging registers, no VALU) into a 3-stage ring of 16 KiB stages, two
-// tiles in flight: 48 KiB per workgroup, so three workgroups share a CU (12 waves) and one's
-// load / store phases run beside the others' compute — the resident kernels hold a whole head
-// (110 KiB) per CU and serialise load -> compute -> store.
-// LDS images are unpadded [64][64] bf16 (128-B rows), swizzled on the DMA's global side:
-//   K (mfma32 A fragment, key on the lane, ds_read_b128): chunk' = chunk ^ ((row >> 1) & 7);
-//   V (transposed fragment, ds_read_b64_tr_b16):         chunk' = chunk ^ (((row >> 1) & 1) << 2);
-// both conflict-free, and every lane's fragment offsets are loop-invariant (a tile base plus
-// compile-time row-block offsets).
+// Tiled kernels with the streamed operand pair going through an LDS-DMA ring (bf16, non-causal,
+// Lq, Lk >= 128: the encoder's self-attention). One workgroup = 4 waves x 32 rows of its own
+// dimension of one (batch, head); grid = B*H x ceil(rows / 128) in XCD-remapped order (the
+// blocks of one head adjacent: they share its streamed operands in one L2). 64-row tiles of the
+// other dimension go HBM/L2 -> LDS by buffer_load ... lds (no staging registers, no VALU) into
+// a 3-stage ring (two tiles in flight), ~48 KiB per workgroup, so three workgroups share a CU
+// (12 waves) and one's load / store phases run beside the others' compute (the resident
+// kernels hold a whole head, 110 KiB, per CU and serialise load -> compute -> store).
+//   forward: stream K, V;   dQ: stream K, V (computes delta = rowsum(dO * O), runs first);
+//   dK / dV: stream Q, dO and the 64 lse / delta values of each tile.
+// LDS images are unpadded [64][64] bf16 (128-B rows) whose 16-byte chunk c of row r sits at
+// c ^ swz(r), swz(r) = g ^ ((g & 1) << 2), g = (r >> 1) & 7 (applied on the DMA's global side):
+// conflict-free for both fragment forms — ds_read_b128 rows on the lanes (every 16-lane bank
+// group meets each (row parity, swz) once) and ds_read_b64_tr_b16 transposed reads (rows
+// 4m, 4m + 2 land in opposite 64-B halves) — and every lane's fragment offsets are
+// loop-invariant (tile base + compile-time row-block offsets).
 namespace sq {
 using namespace res;
-constexpr int KT = 64;                   // keys per tile
+constexpr int KT = 64;                   // rows per streamed tile
 constexpr int NS = 3;                    // ring stages
 constexpr int IMGB = KT * 128;           // bytes of one [64][64] bf16 image
-constexpr int STAGEB = 2 * IMGB;         // K image | V image
-constexpr int LDSB = NS * STAGEB;        // 48 KiB (>= the 4 waves' 32 x 65 fp32 store slabs)
-static_assert(4 * 32 * 65 * 4 <= LDSB, "store slabs exceed the ring");
+constexpr int STAGEB = 2 * IMGB;         // two images (K | V, or Q | dO)
+constexpr int STAGEB_F = STAGEB + 2 * KT * 4;   // + lse | delta of the tile (dK / dV kernel)
+static_assert(4 * 32 * 65 * 4 <= NS * STAGEB, "store slabs exceed the ring");
 
 typedef __attribute__((address_space(3))) void lds_void_t;
 typedef short s4v __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) s4v lds_s4v;
 
+AVSR_DEV int swz(int row) { const int g = (row >> 1) & 7; return g ^ ((g & 1) << 2); }
 AVSR_DEV __amdgpu_buffer_rsrc_t rsrc(const void* base, uint32_t bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
 }
-// one wave-instruction: 64 lanes x 16 B -> 1 KiB of LDS at lds_wave_base (see gemm_glds.h
-// bglds16: inline asm so the compiler's waitcnt pass does not drain the ring before each
-// transposed LDS read; the ring is ordered by the explicit vmcnt waits + barriers below)
+// one wave-instruction: 64 lanes x 16 B (x4: 4 B) -> 1 KiB (256 B) of LDS at lds_wave_base.
+// Inline asm as gemm_glds.h bglds16: the compiler's waitcnt pass would otherwise drain the
+// ring before each transposed LDS read; the ring is ordered by explicit vmcnt waits + barriers.
 AVSR_DEV void dma16(__amdgpu_buffer_rsrc_t r, uint32_t voff, char* lds_wave_base) {
   const uint32_t m = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_void_t*)lds_wave_base);
   asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" ::"s"(m), "v"(voff), "s"(r)
                : "memory", "m0");
 }
+AVSR_DEV void dma4(__amdgpu_buffer_rsrc_t r, uint32_t voff, char* lds_wave_base) {
+  const uint32_t m = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_void_t*)lds_wave_base);
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dword %1, %2, 0 offen lds" ::"s"(m), "v"(voff), "s"(r)
+               : "memory", "m0");
+}
 template <int N> AVSR_DEV void vmwait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
 
-// the DMA pieces of one tile of one (b, h): wave w moves 8-row pieces 2w, 2w+1 of K and of V
-struct TileDma {
-  const bf16* kg; const bf16* vg; int64_t ldk, ldv; int Lk;
-  uint32_t ko[2], vo[2];                 // per-lane byte offsets inside a tile (row, swizzled chunk)
-  AVSR_DEV void init(const bf16* k, int64_t ldk_, const bf16* v, int64_t ldv_, int Lk_, int w, int l) {
-    kg = k; vg = v; ldk = ldk_; ldv = ldv_; Lk = Lk_;
+// per-lane byte offsets of the two fragment forms inside an image
+struct FragOff {
+  uint32_t row[4];       // b128 fragment, row on the lane: row c (+4096: rows 32..63), d-chunk 2s + hh
+  uint32_t tr[2][2];     // transposed fragment of a 16-row block (+ r0 * 128): [d half][second 8 rows]
+  AVSR_DEV void init(int l) {
+    const int c = l & 31, hh = l >> 5, i = l & 15, gl = (l >> 4) & 1;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) row[s] = c * 128 + (((2 * s + hh) ^ swz(c)) << 4);
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int R = 4 * hh + (i >> 2) + 8 * e, ch = 4 * cb + 2 * gl + ((i & 3) >> 1);
+        tr[cb][e] = R * 128 + ((ch ^ swz(R)) << 4) + (i & 1) * 8;
+      }
+  }
+};
+AVSR_DEV bf16x8 ldA(const char* img, uint32_t off) { return *(const bf16x8*)(img + off); }
+// lane l: X^T[d = 32 cb + (l & 31)][rows r0 + 4hh + {0..3, 8..11}] (see v2::rdT)
+AVSR_DEV bf16x8 ldT(const char* img, int r0, const FragOff& f, int cb) {
+  union { s4v s[2]; bf16x8 x; } u;
+  u.s[0] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4v*)(img + r0 * 128 + f.tr[cb][0]));
+  u.s[1] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4v*)(img + r0 * 128 + f.tr[cb][1]));
+  return u.x;
+}
+
+// the DMA pieces of one tile: wave w moves 8-row pieces 2w, 2w+1 of both images; with fp32
+// row arrays (lse, delta) waves 0 / 1 also move the tile's 64 values of one each
+struct Ring {
+  const bf16* s0; const bf16* s1; int64_t ld0, ld1; int n;
+  const float* f0; const float* f1;
+  uint32_t o0[2], o1[2];
+  static constexpr int DMAS = 4;         // per wave per tile (+1 on waves 0, 1 with arrays)
+  AVSR_DEV void init(const bf16* a, int64_t la, const bf16* b, int64_t lb, int n_, const float* fa, const float* fb,
+                     int w, int l) {
+    s0 = a; s1 = b; ld0 = la; ld1 = lb; n = n_; f0 = fa; f1 = fb;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      const int row = 8 * (2 * w + i) + (l >> 3), ch = l & 7;
-      ko[i] = (uint32_t)((row * ldk + ((ch ^ ((row >> 1) & 7)) * 8)) * 2);
-      vo[i] = (uint32_t)((row * ldv + ((ch ^ (((row >> 1) & 1) << 2)) * 8)) * 2);
+      const int row = 8 * (2 * w + i) + (l >> 3), ch = (l & 7) ^ swz(row);
+      o0[i] = (uint32_t)((row * ld0 + ch * 8) * 2);
+      o1[i] = (uint32_t)((row * ld1 + ch * 8) * 2);
     }
   }
-  // rows of tile t past Lk fall outside the buffer extent: the DMA writes zeros for them
-  AVSR_DEV void issue(char* stage, int t, int w) const {
-    const int r0 = t * KT, nr = min(KT, Lk - r0);
-    const __amdgpu_buffer_rsrc_t rk = rsrc(kg + (int64_t)r0 * ldk, (uint32_t)(((nr - 1) * ldk + DH) * 2));
-    const __amdgpu_buffer_rsrc_t rv = rsrc(vg + (int64_t)r0 * ldv, (uint32_t)(((nr - 1) * ldv + DH) * 2));
+  // rows of tile t past n lie outside the buffer extent: the DMA writes zeros for them
+  AVSR_DEV void issue(char* stage, int t, int w, int l) const {
+    const int r0 = t * KT, nr = min(KT, n - r0);
+    const __amdgpu_buffer_rsrc_t ra = rsrc(s0 + (int64_t)r0 * ld0, (uint32_t)(((nr - 1) * ld0 + DH) * 2));
+    const __amdgpu_buffer_rsrc_t rb = rsrc(s1 + (int64_t)r0 * ld1, (uint32_t)(((nr - 1) * ld1 + DH) * 2));
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      dma16(rk, ko[i], stage + (2 * w + i) * 1024);
-      dma16(rv, vo[i], stage + IMGB + (2 * w + i) * 1024);
+      dma16(ra, o0[i], stage + (2 * w + i) * 1024);
+      dma16(rb, o1[i], stage + IMGB + (2 * w + i) * 1024);
     }
+    if (f0 != nullptr && w < 2) {
+      const float* f = w == 0 ? f0 : f1;
+      dma4(rsrc(f + r0, (uint32_t)(nr * 4)), (uint32_t)(l * 4), stage + STAGEB + w * KT * 4);
+    }
+  }
+  // wait until tile t has landed (tile t+1 may still be in flight), then the workgroup barrier
+  AVSR_DEV void arrive(int t, int nt, int w) const {
+    const bool more = t + 1 < nt;
+    if (f0 != nullptr && w < 2) { if (more) vmwait<DMAS + 1>(); else vmwait<0>(); }
+    else { if (more) vmwait<DMAS>(); else vmwait<0>(); }
+    __builtin_amdgcn_s_barrier();          // tile t visible; every wave is done with tile t-1
+    asm volatile("" ::: "memory");
   }
 };
 
+AVSR_DEV int next_stage(int s) { return s + 1 == NS ? 0 : s + 1; }
+AVSR_DEV int prev_stage(int s) { return s == 0 ? NS - 1 : s - 1; }
+
+// ----------------------------------------------------------------------------- forward
 __global__ __launch_bounds__(256, 3) void attn_fwd_kernel(AttnArgs a, int nqb) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int id = xcd_id(blockIdx.x, gridDim.x);
   const int bh = id / nqb, qb = id - bh * nqb, b = bh / a.H, h = bh % a.H;
   const int tid = threadIdx.x, w = __builtin_amdgcn_readfirstlane(tid >> 6), l = tid & 63, c = l & 31, hh = l >> 5;
   const int q0 = qb * 128 + w * 32, qi = q0 + c;
-  TileDma dma;
-  dma.init((const bf16*)a.k + (int64_t)b * a.Lk * a.ldk + h * DH, a.ldk,
-           (const bf16*)a.v + (int64_t)b * a.Lk * a.ldv + h * DH, a.ldv, a.Lk, w, l);
+  Ring ring;
+  ring.init((const bf16*)a.k + (int64_t)b * a.Lk * a.ldk + h * DH, a.ldk,
+            (const bf16*)a.v + (int64_t)b * a.Lk * a.ldv + h * DH, a.ldv, a.Lk, nullptr, nullptr, w, l);
   const int klen = a.klen ? min(a.klen[b], a.Lk) : a.Lk;
   const int nt = (klen + KT - 1) / KT;
-  // tile 0's DMA, then the Q fragments; an empty asm reading them makes the compiler's own
-  // wait for these loads (vmcnt(0), which also covers tile 0) happen here, once, instead of at
-  // their first use inside the tile loop, where it would drain the ring's prefetch every tile
-  if (nt > 0) dma.issue(smem, 0, w);
+  // tile 0's DMA, then the Q fragments; the empty asm reading them makes the compiler's own wait
+  // for these loads (vmcnt(0), covering tile 0 too) happen here once instead of at their first
+  // use inside the tile loop, where it would drain the ring's prefetch every tile
+  if (nt > 0) ring.issue(smem, 0, w, l);
   const bf16* Q = (const bf16*)a.q + (int64_t)b * a.Lq * a.ldq + h * DH;
   bf16x8 qf[4];
 #pragma unroll
   for (int s = 0; s < 4; ++s) qf[s] = ldrow_sel(Q, a.ldq, qi, a.Lq, s * 16 + 8 * hh);
 #pragma unroll
   for (int s = 0; s < 4; ++s) asm volatile("" ::"v"(qf[s]));
-  if (nt > 1) dma.issue(smem + STAGEB, 1, w);
-  // loop-invariant fragment offsets: K rows c (+32 for the second key block), d-chunk 2s + hh;
-  // V rows 4hh + (i >> 2) (+8, + the 16-key block), columns 16g + 4(i & 3) (+32 for d 32..63)
-  uint32_t kof[4];
-#pragma unroll
-  for (int s = 0; s < 4; ++s) kof[s] = c * 128 + (((2 * s + hh) ^ ((c >> 1) & 7)) << 4);
-  const int vi = l & 15, vg = (l >> 4) & 1;
-  const int vcc = 2 * vg + ((vi & 3) >> 1), vf = ((vi >> 3) & 1) << 2;
-  const uint32_t vrow = (4 * hh + (vi >> 2)) * 128 + (vi & 1) * 8;
-  const uint32_t vof0 = vrow + ((vcc ^ vf) << 4), vof1 = vrow + ((vcc ^ 4 ^ vf) << 4);
+  if (nt > 1) ring.issue(smem + STAGEB, 1, w, l);
+  FragOff fo;
+  fo.init(l);
   const float sl2 = a.scale * LOG2E;
   const AttnDrop drop(a.drop_p, a.seed, a.B, a.H, a.Lq, a.Lk);
   const uint32_t rowG = ((uint32_t)bh * (uint32_t)a.Lq + (uint32_t)min(qi, a.Lq - 1)) * drop.npair * GOLD;
@@ -1302,18 +1350,16 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_kernel(AttnArgs a, int nqb) {
   float lsum = 0.f, mb = -INFINITY;          // lazy reference max, as res::attn_fwd_kernel
   int cs = 0;                                // stage of tile t
   for (int t = 0; t < nt; ++t) {
-    if (t + 1 < nt) vmwait<4>(); else vmwait<0>();
-    __builtin_amdgcn_s_barrier();            // tile t visible; every wave is done with tile t-1
-    asm volatile("" ::: "memory");
-    if (t + 2 < nt) dma.issue(smem + (cs == 0 ? 2 : cs - 1) * STAGEB, t + 2, w);
+    ring.arrive(t, nt, w);
+    if (t + 2 < nt) ring.issue(smem + prev_stage(cs) * STAGEB, t + 2, w, l);
     const char* Ks = smem + cs * STAGEB;
     const char* Vs = Ks + IMGB;
     f32x16 s0, s1;
     zacc(s0); zacc(s1);
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-      s0 = mfma32(*(const bf16x8*)(Ks + kof[s]), qf[s], s0);
-      s1 = mfma32(*(const bf16x8*)(Ks + 4096 + kof[s]), qf[s], s1);
+      s0 = mfma32(ldA(Ks, fo.row[s]), qf[s], s0);
+      s1 = mfma32(ldA(Ks + 4096, fo.row[s]), qf[s], s1);
     }
     const int k0 = t * KT;
     if (k0 + KT > klen) {
@@ -1347,21 +1393,15 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_kernel(AttnArgs a, int nqb) {
       drop_tile_sel(s1, rowG + (uint32_t)((k0 + 32) >> 1) * GOLD, drop, hh);
     }
     const bf16x8 p0a = accb(s0, 0), p0b = accb(s0, 1), p1a = accb(s1, 0), p1b = accb(s1, 1);
-    auto vt = [&](int r0, uint32_t vof) -> bf16x8 {      // rows r0 + {4hh + 0..3, +8}
-      union { s4v s[2]; bf16x8 x; } u;
-      u.s[0] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4v*)(Vs + r0 * 128 + vof));
-      u.s[1] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4v*)(Vs + r0 * 128 + 1024 + vof));
-      return u.x;
-    };
-    o0 = mfma32(vt(0, vof0), p0a, o0);
-    o1 = mfma32(vt(0, vof1), p0a, o1);
-    o0 = mfma32(vt(16, vof0), p0b, o0);
-    o1 = mfma32(vt(16, vof1), p0b, o1);
-    o0 = mfma32(vt(32, vof0), p1a, o0);
-    o1 = mfma32(vt(32, vof1), p1a, o1);
-    o0 = mfma32(vt(48, vof0), p1b, o0);
-    o1 = mfma32(vt(48, vof1), p1b, o1);
-    cs = cs + 1 == NS ? 0 : cs + 1;
+    o0 = mfma32(ldT(Vs, 0, fo, 0), p0a, o0);
+    o1 = mfma32(ldT(Vs, 0, fo, 1), p0a, o1);
+    o0 = mfma32(ldT(Vs, 16, fo, 0), p0b, o0);
+    o1 = mfma32(ldT(Vs, 16, fo, 1), p0b, o1);
+    o0 = mfma32(ldT(Vs, 32, fo, 0), p1a, o0);
+    o1 = mfma32(ldT(Vs, 32, fo, 1), p1a, o1);
+    o0 = mfma32(ldT(Vs, 48, fo, 0), p1b, o0);
+    o1 = mfma32(ldT(Vs, 48, fo, 1), p1b, o1);
+    cs = next_stage(cs);
   }
   lsum += __shfl_xor(lsum, 32, 64);
   if (hh == 0 && qi < a.Lq) a.lse[(int64_t)bh * a.Lq + qi] = lsum > 0.f ? (mb + log2f(lsum)) * LN2 : -INFINITY;
@@ -1369,6 +1409,207 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_kernel(AttnArgs a, int nqb) {
   const float inv = lsum > 0.f ? (a.drop_p > 0.f ? drop.scale : 1.f) / lsum : 0.f;
   bf16* O = (bf16*)a.o + ((int64_t)b * a.Lq + q0) * a.ldo + h * DH;
   store_t<bf16>(o0, o1, inv, (float*)smem + w * 32 * 65, O, a.ldo, a.Lq - q0);
+}
+
+// ----------------------------------------------------------------------------- dQ (+ delta)
+// per wave 32 queries on the lanes (Q, dO rows in registers; delta = rowsum(dO * O) computed
+// from this lane's O / dO halves and published for the dK / dV kernel, which runs after);
+// 64-key tiles of K, V: S^T = K Q^T, dP^T = V dO^T, dQ^T += K^T dS^T
+template <typename OutT>
+__global__ __launch_bounds__(256, 3) void attn_bwd_dq_kernel(AttnArgs a, int nqb, OutT* dq, int64_t lddq) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int id = xcd_id(blockIdx.x, gridDim.x);
+  const int bh = id / nqb, qb = id - bh * nqb, b = bh / a.H, h = bh % a.H;
+  const int tid = threadIdx.x, w = __builtin_amdgcn_readfirstlane(tid >> 6), l = tid & 63, c = l & 31, hh = l >> 5;
+  const int q0 = qb * 128 + w * 32, qi = q0 + c;
+  const bool qok = qi < a.Lq;
+  Ring ring;
+  ring.init((const bf16*)a.k + (int64_t)b * a.Lk * a.ldk + h * DH, a.ldk,
+            (const bf16*)a.v + (int64_t)b * a.Lk * a.ldv + h * DH, a.ldv, a.Lk, nullptr, nullptr, w, l);
+  const int klen = a.klen ? min(a.klen[b], a.Lk) : a.Lk;
+  const int nt = (klen + KT - 1) / KT;
+  if (nt > 0) ring.issue(smem, 0, w, l);
+  const bf16* Q = (const bf16*)a.q + (int64_t)b * a.Lq * a.ldq + h * DH;
+  const bf16* dO = (const bf16*)a.dout + (int64_t)b * a.Lq * a.lddo + h * DH;
+  const bf16* Og = (const bf16*)a.o + (int64_t)b * a.Lq * a.ldo + h * DH;
+  bf16x8 qf[4], of[4], ov[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    qf[s] = ldrow_sel(Q, a.ldq, qi, a.Lq, s * 16 + 8 * hh);
+    of[s] = ldrow_sel(dO, a.lddo, qi, a.Lq, s * 16 + 8 * hh);
+    ov[s] = ldrow_sel(Og, a.ldo, qi, a.Lq, s * 16 + 8 * hh);
+  }
+  const int64_t bhq = (int64_t)bh * a.Lq + min(qi, a.Lq - 1);
+  const float lq0 = a.lse[bhq];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) asm volatile("" ::"v"(qf[s]), "v"(of[s]), "v"(ov[s]));
+  asm volatile("" ::"v"(lq0));
+  if (nt > 1) ring.issue(smem + STAGEB, 1, w, l);
+  float dsum = 0.f;
+#pragma unroll
+  for (int s = 0; s < 4; ++s)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dsum = fmaf((float)of[s][j], (float)ov[s][j], dsum);
+  dsum += __shfl_xor(dsum, 32, 64);
+  if (hh == 0 && qok) a.delta[bhq] = dsum;
+  const float lq = qok ? lq0 * LOG2E : 0.f;
+  const float dl = qok ? dsum : 0.f;
+  FragOff fo;
+  fo.init(l);
+  const float sl2 = a.scale * LOG2E;
+  const AttnDrop drop(a.drop_p, a.seed, a.B, a.H, a.Lq, a.Lk);
+  const uint32_t rowG = ((uint32_t)bh * (uint32_t)a.Lq + (uint32_t)min(qi, a.Lq - 1)) * drop.npair * GOLD;
+  const float dscale = drop.scale;
+  f32x16 dq0, dq1;
+  zacc(dq0); zacc(dq1);
+  int cs = 0;
+  for (int t = 0; t < nt; ++t) {
+    ring.arrive(t, nt, w);
+    if (t + 2 < nt) ring.issue(smem + prev_stage(cs) * STAGEB, t + 2, w, l);
+    const char* Ks = smem + cs * STAGEB;
+    const char* Vs = Ks + IMGB;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int k0 = t * KT + 32 * j;
+      f32x16 st, dpt;
+      zacc(st); zacc(dpt);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        st = mfma32(ldA(Ks + 4096 * j, fo.row[s]), qf[s], st);
+        dpt = mfma32(ldA(Vs + 4096 * j, fo.row[s]), of[s], dpt);
+      }
+      if (a.drop_p > 0.f) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) dpt[r] *= dscale;
+        drop_tile_sel(dpt, rowG + (uint32_t)(k0 >> 1) * GOLD, drop, hh);
+      }
+      if (k0 + 32 <= klen) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) dpt[r] = fexp2(fmaf(st[r], sl2, -lq)) * (dpt[r] - dl);
+      } else {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float p = k0 + qrow(r, hh) < klen ? fexp2(fmaf(st[r], sl2, -lq)) : 0.f;
+          dpt[r] = p * (dpt[r] - dl);
+        }
+      }
+      const bf16x8 sa = accb(dpt, 0), sb = accb(dpt, 1);
+      dq0 = mfma32(ldT(Ks, 32 * j, fo, 0), sa, dq0);
+      dq1 = mfma32(ldT(Ks, 32 * j, fo, 1), sa, dq1);
+      dq0 = mfma32(ldT(Ks, 32 * j + 16, fo, 0), sb, dq0);
+      dq1 = mfma32(ldT(Ks, 32 * j + 16, fo, 1), sb, dq1);
+    }
+    cs = next_stage(cs);
+  }
+  __syncthreads();
+  OutT* DQ = dq + ((int64_t)b * a.Lq + q0) * lddq + h * DH;
+  store_t<OutT>(dq0, dq1, a.scale, (float*)smem + w * 32 * 65, DQ, lddq, a.Lq - q0);
+}
+
+// ----------------------------------------------------------------------------- dK / dV
+// per wave 32 keys on the lanes (K, V rows in registers); 64-query tiles of Q, dO and their
+// lse / delta streamed; per 32-query block S = Q K^T, dP = dO V^T with the key on the lane,
+// dV^T += dO^T P', dK^T += Q^T dS (as res::attn_bwd_dkdv_kernel, delta from the dQ kernel)
+__global__ __launch_bounds__(256, 3) void attn_bwd_dkdv_kernel(AttnArgs a, int nkb) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int id = xcd_id(blockIdx.x, gridDim.x);
+  const int bh = id / nkb, kbk = id - bh * nkb, b = bh / a.H, h = bh % a.H;
+  const int tid = threadIdx.x, w = __builtin_amdgcn_readfirstlane(tid >> 6), l = tid & 63, c = l & 31, hh = l >> 5;
+  const int kb0 = kbk * 128 + w * 32, key = kb0 + c;
+  Ring ring;
+  ring.init((const bf16*)a.q + (int64_t)b * a.Lq * a.ldq + h * DH, a.ldq,
+            (const bf16*)a.dout + (int64_t)b * a.Lq * a.lddo + h * DH, a.lddo, a.Lq,
+            a.lse + (int64_t)bh * a.Lq, a.delta + (int64_t)bh * a.Lq, w, l);
+  const int nt = (a.Lq + KT - 1) / KT;
+  if (nt > 0) ring.issue(smem, 0, w, l);
+  const bf16* K = (const bf16*)a.k + (int64_t)b * a.Lk * a.ldk + h * DH;
+  const bf16* V = (const bf16*)a.v + (int64_t)b * a.Lk * a.ldv + h * DH;
+  bf16x8 kf[4], vf[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    kf[s] = ldrow_sel(K, a.ldk, key, a.Lk, s * 16 + 8 * hh);
+    vf[s] = ldrow_sel(V, a.ldv, key, a.Lk, s * 16 + 8 * hh);
+  }
+#pragma unroll
+  for (int s = 0; s < 4; ++s) asm volatile("" ::"v"(kf[s]), "v"(vf[s]));
+  if (nt > 1) ring.issue(smem + STAGEB_F, 1, w, l);
+  FragOff fo;
+  fo.init(l);
+  const int klen = a.klen ? min(a.klen[b], a.Lk) : a.Lk;
+  const bool active = kb0 < klen;            // wave-uniform: a wave past klen only keeps the ring going
+  const bool kok = key < klen;
+  const float sl2 = a.scale * LOG2E;
+  const AttnDrop drop(a.drop_p, a.seed, a.B, a.H, a.Lq, a.Lk);
+  const uint32_t nG = drop.npair * GOLD;
+  const uint32_t keyG = ((uint32_t)bh * (uint32_t)a.Lq * drop.npair + (uint32_t)(min(key, a.Lk - 1) >> 1)) * GOLD;
+  const bool odd = c & 1;
+  const float dscale = a.drop_p > 0.f ? drop.scale : 1.f;
+  f32x16 dv0, dv1, dk0, dk1;
+  zacc(dv0); zacc(dv1); zacc(dk0); zacc(dk1);
+  int cs = 0;
+  for (int t = 0; t < nt; ++t) {
+    ring.arrive(t, nt, w);
+    if (t + 2 < nt) ring.issue(smem + prev_stage(cs) * STAGEB_F, t + 2, w, l);
+    if (active) {
+      const char* Qs = smem + cs * STAGEB_F;
+      const char* dOs = Qs + IMGB;
+      const float* lsS = (const float*)(Qs + STAGEB);
+      const float* dlS = lsS + KT;
+#pragma nounroll
+      for (int j = 0; j < 2; ++j) {
+        const int qt0 = t * KT + 32 * j;
+        f32x16 sc, dp;
+        zacc(sc); zacc(dp);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          sc = mfma32(ldA(Qs + 4096 * j, fo.row[s]), kf[s], sc);
+          dp = mfma32(ldA(dOs + 4096 * j, fo.row[s]), vf[s], dp);
+        }
+        const uint32_t tG = keyG + (uint32_t)(qt0 + 4 * hh) * nG;
+        const bool full = kok && qt0 + 32 <= a.Lq;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {            // registers 4i..4i+3 = queries qt0 + 8i + 4hh + 0..3
+          const f32x4 ls = *(const f32x4*)&lsS[32 * j + 8 * i + 4 * hh] * LOG2E;
+          const f32x4 ds = *(const f32x4*)&dlS[32 * j + 8 * i + 4 * hh];
+          bool kb[4] = {true, true, true, true};
+          if (a.drop_p > 0.f) {
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+              const uint32_t mine = hashG(tG + (uint32_t)(8 * i + (odd ? 2 : 0) + u) * nG, drop.pre);
+              const uint32_t other = __shfl_xor(mine, 1, 64);
+              const uint32_t h0 = odd ? other : mine, h1 = odd ? mine : other;
+              kb[u] = (odd ? (h0 >> 16) : (h0 & 0xFFFFu)) >= drop.thr;
+              kb[u + 2] = (odd ? (h1 >> 16) : (h1 & 0xFFFFu)) >= drop.thr;
+            }
+          }
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int r = 4 * i + e, ql = qt0 + 8 * i + 4 * hh + e;
+            const bool ok = full || (kok & (ql < a.Lq));
+            const float p = ok ? fexp2(fmaf(sc[r], sl2, -ls[e])) : 0.f;
+            sc[r] = kb[e] ? p : 0.f;
+            dp[r] = p * ((kb[e] ? dp[r] * dscale : 0.f) - ds[e]);
+          }
+        }
+        const bf16x8 pa = accb(sc, 0), pb = accb(sc, 1), sa = accb(dp, 0), sb = accb(dp, 1);
+        dv0 = mfma32(ldT(dOs, 32 * j, fo, 0), pa, dv0);
+        dv1 = mfma32(ldT(dOs, 32 * j, fo, 1), pa, dv1);
+        dv0 = mfma32(ldT(dOs, 32 * j + 16, fo, 0), pb, dv0);
+        dv1 = mfma32(ldT(dOs, 32 * j + 16, fo, 1), pb, dv1);
+        dk0 = mfma32(ldT(Qs, 32 * j, fo, 0), sa, dk0);
+        dk1 = mfma32(ldT(Qs, 32 * j, fo, 1), sa, dk1);
+        dk0 = mfma32(ldT(Qs, 32 * j + 16, fo, 0), sb, dk0);
+        dk1 = mfma32(ldT(Qs, 32 * j + 16, fo, 1), sb, dk1);
+      }
+    }
+    cs = next_stage(cs);
+  }
+  __syncthreads();
+  float* scr = (float*)smem + w * 32 * 65;
+  bf16* DK = (bf16*)a.dk + ((int64_t)b * a.Lk + kb0) * a.lddk + h * DH;
+  store_t<bf16>(dk0, dk1, a.scale, scr, DK, a.lddk, a.Lk - kb0);
+  bf16* DV = (bf16*)a.dv + ((int64_t)b * a.Lk + kb0) * a.lddv + h * DH;
+  store_t<bf16>(dv0, dv1, dscale, scr, DV, a.lddv, a.Lk - kb0);
 }
 }  // namespace sq
 
@@ -1415,7 +1656,8 @@ extern "C" int avsr_attn_fwd(const avsr_attn_params* p, void* stream) {
     const int nqb = (p->Lq + 127) / 128;
     const long nwg = (long)p->B * p->H * nqb;
     if (nwg > 0x7fffffffL) return AVSR_E_SHAPE;
-    hipLaunchKernelGGL(sq::attn_fwd_kernel, dim3((unsigned)nwg), dim3(256), sq::LDSB, (hipStream_t)stream, a, nqb);
+    hipLaunchKernelGGL(sq::attn_fwd_kernel, dim3((unsigned)nwg), dim3(256), sq::NS * sq::STAGEB, (hipStream_t)stream, a,
+                       nqb);
     AVSR_CHECK_LAUNCH();
     return 0;
   }
@@ -1435,6 +1677,10 @@ extern "C" int avsr_attn_fwd(const avsr_attn_params* p, void* stream) {
   return 0;
 }
 
+// the query-tiled bf16 backward computes delta in its dQ kernel (which runs first)
+static bool sq_bwd(const avsr_attn_params* p) {
+  return p->dtype == AVSR_BF16 && !p->causal && p->Lq >= 128 && p->Lk >= 128 && res::small_index(p) && sq_enabled();
+}
 // the resident bf16 backward computes delta inside its dK/dV kernel (Q / dO already in LDS)
 static bool resident_bwd(const avsr_attn_params* p) {
   return p->dtype == AVSR_BF16 && p->Lq <= res::MAXR && p->Lk <= res::MAXR && res::small_index(p);
@@ -1443,7 +1689,7 @@ static bool resident_bwd(const avsr_attn_params* p) {
 extern "C" int avsr_attn_bwd_prep(const avsr_attn_params* p, void* stream) {
   int rc = check(p);
   if (rc) return rc;
-  if (resident_bwd(p)) return 0;
+  if (sq_bwd(p) || resident_bwd(p)) return 0;
   AttnArgs a = args(p);
   const int g = avsr_grid((int64_t)p->B * p->Lq * p->H);
   if (p->dtype == AVSR_BF16) hipLaunchKernelGGL(attn_prep_kernel<bf16>, dim3(g), dim3(256), 0, (hipStream_t)stream, a);
@@ -1462,6 +1708,21 @@ extern "C" int avsr_attn_bwd(const avsr_attn_params* p, void* stream) {
   if (p->dtype == AVSR_BF16) {
     if (p->dq_out && (p->lddq_out % 8 || !avsr_aligned16(p->dq_out))) return AVSR_E_ALIGN;
     if (!p->dq_out && (p->lddq % 4 || !avsr_aligned16(p->dq))) return AVSR_E_ALIGN;
+    if (sq_bwd(p)) {
+      const int nqb = (p->Lq + 127) / 128, nkb = (p->Lk + 127) / 128;
+      const long gq = (long)p->B * p->H * nqb, gk = (long)p->B * p->H * nkb;
+      if (gq > 0x7fffffffL || gk > 0x7fffffffL) return AVSR_E_SHAPE;
+      if (p->dq_out)
+        hipLaunchKernelGGL(sq::attn_bwd_dq_kernel<bf16>, dim3((unsigned)gq), dim3(256), sq::NS * sq::STAGEB, st, a, nqb,
+                           (bf16*)p->dq_out, p->lddq_out);
+      else
+        hipLaunchKernelGGL(sq::attn_bwd_dq_kernel<float>, dim3((unsigned)gq), dim3(256), sq::NS * sq::STAGEB, st, a, nqb,
+                           p->dq, p->lddq);
+      AVSR_CHECK_LAUNCH();
+      hipLaunchKernelGGL(sq::attn_bwd_dkdv_kernel, dim3((unsigned)gk), dim3(256), sq::NS * sq::STAGEB_F, st, a, nkb);
+      AVSR_CHECK_LAUNCH();
+      return 0;
+    }
     if (resident_bwd(p)) {
       // dK/dV: 12 waves (3 per SIMD; a few registers spill to scratch, measured 5 % faster than
       // 8 spill-free waves at 2 per SIMD); AVSR_DKDV_WAVES=8 selects the other
