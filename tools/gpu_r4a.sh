@@ -5,7 +5,7 @@ cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 O=gpurun_out/${1:-r4a}; mkdir -p $O
 export AVSR_REPORT_DIR=$O/report
-timeout -k 10 600 python -u -m pytest tests/test_gpu_gemm.py tests/test_gpu_attention.py tests/test_gpu_dp.py -x -q --timeout 300 --timeout-method thread > $O/new.log 2>&1 || { echo new tests failed; tail -30 $O/new.log; exit 1; }
+timeout -k 10 600 python -u -m pytest tests/test_gpu_attention.py tests/test_gpu_gemm.py tests/test_gpu_dp.py -x -q --timeout 300 --timeout-method thread > $O/new.log 2>&1 || { echo new tests failed; tail -30 $O/new.log; exit 1; }
 tail -1 $O/new.log
 for v in 1 0; do AVSR_ATTN_SQ=$v timeout -k 10 120 python -u tools/attn_bench.py > $O/attn_sq$v.txt 2>&1 || { echo attn bench failed; exit 1; }; echo sq=$v; cat $O/attn_sq$v.txt; done
 timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/tests.log 2>&1 || { echo tests failed; tail -30 $O/tests.log; exit 1; }
