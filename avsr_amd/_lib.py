@@ -146,6 +146,7 @@ class EmbedParams(ctypes.Structure):
     _fields_ = [
         ("dtype", _i), ("rows", _i), ("L", _i), ("D", _i), ("tok", _c_p), ("table", _c_p), ("pe", _c_p),
         ("scale", _f), ("y", _c_p), ("drop_p", _f), ("seed", ctypes.c_uint64), ("dy", _c_p), ("dtable", _c_p),
+        ("pe_row", _c_p),
     ]
 
 
@@ -179,7 +180,7 @@ class DecAttnParams(ctypes.Structure):
         ("dtype", _i), ("n", _i), ("H", _i), ("klen_max", _i), ("scale", _f),
         ("q", _c_p), ("ldq", _i64), ("k", _c_p), ("ldk", _i64), ("k_bstride", _i64),
         ("v", _c_p), ("ldv", _i64), ("v_bstride", _i64), ("klen", _c_p), ("o", _c_p), ("ldo", _i64),
-        ("kidx", _c_p),
+        ("kidx", _c_p), ("kmap", _c_p), ("ldmap", _i64),
     ]
 
 
@@ -191,7 +192,7 @@ class CtcPrefixParams(ctypes.Structure):
     _fields_ = [
         ("n", _i), ("T", _i), ("V", _i), ("P", _i), ("blank", _i), ("eos", _i), ("out_len", _i),
         ("logp", _c_p), ("r_prev", _c_p), ("last", _c_p), ("ids", _c_p), ("r_new", _c_p), ("psi", _c_p),
-        ("uidx", _c_p), ("logp_ustride", _i64), ("tlen", _c_p),
+        ("uidx", _c_p), ("logp_ustride", _i64), ("tlen", _c_p), ("out_len_dev", _c_p),
     ]
 
 
@@ -201,6 +202,18 @@ class BeamSelectParams(ctypes.Structure):
         ("dec", _c_p), ("ld", _i64), ("ids", _c_p), ("psi", _c_p), ("s_prev", _c_p), ("score", _c_p),
         ("out_prev", _c_p), ("out_tok", _c_p), ("out_col", _c_p), ("out_score", _c_p), ("out_dec", _c_p),
         ("out_ctc", _c_p), ("out_s", _c_p), ("nseg", _i), ("seg", _c_p),
+    ]
+
+
+class BeamPostParams(ctypes.Structure):
+    _fields_ = [
+        ("U", _i), ("beam", _i), ("P", _i), ("R", _i), ("Lmax", _i), ("steps_cap", _i), ("eos", _i),
+        ("end_detect", _i), ("d_end", ctypes.c_double), ("pos", _c_p), ("maxlen", _c_p),
+        ("sel_prev", _c_p), ("sel_tok", _c_p), ("sel_col", _c_p), ("sel_score", _c_p), ("sel_dec", _c_p),
+        ("sel_ctc", _c_p), ("sel_s", _c_p),
+        ("tok", _c_p), ("score", _c_p), ("sdec", _c_p), ("sctc", _c_p), ("s_prev", _c_p), ("src", _c_p),
+        ("bp_prev", _c_p), ("bp_tok", _c_p), ("end_flag", _c_p), ("end_score", _c_p), ("end_dec", _c_p),
+        ("end_ctc", _c_p), ("best_len", _c_p), ("best_end", _c_p), ("done", _c_p),
     ]
 
 
@@ -285,6 +298,9 @@ SYMBOLS = {
     "avsr_row_topk": ([ctypes.POINTER(TopkParams), _c_p], _i),
     "avsr_ctc_prefix": ([ctypes.POINTER(CtcPrefixParams), _c_p], _i),
     "avsr_beam_select": ([ctypes.POINTER(BeamSelectParams), _c_p], _i),
+    "avsr_beam_step_prep": ([_i, _i, _c_p, _c_p, _c_p, _c_p], _i),
+    "avsr_beam_kv_put": ([_i, _i, _i, _c_p, _i64, _c_p, _c_p, _c_p, _c_p], _i),
+    "avsr_beam_post": ([ctypes.POINTER(BeamPostParams), _c_p], _i),
     "avsr_gather_rows": ([_i, _i, _i64, _c_p, _i64, _i64, _c_p, _i64, _i64, _c_p, _c_p], _i),
     "avsr_fbank_stack": ([ctypes.POINTER(FbankParams), _c_p], _i),
     "avsr_video_normalize": ([ctypes.POINTER(VideoNormParams), _c_p], _i),

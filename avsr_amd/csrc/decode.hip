@@ -80,15 +80,16 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(avsr_dec_attn_params p) {
   const int h = blockIdx.x, i = blockIdx.y;
   const int klen = p.klen ? min(p.klen[i], p.klen_max) : p.klen_max;
   const T* q = (const T*)p.q + (int64_t)i * p.ldq + h * 64;
-  const int kb = p.kidx ? p.kidx[i] : i;
+  const int kb = p.kmap ? 0 : (p.kidx ? p.kidx[i] : i);
   const T* K = (const T*)p.k + (int64_t)kb * p.k_bstride + h * 64;
   const T* Vv = (const T*)p.v + (int64_t)kb * p.v_bstride + h * 64;
+  const int* km = p.kmap ? p.kmap + (int64_t)i * p.ldmap : nullptr;   // key j -> row km[j]
   float qr[64];
 #pragma unroll
   for (int d = 0; d < 64; ++d) qr[d] = to_f(q[d]);
   float m = -INFINITY;
   for (int j = threadIdx.x; j < klen; j += 256) {
-    const T* kr = K + (int64_t)j * p.ldk;
+    const T* kr = K + (int64_t)(km ? km[j] : j) * p.ldk;
     float s = 0.f;
 #pragma unroll
     for (int d = 0; d < 64; ++d) s += qr[d] * to_f(kr[d]);
@@ -106,7 +107,7 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(avsr_dec_attn_params p) {
   l = block_sum256(l, sh);     // includes a barrier: every sc[j] is final
   const int d = threadIdx.x & 63, g = threadIdx.x >> 6;
   float acc = 0.f;
-  for (int j = g; j < klen; j += 4) acc += sc[j] * to_f(Vv[(int64_t)j * p.ldv + d]);
+  for (int j = g; j < klen; j += 4) acc += sc[j] * to_f(Vv[(int64_t)(km ? km[j] : j) * p.ldv + d]);
   float* part = sc + p.klen_max;
   part[g * 64 + d] = acc;
   __syncthreads();
@@ -158,6 +159,7 @@ __global__ __launch_bounds__(256) void row_topk_kernel(avsr_topk_params p) {
 // hypothesis, lane j = its j-th scored token; the T recursion is sequential per lane.
 __global__ __launch_bounds__(64) void ctc_prefix_kernel(avsr_ctc_prefix_params p) {
   const int h = blockIdx.x, j = threadIdx.x;
+  if (p.out_len_dev) p.out_len = p.out_len_dev[0];
   const int V = p.V;
   const int u = p.uidx ? p.uidx[h] : 0;
   const int T = p.uidx ? p.tlen[u] : p.T;         // this utterance's frames
@@ -224,6 +226,7 @@ __global__ __launch_bounds__(64) void ctc_prefix_kernel(avsr_ctc_prefix_params p
 __global__ __launch_bounds__(64) void ctc_prefix_lds_kernel(avsr_ctc_prefix_params p) {
   extern __shared__ float sm[];
   const int h = blockIdx.x, j = threadIdx.x;
+  if (p.out_len_dev) p.out_len = p.out_len_dev[0];
   const int V = p.V, P = p.P, W = P + 1;
   const int u = p.uidx ? p.uidx[h] : 0;
   const int T = p.uidx ? p.tlen[u] : p.T;
@@ -312,6 +315,7 @@ __global__ __launch_bounds__(256) void beam_select_kernel(avsr_beam_select_param
   const int W = p.P + 1;
   auto weighted = [&](int f) -> float {
     const int h = r0 + f / p.V, v = f - (f / p.V) * p.V;
+    if (p.score[h] == -INFINITY) return -INFINITY;      // a dead row of the device-side search
     float psi = LOGZERO;
     if (v == p.eos) psi = p.psi[h * (p.P + 1) + p.P];
     else if (v != p.blank)
@@ -369,6 +373,18 @@ __global__ __launch_bounds__(256) void beam_select_kernel(avsr_beam_select_param
     for (int k = 0; k < KMAX; ++k) { tv[k] = -INFINITY; ti[k] = 0x7fffffff; }
   };
   bool full = !(nrow * W <= 256 && p.w_ctc > 0.f);     // block-uniform
+  {   // a segment with no live row (a finished utterance of the device-side search): nothing to select
+    bool any = false;
+    for (int hl = 0; hl < nrow; ++hl) any |= p.score[r0 + hl] != -INFINITY;
+    if (!any) {
+      for (int r = threadIdx.x; r < p.beam; r += 256) {
+        const int o = u * p.beam + r;
+        p.out_prev[o] = r0; p.out_tok[o] = p.eos; p.out_col[o] = p.P - 1; p.out_score[o] = -INFINITY;
+        p.out_dec[o] = 0.f; p.out_ctc[o] = 0.f; p.out_s[o] = 0.f;
+      }
+      return;
+    }
+  }
   if (!full) {
     reset();
     const int c = threadIdx.x;
@@ -422,6 +438,130 @@ extern "C" int avsr_log_softmax_rows(int dtype, int rows, int V, const void* x, 
   else if (dtype == AVSR_F32)
     hipLaunchKernelGGL(log_softmax_kernel<float>, dim3(rows), dim3(256), 0, (hipStream_t)stream, V, (const float*)x, ldx, out, ldo);
   else return AVSR_E_DTYPE;
+  AVSR_CHECK_LAUNCH();
+  return 0;
+}
+
+// ---------------------------------------------------------------- device-side bookkeeping
+__global__ __launch_bounds__(256) void beam_step_prep_kernel(int R, int Lmax, const int* pos_p, int* anc, int* klen) {
+  const int pos = pos_p[0];
+  for (int r = blockIdx.x * 256 + threadIdx.x; r < R; r += gridDim.x * 256) {
+    anc[(int64_t)r * Lmax + pos] = pos * R + r;
+    klen[r] = pos + 1;
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void beam_kv_put_kernel(int R, int D, const T* qkv, int64_t ld, T* ck, T* cv,
+                                                          const int* pos_p) {
+  const int pos = pos_p[0];
+  const int nv = D / VecW<T>::VE;
+  for (int e = blockIdx.x * 256 + threadIdx.x; e < R * nv; e += gridDim.x * 256) {
+    const int r = e / nv, c = (e - r * nv) * VecW<T>::VE;
+    const int64_t dst = ((int64_t)pos * R + r) * D + c;
+    *(v16*)(ck + dst) = *(const v16*)(qkv + (int64_t)r * ld + D + c);
+    *(v16*)(cv + dst) = *(const v16*)(qkv + (int64_t)r * ld + 2 * D + c);
+  }
+}
+
+// one workgroup: rows of the step (R <= 1024), then one thread per utterance
+__global__ __launch_bounds__(256) void beam_post_kernel(avsr_beam_post_params p) {
+  extern __shared__ __attribute__((aligned(16))) char sm[];
+  double* od = (double*)sm;                   // [R] old decoder sums
+  double* oc = od + p.R;                      // [R] old CTC sums
+  int* ended = (int*)(oc + p.R);              // [R] 0 running, 1 eos, 2 forced eos at maxlen
+  const int pos = p.pos[0];
+  for (int r = threadIdx.x; r < p.R; r += 256) { od[r] = p.sdec[r]; oc[r] = p.sctc[r]; }
+  __syncthreads();
+  const int64_t so = (int64_t)pos * p.R;
+  for (int r = threadIdx.x; r < p.R; r += 256) {
+    const int u = r / p.beam;
+    ended[r] = 0;
+    if (p.done[u]) {                          // finished before this step: stays dead
+      p.score[r] = -INFINITY;
+      p.src[r] = r; p.src[p.R + r] = r * p.P;
+      p.bp_prev[so + r] = r; p.bp_tok[so + r] = p.eos; p.end_flag[so + r] = 0;
+      continue;
+    }
+    const int h = p.sel_prev[r], t = p.sel_tok[r];
+    const float sc = p.sel_score[r];
+    const double nd = od[h] + (double)p.sel_dec[r], nc = oc[h] + (double)p.sel_ctc[r];
+    const bool forced = pos == p.maxlen[u] - 1;   // eos appended to every hypothesis at the last step
+    const int e = forced ? 2 : (t == p.eos ? 1 : 0);
+    ended[r] = e;
+    p.bp_prev[so + r] = h; p.bp_tok[so + r] = t; p.end_flag[so + r] = e;
+    if (e) { p.end_score[so + r] = sc; p.end_dec[so + r] = nd; p.end_ctc[so + r] = nc; }
+    p.tok[r] = t;
+    p.score[r] = e ? -INFINITY : sc;
+    p.sdec[r] = nd; p.sctc[r] = nc; p.s_prev[r] = p.sel_s[r];
+    p.src[r] = h; p.src[p.R + r] = h * p.P + p.sel_col[r];
+  }
+  __syncthreads();
+  const int LB = p.Lmax + 3;
+  for (int u = threadIdx.x; u < p.U; u += 256) {
+    if (p.done[u]) continue;
+    bool any_live = false;
+    float* bl = p.best_len + (int64_t)u * LB;
+    for (int k = 0; k < p.beam; ++k) {         // this step's ended hypotheses, in selection order
+      const int r = u * p.beam + k;
+      if (!ended[r]) { any_live = true; continue; }
+      const int len = pos + 2 + (ended[r] == 2 ? 1 : 0);     // sos + pos+1 tokens (+ the forced eos)
+      const float s = p.end_score[so + r];
+      if (len < LB && s > bl[len]) bl[len] = s;
+      if (s > p.best_end[u]) p.best_end[u] = s;
+    }
+    bool det = false;
+    if (p.end_detect && p.best_end[u] != -INFINITY) {
+      int count = 0;
+      for (int m = 0; m < 3; ++m) {
+        const int len = pos - m;
+        if (len >= 0 && len < LB && bl[len] != -INFINITY && (double)bl[len] - (double)p.best_end[u] < p.d_end) ++count;
+      }
+      det = count == 3;
+    }
+    if (det || !any_live || pos >= p.maxlen[u] - 1) {
+      p.done[u] = 1;
+      for (int k = 0; k < p.beam; ++k) p.score[u * p.beam + k] = -INFINITY;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int n = 0;
+    for (int u = 0; u < p.U; ++u) n += p.done[u];
+    p.done[p.U] = n;
+    p.pos[0] = pos + 1;
+  }
+}
+
+extern "C" int avsr_beam_step_prep(int R, int Lmax, const int* pos, int* anc, int* klen, void* stream) {
+  if (R <= 0 || Lmax <= 0 || !pos || !anc || !klen) return AVSR_E_ARG;
+  hipLaunchKernelGGL(beam_step_prep_kernel, dim3((R + 255) / 256), dim3(256), 0, (hipStream_t)stream, R, Lmax, pos, anc,
+                     klen);
+  AVSR_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int avsr_beam_kv_put(int dtype, int R, int D, const void* qkv, int64_t ldqkv, void* cache_k, void* cache_v,
+                                const int* pos, void* stream) {
+  const int ve = dtype == AVSR_BF16 ? 8 : 4;
+  if (R <= 0 || D % ve || ldqkv % ve || !pos) return AVSR_E_ARG;
+  if (!avsr_aligned16(qkv) || !avsr_aligned16(cache_k) || !avsr_aligned16(cache_v)) return AVSR_E_ALIGN;
+  const int g = avsr_grid((int64_t)R * D / ve, 256, 1024);
+  if (dtype == AVSR_BF16)
+    hipLaunchKernelGGL(beam_kv_put_kernel<bf16>, dim3(g), dim3(256), 0, (hipStream_t)stream, R, D, (const bf16*)qkv, ldqkv,
+                       (bf16*)cache_k, (bf16*)cache_v, pos);
+  else if (dtype == AVSR_F32)
+    hipLaunchKernelGGL(beam_kv_put_kernel<float>, dim3(g), dim3(256), 0, (hipStream_t)stream, R, D, (const float*)qkv,
+                       ldqkv, (float*)cache_k, (float*)cache_v, pos);
+  else return AVSR_E_DTYPE;
+  AVSR_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int avsr_beam_post(const avsr_beam_post_params* p, void* stream) {
+  if (!p || p->U <= 0 || p->beam <= 0 || p->R != p->U * p->beam || p->R > 2048) return AVSR_E_ARG;
+  const size_t lds = (size_t)p->R * (2 * sizeof(double) + sizeof(int));
+  hipLaunchKernelGGL(beam_post_kernel, dim3(1), dim3(256), lds, (hipStream_t)stream, *p);
   AVSR_CHECK_LAUNCH();
   return 0;
 }

@@ -96,7 +96,7 @@ __global__ __launch_bounds__(256) void embed_kernel(avsr_embed_params p, int bwd
   for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
     const int r = (int)(i / nv), d0 = (int)(i % nv) * VE;
     const int tok = p.tok[r];
-    const int pos = r % p.L;
+    const int pos = p.pe_row ? p.pe_row[0] : r % p.L;
     if (!bwd) {
       float e[VE], o[VE];
       ldv((const T*)p.table + (int64_t)tok * p.D + d0, e);

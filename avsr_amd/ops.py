@@ -603,10 +603,12 @@ def mask_rows(x, B, T, lengths):
     return x
 
 
-def embed_fwd(tok, table, pe, scale, y, L_, drop_p=0.0, seed=0):
+def embed_fwd(tok, table, pe, scale, y, L_, drop_p=0.0, seed=0, pe_row=None):
+    """pe_row: optional device int32 [1]: every row adds pe[pe_row[0]] (a beam-search step's
+    position kept on the device)"""
     _call("avsr_embed_fwd", L.fill(L.EmbedParams, dtype=dtype_code(table), rows=tok.shape[0], L=L_,
                                     D=table.shape[1], tok=tok, table=table, pe=pe, scale=scale, y=y,
-                                    drop_p=float(drop_p), seed=int(seed) & (2 ** 64 - 1)))
+                                    drop_p=float(drop_p), seed=int(seed) & (2 ** 64 - 1), pe_row=pe_row))
     return y
 
 
@@ -734,13 +736,14 @@ def log_softmax_rows(x, V, out):
     return out
 
 
-def dec_attn(q, k, v, o, *, n, H, klen_max, k_bstride, v_bstride, klen=None, scale=0.125, kidx=None):
+def dec_attn(q, k, v, o, *, n, H, klen_max, k_bstride, v_bstride, klen=None, scale=0.125, kidx=None, kmap=None):
     """one query per hypothesis: q/o rows i (ld = stride(0)), keys j of hypothesis i at
-    k[b*k_bstride + j*k.stride(-2)] with b = kidx[i] (kidx None: b = i; bstride 0: shared keys)."""
+    k[b*k_bstride + j*k.stride(-2)] with b = kidx[i] (kidx None: b = i; bstride 0: shared keys);
+    kmap (int32 [n][ldmap]): key j of hypothesis i is row kmap[i][j] of k instead."""
     _call("avsr_dec_attn", L.fill(L.DecAttnParams, dtype=dtype_code(q), n=n, H=H, klen_max=klen_max, scale=scale,
                                    q=q, ldq=q.stride(0), k=k, ldk=k.stride(-2), k_bstride=k_bstride, v=v,
                                    ldv=v.stride(-2), v_bstride=v_bstride, klen=klen, o=o, ldo=o.stride(0),
-                                   kidx=kidx))
+                                   kidx=kidx, kmap=kmap, ldmap=0 if kmap is None else kmap.stride(0)))
     return o
 
 
@@ -749,14 +752,16 @@ def row_topk(x, V, K, ids):
     return ids
 
 
-def ctc_prefix(logp, r_prev, last, ids, r_new, psi, *, n, out_len, blank, eos, uidx=None, tlen=None):
+def ctc_prefix(logp, r_prev, last, ids, r_new, psi, *, n, out_len, blank, eos, uidx=None, tlen=None,
+               out_len_dev=None):
     """logp (T, V) of one utterance, or (U, Tmax, V) with uidx (per-hypothesis utterance) and
-    tlen (per-utterance frames) for batched decoding"""
+    tlen (per-utterance frames) for batched decoding; out_len_dev: device int32 [1] overriding
+    out_len (graph-captured steps)"""
     T, V = logp.shape[-2:]
     _call("avsr_ctc_prefix", L.fill(L.CtcPrefixParams, n=n, T=T, V=V, P=ids.shape[1], blank=blank, eos=eos,
                                      out_len=out_len, logp=logp, r_prev=r_prev, last=last, ids=ids, r_new=r_new,
                                      psi=psi, uidx=uidx, logp_ustride=T * V if uidx is not None else 0,
-                                     tlen=tlen))
+                                     tlen=tlen, out_len_dev=out_len_dev))
 
 
 def beam_select(dec, V, ids, psi, s_prev, score, out, *, n, beam, blank, eos, w_dec, w_ctc, seg=None):
@@ -775,3 +780,20 @@ def gather_rows(src, dst, idx, *, groups, n, row_bytes, src_gstride, src_rstride
     """dst[g][i] = src[g][idx[i]] (strides in bytes)"""
     L.check(L.load().avsr_gather_rows(groups, n, row_bytes, src.data_ptr(), src_gstride, src_rstride, dst.data_ptr(),
                                       dst_gstride, dst_rstride, idx.data_ptr(), L.stream_ptr()), "avsr_gather_rows")
+
+
+def beam_step_prep(R, pos, anc, klen):
+    """anc[r][pos] = pos*R + r, klen[r] = pos + 1 (pos: device int32 [1]); avsr_hip.h"""
+    L.check(L.load().avsr_beam_step_prep(R, anc.shape[1], pos.data_ptr(), anc.data_ptr(), klen.data_ptr(),
+                                         L.stream_ptr()), "avsr_beam_step_prep")
+
+
+def beam_kv_put(qkv, cache_k, cache_v, pos, R, D):
+    """this step's self-attention K / V rows -> cache rows pos*R + r"""
+    L.check(L.load().avsr_beam_kv_put(dtype_code(qkv), R, D, qkv.data_ptr(), qkv.stride(0), cache_k.data_ptr(),
+                                      cache_v.data_ptr(), pos.data_ptr(), L.stream_ptr()), "avsr_beam_kv_put")
+
+
+def beam_post(**kw):
+    """device-side bookkeeping after avsr_beam_select (avsr_hip.h avsr_beam_post)"""
+    _call("avsr_beam_post", L.fill(L.BeamPostParams, **kw))

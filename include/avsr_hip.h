@@ -417,6 +417,8 @@ typedef struct {
   const int* tok; const void* table; const float* pe; float scale;
   void* y; float drop_p; uint64_t seed;
   const void* dy; float* dtable;
+  const int* pe_row;         /* forward, optional: device int, every row adds pe[pe_row[0]] (L ignored):
+                                the position of a beam-search step kept on the device */
 } avsr_embed_params;
 int avsr_embed_fwd(const avsr_embed_params* p, void* stream);
 int avsr_embed_bwd(const avsr_embed_params* p, void* stream);
@@ -500,6 +502,10 @@ typedef struct {
   const int* kidx;            /* [n] or NULL: hypothesis i reads key block kidx[i] (base kidx[i]*k_bstride,
                                  v likewise) instead of block i — batched decoding of several
                                  utterances whose memories sit in one [U][T][..] buffer */
+  const int* kmap; int64_t ldmap;   /* optional [n][ldmap]: key j of hypothesis i is row kmap[i*ldmap + j]
+                                 of k (v likewise; bstride / kidx ignored) — the self-attention
+                                 cache of a device-side beam search, [step][row] rows addressed
+                                 through each hypothesis's ancestry instead of being reordered */
 } avsr_dec_attn_params;
 int avsr_dec_attn(const avsr_dec_attn_params* p, void* stream);
 
@@ -523,6 +529,7 @@ typedef struct {
    * whose log-probs start at logp + uidx[h]*logp_ustride and whose length is tlen[uidx[h]]
    * (<= T, the row stride of r_prev / r_new) */
   const int* uidx; int64_t logp_ustride; const int* tlen;
+  const int* out_len_dev;     /* optional device int overriding out_len (graph-captured steps) */
 } avsr_ctc_prefix_params;
 int avsr_ctc_prefix(const avsr_ctc_prefix_params* p, void* stream);
 
@@ -546,6 +553,38 @@ int avsr_beam_select(const avsr_beam_select_params* p, void* stream);
 int avsr_gather_rows(int groups, int n, int64_t row_bytes, const void* src, int64_t src_gstride,
                      int64_t src_rstride, void* dst, int64_t dst_gstride, int64_t dst_rstride,
                      const int* idx, void* stream);
+
+/* Device-side beam bookkeeping (avsr_amd.decode: the whole step lives on the device and is
+ * replayed as a HIP graph; the host reads only a done count every few steps and the history at
+ * the end). Fixed geometry: U utterances x beam rows = R rows; a finished hypothesis / utterance
+ * becomes a dead row (score -inf, never selected: identical to the reference removing it,
+ * batch_beam_search.py:262-349, beam_search.py:330-372).
+ * avsr_beam_step_prep: at the start of step pos (= *pos): anc[r][pos] = pos*R + r (the
+ *   self-attention cache row this step writes for row r) and klen[r] = pos + 1.
+ * avsr_beam_kv_put: cache_k[(pos*R + r)*D ..] = qkv[r][D..2D), cache_v from qkv[r][2D..3D).
+ * avsr_beam_post: after avsr_beam_select of step pos: new running state per row (token,
+ *   score, decoder / CTC score sums in double like the reference's Python floats, CTC prefix
+ *   score), the back-pointers and ended-hypothesis records of the step, per-utterance end
+ *   detection (e2e_asr_common.py:18-48 over the per-length best ended scores) and stop rules;
+ *   src[0..R) = rows to gather the ancestry from, src[R..2R) = r_new rows for r_prev; *pos += 1. */
+typedef struct {
+  int U, beam, P, R, Lmax, steps_cap, eos, end_detect;
+  double d_end;
+  int* pos;
+  const int* maxlen;
+  const int* sel_prev; const int* sel_tok; const int* sel_col;
+  const float* sel_score; const float* sel_dec; const float* sel_ctc; const float* sel_s;
+  int* tok; float* score; double* sdec; double* sctc; float* s_prev;
+  int* src;
+  int* bp_prev; int* bp_tok; int* end_flag; float* end_score; double* end_dec; double* end_ctc;
+  float* best_len;           /* [U][Lmax + 3] */
+  float* best_end;           /* [U] */
+  int* done;                 /* [U + 1]: per utterance, then the count */
+} avsr_beam_post_params;
+int avsr_beam_step_prep(int R, int Lmax, const int* pos, int* anc, int* klen, void* stream);
+int avsr_beam_kv_put(int dtype, int R, int D, const void* qkv, int64_t ldqkv, void* cache_k, void* cache_v,
+                     const int* pos, void* stream);
+int avsr_beam_post(const avsr_beam_post_params* p, void* stream);
 
 /* ------------------------------------------------------------------------------------
  * Input front end (the collator's per-clip CPU transforms moved on device).
