@@ -8,15 +8,18 @@ Drop-in for the decoder the reference builds with `get_beam_search_decoder`
 Search semantics follow src/nets/batch_beam_search.py:102-349 and beam_search.py:330-456
 (weights decoder 1-ctc_weight / ctc ctc_weight, length bonus and LM weight 0 => dropped,
 pre-beam of int(1.5*beam) tokens on the decoder score, maxlen = T when maxlenratio = 0,
-eos forced at the last step, end detection M=3, D_end=-10). Per step everything runs on
-the device (decoder one-step with self-attention K/V caches and per-utterance cross-attention
-K/V, pre-beam top-k, CTC prefix recursion, weighted flat top-beam, state reordering); the
-host reads back only the beam's (previous hypothesis, token, scores) to manage ended
-hypotheses — the reference synchronises per hypothesis instead.
+eos forced at the last step, end detection M=3, D_end=-10). Everything runs on the device,
+bookkeeping included (decoder one-step with an ancestry-indexed self-attention K/V cache and
+per-utterance cross-attention K/V, pre-beam top-k, CTC prefix recursion, weighted flat
+top-beam, running scores, back-pointers, ended-hypothesis records, end detection), and every
+step after the first is one HIP-graph replay; the host reads a finished-utterance count every
+8 steps and the history once at the end — the reference synchronises per hypothesis.
 
 Differences that do not change results: the cross-attention K/V of the memory are computed
-once per utterance (the reference recomputes them every step), and the self-attention K/V
-of earlier positions are cached instead of the layer outputs they are computed from.
+once per utterance (the reference recomputes them every step), the self-attention K/V of
+earlier positions are cached instead of the layer outputs they are computed from (rows of
+step j at cache row j*R + r, reached through each hypothesis's ancestry table instead of
+being copied on every reorder), and finished hypotheses stay in the batch as dead rows.
 """
 import math
 from typing import Any, Dict, List, NamedTuple, Union
@@ -27,6 +30,7 @@ import torch
 from . import ops
 
 LOGZERO = -10000000000.0
+D_END = np.log(1 * np.exp(-10))          # end_detect's threshold (e2e_asr_common.py:18)
 
 
 class Hypothesis(NamedTuple):
@@ -44,8 +48,9 @@ class Hypothesis(NamedTuple):
         )._asdict()
 
 
-def end_detect(ended_hyps, i, M=3, D_end=np.log(1 * np.exp(-10))):
-    """src/nets/e2e_asr_common.py:18-48"""
+def end_detect(ended_hyps, i, M=3, D_end=D_END):
+    """src/nets/e2e_asr_common.py:18-48 (host form; the search evaluates it on the device,
+    decode.hip beam_post_kernel, over the per-length best ended scores)"""
     if len(ended_hyps) == 0:
         return False
     count = 0
@@ -85,171 +90,92 @@ class BatchBeamSearch:
     def __call__(self, x, maxlenratio: float = 0.0, minlenratio: float = 0.0):
         return self.forward(x, maxlenratio, minlenratio)
 
-    # ----------------------------------------------------------------------- per utterance
-    def _prepare(self, eng, x):
-        x = x.to(eng.device, eng.dtype).contiguous()
-        T = x.shape[0]
-        ar = eng.arena
-        # CTC log-probs (ctc.py:153-160 log_softmax(ctc_lo(x)))
-        cl = eng._e(T, eng.Vp)
-        ops.linear_fwd(x, eng.w("ctc.ctc_lo.weight"), ar.master("ctc.ctc_lo.bias"), out=cl[:, :eng.V])
-        logp = torch.empty(T, eng.V, device=eng.device, dtype=torch.float32)
-        ops.log_softmax_rows(cl, eng.V, logp)
-        # cross-attention K/V of the memory, once per utterance and layer
-        mem = []
-        for i in range(eng.dl):
-            ca = f"decoder.decoders.{i}.src_attn."
-            mem.append(ops.linear_fwd(x, ar.span([ca + "linear_k.weight", ca + "linear_v.weight"]),
-                                      ar.span([ca + "linear_k.bias", ca + "linear_v.bias"], buf="master")))
-        return x, logp, mem
-
     # ----------------------------------------------------------------------- decoder step
-    def _decoder_step(self, eng, toks, pos, n, cache, mem, T, kidx=None, klen=None):
-        """Decoder.forward_one_step for n prefixes whose last token (position pos) is toks:
-        returns log-probs (n, V) fp32; appends this position's self-attention K/V to cache.
-        Batched utterances: memory rows [U*T][2D], hypothesis i attends to block kidx[i] over
-        klen[i] frames."""
+    def _decoder_step(self, eng, st):
+        """Decoder.forward_one_step for the R rows of the search state `st` (position and
+        tokens on the device): returns log-probs (R, V) fp32. This step's self-attention K / V
+        go to cache rows pos*R + r; key j of row r is cache row anc[r][j] (its ancestry), the
+        memory of row r is utterance r // beam over klen[r] frames."""
         ar = eng.arena
-        D, H = eng.dD, eng.dH
-        x = eng._e(n, D)
-        if eng._pe.shape[0] <= pos:
-            from .engine import positional_encoding
-            eng._pe = positional_encoding(2 * (pos + 1), D, eng.device)
-        ops.embed_fwd(toks, eng.w("decoder.embed.0.weight"), eng._pe[pos:pos + 1], math.sqrt(D), x, 1)
-        Lmax = cache.shape[3]
+        D, H, R = eng.dD, eng.dH, st["R"]
+        pos, cache, anc = st["pos"], st["cache"], st["anc_in"]
+        x = eng._e(R, D)
+        ops.embed_fwd(st["tok"], eng.w("decoder.embed.0.weight"), eng._pe, math.sqrt(D), x, 1, pe_row=pos)
+        Tm = st["Tm"]
         for i in range(eng.dl):
             p = f"decoder.decoders.{i}."
             sa, ca, ff = p + "self_attn.", p + "src_attn.", p + "feed_forward."
             n1, _, _ = ops.layernorm_fwd(x, ar.master(p + "norm1.weight"), ar.master(p + "norm1.bias"), 1e-12)
             qkv = ops.linear_fwd(n1, ar.span([sa + "linear_q.weight", sa + "linear_k.weight", sa + "linear_v.weight"]),
                                  ar.span([sa + "linear_q.bias", sa + "linear_k.bias", sa + "linear_v.bias"], buf="master"))
-            kc, vc = cache[i, 0, :n], cache[i, 1, :n]            # (n, Lmax, D)
-            ops.cast(qkv[:, D:2 * D], kc[:, pos, :])
-            ops.cast(qkv[:, 2 * D:], vc[:, pos, :])
-            o1 = eng._e(n, D)
-            ops.dec_attn(qkv[:, :D], kc, vc, o1, n=n, H=H, klen_max=pos + 1, k_bstride=Lmax * D,
-                         v_bstride=Lmax * D)
+            kc, vc = cache[i, 0], cache[i, 1]               # (Lmax * R, D): rows step * R + r
+            ops.beam_kv_put(qkv, kc, vc, pos, R, D)
+            o1 = eng._e(R, D)
+            ops.dec_attn(qkv[:, :D], kc, vc, o1, n=R, H=H, klen_max=st["Lmax"], k_bstride=0, v_bstride=0,
+                         klen=st["klen_self"], kmap=anc)
             y1 = ops.linear_fwd(o1, eng.w(sa + "linear_out.weight"), ar.master(sa + "linear_out.bias"), res=x)
             n2, _, _ = ops.layernorm_fwd(y1, ar.master(p + "norm2.weight"), ar.master(p + "norm2.bias"), 1e-12)
             q2 = ops.linear_fwd(n2, eng.w(ca + "linear_q.weight"), ar.master(ca + "linear_q.bias"))
-            o2 = eng._e(n, D)
-            kv = mem[i]
-            bs = 0 if kidx is None else T * kv.stride(0)
-            ops.dec_attn(q2, kv[:, :D], kv[:, D:], o2, n=n, H=H, klen_max=T, k_bstride=bs, v_bstride=bs,
-                         kidx=kidx, klen=klen)
+            o2 = eng._e(R, D)
+            kv = st["mem"][i]
+            ops.dec_attn(q2, kv[:, :D], kv[:, D:], o2, n=R, H=H, klen_max=Tm, k_bstride=Tm * kv.stride(0),
+                         v_bstride=Tm * kv.stride(0), kidx=st["uidx"], klen=st["klen_mem"])
             y2 = ops.linear_fwd(o2, eng.w(ca + "linear_out.weight"), ar.master(ca + "linear_out.bias"), res=y1)
             n3, _, _ = ops.layernorm_fwd(y2, ar.master(p + "norm3.weight"), ar.master(p + "norm3.bias"), 1e-12)
             a = ops.linear_fwd(n3, eng.w(ff + "w_1.weight"), ar.master(ff + "w_1.bias"), act=ops.L.ACT_RELU)
             x = ops.linear_fwd(a, eng.w(ff + "w_2.weight"), ar.master(ff + "w_2.bias"), res=y2)
         yn, _, _ = ops.layernorm_fwd(x, ar.master("decoder.after_norm.weight"), ar.master("decoder.after_norm.bias"),
                                      1e-12)
-        logits = eng._e(n, eng.Vp)
+        logits = eng._e(R, eng.Vp)
         ops.linear_fwd(yn, eng.w("decoder.output_layer.weight"), ar.master("decoder.output_layer.bias"),
                        out=logits[:, :eng.V])
-        logp = torch.empty(n, eng.V, device=eng.device, dtype=torch.float32)
+        logp = torch.empty(R, eng.V, device=eng.device, dtype=torch.float32)
         return ops.log_softmax_rows(logits, eng.V, logp)
+
+    def _step(self, eng, st, first, k):
+        """one search step on the device (no host sync): decoder, pre-beam, CTC prefix scores,
+        per-utterance beam selection, bookkeeping, state reorder. k = 0 / 1 picks the ancestry
+        and CTC-state ping-pong buffers (read k, write 1 - k)."""
+        R, P, beam = st["R"], self.pre_beam_size, self.beam_size
+        st["anc_in"] = st["anc"][k]
+        ops.beam_step_prep(R, st["pos"], st["anc"][k], st["klen_self"])
+        dec = self._decoder_step(eng, st)
+        ops.row_topk(dec, self.n_vocab, P, st["ids"])
+        ops.ctc_prefix(st["logp"], None if first else st["r_prev"][k], st["tok"], st["ids"], st["r_new"], st["psi"],
+                       n=R, out_len=0, out_len_dev=st["pos"], blank=self.blank, eos=self.eos, uidx=st["uidx"],
+                       tlen=st["tlen"])
+        out = st["out"]
+        ops.beam_select(dec, self.n_vocab, st["ids"], st["psi"], st["s_prev"], st["score"], out, n=R, beam=beam,
+                        blank=self.blank, eos=self.eos, w_dec=self.w_dec, w_ctc=self.w_ctc, seg=st["seg"])
+        ops.beam_post(U=st["U"], beam=beam, P=P, R=R, Lmax=st["Lmax"], steps_cap=st["steps"], eos=self.eos,
+                      end_detect=st["end_detect"], d_end=float(D_END), pos=st["pos"], maxlen=st["maxlen"],
+                      sel_prev=out["prev"], sel_tok=out["tok"], sel_col=out["col"], sel_score=out["score"],
+                      sel_dec=out["dec"], sel_ctc=out["ctc"], sel_s=out["s"], tok=st["tok"], score=st["score"],
+                      sdec=st["sdec"], sctc=st["sctc"], s_prev=st["s_prev"], src=st["src"], bp_prev=st["bp_prev"],
+                      bp_tok=st["bp_tok"], end_flag=st["end_flag"], end_score=st["end_score"], end_dec=st["end_dec"],
+                      end_ctc=st["end_ctc"], best_len=st["best_len"], best_end=st["best_end"], done=st["done"])
+        Lm, Tm = st["Lmax"], st["Tm"]
+        ops.gather_rows(st["anc"][k], st["anc"][1 - k], st["src"][:R], groups=1, n=R, row_bytes=Lm * 4,
+                        src_gstride=0, src_rstride=Lm * 4, dst_gstride=0, dst_rstride=Lm * 4)
+        ops.gather_rows(st["r_new"], st["r_prev"][1 - k], st["src"][R:], groups=1, n=R, row_bytes=Tm * 2 * 4,
+                        src_gstride=0, src_rstride=Tm * 2 * 4, dst_gstride=0, dst_rstride=Tm * 2 * 4)
 
     # ----------------------------------------------------------------------- search
     def forward(self, x, maxlenratio: float = 0.0, minlenratio: float = 0.0) -> List[Hypothesis]:
-        eng = self.e2e.engine()
-        dev = eng.device
-        T = x.shape[0]
-        if maxlenratio == 0:
-            maxlen = T
-        elif maxlenratio < 0:
-            maxlen = -1 * int(maxlenratio)
-        else:
-            maxlen = max(1, int(maxlenratio * T))
-        x, logp, mem = self._prepare(eng, x)
-        V, P, beam = self.n_vocab, self.pre_beam_size, self.beam_size
-        D = eng.dD
-        Lmax = maxlen + 1
-        cache = torch.empty(eng.dl, 2, beam, Lmax, D, device=dev, dtype=eng.dtype)
-        cache2 = torch.empty_like(cache)
-        ids = torch.empty(beam, P, device=dev, dtype=torch.int32)
-        psi = torch.empty(beam, P + 1, device=dev, dtype=torch.float32)
-        r_new = torch.empty(beam, P, T, 2, device=dev, dtype=torch.float32)
-        r_prev = torch.empty(beam, T, 2, device=dev, dtype=torch.float32)
-        r_prev2 = torch.empty_like(r_prev)
-        out = {k: torch.empty(beam, device=dev, dtype=torch.int32) for k in ("prev", "tok", "col")}
-        out.update({k: torch.empty(beam, device=dev, dtype=torch.float32) for k in ("score", "dec", "ctc", "s")})
-        esz = cache.element_size()
+        """the reference's call form bs(x) on one encoded utterance (T, d)"""
+        return self.decode_batch([x], maxlenratio, minlenratio)[0]
 
-        # running hypotheses (host side): token lists, scores; device side: caches, r_prev
-        yseqs = [[self.sos]]
-        score = [0.0]
-        sc_dec, sc_ctc = [0.0], [0.0]
-        s_prev = [0.0]
-        first = True
-        ended = []
-        for i in range(maxlen):
-            n = len(yseqs)
-            pos = len(yseqs[0]) - 1
-            toks = torch.tensor([y[-1] for y in yseqs], dtype=torch.int32).to(dev, non_blocking=True)
-            dec = self._decoder_step(eng, toks, pos, n, cache, mem, T)
-            ops.row_topk(dec, V, P, ids[:n])
-            ops.ctc_prefix(logp, None if first else r_prev[:n], toks, ids[:n], r_new[:n], psi[:n], n=n,
-                           out_len=pos, blank=self.blank, eos=self.eos)
-            sp = torch.tensor(s_prev, dtype=torch.float32).to(dev, non_blocking=True)
-            scv = torch.tensor(score, dtype=torch.float32).to(dev, non_blocking=True)
-            nb = min(beam, n * V)
-            ops.beam_select(dec, V, ids[:n], psi[:n], sp, scv, out, n=n, beam=nb, blank=self.blank, eos=self.eos,
-                            w_dec=self.w_dec, w_ctc=self.w_ctc)
-            res = {k: v[:nb].cpu() for k, v in out.items()}     # the one host sync per step
-            prev, tok, col = res["prev"].tolist(), res["tok"].tolist(), res["col"].tolist()
-            # new hypotheses (batch_beam_search.py:228-260)
-            new = []
-            for j in range(nb):
-                h = prev[j]
-                new.append(dict(yseq=yseqs[h] + [tok[j]], score=float(res["score"][j]),
-                                dec=sc_dec[h] + float(res["dec"][j]), ctc=sc_ctc[h] + float(res["ctc"][j]),
-                                s=float(res["s"][j]), src=h, col=col[j]))
-            # post_process (batch_beam_search.py:262-349)
-            if i == maxlen - 1:
-                for hyp in new:
-                    hyp["yseq"] = hyp["yseq"] + [self.eos]
-            keep = []
-            for hyp in new:
-                if hyp["yseq"][-1] == self.eos:
-                    ended.append(self._make_hyp(hyp))
-                else:
-                    keep.append(hyp)
-            # beam_search.py:369: end detection only when the length limit is the input length
-            if maxlenratio == 0.0 and end_detect([h.asdict() for h in ended], i):
-                break
-            if not keep:
-                break
-            # reorder the device state of the surviving hypotheses
-            m = len(keep)
-            src_idx = torch.tensor([hyp["src"] for hyp in keep], dtype=torch.int32).to(dev, non_blocking=True)
-            rsel = torch.tensor([hyp["src"] * P + hyp["col"] for hyp in keep], dtype=torch.int32).to(dev, non_blocking=True)
-            row = Lmax * D * esz
-            ops.gather_rows(cache, cache2, src_idx, groups=eng.dl * 2, n=m, row_bytes=(pos + 1) * D * esz,
-                            src_gstride=beam * row, src_rstride=row, dst_gstride=beam * row, dst_rstride=row)
-            cache, cache2 = cache2, cache
-            ops.gather_rows(r_new, r_prev2, rsel, groups=1, n=m, row_bytes=T * 2 * 4, src_gstride=0,
-                            src_rstride=T * 2 * 4, dst_gstride=0, dst_rstride=T * 2 * 4)
-            r_prev, r_prev2 = r_prev2, r_prev
-            first = False
-            yseqs = [hyp["yseq"] for hyp in keep]
-            score = [hyp["score"] for hyp in keep]
-            sc_dec = [hyp["dec"] for hyp in keep]
-            sc_ctc = [hyp["ctc"] for hyp in keep]
-            s_prev = [hyp["s"] for hyp in keep]
-        nbest = sorted(ended, key=lambda h: float(h.score), reverse=True)
-        if len(nbest) == 0:
-            return [] if minlenratio < 0.1 else self.forward(x, maxlenratio, max(0.0, minlenratio - 0.1))
-        return nbest
-
-    # ----------------------------------------------------------------- batched utterances
     def decode_batch(self, xs, maxlenratio: float = 0.0, minlenratio: float = 0.0):
-        """Beam search of several utterances at once: xs = list of encoded utterances (T_u, d).
-        Every step runs the decoder, pre-beam, CTC prefix scoring and the per-utterance beam
-        selection for all running hypotheses of all utterances in the same launches (the
-        hypotheses of utterance u are rows [seg[u], seg[u+1])), with one host read-back per
-        step. Per utterance the search is exactly `self(x)`: same scores, same stopping rules
-        (maxlen = T_u, end detection, eos forced at the last step); an utterance that finishes
-        leaves the batch. Returns one n-best list per utterance."""
+        """Beam search of U utterances at once: xs = list of encoded utterances (T_u, d). Per
+        utterance the search is exactly `self(x)` of the reference (batch_beam_search.py:102-349,
+        beam_search.py:330-456): same scores, same stopping rules (maxlen = T_u, end detection,
+        eos forced at the last step). The whole search state lives on the device in a fixed
+        geometry of U x beam rows (a finished hypothesis or utterance becomes a dead row with
+        score -inf, which no selection picks — the same outcome as the reference removing it);
+        the first step runs eagerly, every later step is ONE replay of a captured HIP graph (two
+        graphs: the ancestry / CTC-state ping-pong buffers alternate), the host only reads the
+        count of finished utterances every few steps and the history once at the end. Returns
+        one n-best list per utterance."""
         eng = self.e2e.engine()
         dev = eng.device
         U = len(xs)
@@ -259,7 +185,7 @@ class BatchBeamSearch:
         Tm = max(Ts)
         maxlens = [T if maxlenratio == 0 else (-int(maxlenratio) if maxlenratio < 0 else max(1, int(maxlenratio * T)))
                    for T in Ts]
-        D, V, P, beam = eng.dD, self.n_vocab, self.pre_beam_size, self.beam_size
+        D, P, beam = eng.dD, self.pre_beam_size, self.beam_size
         ar = eng.arena
         # padded memory [U][Tm][D] -> CTC log-probs [U][Tm][V] and per-layer cross K/V [U*Tm][2D]
         xp = torch.zeros(U, Tm, D, device=dev, dtype=eng.dtype)
@@ -275,89 +201,83 @@ class BatchBeamSearch:
             ca = f"decoder.decoders.{i}.src_attn."
             mem.append(ops.linear_fwd(x2, ar.span([ca + "linear_k.weight", ca + "linear_v.weight"]),
                                       ar.span([ca + "linear_k.bias", ca + "linear_v.bias"], buf="master")))
-        tlen = torch.tensor(Ts, dtype=torch.int32).to(dev)
-        NM = U * beam
-        Lmax = max(maxlens) + 1
-        cache = torch.empty(eng.dl, 2, NM, Lmax, D, device=dev, dtype=eng.dtype)
-        cache2 = torch.empty_like(cache)
-        ids = torch.empty(NM, P, device=dev, dtype=torch.int32)
-        psi = torch.empty(NM, P + 1, device=dev, dtype=torch.float32)
-        r_new = torch.empty(NM, P, Tm, 2, device=dev, dtype=torch.float32)
-        r_prev = torch.empty(NM, Tm, 2, device=dev, dtype=torch.float32)
-        r_prev2 = torch.empty_like(r_prev)
-        out = {k: torch.empty(NM, device=dev, dtype=torch.int32) for k in ("prev", "tok", "col")}
-        out.update({k: torch.empty(NM, device=dev, dtype=torch.float32) for k in ("score", "dec", "ctc", "s")})
-        esz = cache.element_size()
-        # running hypotheses, grouped by utterance: host lists
-        run = [[dict(yseq=[self.sos], score=0.0, dec=0.0, ctc=0.0, s=0.0)] for _ in range(U)]
-        active = list(range(U))
+        steps = max(maxlens)
+        Lmax = steps + 1
+        eng.ensure_pe(Lmax)
+        R = U * beam
+        i32 = dict(device=dev, dtype=torch.int32)
+        f32 = dict(device=dev, dtype=torch.float32)
+        f64 = dict(device=dev, dtype=torch.float64)
+        rows = torch.arange(R, dtype=torch.int32)
+        score0 = torch.full((R,), float("-inf"))
+        score0[::beam] = 0.0                  # one live hypothesis (sos) per utterance
+        st = dict(
+            U=U, R=R, Lmax=Lmax, Tm=Tm, steps=steps, end_detect=int(maxlenratio == 0.0), mem=mem, logp=logp,
+            pos=torch.zeros(1, **i32), maxlen=torch.tensor(maxlens, dtype=torch.int32).to(dev),
+            tok=torch.full((R,), self.sos, **i32), score=score0.to(dev),
+            sdec=torch.zeros(R, **f64), sctc=torch.zeros(R, **f64), s_prev=torch.zeros(R, **f32),
+            cache=torch.empty(eng.dl, 2, Lmax * R, D, device=dev, dtype=eng.dtype),
+            anc=[torch.zeros(R, Lmax, **i32), torch.zeros(R, Lmax, **i32)], klen_self=torch.empty(R, **i32),
+            uidx=(rows // beam).to(dev), klen_mem=torch.tensor(Ts, dtype=torch.int32)[rows // beam].to(dev),
+            tlen=torch.tensor(Ts, dtype=torch.int32).to(dev),
+            seg=(torch.arange(U + 1, dtype=torch.int32) * beam).to(dev),
+            ids=torch.empty(R, P, **i32), psi=torch.empty(R, P + 1, **f32),
+            r_new=torch.empty(R, P, Tm, 2, **f32), r_prev=[torch.empty(R, Tm, 2, **f32), torch.empty(R, Tm, 2, **f32)],
+            out={**{k: torch.empty(R, **i32) for k in ("prev", "tok", "col")},
+                 **{k: torch.empty(R, **f32) for k in ("score", "dec", "ctc", "s")}},
+            src=torch.empty(2 * R, **i32),
+            bp_prev=torch.zeros(steps, R, **i32), bp_tok=torch.zeros(steps, R, **i32),
+            end_flag=torch.zeros(steps, R, **i32), end_score=torch.zeros(steps, R, **f32),
+            end_dec=torch.zeros(steps, R, **f64), end_ctc=torch.zeros(steps, R, **f64),
+            best_len=torch.full((U, Lmax + 3), float("-inf"), **f32), best_end=torch.full((U,), float("-inf"), **f32),
+            done=torch.zeros(U + 1, **i32))
+        self._step(eng, st, True, 0)           # step 0: CTC state from scratch; reads ancestry 0, writes 1
+        if steps > 1:
+            graphs = self._capture(eng, st)
+            done_host = st["done"][U:]
+            for i in range(1, steps):
+                graphs[i & 1].replay()         # step i reads ping-pong buffer i & 1
+                if i % 8 == 0 and int(done_host.item()) == U:
+                    break
+        torch.cuda.current_stream(dev).synchronize()
+        return self._collect(st, xs, maxlenratio, minlenratio)
+
+    def _capture(self, eng, st):
+        """two graphs of the generic step (k = 0, 1): capture records, it does not run"""
+        dev = eng.device
+        graphs = []
+        s = torch.cuda.Stream(device=dev)
+        s.wait_stream(torch.cuda.current_stream(dev))
+        for k in (0, 1):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=s):
+                self._step(eng, st, False, k)
+            graphs.append(g)
+        torch.cuda.current_stream(dev).wait_stream(s)
+        return graphs
+
+    def _collect(self, st, xs, maxlenratio, minlenratio):
+        """ended hypotheses from the device history, per utterance in the reference's order
+        (step, then selection rank), yseq rebuilt from the back-pointers"""
+        U, R, beam = st["U"], st["R"], self.beam_size
+        n = min(int(st["pos"].item()), st["steps"])
+        bp_prev = st["bp_prev"][:n].cpu().numpy()
+        bp_tok = st["bp_tok"][:n].cpu().numpy()
+        flag = st["end_flag"][:n].cpu().numpy()
+        esc = st["end_score"][:n].cpu().numpy()
+        edec = st["end_dec"][:n].cpu().numpy()
+        ectc = st["end_ctc"][:n].cpu().numpy()
         ended = [[] for _ in range(U)]
-        first = True
-        i = 0
-        while active:
-            hyps = [(u, h) for u in active for h in run[u]]
-            n = len(hyps)
-            pos = i
-            seg_h = [0]
-            for u in active:
-                seg_h.append(seg_h[-1] + len(run[u]))
-            host = torch.tensor([h["yseq"][-1] for _, h in hyps] + [u for u, _ in hyps] +
-                                [Ts[u] for u, _ in hyps] + seg_h, dtype=torch.int32)
-            dv = host.to(dev, non_blocking=True)
-            toks, uidx, klen, seg = dv[:n], dv[n:2 * n], dv[2 * n:3 * n], dv[3 * n:]
-            dec = self._decoder_step(eng, toks, pos, n, cache, mem, Tm, kidx=uidx, klen=klen)
-            ops.row_topk(dec, V, P, ids[:n])
-            ops.ctc_prefix(logp, None if first else r_prev[:n], toks, ids[:n], r_new[:n], psi[:n], n=n, out_len=pos,
-                           blank=self.blank, eos=self.eos, uidx=uidx, tlen=tlen)
-            fv = torch.tensor([h["s"] for _, h in hyps] + [h["score"] for _, h in hyps], dtype=torch.float32)
-            fv = fv.to(dev, non_blocking=True)
-            ops.beam_select(dec, V, ids[:n], psi[:n], fv[:n], fv[n:], out, n=n, beam=beam, blank=self.blank,
-                            eos=self.eos, w_dec=self.w_dec, w_ctc=self.w_ctc, seg=seg)
-            nsel = len(active) * beam
-            res = {k: v[:nsel].cpu() for k, v in out.items()}     # the one host sync per step
-            prev, tok, col = res["prev"].tolist(), res["tok"].tolist(), res["col"].tolist()
-            keep_src, keep_col, still = [], [], []
-            for a, u in enumerate(active):
-                new = []
-                for r in range(beam):
-                    o = a * beam + r
-                    g = prev[o]
-                    h = hyps[g][1]
-                    new.append(dict(yseq=h["yseq"] + [tok[o]], score=float(res["score"][o]),
-                                    dec=h["dec"] + float(res["dec"][o]), ctc=h["ctc"] + float(res["ctc"][o]),
-                                    s=float(res["s"][o]), src=g, col=col[o]))
-                if i == maxlens[u] - 1:
-                    for hyp in new:
-                        hyp["yseq"] = hyp["yseq"] + [self.eos]
-                keep = []
-                for hyp in new:
-                    if hyp["yseq"][-1] == self.eos:
-                        ended[u].append(self._make_hyp(hyp))
-                    else:
-                        keep.append(hyp)
-                done = (maxlenratio == 0.0 and end_detect([h.asdict() for h in ended[u]], i)) or not keep \
-                    or i >= maxlens[u] - 1
-                if done:
-                    run[u] = []
-                    continue
-                run[u] = keep
-                still.append(u)
-                keep_src += [hyp["src"] for hyp in keep]
-                keep_col += [hyp["src"] * P + hyp["col"] for hyp in keep]
-            active = still
-            if not active:
-                break
-            m = len(keep_src)
-            idx = torch.tensor(keep_src + keep_col, dtype=torch.int32).to(dev, non_blocking=True)
-            row = Lmax * D * esz
-            ops.gather_rows(cache, cache2, idx[:m], groups=eng.dl * 2, n=m, row_bytes=(pos + 1) * D * esz,
-                            src_gstride=NM * row, src_rstride=row, dst_gstride=NM * row, dst_rstride=row)
-            cache, cache2 = cache2, cache
-            ops.gather_rows(r_new, r_prev2, idx[m:], groups=1, n=m, row_bytes=Tm * 2 * 4, src_gstride=0,
-                            src_rstride=Tm * 2 * 4, dst_gstride=0, dst_rstride=Tm * 2 * 4)
-            r_prev, r_prev2 = r_prev2, r_prev
-            first = False
-            i += 1
+        for i in range(n):
+            for r in np.nonzero(flag[i])[0].tolist():
+                toks = [int(bp_tok[i, r])]
+                h = int(bp_prev[i, r])
+                for j in range(i - 1, -1, -1):
+                    toks.append(int(bp_tok[j, h]))
+                    h = int(bp_prev[j, h])
+                yseq = [self.sos] + toks[::-1] + ([self.eos] if flag[i, r] == 2 else [])
+                ended[r // beam].append(self._make_hyp(dict(yseq=yseq, score=float(esc[i, r]), dec=float(edec[i, r]),
+                                                            ctc=float(ectc[i, r]))))
         results = []
         for u in range(U):
             nbest = sorted(ended[u], key=lambda h: float(h.score), reverse=True)
