@@ -71,31 +71,46 @@ __global__ __launch_bounds__(256) void log_softmax_kernel(int V, const T* x, int
 }
 
 // ---------------------------------------------------------------- one-query attention
-// block (hyp i, head h): scores of all valid keys in LDS, softmax, then o = sum_j p_j v_j
-// with 64 dims x 4 key groups per block and an LDS reduce of the groups.
+// block (hyp i, head h), 4 waves: a wave reads 4 keys per instruction (16 lanes x 4 elements
+// per 64-wide row: coalesced 256-B rows), scores by 16-lane butterfly sums into LDS, block
+// softmax, then o = sum_j p_j v_j with the same row-per-16-lanes reads, reduced over the 4 key
+// slots of a wave (shuffles) and the 4 waves (LDS). Rows come through kmap (ancestry-indexed
+// self-attention cache), kidx (batched memories) or directly.
+template <typename T> AVSR_DEV f32x4 ld4(const T* p) {
+  if constexpr (sizeof(T) == 2) {
+    const bf16x4 v = *(const bf16x4*)p;
+    return f32x4{(float)v[0], (float)v[1], (float)v[2], (float)v[3]};
+  } else {
+    return *(const f32x4*)p;
+  }
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void dec_attn_kernel(avsr_dec_attn_params p) {
   extern __shared__ float sc[];           // [klen_max] scores, then [4][64] partials
   __shared__ float sh[4];
   const int h = blockIdx.x, i = blockIdx.y;
   const int klen = p.klen ? min(p.klen[i], p.klen_max) : p.klen_max;
-  const T* q = (const T*)p.q + (int64_t)i * p.ldq + h * 64;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, sub = lane >> 4, d0 = (lane & 15) * 4;
   const int kb = p.kmap ? 0 : (p.kidx ? p.kidx[i] : i);
-  const T* K = (const T*)p.k + (int64_t)kb * p.k_bstride + h * 64;
-  const T* Vv = (const T*)p.v + (int64_t)kb * p.v_bstride + h * 64;
+  const T* K = (const T*)p.k + (int64_t)kb * p.k_bstride + h * 64 + d0;
+  const T* Vv = (const T*)p.v + (int64_t)kb * p.v_bstride + h * 64 + d0;
   const int* km = p.kmap ? p.kmap + (int64_t)i * p.ldmap : nullptr;   // key j -> row km[j]
-  float qr[64];
-#pragma unroll
-  for (int d = 0; d < 64; ++d) qr[d] = to_f(q[d]);
+  const f32x4 q = ld4((const T*)p.q + (int64_t)i * p.ldq + h * 64 + d0);
   float m = -INFINITY;
-  for (int j = threadIdx.x; j < klen; j += 256) {
-    const T* kr = K + (int64_t)(km ? km[j] : j) * p.ldk;
-    float s = 0.f;
+  for (int j0 = 4 * w; j0 < klen; j0 += 16) {
+    const int j = j0 + sub;
+    const bool ok = j < klen;
+    const int row = ok ? (km ? km[j] : j) : 0;
+    const f32x4 k = ld4(K + (int64_t)row * p.ldk);
+    float s = q[0] * k[0] + q[1] * k[1] + q[2] * k[2] + q[3] * k[3];
 #pragma unroll
-    for (int d = 0; d < 64; ++d) s += qr[d] * to_f(kr[d]);
+    for (int o = 1; o < 16; o <<= 1) s += __shfl_xor(s, o, 64);
     s *= p.scale;
-    sc[j] = s;
-    m = fmaxf(m, s);
+    if (ok) {
+      if ((lane & 15) == 0) sc[j] = s;
+      m = fmaxf(m, s);
+    }
   }
   m = block_max256(m, sh);
   float l = 0.f;
@@ -105,14 +120,26 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(avsr_dec_attn_params p) {
     l += e;
   }
   l = block_sum256(l, sh);     // includes a barrier: every sc[j] is final
-  const int d = threadIdx.x & 63, g = threadIdx.x >> 6;
-  float acc = 0.f;
-  for (int j = g; j < klen; j += 4) acc += sc[j] * to_f(Vv[(int64_t)(km ? km[j] : j) * p.ldv + d]);
-  float* part = sc + p.klen_max;
-  part[g * 64 + d] = acc;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int j0 = 4 * w; j0 < klen; j0 += 16) {
+    const int j = j0 + sub;
+    const bool ok = j < klen;
+    const int row = ok ? (km ? km[j] : j) : 0;
+    const f32x4 v = ld4(Vv + (int64_t)row * p.ldv);
+    const float pj = ok ? sc[j] : 0.f;
+    acc += pj * v;
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    acc[e] += __shfl_xor(acc[e], 16, 64);
+    acc[e] += __shfl_xor(acc[e], 32, 64);
+  }
+  float* part = sc + ((p.klen_max + 3) & ~3);
+  if (sub == 0) *(f32x4*)&part[w * 64 + d0] = acc;
   __syncthreads();
-  if (g == 0) {
-    const float o = (part[d] + part[64 + d] + part[128 + d] + part[192 + d]) / l;
+  if (threadIdx.x < 64) {
+    const int d = threadIdx.x;
+    const float o = ((part[d] + part[64 + d]) + (part[128 + d] + part[192 + d])) / l;
     ((T*)p.o)[(int64_t)i * p.ldo + h * 64 + d] = from_f<T>(o);
   }
 }
@@ -569,7 +596,9 @@ extern "C" int avsr_beam_post(const avsr_beam_post_params* p, void* stream) {
 extern "C" int avsr_dec_attn(const avsr_dec_attn_params* p, void* stream) {
   if (!p || p->n <= 0 || p->H <= 0) return AVSR_E_ARG;
   if (p->klen_max <= 0 || p->klen_max > 16384) return AVSR_E_SHAPE;
-  const size_t lds = (size_t)(p->klen_max + 256) * sizeof(float);
+  const int ve = p->dtype == AVSR_BF16 ? 4 : 4;      // 4-element row pieces: 8 / 16-byte aligned rows
+  if (p->ldq % ve || p->ldk % ve || p->ldv % ve || p->k_bstride % ve || p->v_bstride % ve) return AVSR_E_ALIGN;
+  const size_t lds = ((size_t)(p->klen_max + 3) / 4 * 4 + 256) * sizeof(float);
   const dim3 g(p->H, p->n);
   if (p->dtype == AVSR_BF16) hipLaunchKernelGGL(dec_attn_kernel<bf16>, g, dim3(256), lds, (hipStream_t)stream, *p);
   else if (p->dtype == AVSR_F32) hipLaunchKernelGGL(dec_attn_kernel<float>, g, dim3(256), lds, (hipStream_t)stream, *p);

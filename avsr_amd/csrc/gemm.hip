@@ -381,10 +381,15 @@ template <typename T> AVSR_DEV f32x4 ld4f(const T* p) {
 }
 
 // K split (part != nullptr): block row blockIdx.y sums k in [y * kchunk, (y + 1) * kchunk) and
-// writes the raw sums to part[y][m][n]; skinny_reduce_kernel adds the S partials in a fixed
-// order and runs the epilogue (N / 16 workgroups alone leave most CUs idle at N = 1024)
+// writes the raw sums to part[y][m][n] (N / 16 workgroups alone leave most CUs idle at
+// N = 1024); the last of the S workgroups of a column block to arrive (agent-scope counter
+// cnt[blockIdx.x]) adds the S partials in a fixed order and runs the epilogue. Hand-off:
+// partials stored write-through (sc1, relaxed agent-scope atomic stores), every storing wave
+// drains its stores (s_waitcnt vmcnt(0)) before the barrier that precedes the counter add, the
+// reducer reads them with sc1 loads (cdna_hip_programming.md Guideline 16, counter form) — no
+// fence, no second launch; the reducer resets the counter (zero-initialised by the caller).
 template <typename T, typename OutT, int MR>
-__global__ __launch_bounds__(256) void skinny_kernel(DenseArgs a, float* part, int kchunk) {
+__global__ __launch_bounds__(256) void skinny_kernel(DenseArgs a, float* part, int kchunk, unsigned* cnt) {
   constexpr int SK_KC = MR <= 32 ? 256 : 128;        // K chunk staged per pass (<= 33 KiB of LDS)
   constexpr int XPT = MR * SK_KC / 4 / 256;           // A vectors per thread per chunk
   constexpr int WJ = SK_KC / 128;                     // k groups per thread per chunk
@@ -462,20 +467,31 @@ __global__ __launch_bounds__(256) void skinny_kernel(DenseArgs a, float* part, i
     const int m = o / SK_NB, c = o - m * SK_NB, col = n0 + c;
     if (m < a.M && col < a.N) {
       const float v = (red[0][m][c] + red[1][m][c]) + (red[2][m][c] + red[3][m][c]);
-      if (part) part[((int64_t)blockIdx.y * a.M + m) * a.N + col] = v;
+      if (part) __hip_atomic_store(&part[((int64_t)blockIdx.y * a.M + m) * a.N + col], v, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
       else epi_elems<T, OutT, 1>(a.e, m, col, &v);
     }
   }
-}
-
-template <typename T, typename OutT>
-__global__ __launch_bounds__(256) void skinny_reduce_kernel(DenseArgs a, const float* part, int S) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x, MN = (int64_t)a.M * a.N;
-  if (i >= MN) return;
-  float v = part[i];
-  for (int s = 1; s < S; ++s) v += part[s * MN + i];
-  const int m = (int)(i / a.N), col = (int)(i - (int64_t)m * a.N);
-  epi_elems<T, OutT, 1>(a.e, m, col, &v);
+  if (!part) return;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave: its partials are out
+  __shared__ int last;
+  __syncthreads();
+  if (tid == 0)
+    last = __hip_atomic_fetch_add(&cnt[blockIdx.x], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.y - 1;
+  __syncthreads();
+  if (!last) return;
+  const int S = gridDim.y;
+  const int64_t MN = (int64_t)a.M * a.N;
+  for (int o = tid; o < MR * SK_NB; o += 256) {
+    const int m = o / SK_NB, c = o - m * SK_NB, col = n0 + c;
+    if (m < a.M && col < a.N) {
+      const float* pp = part + (int64_t)m * a.N + col;
+      float v = __hip_atomic_load(pp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      for (int s = 1; s < S; ++s) v += __hip_atomic_load(pp + s * MN, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      epi_elems<T, OutT, 1>(a.e, m, col, &v);
+    }
+  }
+  if (tid == 0) __hip_atomic_store(&cnt[blockIdx.x], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // K split count: enough block rows for >= 512 workgroups, chunks of >= 256 k, and S * 64 * N
@@ -495,8 +511,11 @@ int skinny_launch(const DenseArgs& a, float* ws, hipStream_t st) {
   int kchunk = a.K;
   const int S = ws ? skinny_splits(a.N, a.K, kchunk) : 1;
   float* part = S > 1 ? ws : nullptr;
-  const dim3 g((unsigned)((a.N + SK_NB - 1) / SK_NB), (unsigned)S);
-#define SKL(R) hipLaunchKernelGGL((skinny_kernel<T, OutT, R>), g, dim3(256), 0, st, a, part, kchunk)
+  unsigned* cnt = S > 1 ? (unsigned*)(ws + AVSR_SKINNY_WS) : nullptr;   // AVSR_SKINNY_CNT counters
+  const int nb = (a.N + SK_NB - 1) / SK_NB;
+  if (S > 1 && nb > AVSR_SKINNY_CNT) return AVSR_E_SHAPE;
+  const dim3 g((unsigned)nb, (unsigned)S);
+#define SKL(R) hipLaunchKernelGGL((skinny_kernel<T, OutT, R>), g, dim3(256), 0, st, a, part, kchunk, cnt)
   if (a.M <= 8) SKL(8);
   else if (a.M <= 16) SKL(16);
   else if (a.M <= 24) SKL(24);
@@ -506,12 +525,6 @@ int skinny_launch(const DenseArgs& a, float* ws, hipStream_t st) {
   else SKL(64);
 #undef SKL
   AVSR_CHECK_LAUNCH();
-  if (part) {
-    const int64_t MN = (int64_t)a.M * a.N;
-    hipLaunchKernelGGL((skinny_reduce_kernel<T, OutT>), dim3((unsigned)((MN + 255) / 256)), dim3(256), 0, st, a,
-                       (const float*)part, S);
-    AVSR_CHECK_LAUNCH();
-  }
   return 0;
 }
 

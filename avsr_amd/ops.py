@@ -38,7 +38,8 @@ def _ptr(t):
 
 
 _SKINNY_WS = {}
-SKINNY_WS = 1 << 19        # AVSR_SKINNY_WS
+SKINNY_WS = 1 << 19        # AVSR_SKINNY_WS (fp32 partials), followed by
+SKINNY_CNT = 4096          # AVSR_SKINNY_CNT zeroed uint32 arrival counters
 # few-row (decoder step) linears: split K over more workgroups (gemm(skinny_split=None) default)
 SKINNY_SPLIT = False
 
@@ -54,7 +55,7 @@ def _skinny_ws(device):
     key = (device, L.stream_ptr().value)
     ws = _SKINNY_WS.get(key)
     if ws is None:
-        ws = _SKINNY_WS[key] = torch.empty(SKINNY_WS, device=device, dtype=torch.float32)
+        ws = _SKINNY_WS[key] = torch.zeros(SKINNY_WS + SKINNY_CNT, device=device, dtype=torch.float32)
     return ws
 
 

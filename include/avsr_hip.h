@@ -83,10 +83,13 @@ typedef struct {
                                 {min start, max end} in s_memrealtime ticks (100 MHz) — every
                                 workgroup folds its first / last instant in by vector atomics.
                                 Caller initialises {~0ull, 0}. No output depends on it. */
-  float* skinny_ws;          /* optional, >= AVSR_SKINNY_WS fp32: with splitk <= 1 and M <= 64 (the
+  float* skinny_ws;          /* optional, AVSR_SKINNY_WS_BYTES: with splitk <= 1 and M <= 64 (the
                                 vector-ALU path of decoder steps) the launch splits K over
-                                avsr_gemm_skinny_splits(N, K) workgroup rows (fp32 partials here,
-                                ordered reduce + epilogue). NULL: one workgroup row */
+                                avsr_gemm_skinny_splits(N, K) workgroup rows: AVSR_SKINNY_WS fp32
+                                partials, then AVSR_SKINNY_CNT uint32 arrival counters that the
+                                caller zeroes once (every launch leaves them zero); the last
+                                workgroup of a column block adds the partials in a fixed order
+                                and runs the epilogue. NULL: one workgroup row */
 } avsr_gemm_params;
 #define AVSR_GEMM_COLSUM_WS(M, N) ((int64_t)(((M) + 63) / 64) * (N))
 /* slabs are AVSR_GEMM_SLAB_PAD floats apart beyond M*N: power-of-two slab strides put the
@@ -94,6 +97,8 @@ typedef struct {
  * 8 slabs of 4 MiB) */
 #define AVSR_GEMM_SLAB_PAD 1088
 #define AVSR_SKINNY_WS (1 << 19)
+#define AVSR_SKINNY_CNT 4096
+#define AVSR_SKINNY_WS_BYTES ((int64_t)AVSR_SKINNY_WS * 4 + AVSR_SKINNY_CNT * 4)
 #define AVSR_GEMM_SLAB_WS(batch, splitk, M, N) ((int64_t)(batch) * (splitk) * ((int64_t)(M) * (N) + AVSR_GEMM_SLAB_PAD))
 
 int avsr_gemm(const avsr_gemm_params* p, void* stream);
