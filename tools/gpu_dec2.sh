@@ -4,7 +4,9 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 O=gpurun_out/${1:-dec2}; mkdir -p $O
-timeout -k 10 600 python -u -m pytest tests/test_gpu_decode.py tests/test_gpu_gemm.py -k "skinny or decode or dec_" tests/test_gpu_fullsize_golden.py tests/test_gpu_surface.py -x -v --timeout 300 --timeout-method thread > $O/tests.log 2>&1 || { echo tests failed; grep -E "FAIL|Error|error" $O/tests.log | head -20; tail -40 $O/tests.log; exit 1; }
+timeout -k 10 300 python -u -m pytest tests/test_gpu_gemm.py -k skinny -x -q --timeout 120 --timeout-method thread > $O/gemm.log 2>&1 || { echo gemm tests failed; tail -30 $O/gemm.log; exit 1; }
+tail -1 $O/gemm.log
+timeout -k 10 600 python -u -m pytest tests/test_gpu_decode.py tests/test_gpu_fullsize_golden.py tests/test_gpu_surface.py -x -v --timeout 300 --timeout-method thread > $O/tests.log 2>&1 || { echo tests failed; grep -E "FAIL|Error|error" $O/tests.log | head -20; tail -40 $O/tests.log; exit 1; }
 tail -1 $O/tests.log
 for r in 1 2; do
   timeout -k 10 300 python -u tools/decode_bench.py > $O/dec_nosplit_$r.json 2> $O/dec.err || { echo dec failed; tail -20 $O/dec.err; exit 1; }
