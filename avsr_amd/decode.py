@@ -191,16 +191,21 @@ class BatchBeamSearch:
         xp = torch.zeros(U, Tm, D, device=dev, dtype=eng.dtype)
         for u, x in enumerate(xs):      # (the cast kernel converts fp32 encoder outputs to bf16 if needed)
             ops.cast(x.to(dev).reshape(Ts[u], D).contiguous(), xp[u, :Ts[u]])
-        x2 = xp.view(U * Tm, D)
-        cl = eng._e(U * Tm, eng.Vp)
-        ops.linear_fwd(x2, eng.w("ctc.ctc_lo.weight"), ar.master("ctc.ctc_lo.bias"), out=cl[:, :eng.V])
+        # the CTC head and the cross-attention K / V projections run per utterance (M = T_u rows,
+        # as in the one-utterance call): the few-row and tiled GEMM cores round differently, so
+        # one launch over all U * Tm rows would make an utterance's scores depend on the batch
+        cl = torch.zeros(U * Tm, eng.Vp, device=dev, dtype=eng.dtype)
+        mem = [torch.zeros(U * Tm, 2 * D, device=dev, dtype=eng.dtype) for _ in range(eng.dl)]
+        for u in range(U):
+            xu, r0 = xp[u, :Ts[u]], u * Tm
+            ops.linear_fwd(xu, eng.w("ctc.ctc_lo.weight"), ar.master("ctc.ctc_lo.bias"), out=cl[r0:r0 + Ts[u], :eng.V])
+            for i in range(eng.dl):
+                ca = f"decoder.decoders.{i}.src_attn."
+                ops.linear_fwd(xu, ar.span([ca + "linear_k.weight", ca + "linear_v.weight"]),
+                               ar.span([ca + "linear_k.bias", ca + "linear_v.bias"], buf="master"),
+                               out=mem[i][r0:r0 + Ts[u]])
         logp = torch.empty(U, Tm, eng.V, device=dev, dtype=torch.float32)
         ops.log_softmax_rows(cl, eng.V, logp.view(U * Tm, eng.V))
-        mem = []
-        for i in range(eng.dl):
-            ca = f"decoder.decoders.{i}.src_attn."
-            mem.append(ops.linear_fwd(x2, ar.span([ca + "linear_k.weight", ca + "linear_v.weight"]),
-                                      ar.span([ca + "linear_k.bias", ca + "linear_v.bias"], buf="master")))
         steps = max(maxlens)
         Lmax = steps + 1
         eng.ensure_pe(Lmax)
