@@ -14,4 +14,7 @@ for r in 1 2; do
   timeout -k 10 300 python -u tools/decode_bench.py split > $O/dec_split_$r.json 2> $O/dec.err || { echo dec failed; tail -20 $O/dec.err; exit 1; }
   echo split; cat $O/dec_split_$r.json
 done
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/p -o run -- python3 tools/decode_c5.py split > $O/prof.log 2>&1 || { echo prof failed; tail -20 $O/prof.log; exit 1; }
+grep C5 $O/prof.log
+rm -f $O/p/run_kernel_trace.csv
 echo rc=0
