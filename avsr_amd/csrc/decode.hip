@@ -85,62 +85,84 @@ template <typename T> AVSR_DEV f32x4 ld4(const T* p) {
   }
 }
 
-template <typename T>
+// G hypotheses per workgroup (p.group; G = 1 for per-hypothesis keys): every key / value row is
+// read once for the G queries of the group
+template <typename T, int G>
 __global__ __launch_bounds__(256) void dec_attn_kernel(avsr_dec_attn_params p) {
-  extern __shared__ float sc[];           // [klen_max] scores, then [4][64] partials
+  extern __shared__ float sc[];           // [G][kpad] scores, then [4][G][64] partials
   __shared__ float sh[4];
-  const int h = blockIdx.x, i = blockIdx.y;
-  const int klen = p.klen ? min(p.klen[i], p.klen_max) : p.klen_max;
+  const int h = blockIdx.x, i0 = blockIdx.y * G;
+  const int klen = p.klen ? min(p.klen[i0], p.klen_max) : p.klen_max;
+  const int kpad = (p.klen_max + 3) & ~3;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, sub = lane >> 4, d0 = (lane & 15) * 4;
-  const int kb = p.kmap ? 0 : (p.kidx ? p.kidx[i] : i);
+  const int kb = p.kmap ? 0 : (p.kidx ? p.kidx[i0] : i0);
   const T* K = (const T*)p.k + (int64_t)kb * p.k_bstride + h * 64 + d0;
   const T* Vv = (const T*)p.v + (int64_t)kb * p.v_bstride + h * 64 + d0;
-  const int* km = p.kmap ? p.kmap + (int64_t)i * p.ldmap : nullptr;   // key j -> row km[j]
-  const f32x4 q = ld4((const T*)p.q + (int64_t)i * p.ldq + h * 64 + d0);
-  float m = -INFINITY;
+  const int* km = p.kmap ? p.kmap + (int64_t)i0 * p.ldmap : nullptr;  // key j -> row km[j] (G == 1)
+  const int ng = min(G, p.n - i0);
+  f32x4 q[G];
+#pragma unroll
+  for (int g = 0; g < G; ++g) q[g] = ld4((const T*)p.q + (int64_t)(i0 + min(g, ng - 1)) * p.ldq + h * 64 + d0);
+  float m[G];
+#pragma unroll
+  for (int g = 0; g < G; ++g) m[g] = -INFINITY;
   for (int j0 = 4 * w; j0 < klen; j0 += 16) {
     const int j = j0 + sub;
     const bool ok = j < klen;
     const int row = ok ? (km ? km[j] : j) : 0;
     const f32x4 k = ld4(K + (int64_t)row * p.ldk);
-    float s = q[0] * k[0] + q[1] * k[1] + q[2] * k[2] + q[3] * k[3];
 #pragma unroll
-    for (int o = 1; o < 16; o <<= 1) s += __shfl_xor(s, o, 64);
-    s *= p.scale;
-    if (ok) {
-      if ((lane & 15) == 0) sc[j] = s;
-      m = fmaxf(m, s);
+    for (int g = 0; g < G; ++g) {
+      float s = q[g][0] * k[0] + q[g][1] * k[1] + q[g][2] * k[2] + q[g][3] * k[3];
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) s += __shfl_xor(s, o, 64);
+      s *= p.scale;
+      if (ok) {
+        if ((lane & 15) == 0) sc[g * kpad + j] = s;
+        m[g] = fmaxf(m[g], s);
+      }
     }
   }
-  m = block_max256(m, sh);
-  float l = 0.f;
-  for (int j = threadIdx.x; j < klen; j += 256) {
-    const float e = expf(sc[j] - m);
-    sc[j] = e;
-    l += e;
+  float l[G];
+#pragma unroll
+  for (int g = 0; g < G; ++g) m[g] = block_max256(m[g], sh);
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    float lg = 0.f;
+    for (int j = threadIdx.x; j < klen; j += 256) {
+      const float e = expf(sc[g * kpad + j] - m[g]);
+      sc[g * kpad + j] = e;
+      lg += e;
+    }
+    l[g] = block_sum256(lg, sh);     // includes a barrier: every score of row g is final
   }
-  l = block_sum256(l, sh);     // includes a barrier: every sc[j] is final
-  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  f32x4 acc[G];
+#pragma unroll
+  for (int g = 0; g < G; ++g) acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
   for (int j0 = 4 * w; j0 < klen; j0 += 16) {
     const int j = j0 + sub;
     const bool ok = j < klen;
     const int row = ok ? (km ? km[j] : j) : 0;
     const f32x4 v = ld4(Vv + (int64_t)row * p.ldv);
-    const float pj = ok ? sc[j] : 0.f;
-    acc += pj * v;
-  }
 #pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    acc[e] += __shfl_xor(acc[e], 16, 64);
-    acc[e] += __shfl_xor(acc[e], 32, 64);
+    for (int g = 0; g < G; ++g) acc[g] += (ok ? sc[g * kpad + j] : 0.f) * v;
   }
-  float* part = sc + ((p.klen_max + 3) & ~3);
-  if (sub == 0) *(f32x4*)&part[w * 64 + d0] = acc;
+  float* part = sc + G * kpad;
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      acc[g][e] += __shfl_xor(acc[g][e], 16, 64);
+      acc[g][e] += __shfl_xor(acc[g][e], 32, 64);
+    }
+    if (sub == 0) *(f32x4*)&part[(w * G + g) * 64 + d0] = acc[g];
+  }
   __syncthreads();
-  if (threadIdx.x < 64) {
-    const int d = threadIdx.x;
-    const float o = ((part[d] + part[64 + d]) + (part[128 + d] + part[192 + d])) / l;
-    ((T*)p.o)[(int64_t)i * p.ldo + h * 64 + d] = from_f<T>(o);
+  for (int t = threadIdx.x; t < ng * 64; t += 256) {
+    const int g = t >> 6, d = t & 63;
+    const float o = ((part[(0 * G + g) * 64 + d] + part[(1 * G + g) * 64 + d]) +
+                     (part[(2 * G + g) * 64 + d] + part[(3 * G + g) * 64 + d])) / l[g];
+    ((T*)p.o)[(int64_t)(i0 + g) * p.ldo + h * 64 + d] = from_f<T>(o);
   }
 }
 
@@ -596,13 +618,23 @@ extern "C" int avsr_beam_post(const avsr_beam_post_params* p, void* stream) {
 extern "C" int avsr_dec_attn(const avsr_dec_attn_params* p, void* stream) {
   if (!p || p->n <= 0 || p->H <= 0) return AVSR_E_ARG;
   if (p->klen_max <= 0 || p->klen_max > 16384) return AVSR_E_SHAPE;
-  const int ve = p->dtype == AVSR_BF16 ? 4 : 4;      // 4-element row pieces: 8 / 16-byte aligned rows
-  if (p->ldq % ve || p->ldk % ve || p->ldv % ve || p->k_bstride % ve || p->v_bstride % ve) return AVSR_E_ALIGN;
-  const size_t lds = ((size_t)(p->klen_max + 3) / 4 * 4 + 256) * sizeof(float);
-  const dim3 g(p->H, p->n);
-  if (p->dtype == AVSR_BF16) hipLaunchKernelGGL(dec_attn_kernel<bf16>, g, dim3(256), lds, (hipStream_t)stream, *p);
-  else if (p->dtype == AVSR_F32) hipLaunchKernelGGL(dec_attn_kernel<float>, g, dim3(256), lds, (hipStream_t)stream, *p);
+  if (p->ldq % 4 || p->ldk % 4 || p->ldv % 4 || p->k_bstride % 4 || p->v_bstride % 4) return AVSR_E_ALIGN;
+  const int G = p->group > 1 ? p->group : 1;
+  if (G > 8 || (G > 1 && p->kmap)) return AVSR_E_ARG;
+  const int kpad = (p->klen_max + 3) & ~3;
+  const size_t lds = ((size_t)G * kpad + (size_t)4 * G * 64) * sizeof(float);
+  if (lds > 64 * 1024) return AVSR_E_SHAPE;
+  const dim3 g(p->H, (p->n + G - 1) / G);
+  hipStream_t st = (hipStream_t)stream;
+#define DA(T_, G_) hipLaunchKernelGGL((dec_attn_kernel<T_, G_>), g, dim3(256), lds, st, *p)
+#define DAG(T_) switch (G) { case 1: DA(T_, 1); break; case 2: DA(T_, 2); break; case 3: DA(T_, 3); break;   \
+                              case 4: DA(T_, 4); break; case 5: DA(T_, 5); break; case 6: DA(T_, 6); break;   \
+                              case 7: DA(T_, 7); break; default: DA(T_, 8); }
+  if (p->dtype == AVSR_BF16) { DAG(bf16) }
+  else if (p->dtype == AVSR_F32) { DAG(float) }
   else return AVSR_E_DTYPE;
+#undef DAG
+#undef DA
   AVSR_CHECK_LAUNCH();
   return 0;
 }

@@ -359,6 +359,11 @@ int by_tile(const avsr_gemm_params* p, const DenseArgs& a, hipStream_t st) {
   return by_layout<T, OutT, 2, 2>(p, a, st);
 }
 
+bool getenv_flag(const char* name) {
+  const char* e = getenv(name);
+  return e && e[0] == '1';
+}
+
 // ---------------------------------------------------------------- skinny (M <= 64) linears
 // The decoder's per-step linears during beam search have n = utterances x beam rows (<= 40 at
 // C5). The tiled cores put one 64 x 256 tile per 256 columns on them (4 workgroups for
@@ -494,6 +499,91 @@ __global__ __launch_bounds__(256) void skinny_kernel(DenseArgs a, float* part, i
   if (tid == 0) __hip_atomic_store(&cnt[blockIdx.x], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// fp32 few-row linears on the fp32-input matrix cores (v_mfma_f32_16x16x4_f32: exact fp32
+// products, fp32 accumulation): a workgroup = 4 waves over one 16-column block, wave w takes the
+// 16-k groups w, w+4, ... of the workgroup's K range; per group a lane loads the 4 consecutive
+// weights of its column (16 B) and, per 16-row tile, its row's 4 activations (16 B, L2-resident:
+// no LDS staging, no barrier in the loop), then 4 MFMAs per row tile. The vector-ALU kernel above
+// reads 40 activations from LDS per 2 weights and is LDS-bound near 2 TB/s; here the row blocking
+// is the matrix core's. Groups are issued UNR at a time (all loads first). Same K split / last-
+// arriver reduction as skinny_kernel; a row's result never depends on M (rows are independent in
+// the MFMA, the k order is fixed).
+template <typename OutT, int MT>
+__global__ __launch_bounds__(256) void skinny_mma_kernel(DenseArgs a, float* part, int kchunk, unsigned* cnt) {
+  constexpr int UNR = 4;
+  __shared__ __attribute__((aligned(16))) float red[4][16 * MT][SK_NB + 1];
+  __shared__ int last;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, c = lane & 15;
+  const int n0 = blockIdx.x * SK_NB, col = n0 + c;
+  const bool cok = col < a.N;
+  const float* Wr = (const float*)a.B + (int64_t)min(col, a.N - 1) * a.ldb + 4 * g;
+  const float* Ar[MT];
+  bool rok[MT];
+#pragma unroll
+  for (int t = 0; t < MT; ++t) {
+    const int m = 16 * t + c;
+    rok[t] = m < a.M;
+    Ar[t] = (const float*)a.A + (int64_t)min(m, a.M - 1) * a.lda + 4 * g;
+  }
+  const int kbeg = part ? blockIdx.y * kchunk : 0, kend = part ? min(a.K, kbeg + kchunk) : a.K;
+  const int ng = (kend - kbeg) / 16;                  // K % 16 == 0 (host-checked); kchunk % 16 == 0
+  f32x4 acc[MT];
+#pragma unroll
+  for (int t = 0; t < MT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int q0 = w; q0 < ng; q0 += 4 * UNR) {
+    f32x4 b[UNR], x[UNR][MT];
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      const int q = q0 + 4 * u;
+      const bool ok = q < ng;
+      const int k = kbeg + 16 * (ok ? q : 0);
+      b[u] = (ok && cok) ? *(const f32x4*)(Wr + k) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int t = 0; t < MT; ++t) x[u][t] = (ok && rok[t]) ? *(const f32x4*)(Ar[t] + k) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int u = 0; u < UNR; ++u)
+#pragma unroll
+      for (int t = 0; t < MT; ++t)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(x[u][t][e], b[u][e], acc[t], 0, 0, 0);
+  }
+  // acc[t][r] = this wave's partial of y[16t + 4g + r][n0 + c]; the 4 waves' in a fixed order
+#pragma unroll
+  for (int t = 0; t < MT; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) red[w][16 * t + 4 * g + r][c] = acc[t][r];
+  __syncthreads();
+  for (int o = tid; o < 16 * MT * SK_NB; o += 256) {
+    const int m = o / SK_NB, cc = o - m * SK_NB, cl = n0 + cc;
+    if (m < a.M && cl < a.N) {
+      const float v = (red[0][m][cc] + red[1][m][cc]) + (red[2][m][cc] + red[3][m][cc]);
+      if (part) __hip_atomic_store(&part[((int64_t)blockIdx.y * a.M + m) * a.N + cl], v, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+      else epi_elems<float, OutT, 1>(a.e, m, cl, &v);
+    }
+  }
+  if (!part) return;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave: its partials are out
+  __syncthreads();
+  if (tid == 0)
+    last = __hip_atomic_fetch_add(&cnt[blockIdx.x], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.y - 1;
+  __syncthreads();
+  if (!last) return;
+  const int S = gridDim.y;
+  const int64_t MN = (int64_t)a.M * a.N;
+  for (int o = tid; o < 16 * MT * SK_NB; o += 256) {
+    const int m = o / SK_NB, cc = o - m * SK_NB, cl = n0 + cc;
+    if (m < a.M && cl < a.N) {
+      const float* pp = part + (int64_t)m * a.N + cl;
+      float v = __hip_atomic_load(pp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      for (int s = 1; s < S; ++s) v += __hip_atomic_load(pp + s * MN, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      epi_elems<float, OutT, 1>(a.e, m, cl, &v);
+    }
+  }
+  if (tid == 0) __hip_atomic_store(&cnt[blockIdx.x], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // K split count: enough block rows for >= 512 workgroups, chunks of >= 256 k, and S * 64 * N
 // partials within AVSR_SKINNY_WS (S depends on N and K only, never on M: a row's result does
 // not depend on how many rows share the launch).
@@ -515,6 +605,18 @@ int skinny_launch(const DenseArgs& a, float* ws, hipStream_t st) {
   const int nb = (a.N + SK_NB - 1) / SK_NB;
   if (S > 1 && nb > AVSR_SKINNY_CNT) return AVSR_E_SHAPE;
   const dim3 g((unsigned)nb, (unsigned)S);
+  if constexpr (sizeof(T) == 4) {       // fp32: the matrix-core form (16-byte rows, 16-k groups)
+    if (a.K % 16 == 0 && kchunk % 16 == 0 && a.lda % 4 == 0 && a.ldb % 4 == 0 && !getenv_flag("AVSR_SKINNY_VALU")) {
+#define SKM(T_) hipLaunchKernelGGL((skinny_mma_kernel<OutT, T_>), g, dim3(256), 0, st, a, part, kchunk, cnt)
+      if (a.M <= 16) SKM(1);
+      else if (a.M <= 32) SKM(2);
+      else if (a.M <= 48) SKM(3);
+      else SKM(4);
+#undef SKM
+      AVSR_CHECK_LAUNCH();
+      return 0;
+    }
+  }
 #define SKL(R) hipLaunchKernelGGL((skinny_kernel<T, OutT, R>), g, dim3(256), 0, st, a, part, kchunk, cnt)
   if (a.M <= 8) SKL(8);
   else if (a.M <= 16) SKL(16);
@@ -560,10 +662,6 @@ bool skinny_ok(const avsr_gemm_params* p, int splits) {
          ((uintptr_t)p->B % (4 * esz)) == 0;
 }
 
-bool getenv_flag(const char* name) {
-  const char* e = getenv(name);
-  return e && e[0] == '1';
-}
 
 // AVSR_GEMM_NOGLDS=1 forces the register-staged core (A/B comparisons, debugging)
 bool getenv_flag_noglds() {

@@ -119,7 +119,8 @@ class BatchBeamSearch:
             o2 = eng._e(R, D)
             kv = st["mem"][i]
             ops.dec_attn(q2, kv[:, :D], kv[:, D:], o2, n=R, H=H, klen_max=Tm, k_bstride=Tm * kv.stride(0),
-                         v_bstride=Tm * kv.stride(0), kidx=st["uidx"], klen=st["klen_mem"])
+                         v_bstride=Tm * kv.stride(0), kidx=st["uidx"], klen=st["klen_mem"],
+                         group=self.beam_size if self.beam_size <= 8 else 1)
             y2 = ops.linear_fwd(o2, eng.w(ca + "linear_out.weight"), ar.master(ca + "linear_out.bias"), res=y1)
             n3, _, _ = ops.layernorm_fwd(y2, ar.master(p + "norm3.weight"), ar.master(p + "norm3.bias"), 1e-12)
             a = ops.linear_fwd(n3, eng.w(ff + "w_1.weight"), ar.master(ff + "w_1.bias"), act=ops.L.ACT_RELU)

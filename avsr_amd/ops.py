@@ -737,14 +737,16 @@ def log_softmax_rows(x, V, out):
     return out
 
 
-def dec_attn(q, k, v, o, *, n, H, klen_max, k_bstride, v_bstride, klen=None, scale=0.125, kidx=None, kmap=None):
+def dec_attn(q, k, v, o, *, n, H, klen_max, k_bstride, v_bstride, klen=None, scale=0.125, kidx=None, kmap=None,
+             group=1):
     """one query per hypothesis: q/o rows i (ld = stride(0)), keys j of hypothesis i at
     k[b*k_bstride + j*k.stride(-2)] with b = kidx[i] (kidx None: b = i; bstride 0: shared keys);
-    kmap (int32 [n][ldmap]): key j of hypothesis i is row kmap[i][j] of k instead."""
+    kmap (int32 [n][ldmap]): key j of hypothesis i is row kmap[i][j] of k instead; group: runs of
+    `group` hypotheses share their key block and klen (one read of each row for all of them)."""
     _call("avsr_dec_attn", L.fill(L.DecAttnParams, dtype=dtype_code(q), n=n, H=H, klen_max=klen_max, scale=scale,
                                    q=q, ldq=q.stride(0), k=k, ldk=k.stride(-2), k_bstride=k_bstride, v=v,
                                    ldv=v.stride(-2), v_bstride=v_bstride, klen=klen, o=o, ldo=o.stride(0),
-                                   kidx=kidx, kmap=kmap, ldmap=0 if kmap is None else kmap.stride(0)))
+                                   kidx=kidx, kmap=kmap, ldmap=0 if kmap is None else kmap.stride(0), group=group))
     return o
 
 

@@ -511,6 +511,10 @@ typedef struct {
                                  of k (v likewise; bstride / kidx ignored) — the self-attention
                                  cache of a device-side beam search, [step][row] rows addressed
                                  through each hypothesis's ancestry instead of being reordered */
+  int group;                  /* >= 1 (0 = 1): hypotheses i0 .. i0+group-1 (i0 % group == 0) share one
+                                 key block and klen (kidx / klen equal within a group, no kmap; the
+                                 beams of one utterance over its memory): one workgroup reads each
+                                 key / value row once for all of them */
 } avsr_dec_attn_params;
 int avsr_dec_attn(const avsr_dec_attn_params* p, void* stream);
 

@@ -153,3 +153,35 @@ def test_batched_decode_equals_per_utterance(g, model, beam):
         assert [round(float(h.score), 4) for h in hyps] == [round(float(h.score), 4) for h in want]
     if beam in (1, 3):                       # and the reference's own best hypothesis
         assert got[0][0].asdict()["yseq"] == g[f"yseq_b{beam}_0"].tolist()
+
+
+@pytest.mark.parametrize("G", [3, 5])
+def test_dec_attn_grouped_equals_single(G):
+    """avsr_dec_attn with group = G (the beams of one utterance read each memory row once)
+    equals the per-hypothesis launch bit for bit, with ragged key lengths per utterance, and
+    matches an fp64 softmax attention"""
+    from avsr_amd import ops
+    dev = torch.device("cuda")
+    U, T, H = 3, 37, 4
+    D = 64 * H
+    gen = torch.Generator().manual_seed(G)
+    mem = torch.randn(U * T, 2 * D, generator=gen).to(dev)
+    q = torch.randn(U * G, D, generator=gen).to(dev)
+    uidx = torch.arange(U * G, dtype=torch.int32).div(G, rounding_mode="floor").to(dev, torch.int32)
+    lens = [37, 20, 5]
+    klen = torch.tensor([lens[u] for u in range(U) for _ in range(G)], dtype=torch.int32, device=dev)
+    outs = []
+    for grp in (1, G):
+        o = torch.empty(U * G, D, device=dev)
+        ops.dec_attn(q, mem[:, :D], mem[:, D:], o, n=U * G, H=H, klen_max=T, k_bstride=T * mem.stride(0),
+                     v_bstride=T * mem.stride(0), kidx=uidx, klen=klen, group=grp)
+        outs.append(o)
+    assert torch.equal(outs[0], outs[1])
+    qd, md = q.double().cpu(), mem.double().cpu()
+    for i in range(U * G):
+        u = i // G
+        k = md[u * T:u * T + lens[u], :D].view(-1, H, 64)
+        v = md[u * T:u * T + lens[u], D:].view(-1, H, 64)
+        s = torch.einsum("hd,jhd->hj", qd[i].view(H, 64), k) * 0.125
+        ref = torch.einsum("hj,jhd->hd", torch.softmax(s, -1), v).reshape(D)
+        assert (outs[1][i].double().cpu() - ref).abs().max().item() < 1e-5
