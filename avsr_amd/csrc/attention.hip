@@ -1725,19 +1725,13 @@ extern "C" int avsr_attn_bwd(const avsr_attn_params* p, void* stream) {
     }
     if (resident_bwd(p)) {
       // dK/dV: 12 waves (3 per SIMD; a few registers spill to scratch, measured 5 % faster than
-      // 8 spill-free waves at 2 per SIMD); AVSR_DKDV_WAVES=8 selects the other
-      static const int dkdv_max = getenv("AVSR_DKDV_WAVES") && atoi(getenv("AVSR_DKDV_WAVES")) == 8 ? 8 : 12;
-      const int nwk = std::min(res::nwaves(p->Lk), dkdv_max), nwq = res::nwaves(p->Lq);
+      // 8 spill-free waves at 2 per SIMD)
+      const int nwk = std::min(res::nwaves(p->Lk), 12), nwq = res::nwaves(p->Lq);
       const size_t ldk = std::max(res::img_lds(p->Lq) + (size_t)2 * ((p->Lq + 31) & ~31) * sizeof(float),
                                   res::slab_lds(nwk));
       const dim3 gk(p->B * p->H, (p->Lk + 32 * nwk - 1) / (32 * nwk));
-      if (dkdv_max == 12) {
-        res::allow_lds(res::attn_bwd_dkdv_kernel<768>);
-        hipLaunchKernelGGL(res::attn_bwd_dkdv_kernel<768>, gk, dim3(64 * nwk), ldk, st, a);
-      } else {
-        res::allow_lds(res::attn_bwd_dkdv_kernel<512>);
-        hipLaunchKernelGGL(res::attn_bwd_dkdv_kernel<512>, gk, dim3(64 * nwk), ldk, st, a);
-      }
+      res::allow_lds(res::attn_bwd_dkdv_kernel<768>);
+      hipLaunchKernelGGL(res::attn_bwd_dkdv_kernel<768>, gk, dim3(64 * nwk), ldk, st, a);
       AVSR_CHECK_LAUNCH();
       const size_t ldq = std::max(res::img_lds(p->Lk), res::slab_lds(nwq));
       dim3 gq(p->B * p->H, (p->Lq + 32 * nwq - 1) / (32 * nwq));

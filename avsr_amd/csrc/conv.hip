@@ -425,11 +425,7 @@ int launch_glds(const ConvArgs& a, int groups, hipStream_t st) {
   return 0;
 }
 
-// AVSR_CONV_NOGLDS=1 keeps the register-staged core (A/B comparisons)
-static bool conv_glds_enabled() {
-  const char* e = getenv("AVSR_CONV_NOGLDS");
-  return !(e && e[0] == '1');
-}
+static bool conv_glds_enabled() { return true; }
 
 // 192x128 for the k-major-A directions (forward, data-grad) where it still runs >= 2 blocks per
 // CU and its rounds carry no more work than 128x128's (the dense rule, gemm.hip tile_cfg):
@@ -483,9 +479,7 @@ static int tile_bm_k(int M, int N, int dtype) {
 // extents (elements, one group) of the A / B operands -> buffer-DMA loaders when allowed
 static void set_extents(ConvArgs& a, const avsr_conv_params* p, bool tap_uniform, int64_t ea, int64_t eb) {
   const int64_t lim = ((int64_t)gemmg::OOB - (1 << 20)) / 2;
-  const char* env = getenv("AVSR_CONV_NOBUF");
-  const bool ok = p->dtype == AVSR_BF16 && tap_uniform && ea > 0 && eb > 0 && ea < lim && eb < lim &&
-                  !(env && env[0] == '1');
+  const bool ok = p->dtype == AVSR_BF16 && tap_uniform && ea > 0 && eb > 0 && ea < lim && eb < lim;
   a.a_bytes = ok ? (uint32_t)(ea * 2) : 0u;
   a.b_bytes = ok ? (uint32_t)(eb * 2) : 0u;
 }
@@ -514,8 +508,7 @@ static WgradPlan wgrad_plan(const avsr_conv_params* p, bool glds, bool with_ws) 
   if (splits <= 0) {
     // slab: ~2 full rounds of 512 block slots (2 per CU), rounded DOWN so the last round is
     // not a 1-block tail (513 blocks cost 2 rounds: measured 812 -> ~550 us on stage 1)
-    static const long env_target = getenv("AVSR_CONV_WGRAD_TARGET") ? atol(getenv("AVSR_CONV_WGRAD_TARGET")) : 0;
-    const long target = env_target > 0 ? env_target : (w.slab ? 1024 : 2048);   // env: A/B experiments
+    const long target = w.slab ? 1024 : 2048;   // 512-2048 measured within noise (r02_conv_wgrad_target_ab)
     const long want = w.slab ? (target / tiles > 0 ? target / tiles : 1) : (target + tiles - 1) / tiles;
     const long maxs = w.slab ? (K + 1023) / 1024 : (K + 2047) / 2048;
     splits = want < maxs ? want : maxs;

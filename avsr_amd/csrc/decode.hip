@@ -651,8 +651,7 @@ extern "C" int avsr_ctc_prefix(const avsr_ctc_prefix_params* p, void* stream) {
   if (!p || p->n <= 0) return AVSR_E_ARG;
   if (p->P < 1 || p->P > 64 || p->T < 1) return AVSR_E_SHAPE;
   const size_t lds = (size_t)p->T * (p->P + 1 + 2) * sizeof(float);
-  static const bool nolds = getenv("AVSR_CTC_PREFIX_NOLDS") && getenv("AVSR_CTC_PREFIX_NOLDS")[0] == '1';
-  if (lds <= 64 * 1024 && !nolds)
+  if (lds <= 64 * 1024)
     hipLaunchKernelGGL(ctc_prefix_lds_kernel, dim3(p->n), dim3(64), lds, (hipStream_t)stream, *p);
   else
     hipLaunchKernelGGL(ctc_prefix_kernel, dim3(p->n), dim3(64), 0, (hipStream_t)stream, *p);

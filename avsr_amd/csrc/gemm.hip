@@ -652,23 +652,15 @@ int launch_wgrad_dual(const DenseArgs& a, hipStream_t st) {
   return 0;
 }
 
-// forward linears with few rows (AVSR_GEMM_NOSKINNY=1 keeps the tiled cores: A/B comparisons)
+// forward linears with few rows
 bool skinny_ok(const avsr_gemm_params* p, int splits) {
-  static int off = -1;
-  if (off < 0) { const char* e = getenv("AVSR_GEMM_NOSKINNY"); off = (e && e[0] == '1') ? 1 : 0; }
   const int esz = p->dtype == AVSR_BF16 ? 2 : 4;
-  return !off && p->M <= 64 && p->a_kmajor && p->b_kmajor && p->batch == 1 && splits == 1 && !p->epi_bwd && !p->db &&
+  return p->M <= 64 && p->a_kmajor && p->b_kmajor && p->batch == 1 && splits == 1 && !p->epi_bwd && !p->db &&
          (p->K % 4) == 0 && (p->lda % 4) == 0 && (p->ldb % 4) == 0 && ((uintptr_t)p->A % (4 * esz)) == 0 &&
          ((uintptr_t)p->B % (4 * esz)) == 0;
 }
 
 
-// AVSR_GEMM_NOGLDS=1 forces the register-staged core (A/B comparisons, debugging)
-bool getenv_flag_noglds() {
-  static int v = -1;
-  if (v < 0) { const char* e = getenv("AVSR_GEMM_NOGLDS"); v = (e && e[0] == '1') ? 1 : 0; }
-  return v == 1;
-}
 
 }  // namespace
 
@@ -690,7 +682,7 @@ extern "C" int avsr_gemm(const avsr_gemm_params* p, void* stream) {
   DenseArgs a;
   a.M = p->M; a.N = p->N; a.K = p->K;
   a.splits = splits;
-  const bool glds = glds_ok(p) && !getenv_flag_noglds();
+  const bool glds = glds_ok(p);
   const int kq = glds ? gemmg::GBK : BKE;
   a.kchunk = ((p->K + splits - 1) / splits + kq - 1) / kq * kq;
   a.A = p->A; a.lda = p->lda; a.sA = p->strideA;
@@ -699,7 +691,7 @@ extern "C" int avsr_gemm(const avsr_gemm_params* p, void* stream) {
     const int64_t ea = (p->a_kmajor ? ((int64_t)(p->M - 1) * p->lda + p->K) : ((int64_t)(p->K - 1) * p->lda + p->M)) * esz;
     const int64_t eb = (p->b_kmajor ? ((int64_t)(p->N - 1) * p->ldb + p->K) : ((int64_t)(p->K - 1) * p->ldb + p->N)) * esz;
     const int64_t lim = (int64_t)gemmg::OOB - (1 << 20);
-    const bool ok = ea > 0 && eb > 0 && ea < lim && eb < lim && !getenv_flag("AVSR_GEMM_NOBUF");
+    const bool ok = ea > 0 && eb > 0 && ea < lim && eb < lim;
     a.a_bytes = ok ? (uint32_t)ea : 0u;
     a.b_bytes = ok ? (uint32_t)eb : 0u;
   }

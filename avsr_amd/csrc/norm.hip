@@ -194,12 +194,7 @@ static void ln_bwd_shape(int& W, int& R) {
   if (R != 1 && R != 2) R = 2;
 }
 
-// AVSR_LN_BWD_BLOCKS caps the backward grid below AVSR_LN_BLOCKS (the workspace bound)
-static int ln_bwd_blocks() {
-  const char* e = getenv("AVSR_LN_BWD_BLOCKS");
-  const int b = e ? atoi(e) : 0;
-  return b > 0 && b < AVSR_LN_BLOCKS ? b : AVSR_LN_BLOCKS;
-}
+static int ln_bwd_blocks() { return AVSR_LN_BLOCKS; }
 
 template <typename T>
 int ln_launch(const avsr_layernorm_params* p, bool bwd, hipStream_t st) {

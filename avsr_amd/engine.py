@@ -32,21 +32,23 @@ from . import _lib as L
 from .arena import Arena
 
 GELU, RELU, NONE = L.ACT_GELU, L.ACT_RELU, L.ACT_NONE
-# BatchNorm-backward reductions in the ResNet data-grad epilogues (bf16); 0 = separate passes (A/B)
-_BN_FUSE = os.environ.get("AVSR_BN_FUSE", "1") == "1"
+# One configuration (the A/B switches of rounds 1-3 were removed; their measurements are in
+# DESIGN.md §9 and the git history). Module constants, flipped only by parity tests:
+# BatchNorm-backward reductions in the ResNet data-grad epilogues (bf16; fp32 uses separate passes)
+_BN_FUSE = True
 # bias gradients reduced in the epilogue of the data-grad GEMM that produces their operand
-_DB_FUSE = os.environ.get("AVSR_DB_FUSE", "1") == "1"
+_DB_FUSE = True
 # parameter-gradient column-sum finalise passes batched per flush (ops.colsum_defer)
-_COLSUM_DEFER = os.environ.get("AVSR_COLSUM_DEFER", "1") == "1"
+_COLSUM_DEFER = True
 # bias gradients of operands only the side stream's weight-grads read run on the side stream
-_SIDE_BIAS = os.environ.get("AVSR_SIDE_BIAS", "1") == "1"
+_SIDE_BIAS = True
 # the CTC branch of the forward runs on the side stream beside the decoder forward
-_CTC_SIDE = os.environ.get("AVSR_CTC_SIDE", "1") == "1"
+_CTC_SIDE = True
 # bf16 stem conv straight from the video (stem.hip) instead of pack + general implicit GEMM
-_STEM_DIRECT = os.environ.get("AVSR_STEM_DIRECT", "1") == "1"
+_STEM_DIRECT = True
 # encoder residual-branch dropout backward (+ bias gradient) fused into the LayerNorm backward
-# that produces its input gradient; 0 = separate ew_bwd passes (A/B)
-_LN_EW_FUSE = os.environ.get("AVSR_LN_EW_FUSE", "1") == "1"
+# that produces its input gradient
+_LN_EW_FUSE = True
 
 
 _STEP_STREAMS = {}
@@ -56,8 +58,8 @@ def prioritize_step_stream(device):
     """Make a high-priority stream the current stream of `device` for the training step; the
     weight-gradient side stream keeps the default priority, so the data-gradient chain (which
     bounds the step) wins CU slots over it (bench A/B, profiles/r02_stream_priority_ab.txt:
-    +1.5 %). AVSR_MAIN_PRIO=0 keeps the default stream. Returns the stream (or None)."""
-    if device.type != "cuda" or os.environ.get("AVSR_MAIN_PRIO", "1") != "1":
+    +1.5 %). Returns the stream (or None off the GPU)."""
+    if device.type != "cuda":
         return None
     idx = device.index if device.index is not None else torch.cuda.current_device()
     s = _STEP_STREAMS.get(idx)
@@ -149,8 +151,7 @@ class Engine:
         self._pinned = [(None, None)] * 4
         self._pin_next = 0
         import os
-        self.side = (torch.cuda.Stream(device=self.device)
-                     if self.device.type == "cuda" and os.environ.get("AVSR_SIDE_STREAM", "1") == "1" else None)
+        self.side = torch.cuda.Stream(device=self.device) if self.device.type == "cuda" else None
         # reused events: a stream wait binds the record that precedes it
         self._side_ev = [torch.cuda.Event() for _ in range(8)] if self.side is not None else []
         self._side_i = 0

@@ -149,7 +149,7 @@ def linear_dgrad(dy, W, *, gate=None, act=L.ACT_NONE, drop_p=0.0, seed=0, out=No
         out = torch.empty(M, K, device=dy.device, dtype=dy.dtype)
     # the epilogue reduction needs the LDS-DMA bf16 core (avsr_gemm: glds_ok) and 8-column vectors
     fused = (db is not None and dy.dtype == torch.bfloat16 and M >= 128 and K >= 128 and K % 8 == 0
-             and out.stride(0) % 8 == 0 and os.environ.get("AVSR_GEMM_NOGLDS", "0") != "1")
+             and out.stride(0) % 8 == 0)
     ws = _colsum_ws(((M + 63) // 64) * K, dy.device) if fused else None   # AVSR_GEMM_COLSUM_WS
     gemm(dy, W, out, M=M, N=K, K=N, a_kmajor=True, b_kmajor=False, lda=dy.stride(0), ldb=W.stride(0),
          ldc=out.stride(0), epi_bwd=True, gate=gate, act=act, drop_p=drop_p, seed=seed, beta=beta,
@@ -270,7 +270,7 @@ def conv_bwd_data_bnr(g, dy, w, dx, h, st, prelu, *, res=None, st2=None, alpha=1
     return ws, tiles
 
 
-_WGRAD_SLAB = os.environ.get("AVSR_WGRAD_SLAB", "1") == "1"   # 0: atomic split-K (A/B runs)
+_WGRAD_SLAB = True      # conv weight-grad split-K through slabs (deterministic; fp32 atomics only by request)
 
 
 def conv_bwd_weight(g, x, dy, dw, splitk=0, slab=None):
