@@ -1677,9 +1677,15 @@ extern "C" int avsr_attn_fwd(const avsr_attn_params* p, void* stream) {
   return 0;
 }
 
-// the query-tiled bf16 backward computes delta in its dQ kernel (which runs first)
+// the query-tiled bf16 backward computes delta in its dQ kernel (which runs first). Where the
+// resident kernels apply (Lq, Lk <= 384) they stay the default: isolated the tiled pair is
+// faster (C2 with dropout 93.7 vs 101.5 us), but inside the training step, beside the weight-
+// gradient GEMMs of the side stream, it took 144 vs 100 us per layer (profiles/r04_*)
 static bool sq_bwd(const avsr_attn_params* p) {
-  return p->dtype == AVSR_BF16 && !p->causal && p->Lq >= 128 && p->Lk >= 128 && res::small_index(p) && sq_enabled();
+  const char* e = getenv("AVSR_ATTN_SQ_BWD");
+  const bool force = e && e[0] == '1';
+  return p->dtype == AVSR_BF16 && !p->causal && p->Lq >= 128 && p->Lk >= 128 && res::small_index(p) && sq_enabled() &&
+         (force || p->Lq > res::MAXR || p->Lk > res::MAXR);
 }
 // the resident bf16 backward computes delta inside its dK/dV kernel (Q / dO already in LDS)
 static bool resident_bwd(const avsr_attn_params* p) {

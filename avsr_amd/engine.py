@@ -326,6 +326,18 @@ class Engine:
         self._on_side(run_all, *keep)
         self._side_defer = []
 
+    def zero_grad_async(self):
+        """arena.zero_grad() queued on the side stream (after the work queued so far on the
+        current stream, e.g. the previous optimizer step): nothing in the forward reads
+        gradients, and backward() joins the side stream before its first gradient write, so
+        the 1.3 GB memset leaves the forward's serial chain"""
+        if self.side is None:
+            self.arena.zero_grad()
+            return
+        g = self.arena.grad
+        self._on_side(lambda: g.zero_(), g)
+        self.arena.attach_grads(zero=False)
+
     def join_side(self):
         """make the current stream wait for every weight gradient issued so far"""
         self._flush_side()
@@ -498,11 +510,16 @@ class Engine:
         # returns AVSR_E_SHAPE from 2^31 bytes, ~69 k frames): larger batches take the packed conv
         direct = (self.dtype == torch.bfloat16 and _STEM_DIRECT
                   and vid.numel() * vid.element_size() < ops.STEM_DIRECT_MAX_BYTES)
-        # the packed 8-channel input: the general conv's operand, and the stem weight-grad's
+        # the packed 8-channel input: the general conv's operand, and the stem weight-grad's. With
+        # the direct conv only the weight-grad (end of the backward) reads it: packed on the side
+        # stream, off the forward's serial chain (joined with the CTC branch at the forward's end)
         xp = None
-        if not direct or save:
+        if not direct:
             xp = self._e(N, 88, 88, 8)
             ops.stem_pack(vid, xp)
+        elif save:
+            xp = self._e(N, 88, 88, 8)
+            self._on_side(lambda: ops.stem_pack(vid, xp), vid, xp)
         if direct:      # bf16: the stem conv reads the video itself (stem.hip, K = 288 instead of 392)
             wk = self._e(64, ops.STEM_K)
             ops.stem_wpack2(self.arena.master(R + "frontend3D.0.weight"), wk)
@@ -1065,6 +1082,7 @@ class Engine:
         M = B * T
         d_ctc = d_ctc.reshape(1).to(torch.float32)
         d_att = d_att.reshape(1).to(torch.float32)
+        self.join_side()            # a gradient clear queued on the side stream (zero_grad_async)
         if self.before_backward is not None:
             self.before_backward()
         # bias / LayerNorm parameter-gradient finalise passes are batched: one launch per

@@ -430,7 +430,7 @@ def gpu_bench(args):
             eng.force_modality = forced_all
         elif strat and not variant:
             eng.force_modality = (sched[i],)
-        arena.zero_grad()
+        eng.zero_grad_async()                   # the gradient clear runs on the side stream
         step_seed[0] += 1
         out4, ctx = eng.forward(v, a, lens, lab, train=True, need_grad=True, seed=step_seed[0])
         drops.append(eng.last_modality)
