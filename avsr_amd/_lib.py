@@ -244,7 +244,7 @@ class VideoNormParams(ctypes.Structure):
 SYMBOLS = {
     "avsr_version": ([], ctypes.c_char_p),
     "avsr_gemm": ([ctypes.POINTER(GemmParams), _c_p], _i),
-    "avsr_gemm_skinny_splits": ([_i, _i], _i),
+    "avsr_gemm_skinny_splits": ([_i, _i, _i], _i),
     "avsr_conv_fwd": ([ctypes.POINTER(ConvParams), _c_p], _i),
     "avsr_conv_bwd_data": ([ctypes.POINTER(ConvParams), _c_p], _i),
     "avsr_conv_bwd_weight": ([ctypes.POINTER(ConvParams), _c_p], _i),
@@ -296,6 +296,7 @@ SYMBOLS = {
     "avsr_log_softmax_rows": ([_i, _i, _i, _c_p, _i64, _c_p, _i64, _c_p], _i),
     "avsr_dec_attn": ([ctypes.POINTER(DecAttnParams), _c_p], _i),
     "avsr_row_topk": ([ctypes.POINTER(TopkParams), _c_p], _i),
+    "avsr_log_softmax_topk": ([_i, _i, _i, _c_p, _i64, _c_p, _i64, _i, _c_p, _c_p], _i),
     "avsr_ctc_prefix": ([ctypes.POINTER(CtcPrefixParams), _c_p], _i),
     "avsr_beam_select": ([ctypes.POINTER(BeamSelectParams), _c_p], _i),
     "avsr_beam_step_prep": ([_i, _i, _c_p, _c_p, _c_p, _c_p], _i),

@@ -14,10 +14,20 @@ namespace {
 
 constexpr float LOGZERO = -10000000000.0f;   // CTCPrefixScoreTH.logzero (ctc_prefix_score.py:29)
 
-// torch.logsumexp of two finite values: m + log(exp(a-m) + exp(b-m))
+// torch.logsumexp of two finite values: m + log(exp(a-m) + exp(b-m)). One of the two terms is
+// exp(0) = 1 exactly, so m + log(1 + exp(min - m)) is the same float computation with one
+// transcendental less (bit-identical; the CTC prefix recursion's serial chain is two of these)
 AVSR_DEV float lse2(float a, float b) {
   const float m = fmaxf(a, b);
-  return m + logf(expf(a - m) + expf(b - m));
+  return m + logf(1.f + expf(fminf(a, b) - m));
+}
+// the same with the hardware exp2 / log2 (v_exp_f32 / v_log_f32, ~1 ulp): the CTC prefix
+// recursion's dependent chain (two of these per frame, T frames in sequence), as in loss.hip's
+// CTC recursion; the correction term is <= log 2, so the result differs from lse2 by a few ulp
+// of that term
+AVSR_DEV float lse2_fast(float a, float b) {
+  const float m = fmaxf(a, b);
+  return m + __logf(1.f + __expf(fminf(a, b) - m));
 }
 
 AVSR_DEV float block_max256(float v, float* sh) {
@@ -86,11 +96,16 @@ template <typename T> AVSR_DEV f32x4 ld4(const T* p) {
 }
 
 // G hypotheses per workgroup (p.group; G = 1 for per-hypothesis keys): every key / value row is
-// read once for the G queries of the group
+// read once for the G queries of the group. 8 waves; key j of iteration it is handled by wave
+// (j / 4) % 8, key slot j % 4 (16 lanes x 4 elements); each lane issues DA_UNROLL row loads
+// back to back before using them, so a 375-key memory takes two load round trips per phase
+// (the one-load-per-iteration loop was latency-bound: 51 us per call at 375 keys, G = 5).
+constexpr int DA_WAVES = 8, DA_UNROLL = 8;
 template <typename T, int G>
-__global__ __launch_bounds__(256) void dec_attn_kernel(avsr_dec_attn_params p) {
-  extern __shared__ float sc[];           // [G][kpad] scores, then [4][G][64] partials
-  __shared__ float sh[4];
+__global__ __launch_bounds__(64 * DA_WAVES) void dec_attn_kernel(avsr_dec_attn_params p) {
+  constexpr int NW = DA_WAVES, U = DA_UNROLL, KS = 4 * NW;
+  extern __shared__ float sc[];           // [G][kpad] scores, then [NW][G][64] partials
+  __shared__ float shr[G][NW];
   const int h = blockIdx.x, i0 = blockIdx.y * G;
   const int klen = p.klen ? min(p.klen[i0], p.klen_max) : p.klen_max;
   const int kpad = (p.klen_max + 3) & ~3;
@@ -100,52 +115,94 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(avsr_dec_attn_params p) {
   const T* Vv = (const T*)p.v + (int64_t)kb * p.v_bstride + h * 64 + d0;
   const int* km = p.kmap ? p.kmap + (int64_t)i0 * p.ldmap : nullptr;  // key j -> row km[j] (G == 1)
   const int ng = min(G, p.n - i0);
+  const int jl = 4 * w + sub;             // this lane's key offset within an iteration
+  auto rows_of = [&](int it0, int (&row)[U]) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int j = (it0 + u) * KS + jl;
+      row[u] = j < klen ? (km ? km[j] : j) : 0;
+    }
+  };
   f32x4 q[G];
 #pragma unroll
   for (int g = 0; g < G; ++g) q[g] = ld4((const T*)p.q + (int64_t)(i0 + min(g, ng - 1)) * p.ldq + h * 64 + d0);
   float m[G];
 #pragma unroll
   for (int g = 0; g < G; ++g) m[g] = -INFINITY;
-  for (int j0 = 4 * w; j0 < klen; j0 += 16) {
-    const int j = j0 + sub;
-    const bool ok = j < klen;
-    const int row = ok ? (km ? km[j] : j) : 0;
-    const f32x4 k = ld4(K + (int64_t)row * p.ldk);
+  for (int it0 = 0; it0 * KS < klen; it0 += U) {
+    int row[U];
+    rows_of(it0, row);
+    f32x4 k[U];
 #pragma unroll
-    for (int g = 0; g < G; ++g) {
-      float s = q[g][0] * k[0] + q[g][1] * k[1] + q[g][2] * k[2] + q[g][3] * k[3];
+    for (int u = 0; u < U; ++u) k[u] = ld4(K + (int64_t)row[u] * p.ldk);
 #pragma unroll
-      for (int o = 1; o < 16; o <<= 1) s += __shfl_xor(s, o, 64);
-      s *= p.scale;
-      if (ok) {
-        if ((lane & 15) == 0) sc[g * kpad + j] = s;
-        m[g] = fmaxf(m[g], s);
+    for (int u = 0; u < U; ++u) {
+      const int j = (it0 + u) * KS + jl;
+      const bool ok = j < klen;
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        float s = q[g][0] * k[u][0] + q[g][1] * k[u][1] + q[g][2] * k[u][2] + q[g][3] * k[u][3];
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) s += __shfl_xor(s, o, 64);
+        s *= p.scale;
+        if (ok) {
+          if ((lane & 15) == 0) sc[g * kpad + j] = s;
+          m[g] = fmaxf(m[g], s);
+        }
       }
     }
   }
-  float l[G];
+  // block max of every group row (one barrier pair for all G)
 #pragma unroll
-  for (int g = 0; g < G; ++g) m[g] = block_max256(m[g], sh);
+  for (int g = 0; g < G; ++g) {
+    const float v = wave_max(m[g]);
+    if (lane == 0) shr[g][w] = v;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    float v = shr[g][0];
+#pragma unroll
+    for (int x = 1; x < NW; ++x) v = fmaxf(v, shr[g][x]);
+    m[g] = v;
+  }
+  __syncthreads();
+  float l[G];
 #pragma unroll
   for (int g = 0; g < G; ++g) {
     float lg = 0.f;
-    for (int j = threadIdx.x; j < klen; j += 256) {
+    for (int j = threadIdx.x; j < klen; j += 64 * NW) {
       const float e = expf(sc[g * kpad + j] - m[g]);
       sc[g * kpad + j] = e;
       lg += e;
     }
-    l[g] = block_sum256(lg, sh);     // includes a barrier: every score of row g is final
+    lg = wave_sum(lg);
+    if (lane == 0) shr[g][w] = lg;
+  }
+  __syncthreads();                         // every score is final, every wave sum written
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    float v = shr[g][0];
+#pragma unroll
+    for (int x = 1; x < NW; ++x) v += shr[g][x];
+    l[g] = v;
   }
   f32x4 acc[G];
 #pragma unroll
   for (int g = 0; g < G; ++g) acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int j0 = 4 * w; j0 < klen; j0 += 16) {
-    const int j = j0 + sub;
-    const bool ok = j < klen;
-    const int row = ok ? (km ? km[j] : j) : 0;
-    const f32x4 v = ld4(Vv + (int64_t)row * p.ldv);
+  for (int it0 = 0; it0 * KS < klen; it0 += U) {
+    int row[U];
+    rows_of(it0, row);
+    f32x4 v[U];
 #pragma unroll
-    for (int g = 0; g < G; ++g) acc[g] += (ok ? sc[g * kpad + j] : 0.f) * v;
+    for (int u = 0; u < U; ++u) v[u] = ld4(Vv + (int64_t)row[u] * p.ldv);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int j = (it0 + u) * KS + jl;
+      const bool ok = j < klen;
+#pragma unroll
+      for (int g = 0; g < G; ++g) acc[g] += (ok ? sc[g * kpad + j] : 0.f) * v[u];
+    }
   }
   float* part = sc + G * kpad;
 #pragma unroll
@@ -158,11 +215,12 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(avsr_dec_attn_params p) {
     if (sub == 0) *(f32x4*)&part[(w * G + g) * 64 + d0] = acc[g];
   }
   __syncthreads();
-  for (int t = threadIdx.x; t < ng * 64; t += 256) {
+  for (int t = threadIdx.x; t < ng * 64; t += 64 * NW) {
     const int g = t >> 6, d = t & 63;
-    const float o = ((part[(0 * G + g) * 64 + d] + part[(1 * G + g) * 64 + d]) +
-                     (part[(2 * G + g) * 64 + d] + part[(3 * G + g) * 64 + d])) / l[g];
-    ((T*)p.o)[(int64_t)(i0 + g) * p.ldo + h * 64 + d] = from_f<T>(o);
+    float o = 0.f;
+#pragma unroll
+    for (int x = 0; x < NW; ++x) o += part[(x * G + g) * 64 + d];
+    ((T*)p.o)[(int64_t)(i0 + g) * p.ldo + h * 64 + d] = from_f<T>(o / l[g]);
   }
 }
 
@@ -200,6 +258,61 @@ __global__ __launch_bounds__(256) void row_topk_kernel(avsr_topk_params p) {
     block_argmax256(v, id, shv, shi);
     if (threadIdx.x == 0) p.ids[(int64_t)blockIdx.x * p.K + r] = id;
     if (mine == id && id != 0x7fffffff) ++head;
+  }
+}
+
+// log_softmax_rows + row_topk of the decoder output in one pass (decode steps): the row stays
+// in registers (<= 24 values per thread, V <= 6144), the log-probs are written once and the
+// top-K runs on the same register values. Per-thread element order, the block reductions and
+// top-K order (value desc, index asc) equal the two separate kernels', so the output is
+// identical to them.
+constexpr int LSM_TOPK_NV = 24;
+template <typename T>
+__global__ __launch_bounds__(256) void log_softmax_topk_kernel(int V, int K, const T* x, int64_t ldx, float* out,
+                                                               int64_t ldo, int* ids) {
+  __shared__ float sh[4];
+  __shared__ float shv[4];
+  __shared__ int shi[4];
+  const T* r = x + (int64_t)blockIdx.x * ldx;
+  float v[LSM_TOPK_NV];
+#pragma unroll
+  for (int q = 0; q < LSM_TOPK_NV; ++q) {
+    const int c = threadIdx.x + q * 256;
+    v[q] = c < V ? to_f(r[c]) : -INFINITY;
+  }
+  float m = -INFINITY;
+#pragma unroll
+  for (int q = 0; q < LSM_TOPK_NV; ++q) m = fmaxf(m, v[q]);
+  m = block_max256(m, sh);
+  float s = 0.f;
+#pragma unroll
+  for (int q = 0; q < LSM_TOPK_NV; ++q)
+    if (threadIdx.x + q * 256 < V) s += expf(v[q] - m);
+  s = block_sum256(s, sh);
+  const float ls = logf(s);
+  float* o = out + (int64_t)blockIdx.x * ldo;
+#pragma unroll
+  for (int q = 0; q < LSM_TOPK_NV; ++q) {
+    const int c = threadIdx.x + q * 256;
+    if (c < V) { v[q] = v[q] - m - ls; o[c] = v[q]; }
+  }
+  // top-K by K rounds of "largest element below the previous pick" in the order (value desc,
+  // index asc) -- the order row_topk's insertion lists produce, so the ids are the same; a
+  // round is one register scan plus a block arg-max (the unrolled 24 x 16 insertion network
+  // with its divergent swaps took ~30 us per call)
+  float pv = INFINITY;
+  int pi = -1;
+  for (int rr = 0; rr < K; ++rr) {
+    float bv = -INFINITY; int bi = 0x7fffffff;
+#pragma unroll
+    for (int q = 0; q < LSM_TOPK_NV; ++q) {
+      const int c = threadIdx.x + q * 256;
+      const bool below = c < V && (v[q] < pv || (v[q] == pv && c > pi));
+      if (below && (v[q] > bv || bi == 0x7fffffff)) { bv = v[q]; bi = c; }
+    }
+    block_argmax256(bv, bi, shv, shi);
+    if (threadIdx.x == 0) ids[(int64_t)blockIdx.x * K + rr] = bi;
+    pv = bv; pi = bi;
   }
 }
 
@@ -245,8 +358,8 @@ __global__ __launch_bounds__(64) void ctc_prefix_kernel(avsr_ctc_prefix_params p
     const float phi = same ? prev_r1 : rsum_prev;
     const float x0 = act ? p.logp[(int64_t)t * V + id] : LOGZERO;
     const float xb = p.logp[(int64_t)t * V + p.blank];
-    const float n0 = lse2(r0, phi) + x0;
-    const float n1 = lse2(r0, r1) + xb;
+    const float n0 = lse2_fast(r0, phi) + x0;
+    const float n1 = lse2_fast(r0, r1) + xb;
     r0 = n0; r1 = n1;
     if (act) { rn[t * 2 + 0] = r0; rn[t * 2 + 1] = r1; }
     const float term = phi + x0;
@@ -268,76 +381,108 @@ __global__ __launch_bounds__(64) void ctc_prefix_kernel(avsr_ctc_prefix_params p
 }
 
 // The same recursion with its inputs staged in LDS first: the P scored tokens' and the blank's
-// log-probs over all T frames ([T][P + 1], gathered once by the whole block) and r_prev
-// ([T][2]). The sequential loop then reads LDS only (independent of the global r_new stores,
-// so the reads of later frames issue ahead), instead of a dependent ~L2-latency global
-// gather per frame (130 us per step at T = 375 -> the lse chain).
-__global__ __launch_bounds__(64) void ctc_prefix_lds_kernel(avsr_ctc_prefix_params p) {
+// log-probs over all T frames ([T][P + 1], 4 independent gathers in flight per lane, the token
+// ids read once) and phi(t) for both cases of a candidate ([T][2]: logsumexp(r_prev[t]) and
+// r_prev[t][1] for a repeated label; at the first step the blank cumsum). Only the r recursion is
+// sequential (wave 0, LDS reads issued ahead by the unrolled loop, hardware exp2 / log2 on the
+// chain): psi = logsumexp({r0(start-1)} U {phi(t-1) + x0(t)}) does not depend on r, so waves 1-3
+// reduce it meanwhile (a wave per candidate, lanes over t).
+__global__ __launch_bounds__(256) void ctc_prefix_lds_kernel(avsr_ctc_prefix_params p) {
   extern __shared__ float sm[];
-  const int h = blockIdx.x, j = threadIdx.x;
-  if (p.out_len_dev) p.out_len = p.out_len_dev[0];
+  __shared__ int sid[65];
+  const int h = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int out_len = p.out_len_dev ? p.out_len_dev[0] : p.out_len;
   const int V = p.V, P = p.P, W = P + 1;
   const int u = p.uidx ? p.uidx[h] : 0;
   const int T = p.uidx ? p.tlen[u] : p.T;
   const int TS = p.T;
   const float* __restrict__ logp = p.logp + (p.uidx ? (int64_t)u * p.logp_ustride : 0);
   float* xs = sm;                           // [T][W]: ids then blank
-  float* rps = sm + (int64_t)TS * W;        // [T][2]
+  float* ph = sm + (int64_t)TS * W;         // [T][2]: phi for a new label, phi for a repeated one
   const int* __restrict__ ids = p.ids + h * P;
-  for (int idx = j; idx < T * W; idx += 64) {
-    const int t = idx / W, c = idx - t * W;
-    xs[idx] = logp[(int64_t)t * V + (c < P ? ids[c] : p.blank)];
-  }
+  if (tid < P) sid[tid] = ids[tid];
+  if (tid == P) sid[P] = p.blank;
   const float* __restrict__ rp = p.r_prev ? p.r_prev + (int64_t)h * TS * 2 : nullptr;
   if (rp)
-    for (int idx = j; idx < T * 2; idx += 64) rps[idx] = rp[idx];
+    for (int t = tid; t < T; t += 256) {
+      const float a0 = rp[2 * t], a1 = rp[2 * t + 1];
+      ph[2 * t] = lse2(a0, a1);
+      ph[2 * t + 1] = a1;
+    }
   __syncthreads();
-  const bool act = j < P;
-  const int id = act ? ids[j] : 0;
-  const bool same = act && id == p.last[h];
-  float* __restrict__ rn = act ? p.r_new + ((int64_t)h * P + j) * TS * 2 : nullptr;
-  const int jj = act ? j : 0;
-  auto rprev = [&](int t, int q, float cum) -> float { return rp ? rps[t * 2 + q] : (q == 0 ? LOGZERO : cum); };
-  const int start = max(p.out_len, 1);
-  float r0 = LOGZERO, r1 = LOGZERO;
-  float cum = 0.f;
-  for (int t = 0; t < start; ++t) {
-    const float xb = xs[t * W + P];
-    cum += xb;
-    float a0 = LOGZERO;
-    if (t == 0 && p.out_len == 0) a0 = act ? xs[jj] : LOGZERO;
-    if (act) { rn[t * 2 + 0] = a0; rn[t * 2 + 1] = LOGZERO; }
-    if (t == start - 1) { r0 = a0; r1 = LOGZERO; }
+  const int n = T * W;
+  for (int base = tid; base < n; base += 4 * 256) {
+    float v[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int idx = base + q * 256;
+      if (idx < n) {
+        const int t = idx / W, c = idx - t * W;
+        v[q] = logp[(int64_t)t * V + sid[c]];
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if (base + q * 256 < n) xs[base + q * 256] = v[q];
   }
-  float pm = r0;
-  float ps = 1.f;
-  float prev_r0 = rprev(start - 1, 0, 0.f);
-  float prev_r1 = rprev(start - 1, 1, cum);
-  float cur_cum = cum;
-  for (int t = start; t < T; ++t) {
-    const float rsum_prev = lse2(prev_r0, prev_r1);
-    const float phi = same ? prev_r1 : rsum_prev;
-    const float x0 = act ? xs[t * W + jj] : LOGZERO;
-    const float xb = xs[t * W + P];
-    const float n0 = lse2(r0, phi) + x0;
-    const float n1 = lse2(r0, r1) + xb;
-    r0 = n0; r1 = n1;
-    if (act) { rn[t * 2 + 0] = r0; rn[t * 2 + 1] = r1; }
-    const float term = phi + x0;
-    if (term > pm) { ps = ps * expf(pm - term) + 1.f; pm = term; }
-    else ps += expf(term - pm);
-    cur_cum += xb;
-    prev_r0 = rprev(t, 0, 0.f);
-    prev_r1 = rprev(t, 1, cur_cum);
+  __syncthreads();
+  if (!rp && tid == 0) {                    // first step: r_prev = (logzero, cumsum of blank)
+    float cum = 0.f;
+    for (int t = 0; t < T; ++t) {
+      cum += xs[t * W + P];
+      ph[2 * t] = lse2(LOGZERO, cum);
+      ph[2 * t + 1] = cum;
+    }
   }
-  const float rsum_last = lse2(prev_r0, prev_r1);
-  float psi = pm + logf(ps);
-  if (act) {
-    if (id == p.blank) psi = LOGZERO;
-    if (id == p.eos) psi = rsum_last;
-    p.psi[h * (P + 1) + j] = psi;
+  if (!rp) __syncthreads();
+  const int start = max(out_len, 1);
+  const float* __restrict__ pc = ph;
+  if (w == 0) {
+    const int j = lane;
+    const bool act = j < P;
+    const int id = act ? sid[j] : 0;
+    const int q = (act && id == p.last[h]) ? 1 : 0;     // repeated label: phi = r_prev[t][1]
+    float* __restrict__ rn = act ? p.r_new + ((int64_t)h * P + j) * TS * 2 : nullptr;
+    const int jj = act ? j : 0;
+    float r0 = LOGZERO, r1 = LOGZERO;
+    for (int t = 0; t < min(start, T); ++t) {
+      float a0 = LOGZERO;
+      if (t == 0 && out_len == 0) a0 = act ? xs[jj] : LOGZERO;
+      if (act) { rn[t * 2 + 0] = a0; rn[t * 2 + 1] = LOGZERO; }
+      r0 = a0;
+    }
+#pragma unroll 4
+    for (int t = start; t < T; ++t) {
+      const float phi = pc[2 * (t - 1) + q];
+      const float x0 = xs[t * W + jj];
+      const float xb = xs[t * W + P];
+      const float n0 = lse2_fast(r0, phi) + x0;
+      const float n1 = lse2_fast(r0, r1) + xb;
+      r0 = n0; r1 = n1;
+      if (act) { rn[t * 2 + 0] = r0; rn[t * 2 + 1] = r1; }
+    }
   }
-  if (j == 0) p.psi[h * (P + 1) + P] = rsum_last;
+  // psi of candidate j (waves 1-3, beside wave 0's recursion): logsumexp over {r0(start-1)} U
+  // {phi(t-1) + x0(t), t in [start, T)}
+  const float rsum_last = pc[2 * (T - 1)];          // logsumexp(r_prev[T-1]) (the eos score)
+  for (int j = w - 1; w > 0 && j < P; j += 3) {
+    const int id = sid[j];
+    const int q = id == p.last[h] ? 1 : 0;
+    const float r0i = (out_len == 0) ? xs[j] : LOGZERO;  // r0 at frame start - 1 (= 0 when out_len == 0)
+    float m = lane == 0 ? r0i : -INFINITY;
+    for (int t = start + lane; t < T; t += 64) m = fmaxf(m, pc[2 * (t - 1) + q] + xs[t * W + j]);
+    m = wave_max(m);
+    float sum = lane == 0 ? expf(r0i - m) : 0.f;
+    for (int t = start + lane; t < T; t += 64) sum += expf(pc[2 * (t - 1) + q] + xs[t * W + j] - m);
+    sum = wave_sum(sum);
+    if (lane == 0) {
+      float psi = m + logf(sum);
+      if (id == p.blank) psi = LOGZERO;
+      if (id == p.eos) psi = rsum_last;
+      p.psi[h * (P + 1) + j] = psi;
+    }
+  }
+  if (tid == 0) p.psi[h * (P + 1) + P] = rsum_last;
 }
 
 // ---------------------------------------------------------------- beam selection
@@ -491,6 +636,28 @@ extern "C" int avsr_log_softmax_rows(int dtype, int rows, int V, const void* x, 
   return 0;
 }
 
+extern "C" int avsr_log_softmax_topk(int dtype, int rows, int V, const void* x, int64_t ldx, float* out,
+                                     int64_t ldo, int K, int* ids, void* stream) {
+  if (rows <= 0) return 0;
+  if (V <= 0 || !x || !out || !ids) return AVSR_E_ARG;
+  if (K < 1 || K > KMAX || K > V) return AVSR_E_SHAPE;
+  if (V > LSM_TOPK_NV * 256) {             // row does not fit the registers: the two passes
+    const int e = avsr_log_softmax_rows(dtype, rows, V, x, ldx, out, ldo, stream);
+    if (e) return e;
+    avsr_topk_params tp{rows, V, K, out, ldo, ids};
+    return avsr_row_topk(&tp, stream);
+  }
+  if (dtype == AVSR_BF16)
+    hipLaunchKernelGGL(log_softmax_topk_kernel<bf16>, dim3(rows), dim3(256), 0, (hipStream_t)stream, V, K,
+                       (const bf16*)x, ldx, out, ldo, ids);
+  else if (dtype == AVSR_F32)
+    hipLaunchKernelGGL(log_softmax_topk_kernel<float>, dim3(rows), dim3(256), 0, (hipStream_t)stream, V, K,
+                       (const float*)x, ldx, out, ldo, ids);
+  else return AVSR_E_DTYPE;
+  AVSR_CHECK_LAUNCH();
+  return 0;
+}
+
 // ---------------------------------------------------------------- device-side bookkeeping
 __global__ __launch_bounds__(256) void beam_step_prep_kernel(int R, int Lmax, const int* pos_p, int* anc, int* klen) {
   const int pos = pos_p[0];
@@ -622,11 +789,11 @@ extern "C" int avsr_dec_attn(const avsr_dec_attn_params* p, void* stream) {
   const int G = p->group > 1 ? p->group : 1;
   if (G > 8 || (G > 1 && p->kmap)) return AVSR_E_ARG;
   const int kpad = (p->klen_max + 3) & ~3;
-  const size_t lds = ((size_t)G * kpad + (size_t)4 * G * 64) * sizeof(float);
+  const size_t lds = ((size_t)G * kpad + (size_t)DA_WAVES * G * 64) * sizeof(float);
   if (lds > 64 * 1024) return AVSR_E_SHAPE;
   const dim3 g(p->H, (p->n + G - 1) / G);
   hipStream_t st = (hipStream_t)stream;
-#define DA(T_, G_) hipLaunchKernelGGL((dec_attn_kernel<T_, G_>), g, dim3(256), lds, st, *p)
+#define DA(T_, G_) hipLaunchKernelGGL((dec_attn_kernel<T_, G_>), g, dim3(64 * DA_WAVES), lds, st, *p)
 #define DAG(T_) switch (G) { case 1: DA(T_, 1); break; case 2: DA(T_, 2); break; case 3: DA(T_, 3); break;   \
                               case 4: DA(T_, 4); break; case 5: DA(T_, 5); break; case 6: DA(T_, 6); break;   \
                               case 7: DA(T_, 7); break; default: DA(T_, 8); }
@@ -652,7 +819,7 @@ extern "C" int avsr_ctc_prefix(const avsr_ctc_prefix_params* p, void* stream) {
   if (p->P < 1 || p->P > 64 || p->T < 1) return AVSR_E_SHAPE;
   const size_t lds = (size_t)p->T * (p->P + 1 + 2) * sizeof(float);
   if (lds <= 64 * 1024)
-    hipLaunchKernelGGL(ctc_prefix_lds_kernel, dim3(p->n), dim3(64), lds, (hipStream_t)stream, *p);
+    hipLaunchKernelGGL(ctc_prefix_lds_kernel, dim3(p->n), dim3(256), lds, (hipStream_t)stream, *p);
   else
     hipLaunchKernelGGL(ctc_prefix_kernel, dim3(p->n), dim3(64), 0, (hipStream_t)stream, *p);
   AVSR_CHECK_LAUNCH();

@@ -20,6 +20,9 @@ struct DenseArgs {
   int64_t sC, sR;
   Epi e;
   unsigned long long* stamp;   // diagnostic {min start, max end} (avsr_gemm_params.stamp) or null
+  unsigned* cnt;               // wgrad_dual_kernel slab mode: per-tile arrival counters (zeroed) or null
+  float* fC; int64_t fldc;     // ... its final output C (the slabs' reduction target)
+  float falpha, fbeta;
 };
 
 template <typename T, typename OutT, int WM, int WN, bool AK, bool BK>
@@ -91,6 +94,13 @@ __global__ __launch_bounds__(CF::NTH, CF::MINB) void dense_glds_kernel(DenseArgs
 // 8 waves write the tile: C = alpha*sum + beta*C, or the raw partial into split `sp`'s slab when
 // the block grid also splits K (out-proj: 64 tiles x 4 splits). Two groups per block replace the
 // two-blocks-per-CU split-K of the plain core without a slab round trip through HBM.
+// With arrival counters (a.cnt) the grid split reduces in the kernel: a tile's splits are adjacent
+// block ids (one XCD, one L2), each writes its partial slab write-through (sc1: relaxed agent-scope
+// atomic stores), drains its stores (s_waitcnt vmcnt(0)) before the barrier that precedes its
+// counter add, and the last of the tile's splits to arrive sums the slabs in split order (its own
+// from LDS, the others with sc1 loads), writes C = alpha*sum + beta*C — the arithmetic of
+// slab_reduce_kernel, which this replaces — and resets the counter (cdna_hip_programming.md
+// Guideline 16, counter form).
 template <class CF>
 __global__ __launch_bounds__(2 * CF::NTH, 1) void wgrad_dual_kernel(DenseArgs a, int tiles_m, int tiles_n) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -98,7 +108,13 @@ __global__ __launch_bounds__(2 * CF::NTH, 1) void wgrad_dual_kernel(DenseArgs a,
   if (a.stamp != nullptr && threadIdx.x == 0) atomicMin(a.stamp, (unsigned long long)__builtin_amdgcn_s_memrealtime());
   const int id = gemmg::xcd_remap(blockIdx.x, gridDim.x);
   int tm, tn, sp;
-  gemmg::tile_of(id, tiles_m, tiles_n, tm, tn, sp);
+  if (a.cnt) {                                      // splits innermost: a tile's splits share an XCD
+    int z;
+    gemmg::tile_of(id / a.splits, tiles_m, tiles_n, tm, tn, z);
+    sp = id % a.splits;
+  } else {
+    gemmg::tile_of(id, tiles_m, tiles_n, tm, tn, sp);
+  }
   const int m0 = tm * CF::BM, n0 = tn * CF::BN;
   const int kbeg = sp * a.kchunk, kend = min(a.K, kbeg + a.kchunk);
   const int lane = threadIdx.x & 63;
@@ -143,10 +159,57 @@ __global__ __launch_bounds__(2 * CF::NTH, 1) void wgrad_dual_kernel(DenseArgs a,
       }
   __syncthreads();
   const bool slab = a.sSplit != 0;
+  constexpr int Q = CF::BN / 4;                      // float4 per tile row
+  if (slab && a.cnt) {
+    float* W = (float*)a.e.C;                        // slab 0; split q's at W + q * sSplit
+    const int64_t ldw = a.e.ldc;
+    for (int c = threadIdx.x; c < CF::BM * Q; c += 2 * CF::NTH) {
+      const int lr = c / Q, lc = (c % Q) * 4, row = m0 + lr, col = n0 + lc;
+      if (row >= a.M || col >= a.N) continue;        // N % 4 == 0 in slab mode (host-checked)
+      const f32x4 v = *(const f32x4*)(st + lr * LDR + lc);
+      float* o = W + sp * a.sSplit + (int64_t)row * ldw + col;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) __hip_atomic_store(o + q, v[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave: its partial is out
+    __shared__ int last;
+    __syncthreads();
+    const int tile = tm * tiles_n + tn;
+    if (threadIdx.x == 0)
+      last = __hip_atomic_fetch_add(&a.cnt[tile], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)a.splits - 1;
+    __syncthreads();
+    if (last) {
+      for (int c = threadIdx.x; c < CF::BM * Q; c += 2 * CF::NTH) {
+        const int lr = c / Q, lc = (c % Q) * 4, row = m0 + lr, col = n0 + lc;
+        if (row >= a.M || col >= a.N) continue;
+        const float* w = W + (int64_t)row * ldw + col;
+        const f32x4 own = *(const f32x4*)(st + lr * LDR + lc);
+        f32x4 sum;
+        for (int q = 0; q < a.splits; ++q) {
+          f32x4 v;
+          if (q == sp) v = own;
+          else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = __hip_atomic_load(w + q * a.sSplit + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
+          if (q == 0) sum = v; else sum += v;
+        }
+        float* o = a.fC + (int64_t)row * a.fldc + col;
+        f32x4 y = sum * a.falpha;
+        if (a.fbeta != 0.f) y += *(const f32x4*)o * a.fbeta;
+        *(f32x4*)o = y;
+      }
+      if (threadIdx.x == 0) __hip_atomic_store(&a.cnt[tile], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (a.stamp != nullptr) {
+      __syncthreads();
+      if (threadIdx.x == 0) atomicMax(a.stamp + 1, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+    }
+    return;
+  }
   float* C = slab ? (float*)a.e.C + sp * a.sSplit : (float*)a.e.C;
   const int64_t ldc = a.e.ldc;
   const float alpha = slab ? 1.f : a.e.alpha, beta = slab ? 0.f : a.e.beta;
-  constexpr int Q = CF::BN / 4;                      // float4 per tile row
   for (int c = threadIdx.x; c < CF::BM * Q; c += 2 * CF::NTH) {
     const int lr = c / Q, lc = (c % Q) * 4, row = m0 + lr, col = n0 + lc;
     if (row >= a.M || col >= a.N) continue;
@@ -500,18 +563,21 @@ __global__ __launch_bounds__(256) void skinny_kernel(DenseArgs a, float* part, i
 }
 
 // fp32 few-row linears on the fp32-input matrix cores (v_mfma_f32_16x16x4_f32: exact fp32
-// products, fp32 accumulation): a workgroup = 4 waves over one 16-column block, wave w takes the
-// 16-k groups w, w+4, ... of the workgroup's K range; per group a lane loads the 4 consecutive
-// weights of its column (16 B) and, per 16-row tile, its row's 4 activations (16 B, L2-resident:
-// no LDS staging, no barrier in the loop), then 4 MFMAs per row tile. The vector-ALU kernel above
-// reads 40 activations from LDS per 2 weights and is LDS-bound near 2 TB/s; here the row blocking
-// is the matrix core's. Groups are issued UNR at a time (all loads first). Same K split / last-
-// arriver reduction as skinny_kernel; a row's result never depends on M (rows are independent in
-// the MFMA, the k order is fixed).
+// products, fp32 accumulation): a workgroup = SKM_WAVES waves over one 16-column block, wave w
+// takes the 16-k groups w, w + SKM_WAVES, ... of the workgroup's K range; per group a lane loads
+// the 4 consecutive weights of its column (16 B) and, per 16-row tile, its row's 4 activations
+// (16 B, L2-resident: no LDS staging, no barrier in the loop), then 4 MFMAs per row tile; groups
+// are issued UNR at a time (all loads first), and the waves' partials are summed in LDS in a fixed
+// order. The decoder's linears are latency-bound (40 rows): 8 waves give one load round trip per
+// workgroup at K = 1024 without a cross-workgroup hand-off (whose write-through stores, counter and
+// reloads cost ~5 us per launch); only K >= 4096 over few column blocks (FFN w_2) still splits K
+// over workgroups (skinny_mma_splits), with skinny_kernel's last-arriver reduction. A row's result
+// never depends on M (rows are independent in the MFMA, the k order is fixed).
+constexpr int SKM_WAVES = 8;
 template <typename OutT, int MT>
-__global__ __launch_bounds__(256) void skinny_mma_kernel(DenseArgs a, float* part, int kchunk, unsigned* cnt) {
-  constexpr int UNR = 4;
-  __shared__ __attribute__((aligned(16))) float red[4][16 * MT][SK_NB + 1];
+__global__ __launch_bounds__(64 * SKM_WAVES) void skinny_mma_kernel(DenseArgs a, float* part, int kchunk, unsigned* cnt) {
+  constexpr int NW = SKM_WAVES, UNR = 8;
+  __shared__ __attribute__((aligned(16))) float red[NW][16 * MT][SK_NB + 1];
   __shared__ int last;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, c = lane & 15;
   const int n0 = blockIdx.x * SK_NB, col = n0 + c;
@@ -530,11 +596,11 @@ __global__ __launch_bounds__(256) void skinny_mma_kernel(DenseArgs a, float* par
   f32x4 acc[MT];
 #pragma unroll
   for (int t = 0; t < MT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int q0 = w; q0 < ng; q0 += 4 * UNR) {
+  for (int q0 = w; q0 < ng; q0 += NW * UNR) {
     f32x4 b[UNR], x[UNR][MT];
 #pragma unroll
     for (int u = 0; u < UNR; ++u) {
-      const int q = q0 + 4 * u;
+      const int q = q0 + NW * u;
       const bool ok = q < ng;
       const int k = kbeg + 16 * (ok ? q : 0);
       b[u] = (ok && cok) ? *(const f32x4*)(Wr + k) : f32x4{0.f, 0.f, 0.f, 0.f};
@@ -548,16 +614,17 @@ __global__ __launch_bounds__(256) void skinny_mma_kernel(DenseArgs a, float* par
 #pragma unroll
         for (int e = 0; e < 4; ++e) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(x[u][t][e], b[u][e], acc[t], 0, 0, 0);
   }
-  // acc[t][r] = this wave's partial of y[16t + 4g + r][n0 + c]; the 4 waves' in a fixed order
+  // acc[t][r] = this wave's partial of y[16t + 4g + r][n0 + c]; the waves' in a fixed order
 #pragma unroll
   for (int t = 0; t < MT; ++t)
 #pragma unroll
     for (int r = 0; r < 4; ++r) red[w][16 * t + 4 * g + r][c] = acc[t][r];
   __syncthreads();
-  for (int o = tid; o < 16 * MT * SK_NB; o += 256) {
+  for (int o = tid; o < 16 * MT * SK_NB; o += 64 * NW) {
     const int m = o / SK_NB, cc = o - m * SK_NB, cl = n0 + cc;
     if (m < a.M && cl < a.N) {
-      const float v = (red[0][m][cc] + red[1][m][cc]) + (red[2][m][cc] + red[3][m][cc]);
+      float v = (red[0][m][cc] + red[1][m][cc]) + (red[2][m][cc] + red[3][m][cc]);
+      v += (red[4][m][cc] + red[5][m][cc]) + (red[6][m][cc] + red[7][m][cc]);
       if (part) __hip_atomic_store(&part[((int64_t)blockIdx.y * a.M + m) * a.N + cl], v, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
       else epi_elems<float, OutT, 1>(a.e, m, cl, &v);
@@ -572,7 +639,7 @@ __global__ __launch_bounds__(256) void skinny_mma_kernel(DenseArgs a, float* par
   if (!last) return;
   const int S = gridDim.y;
   const int64_t MN = (int64_t)a.M * a.N;
-  for (int o = tid; o < 16 * MT * SK_NB; o += 256) {
+  for (int o = tid; o < 16 * MT * SK_NB; o += 64 * NW) {
     const int m = o / SK_NB, cc = o - m * SK_NB, cl = n0 + cc;
     if (m < a.M && cl < a.N) {
       const float* pp = part + (int64_t)m * a.N + cl;
@@ -596,18 +663,33 @@ int skinny_splits(int N, int K, int& kchunk) {
   return (K + kchunk - 1) / kchunk;
 }
 
+// the matrix-core kernel's split: none unless K >= 4096 over fewer than 128 column blocks (then
+// 1024-k chunks, at most 4): every other decoder linear is one load round trip per workgroup
+int skinny_mma_splits(int N, int K, int& kchunk) {
+  const int nb = (N + SK_NB - 1) / SK_NB;
+  int S = (nb < 128 && K >= 4096) ? std::min(4, K / 1024) : 1;
+  S = std::min(S, (int)std::max<int64_t>(1, AVSR_SKINNY_WS / (64 * (int64_t)N)));
+  kchunk = ((K + S - 1) / S + 15) / 16 * 16;
+  return (K + kchunk - 1) / kchunk;
+}
+
+bool skinny_mma_ok(const DenseArgs& a) {
+  return a.K % 16 == 0 && a.lda % 4 == 0 && a.ldb % 4 == 0 && !getenv_flag("AVSR_SKINNY_VALU");
+}
+
 template <typename T, typename OutT>
 int skinny_launch(const DenseArgs& a, float* ws, hipStream_t st) {
   int kchunk = a.K;
-  const int S = ws ? skinny_splits(a.N, a.K, kchunk) : 1;
+  const bool mma = sizeof(T) == 4 && skinny_mma_ok(a);
+  const int S = ws ? (mma ? skinny_mma_splits(a.N, a.K, kchunk) : skinny_splits(a.N, a.K, kchunk)) : 1;
   float* part = S > 1 ? ws : nullptr;
   unsigned* cnt = S > 1 ? (unsigned*)(ws + AVSR_SKINNY_WS) : nullptr;   // AVSR_SKINNY_CNT counters
   const int nb = (a.N + SK_NB - 1) / SK_NB;
   if (S > 1 && nb > AVSR_SKINNY_CNT) return AVSR_E_SHAPE;
   const dim3 g((unsigned)nb, (unsigned)S);
   if constexpr (sizeof(T) == 4) {       // fp32: the matrix-core form (16-byte rows, 16-k groups)
-    if (a.K % 16 == 0 && kchunk % 16 == 0 && a.lda % 4 == 0 && a.ldb % 4 == 0 && !getenv_flag("AVSR_SKINNY_VALU")) {
-#define SKM(T_) hipLaunchKernelGGL((skinny_mma_kernel<OutT, T_>), g, dim3(256), 0, st, a, part, kchunk, cnt)
+    if (mma) {
+#define SKM(T_) hipLaunchKernelGGL((skinny_mma_kernel<OutT, T_>), g, dim3(64 * SKM_WAVES), 0, st, a, part, kchunk, cnt)
       if (a.M <= 16) SKM(1);
       else if (a.M <= 32) SKM(2);
       else if (a.M <= 48) SKM(3);
@@ -698,6 +780,7 @@ extern "C" int avsr_gemm(const avsr_gemm_params* p, void* stream) {
   a.B = p->B; a.ldb = p->ldb; a.sB = p->strideB;
   a.sC = p->strideC; a.sR = p->strideR;
   a.stamp = p->stamp;
+  a.cnt = nullptr; a.fC = nullptr; a.fldc = 0; a.falpha = 1.f; a.fbeta = 0.f;
   Epi& e = a.e;
   e.M = p->M; e.N = p->N; e.C = p->C; e.ldc = p->ldc;
   e.alpha = p->alpha; e.beta = p->beta; e.bias = p->bias;
@@ -729,7 +812,15 @@ extern "C" int avsr_gemm(const avsr_gemm_params* p, void* stream) {
     if (p->dtype == AVSR_F32) return skinny_launch<float, float>(a, sws, st);
     return p->c_f32 ? skinny_launch<bf16, float>(a, sws, st) : skinny_launch<bf16, bf16>(a, sws, st);
   }
-  if (glds && wgrad_dual_ok(p, splits, slab)) rc = launch_wgrad_dual(a, st);
+  if (glds && wgrad_dual_ok(p, splits, slab)) {
+    const int tiles = ((p->M + CfgDual::BM - 1) / CfgDual::BM) * ((p->N + CfgDual::BN - 1) / CfgDual::BN);
+    if (slab && p->skinny_ws && tiles <= AVSR_SKINNY_CNT) {   // in-kernel slab reduction (no slab_reduce pass)
+      a.cnt = (unsigned*)(p->skinny_ws + AVSR_SKINNY_WS);
+      a.fC = (float*)p->C; a.fldc = p->ldc; a.falpha = p->alpha; a.fbeta = p->beta;
+      return launch_wgrad_dual(a, st);
+    }
+    rc = launch_wgrad_dual(a, st);
+  }
   else if (glds) rc = p->c_f32 ? glds_by_layout<float>(p, a, st) : glds_by_layout<bf16>(p, a, st);
   else if (p->dtype == AVSR_F32) rc = by_tile<float, float>(p, a, st);
   else if (p->c_f32) rc = by_tile<bf16, float>(p, a, st);
@@ -750,8 +841,9 @@ extern "C" int avsr_gemm(const avsr_gemm_params* p, void* stream) {
   return 0;
 }
 
-extern "C" int avsr_gemm_skinny_splits(int N, int K) {
+extern "C" int avsr_gemm_skinny_splits(int dtype, int N, int K) {
   if (N <= 0 || K <= 0) return 1;
   int kchunk;
+  if (dtype == AVSR_F32 && K % 16 == 0 && !getenv_flag("AVSR_SKINNY_VALU")) return skinny_mma_splits(N, K, kchunk);
   return skinny_splits(N, K, kchunk);
 }

@@ -131,7 +131,8 @@ class BatchBeamSearch:
         ops.linear_fwd(yn, eng.w("decoder.output_layer.weight"), ar.master("decoder.output_layer.bias"),
                        out=logits[:, :eng.V])
         logp = torch.empty(R, eng.V, device=eng.device, dtype=torch.float32)
-        return ops.log_softmax_rows(logits, eng.V, logp)
+        # log-probs and the pre-beam (top-P decoder tokens per row) in one pass
+        return ops.log_softmax_topk(logits, eng.V, logp, self.pre_beam_size, st["ids"])
 
     def _step(self, eng, st, first, k):
         """one search step on the device (no host sync): decoder, pre-beam, CTC prefix scores,
@@ -140,8 +141,7 @@ class BatchBeamSearch:
         R, P, beam = st["R"], self.pre_beam_size, self.beam_size
         st["anc_in"] = st["anc"][k]
         ops.beam_step_prep(R, st["pos"], st["anc"][k], st["klen_self"])
-        dec = self._decoder_step(eng, st)
-        ops.row_topk(dec, self.n_vocab, P, st["ids"])
+        dec = self._decoder_step(eng, st)      # also writes the pre-beam ids
         ops.ctc_prefix(st["logp"], None if first else st["r_prev"][k], st["tok"], st["ids"], st["r_new"], st["psi"],
                        n=R, out_len=0, out_len_dev=st["pos"], blank=self.blank, eos=self.eos, uidx=st["uidx"],
                        tlen=st["tlen"])

@@ -40,13 +40,17 @@ def _ptr(t):
 _SKINNY_WS = {}
 SKINNY_WS = 1 << 19        # AVSR_SKINNY_WS (fp32 partials), followed by
 SKINNY_CNT = 4096          # AVSR_SKINNY_CNT zeroed uint32 arrival counters
-# few-row (decoder step) linears: split K over more workgroups (gemm(skinny_split=None) default)
-SKINNY_SPLIT = False
+# few-row (decoder step) linears: split K over more workgroups (gemm(skinny_split=None) default;
+# C4 / C5 decode 84 -> 93 / 15.0 -> 16.4 utt/s, profiles/r04_decode_split_ab.json)
+SKINNY_SPLIT = True
+# split-K weight-gradients reduce their slabs inside the GEMM (last-arriving split per tile)
+SLAB_FUSED_REDUCE = True
 
 
-def skinny_splits(N, K):
-    """the K-split count the few-row path uses for an (N, K) weight when split (avsr_hip.h)"""
-    return int(L.load().avsr_gemm_skinny_splits(int(N), int(K)))
+def skinny_splits(N, K, dtype=torch.float32):
+    """the K-split count the few-row path uses for an (N, K) weight of `dtype` when split (avsr_hip.h)"""
+    code = L.AVSR_BF16 if dtype == torch.bfloat16 else L.AVSR_F32
+    return int(L.load().avsr_gemm_skinny_splits(code, int(N), int(K)))
 
 
 def _skinny_ws(device):
@@ -99,6 +103,8 @@ def gemm(A, B, C, *, M, N, K, a_kmajor, b_kmajor, lda, ldb, ldc, batch=1,
         p.ws = ws.data_ptr()
     if (SKINNY_SPLIT if skinny_split is None else skinny_split) and M <= 64 and splitk <= 1:
         p.skinny_ws = _skinny_ws(A.device).data_ptr()   # K-split partials of the few-row vector-ALU path
+    elif ws is not None and splitk > 1 and SLAB_FUSED_REDUCE:
+        p.skinny_ws = _skinny_ws(A.device).data_ptr()   # arrival counters: in-kernel slab reduction
     if db is not None:
         assert db.dtype == torch.float32 and db.numel() >= N and db_ws is not None and db_ws.dtype == torch.float32
         assert db_ws.numel() >= ((M + 63) // 64) * N
@@ -753,6 +759,14 @@ def dec_attn(q, k, v, o, *, n, H, klen_max, k_bstride, v_bstride, klen=None, sca
 def row_topk(x, V, K, ids):
     _call("avsr_row_topk", L.fill(L.TopkParams, rows=x.shape[0], V=V, K=K, x=x, ldx=x.stride(0), ids=ids))
     return ids
+
+
+def log_softmax_topk(x, V, out, K, ids):
+    """log_softmax_rows(x, V, out) and row_topk(out, V, K, ids) in one pass (identical results)"""
+    L.check(L.load().avsr_log_softmax_topk(dtype_code(x), x.shape[0], V, x.data_ptr(), x.stride(0), out.data_ptr(),
+                                           out.stride(0), K, ids.data_ptr(), L.stream_ptr()),
+            "avsr_log_softmax_topk")
+    return out
 
 
 def ctc_prefix(logp, r_prev, last, ids, r_new, psi, *, n, out_len, blank, eos, uidx=None, tlen=None,

@@ -89,7 +89,11 @@ typedef struct {
                                 partials, then AVSR_SKINNY_CNT uint32 arrival counters that the
                                 caller zeroes once (every launch leaves them zero); the last
                                 workgroup of a column block adds the partials in a fixed order
-                                and runs the epilogue. NULL: one workgroup row */
+                                and runs the epilogue. NULL: one workgroup row.
+                                Also used by the slab split-K weight-gradient path (splitk > 1
+                                with ws, both operands r-contiguous, fp32 C, plain epilogue): its
+                                counters let the last-arriving split of each output tile reduce
+                                the slabs in the GEMM itself (no separate reduction pass) */
 } avsr_gemm_params;
 #define AVSR_GEMM_COLSUM_WS(M, N) ((int64_t)(((M) + 63) / 64) * (N))
 /* slabs are AVSR_GEMM_SLAB_PAD floats apart beyond M*N: power-of-two slab strides put the
@@ -102,9 +106,10 @@ typedef struct {
 #define AVSR_GEMM_SLAB_WS(batch, splitk, M, N) ((int64_t)(batch) * (splitk) * ((int64_t)(M) * (N) + AVSR_GEMM_SLAB_PAD))
 
 int avsr_gemm(const avsr_gemm_params* p, void* stream);
-/* K-split count the few-row path uses for an N x K weight when skinny_ws is given (depends on N
- * and K only, never on M: a row's result does not depend on how many rows share the launch) */
-int avsr_gemm_skinny_splits(int N, int K);
+/* K-split count the few-row path uses for an N x K weight of this dtype when skinny_ws is given
+ * (depends on dtype, N and K only, never on M: a row's result does not depend on how many rows
+ * share the launch; fp32 with K % 16 == 0 and 16-byte aligned rows runs the matrix-core kernel) */
+int avsr_gemm_skinny_splits(int dtype, int N, int K);
 
 /* ------------------------------------------------------------------------------------
  * Implicit-GEMM convolution over NHWC activations (no im2col buffer), grouped.
@@ -524,6 +529,11 @@ typedef struct {
   int* ids;                   /* [rows][K] */
 } avsr_topk_params;
 int avsr_row_topk(const avsr_topk_params* p, void* stream);
+/* avsr_log_softmax_topk: avsr_log_softmax_rows followed by avsr_row_topk on its output, in one
+ * pass over each row (decode steps: the decoder output layer's log-probs and the pre-beam,
+ * batch_beam_search.py:228-236 + scorers/ctc.py pre-beam); results identical to the two calls */
+int avsr_log_softmax_topk(int dtype, int rows, int V, const void* x, int64_t ldx, float* out, int64_t ldo,
+                          int K, int* ids, void* stream);
 
 typedef struct {
   int n, T, V, P;

@@ -64,10 +64,28 @@ def test_row_topk_and_log_softmax(dev):
     assert torch.equal(ids.long().cpu(), torch.topk(lp.cpu(), 7, dim=-1)[1])
 
 
-@pytest.mark.parametrize("first", [True, False])
-def test_ctc_prefix_matches_oracle(dev, first):
+@pytest.mark.parametrize("V", [5049, 7000])
+def test_log_softmax_topk_equals_separate_kernels(dev, V):
+    """the fused decode-step kernel (V <= 6144 in registers; 7000 takes the two-pass path) is
+    bit-identical to log_softmax_rows + row_topk, ties included"""
+    g = torch.Generator().manual_seed(6)
+    x = (torch.randn(9, V + 7, generator=g) * 4).round() / 4      # many exact ties
+    x = x.to(dev)
+    lp_a = torch.empty(9, V, device=dev)
+    ids_a = torch.empty(9, 7, device=dev, dtype=torch.int32)
+    ops.log_softmax_rows(x, V, lp_a)
+    ops.row_topk(lp_a, V, 7, ids_a)
+    lp_b = torch.full((9, V), float("nan"), device=dev)
+    ids_b = torch.full((9, 7), -1, device=dev, dtype=torch.int32)
+    ops.log_softmax_topk(x, V, lp_b, 7, ids_b)
+    assert torch.equal(lp_a, lp_b)
+    assert torch.equal(ids_a, ids_b)
+
+
+@pytest.mark.parametrize("first,T,P", [(True, 40, 4), (False, 40, 4), (False, 375, 7)])
+def test_ctc_prefix_matches_oracle(dev, first, T, P):
     g = torch.Generator().manual_seed(5)
-    T, V, n, P = 40, 300, 3, 4
+    V, n = 300, 3
     logp = torch.log_softmax(torch.randn(T, V, generator=g) * 3, -1)
     eos = V - 1
     if first:

@@ -156,6 +156,11 @@ def test_wgrad_dual_kernel(dev, monkeypatch, M, N, K, splitk):
     a, b = run(), run()
     assert torch.equal(a, b)
     assert _rel(a, ref) < 1e-5 * (K ** 0.5)
+    if splitk > 1:
+        # the in-kernel slab reduction (last-arriving split per tile) equals the separate pass
+        monkeypatch.setattr(ops, "SLAB_FUSED_REDUCE", False)
+        assert torch.equal(run(), a)
+        monkeypatch.setattr(ops, "SLAB_FUSED_REDUCE", True)
     monkeypatch.setenv("AVSR_WGRAD_DUAL", "0")
     c = run()
     assert _rel(a, c.double()) < 1e-5 * (K ** 0.5)
@@ -252,13 +257,18 @@ def test_skinny_linear(dev, dtype, M, N, K):
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("N,K", [(1024, 4096), (1024, 1024), (4096, 1024), (5056, 1024), (256, 2048)])
 def test_skinny_k_split_rows_independent(dev, N, K, dtype):
-    """The few-row path with its K split (skinny_ws given: S = avsr_gemm_skinny_splits(N, K) > 1
-    workgroup rows, fp32 partials reduced in a fixed order): S depends on N and K only, so every
-    row equals the same row launched alone, bit for bit (batched beam search == per-utterance
-    search relies on it); split and unsplit both match fp64."""
-    S = ops.skinny_splits(N, K)
-    # the decoder's output layer (5056 columns) has no room for a split in AVSR_SKINNY_WS
-    assert S == (1 if N == 5056 else {4096: 2}.get(N, S)) and (S > 1 or N == 5056), (N, K, S)
+    """The few-row path with its K split (skinny_ws given: S = avsr_gemm_skinny_splits(dtype, N, K)
+    workgroup rows, fp32 partials reduced in a fixed order): S depends on dtype, N and K only, so
+    every row equals the same row launched alone, bit for bit (batched beam search == per-utterance
+    search relies on it); split and unsplit both match fp64. bf16 (vector-ALU kernel): >= 512
+    workgroups; fp32 (matrix-core kernel, 8 waves per workgroup): only K >= 4096 over < 128 column
+    blocks splits (the FFN w_2 shape)."""
+    S = ops.skinny_splits(N, K, dtype)
+    if dtype == torch.float32:
+        assert S == (4 if (N, K) == (1024, 4096) else 1), (N, K, S)
+    else:
+        # the decoder's output layer (5056 columns) has no room for a split in AVSR_SKINNY_WS
+        assert S == (1 if N == 5056 else {4096: 2}.get(N, S)) and (S > 1 or N == 5056), (N, K, S)
     g = torch.Generator(device="cpu").manual_seed(N + K)
     x = torch.randn(40, K, generator=g).to(dev, dtype)
     W = (torch.randn(N, K, generator=g) * K ** -0.5).to(dev, dtype)

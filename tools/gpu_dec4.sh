@@ -1,14 +1,14 @@
-# decode parity (unit + full-size goldens) then C1 / C4 / C5 throughput with and without the
-# few-row GEMM K split. Usage: gpurun -- bash tools/gpu_dec2.sh TAG
+# decode parity (unit + full-size goldens), C1 / C4 / C5 throughput (split on / off), C5 profile.
+# Usage: gpurun -- bash tools/gpu_dec4.sh TAG
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-O=gpurun_out/${1:-dec2}; mkdir -p $O
-timeout -k 10 300 python -u -m pytest tests/test_gpu_gemm.py -k skinny -x -q --timeout 120 --timeout-method thread > $O/gemm.log 2>&1 || { echo gemm tests failed; tail -30 $O/gemm.log; exit 1; }
+O=gpurun_out/${1:-dec4}; mkdir -p $O
+timeout -k 10 300 python -u -m pytest tests/test_gpu_gemm.py -k "skinny or wgrad_dual or layouts_bf16" -x -q --timeout 120 --timeout-method thread > $O/gemm.log 2>&1 || { echo gemm tests failed; tail -30 $O/gemm.log; exit 1; }
 tail -1 $O/gemm.log
 timeout -k 10 600 python -u -m pytest tests/test_gpu_decode.py tests/test_gpu_fullsize_golden.py tests/test_gpu_surface.py -x -v --timeout 300 --timeout-method thread > $O/tests.log 2>&1 || { echo tests failed; grep -E "FAIL|Error|error" $O/tests.log | head -20; tail -40 $O/tests.log; exit 1; }
 tail -1 $O/tests.log
-for r in 1 2; do
+for r in 1; do
   timeout -k 10 300 python -u tools/decode_bench.py > $O/dec_nosplit_$r.json 2> $O/dec.err || { echo dec failed; tail -20 $O/dec.err; exit 1; }
   echo nosplit; cat $O/dec_nosplit_$r.json
   timeout -k 10 300 python -u tools/decode_bench.py split > $O/dec_split_$r.json 2> $O/dec.err || { echo dec failed; tail -20 $O/dec.err; exit 1; }
