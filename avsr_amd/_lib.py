@@ -41,7 +41,7 @@ class GemmParams(ctypes.Structure):
         ("db", _c_p),
         ("db_ws", _c_p),
         ("stamp", _c_p),
-        ("skinny_ws", _c_p),
+        ("skinny_ws", _c_p), ("ln_c1", _c_p), ("ln_eps", ctypes.c_float),
     ]
 
 
@@ -180,7 +180,8 @@ class DecAttnParams(ctypes.Structure):
         ("dtype", _i), ("n", _i), ("H", _i), ("klen_max", _i), ("scale", _f),
         ("q", _c_p), ("ldq", _i64), ("k", _c_p), ("ldk", _i64), ("k_bstride", _i64),
         ("v", _c_p), ("ldv", _i64), ("v_bstride", _i64), ("klen", _c_p), ("o", _c_p), ("ldo", _i64),
-        ("kidx", _c_p), ("kmap", _c_p), ("ldmap", _i64), ("group", _i),
+        ("kidx", _c_p), ("kmap", _c_p), ("ldmap", _i64), ("group", _i), ("ksplit", _i), ("ws", _c_p),
+        ("cnt", _c_p),
     ]
 
 

@@ -101,14 +101,26 @@ template <typename T> AVSR_DEV f32x4 ld4(const T* p) {
 // back to back before using them, so a 375-key memory takes two load round trips per phase
 // (the one-load-per-iteration loop was latency-bound: 51 us per call at 375 keys, G = 5).
 constexpr int DA_WAVES = 8, DA_UNROLL = 8;
+// Key split (p.ksplit >= 2, blockIdx.z): workgroup z of a (group, head) takes keys
+// [z * chunk, (z + 1) * chunk) of its rows' klen, with nz = min(ksplit, ceil(klen / 192)) chunks
+// (a function of klen alone, so a hypothesis's result never depends on the batch); it writes its
+// per-query (max, sum of exp, unnormalised o) to p.ws and the last of the nz to arrive merges them
+// in split order (write-through partials, drained before the counter add; Guideline 16).
+constexpr int DA_SPLIT_KEYS = 192;
 template <typename T, int G>
 __global__ __launch_bounds__(64 * DA_WAVES) void dec_attn_kernel(avsr_dec_attn_params p) {
   constexpr int NW = DA_WAVES, U = DA_UNROLL, KS = 4 * NW;
   extern __shared__ float sc[];           // [G][kpad] scores, then [NW][G][64] partials
   __shared__ float shr[G][NW];
+  __shared__ int last;
   const int h = blockIdx.x, i0 = blockIdx.y * G;
   const int klen = p.klen ? min(p.klen[i0], p.klen_max) : p.klen_max;
   const int kpad = (p.klen_max + 3) & ~3;
+  const int nz = p.ksplit > 1 ? max(1, min(p.ksplit, (klen + DA_SPLIT_KEYS - 1) / DA_SPLIT_KEYS)) : 1;
+  const int z = blockIdx.z;
+  if (z >= nz) return;                    // (no arrival: the merge counts nz workgroups)
+  const int chunk = (klen + nz - 1) / nz;
+  const int jbeg = z * chunk, jend = min(klen, jbeg + chunk), jn = jend - jbeg;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, sub = lane >> 4, d0 = (lane & 15) * 4;
   const int kb = p.kmap ? 0 : (p.kidx ? p.kidx[i0] : i0);
   const T* K = (const T*)p.k + (int64_t)kb * p.k_bstride + h * 64 + d0;
@@ -119,8 +131,8 @@ __global__ __launch_bounds__(64 * DA_WAVES) void dec_attn_kernel(avsr_dec_attn_p
   auto rows_of = [&](int it0, int (&row)[U]) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int j = (it0 + u) * KS + jl;
-      row[u] = j < klen ? (km ? km[j] : j) : 0;
+      const int j = jbeg + (it0 + u) * KS + jl;
+      row[u] = j < jend ? (km ? km[j] : j) : 0;
     }
   };
   f32x4 q[G];
@@ -129,7 +141,7 @@ __global__ __launch_bounds__(64 * DA_WAVES) void dec_attn_kernel(avsr_dec_attn_p
   float m[G];
 #pragma unroll
   for (int g = 0; g < G; ++g) m[g] = -INFINITY;
-  for (int it0 = 0; it0 * KS < klen; it0 += U) {
+  for (int it0 = 0; it0 * KS < jn; it0 += U) {
     int row[U];
     rows_of(it0, row);
     f32x4 k[U];
@@ -137,8 +149,8 @@ __global__ __launch_bounds__(64 * DA_WAVES) void dec_attn_kernel(avsr_dec_attn_p
     for (int u = 0; u < U; ++u) k[u] = ld4(K + (int64_t)row[u] * p.ldk);
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int j = (it0 + u) * KS + jl;
-      const bool ok = j < klen;
+      const int j = jbeg + (it0 + u) * KS + jl;
+      const bool ok = j < jend;
 #pragma unroll
       for (int g = 0; g < G; ++g) {
         float s = q[g][0] * k[u][0] + q[g][1] * k[u][1] + q[g][2] * k[u][2] + q[g][3] * k[u][3];
@@ -171,7 +183,7 @@ __global__ __launch_bounds__(64 * DA_WAVES) void dec_attn_kernel(avsr_dec_attn_p
 #pragma unroll
   for (int g = 0; g < G; ++g) {
     float lg = 0.f;
-    for (int j = threadIdx.x; j < klen; j += 64 * NW) {
+    for (int j = jbeg + threadIdx.x; j < jend; j += 64 * NW) {
       const float e = expf(sc[g * kpad + j] - m[g]);
       sc[g * kpad + j] = e;
       lg += e;
@@ -190,7 +202,7 @@ __global__ __launch_bounds__(64 * DA_WAVES) void dec_attn_kernel(avsr_dec_attn_p
   f32x4 acc[G];
 #pragma unroll
   for (int g = 0; g < G; ++g) acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int it0 = 0; it0 * KS < klen; it0 += U) {
+  for (int it0 = 0; it0 * KS < jn; it0 += U) {
     int row[U];
     rows_of(it0, row);
     f32x4 v[U];
@@ -198,8 +210,8 @@ __global__ __launch_bounds__(64 * DA_WAVES) void dec_attn_kernel(avsr_dec_attn_p
     for (int u = 0; u < U; ++u) v[u] = ld4(Vv + (int64_t)row[u] * p.ldv);
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int j = (it0 + u) * KS + jl;
-      const bool ok = j < klen;
+      const int j = jbeg + (it0 + u) * KS + jl;
+      const bool ok = j < jend;
 #pragma unroll
       for (int g = 0; g < G; ++g) acc[g] += (ok ? sc[g * kpad + j] : 0.f) * v[u];
     }
@@ -215,13 +227,57 @@ __global__ __launch_bounds__(64 * DA_WAVES) void dec_attn_kernel(avsr_dec_attn_p
     if (sub == 0) *(f32x4*)&part[(w * G + g) * 64 + d0] = acc[g];
   }
   __syncthreads();
+  if (nz == 1) {
+    for (int t = threadIdx.x; t < ng * 64; t += 64 * NW) {
+      const int g = t >> 6, d = t & 63;
+      float o = 0.f;
+#pragma unroll
+      for (int x = 0; x < NW; ++x) o += part[(x * G + g) * 64 + d];
+      ((T*)p.o)[(int64_t)(i0 + g) * p.ldo + h * 64 + d] = from_f<T>(o / l[g]);
+    }
+    return;
+  }
+  // split: this chunk's (o[64], max, sum) per query -> ws[(group, head)][z][g][66]
+  const int64_t slot = (int64_t)blockIdx.y * gridDim.x + h;
+  float* wz = p.ws + (slot * p.ksplit) * G * 66;
   for (int t = threadIdx.x; t < ng * 64; t += 64 * NW) {
     const int g = t >> 6, d = t & 63;
     float o = 0.f;
 #pragma unroll
     for (int x = 0; x < NW; ++x) o += part[(x * G + g) * 64 + d];
-    ((T*)p.o)[(int64_t)(i0 + g) * p.ldo + h * 64 + d] = from_f<T>(o / l[g]);
+    __hip_atomic_store(wz + ((int64_t)z * G + g) * 66 + d, o, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
+  if (threadIdx.x < ng) {
+    const int g = threadIdx.x;
+#pragma unroll
+    for (int gg = 0; gg < G; ++gg)
+      if (gg == g) {
+        __hip_atomic_store(wz + ((int64_t)z * G + g) * 66 + 64, m[gg], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(wz + ((int64_t)z * G + g) * 66 + 65, l[gg], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave: its partials are out
+  __syncthreads();
+  if (threadIdx.x == 0)
+    last = __hip_atomic_fetch_add(&p.cnt[slot], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)nz - 1;
+  __syncthreads();
+  if (!last) return;
+  for (int t = threadIdx.x; t < ng * 64; t += 64 * NW) {
+    const int g = t >> 6, d = t & 63;
+    auto ld = [&](int q, int e) {
+      return __hip_atomic_load(wz + ((int64_t)q * G + g) * 66 + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    };
+    float mx = -INFINITY;
+    for (int q = 0; q < nz; ++q) mx = fmaxf(mx, ld(q, 64));
+    float lsum = 0.f, o = 0.f;
+    for (int q = 0; q < nz; ++q) {
+      const float f = expf(ld(q, 64) - mx);
+      lsum += ld(q, 65) * f;
+      o += ld(q, d) * f;
+    }
+    ((T*)p.o)[(int64_t)(i0 + g) * p.ldo + h * 64 + d] = from_f<T>(o / lsum);
+  }
+  if (threadIdx.x == 0) __hip_atomic_store(&p.cnt[slot], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // ---------------------------------------------------------------- pre-beam top-P
@@ -791,7 +847,9 @@ extern "C" int avsr_dec_attn(const avsr_dec_attn_params* p, void* stream) {
   const int kpad = (p->klen_max + 3) & ~3;
   const size_t lds = ((size_t)G * kpad + (size_t)DA_WAVES * G * 64) * sizeof(float);
   if (lds > 64 * 1024) return AVSR_E_SHAPE;
-  const dim3 g(p->H, (p->n + G - 1) / G);
+  const int ks = p->ksplit > 1 ? p->ksplit : 1;
+  if (ks > 8 || (ks > 1 && (!p->ws || !p->cnt))) return AVSR_E_ARG;
+  const dim3 g(p->H, (p->n + G - 1) / G, ks);
   hipStream_t st = (hipStream_t)stream;
 #define DA(T_, G_) hipLaunchKernelGGL((dec_attn_kernel<T_, G_>), g, dim3(64 * DA_WAVES), lds, st, *p)
 #define DAG(T_) switch (G) { case 1: DA(T_, 1); break; case 2: DA(T_, 2); break; case 3: DA(T_, 3); break;   \

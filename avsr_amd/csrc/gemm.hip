@@ -23,6 +23,8 @@ struct DenseArgs {
   unsigned* cnt;               // wgrad_dual_kernel slab mode: per-tile arrival counters (zeroed) or null
   float* fC; int64_t fldc;     // ... its final output C (the slabs' reduction target)
   float falpha, fbeta;
+  const float* ln_c1; float ln_eps;   // skinny_mma_kernel LayerNorm prologue (avsr_gemm_params.ln_c1)
+  float* lnst;                        // ... its per-chunk row statistics (split launches)
 };
 
 template <typename T, typename OutT, int WM, int WN, bool AK, bool BK>
@@ -563,24 +565,44 @@ __global__ __launch_bounds__(256) void skinny_kernel(DenseArgs a, float* part, i
 }
 
 // fp32 few-row linears on the fp32-input matrix cores (v_mfma_f32_16x16x4_f32: exact fp32
-// products, fp32 accumulation): a workgroup = SKM_WAVES waves over one 16-column block, wave w
-// takes the 16-k groups w, w + SKM_WAVES, ... of the workgroup's K range; per group a lane loads
-// the 4 consecutive weights of its column (16 B) and, per 16-row tile, its row's 4 activations
-// (16 B, L2-resident: no LDS staging, no barrier in the loop), then 4 MFMAs per row tile; groups
-// are issued UNR at a time (all loads first), and the waves' partials are summed in LDS in a fixed
-// order. The decoder's linears are latency-bound (40 rows): 8 waves give one load round trip per
-// workgroup at K = 1024 without a cross-workgroup hand-off (whose write-through stores, counter and
-// reloads cost ~5 us per launch); only K >= 4096 over few column blocks (FFN w_2) still splits K
-// over workgroups (skinny_mma_splits), with skinny_kernel's last-arriver reduction. A row's result
-// never depends on M (rows are independent in the MFMA, the k order is fixed).
+// products, fp32 accumulation): a workgroup = SKM_WAVES waves over one 16-column block and one K
+// chunk; wave w takes the 16-k groups w, w + SKM_WAVES, ... of the chunk; per group a lane loads the
+// 4 consecutive weights of its column (16 B) and, per 16-row tile, its row's 4 activations (16 B,
+// L2-resident: no LDS staging), then 4 MFMAs per row tile; the chunk is one load batch (all loads
+// in flight at once), and the waves' partials are summed in LDS in a fixed order. The decoder's
+// weights arrive cold from HBM every step, so the grid is sized to occupy every CU
+// (skinny_mma_splits: K chunks until N/16 x S >= 256); the S partials of a column block go
+// through the last-arriver hand-off of skinny_kernel. A row's result never depends on M (rows are
+// independent in the MFMA, the k order is fixed).
+// The epilogue's bias / residual operands are read at the start, beside the weight loads.
+// UNR = 4 where the grid exceeds one workgroup per CU (fewer registers, two per CU).
+// LNP (LayerNorm prologue, a.ln_c1): the batch holds whole rows of the chunk, so each row's chunk
+// mean and M2 (two passes over the registers, partials over the 4 lanes of a row and the 8 waves in
+// a fixed order) come for free; split launches hand them over with the partial sums (a.lnst) and
+// the last arriver combines them (Chan et al.'s pairwise formula, split order); the MFMAs run on the
+// raw x against gamma o W, and the epilogue applies rstd * (acc - mean * c1[n]).
 constexpr int SKM_WAVES = 8;
-template <typename OutT, int MT>
+template <typename OutT, int MT, int UNR, bool LNP = false>
 __global__ __launch_bounds__(64 * SKM_WAVES) void skinny_mma_kernel(DenseArgs a, float* part, int kchunk, unsigned* cnt) {
-  constexpr int NW = SKM_WAVES, UNR = 8;
+  constexpr int NW = SKM_WAVES, NE = (16 * MT * SK_NB + 64 * NW - 1) / (64 * NW);
   __shared__ __attribute__((aligned(16))) float red[NW][16 * MT][SK_NB + 1];
+  __shared__ float st1[LNP ? NW : 1][16 * MT], st2[LNP ? NW : 1][16 * MT];
+  __shared__ float rmean[LNP ? 16 * MT : 1], rrstd[LNP ? 16 * MT : 1];
   __shared__ int last;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, c = lane & 15;
   const int n0 = blockIdx.x * SK_NB, col = n0 + c;
+  const Epi& e = a.e;
+  const bool fast = !e.bwd && !e.preact && e.drop_p == 0.f && e.beta == 0.f && !e.atomic;
+  float pb[NE], pr[NE];
+  if (fast) {
+#pragma unroll
+    for (int i = 0; i < NE; ++i) {
+      const int o = tid + 64 * NW * i, m = o / SK_NB, cl = n0 + (o - m * SK_NB);
+      const bool ok = o < 16 * MT * SK_NB && m < a.M && cl < a.N;
+      pb[i] = ok && e.bias ? e.bias[cl] : 0.f;
+      pr[i] = ok && e.res ? ((const float*)e.res)[(int64_t)m * e.ldr + cl] : 0.f;
+    }
+  }
   const bool cok = col < a.N;
   const float* Wr = (const float*)a.B + (int64_t)min(col, a.N - 1) * a.ldb + 4 * g;
   const float* Ar[MT];
@@ -596,7 +618,8 @@ __global__ __launch_bounds__(64 * SKM_WAVES) void skinny_mma_kernel(DenseArgs a,
   f32x4 acc[MT];
 #pragma unroll
   for (int t = 0; t < MT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int q0 = w; q0 < ng; q0 += NW * UNR) {
+  // LNP: exactly one pass for every wave (ng <= NW * UNR, host-checked), so all reach its barrier
+  for (int q0 = w; LNP ? q0 == w : q0 < ng; q0 += NW * UNR) {
     f32x4 b[UNR], x[UNR][MT];
 #pragma unroll
     for (int u = 0; u < UNR; ++u) {
@@ -607,12 +630,42 @@ __global__ __launch_bounds__(64 * SKM_WAVES) void skinny_mma_kernel(DenseArgs a,
 #pragma unroll
       for (int t = 0; t < MT; ++t) x[u][t] = (ok && rok[t]) ? *(const f32x4*)(Ar[t] + k) : f32x4{0.f, 0.f, 0.f, 0.f};
     }
+    if constexpr (LNP) {       // the batch holds the chunk's rows: chunk mean and M2 per row
+      const float inv_n = 1.f / (float)(kend - kbeg);
+#pragma unroll
+      for (int t = 0; t < MT; ++t) {
+        float s1 = 0.f;
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) s1 += (x[u][t][0] + x[u][t][1]) + (x[u][t][2] + x[u][t][3]);
+        s1 += __shfl_xor(s1, 16, 64);
+        s1 += __shfl_xor(s1, 32, 64);
+        if (g == 0) st1[w][16 * t + c] = s1;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int t = 0; t < MT; ++t) {
+        float sm = 0.f;
+#pragma unroll
+        for (int v = 0; v < NW; ++v) sm += st1[v][16 * t + c];
+        const float mu = sm * inv_n;
+        float s2 = 0.f;
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) {
+          if (q0 + NW * u >= ng) continue;
+#pragma unroll
+          for (int e2 = 0; e2 < 4; ++e2) { const float d = x[u][t][e2] - mu; s2 += d * d; }
+        }
+        s2 += __shfl_xor(s2, 16, 64);
+        s2 += __shfl_xor(s2, 32, 64);
+        if (g == 0) st2[w][16 * t + c] = s2;
+      }
+    }
 #pragma unroll
     for (int u = 0; u < UNR; ++u)
 #pragma unroll
       for (int t = 0; t < MT; ++t)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(x[u][t][e], b[u][e], acc[t], 0, 0, 0);
+        for (int e2 = 0; e2 < 4; ++e2) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(x[u][t][e2], b[u][e2], acc[t], 0, 0, 0);
   }
   // acc[t][r] = this wave's partial of y[16t + 4g + r][n0 + c]; the waves' in a fixed order
 #pragma unroll
@@ -620,17 +673,61 @@ __global__ __launch_bounds__(64 * SKM_WAVES) void skinny_mma_kernel(DenseArgs a,
 #pragma unroll
     for (int r = 0; r < 4; ++r) red[w][16 * t + 4 * g + r][c] = acc[t][r];
   __syncthreads();
+  // row statistics of this chunk (LNP): mean and M2 over the waves' partials in a fixed order
+  auto chunk_stats = [&](int m, float& mean, float& m2) {
+    float sm = 0.f, sq = 0.f;
+#pragma unroll
+    for (int v = 0; v < NW; ++v) { sm += st1[v][m]; sq += st2[v][m]; }
+    mean = sm / (float)(kend - kbeg);
+    m2 = sq;
+  };
+  auto epi = [&](int i, int m, int cl, float v) {
+    if (fast) {                // epi_elems' arithmetic, operands already in registers
+      float y = e.alpha * v;
+      if (e.bias) y += pb[i];
+      y = act_fwd_t<float>(e.act, y);
+      if (e.res) y += pr[i];
+      ((OutT*)e.C)[(int64_t)m * e.ldc + cl] = from_f<OutT>(y);
+    } else {
+      epi_elems<float, OutT, 1>(a.e, m, cl, &v);
+    }
+  };
+  if (!part) {
+#pragma unroll
+    for (int i = 0; i < NE; ++i) {
+      const int o = tid + 64 * NW * i;
+      if (o >= 16 * MT * SK_NB) break;
+      const int m = o / SK_NB, cc = o - m * SK_NB, cl = n0 + cc;
+      if (m < a.M && cl < a.N) {
+        float v = (red[0][m][cc] + red[1][m][cc]) + (red[2][m][cc] + red[3][m][cc]);
+        v += (red[4][m][cc] + red[5][m][cc]) + (red[6][m][cc] + red[7][m][cc]);
+        if constexpr (LNP) {
+          float mean, m2;
+          chunk_stats(m, mean, m2);
+          v = (1.f / sqrtf(m2 / (float)a.K + a.ln_eps)) * (v - mean * a.ln_c1[cl]);
+        }
+        epi(i, m, cl, v);
+      }
+    }
+    return;
+  }
   for (int o = tid; o < 16 * MT * SK_NB; o += 64 * NW) {
     const int m = o / SK_NB, cc = o - m * SK_NB, cl = n0 + cc;
     if (m < a.M && cl < a.N) {
       float v = (red[0][m][cc] + red[1][m][cc]) + (red[2][m][cc] + red[3][m][cc]);
       v += (red[4][m][cc] + red[5][m][cc]) + (red[6][m][cc] + red[7][m][cc]);
-      if (part) __hip_atomic_store(&part[((int64_t)blockIdx.y * a.M + m) * a.N + cl], v, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-      else epi_elems<float, OutT, 1>(a.e, m, cl, &v);
+      __hip_atomic_store(&part[((int64_t)blockIdx.y * a.M + m) * a.N + cl], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
-  if (!part) return;
+  if constexpr (LNP) {         // this chunk's (mean, M2) per row, per column block and split
+    if (tid < a.M) {
+      float mean, m2;
+      chunk_stats(tid, mean, m2);
+      float* sp = a.lnst + (((int64_t)blockIdx.x * gridDim.y + blockIdx.y) * a.M + tid) * 2;
+      __hip_atomic_store(sp, mean, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(sp + 1, m2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave: its partials are out
   __syncthreads();
   if (tid == 0)
@@ -638,14 +735,36 @@ __global__ __launch_bounds__(64 * SKM_WAVES) void skinny_mma_kernel(DenseArgs a,
   __syncthreads();
   if (!last) return;
   const int S = gridDim.y;
+  if constexpr (LNP) {         // combine the S chunks' (n, mean, M2) in split order
+    if (tid < a.M) {
+      const float* sp = a.lnst + ((int64_t)blockIdx.x * S * a.M + tid) * 2;
+      float n = 0.f, mean = 0.f, m2 = 0.f;
+      for (int q = 0; q < S; ++q) {
+        const float nq = (float)(min(a.K, (q + 1) * kchunk) - q * kchunk);
+        const float mq = __hip_atomic_load(sp + (int64_t)q * a.M * 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const float vq = __hip_atomic_load(sp + (int64_t)q * a.M * 2 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const float nn = n + nq, d = mq - mean;
+        mean += d * (nq / nn);
+        m2 += vq + d * d * (n * nq / nn);
+        n = nn;
+      }
+      rmean[tid] = mean;
+      rrstd[tid] = 1.f / sqrtf(m2 / (float)a.K + a.ln_eps);
+    }
+    __syncthreads();
+  }
   const int64_t MN = (int64_t)a.M * a.N;
-  for (int o = tid; o < 16 * MT * SK_NB; o += 64 * NW) {
+#pragma unroll
+  for (int i = 0; i < NE; ++i) {
+    const int o = tid + 64 * NW * i;
+    if (o >= 16 * MT * SK_NB) break;
     const int m = o / SK_NB, cc = o - m * SK_NB, cl = n0 + cc;
     if (m < a.M && cl < a.N) {
       const float* pp = part + (int64_t)m * a.N + cl;
       float v = __hip_atomic_load(pp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      for (int s = 1; s < S; ++s) v += __hip_atomic_load(pp + s * MN, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      epi_elems<float, OutT, 1>(a.e, m, cl, &v);
+      for (int q = 1; q < S; ++q) v += __hip_atomic_load(pp + q * MN, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if constexpr (LNP) v = rrstd[m] * (v - rmean[m] * a.ln_c1[cl]);
+      epi(i, m, cl, v);
     }
   }
   if (tid == 0) __hip_atomic_store(&cnt[blockIdx.x], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -663,12 +782,14 @@ int skinny_splits(int N, int K, int& kchunk) {
   return (K + kchunk - 1) / kchunk;
 }
 
-// the matrix-core kernel's split: none unless K >= 4096 over fewer than 128 column blocks (then
-// 1024-k chunks, at most 4): every other decoder linear is one load round trip per workgroup
+// the matrix-core kernel's split: enough K chunks for N/16 x S >= 256 workgroups (every CU pulls
+// weights from HBM) and chunks of <= 1024 k (one load batch), chunks of >= 256 k, the partials
+// plus the LayerNorm chunk statistics within AVSR_SKINNY_WS
 int skinny_mma_splits(int N, int K, int& kchunk) {
   const int nb = (N + SK_NB - 1) / SK_NB;
-  int S = (nb < 128 && K >= 4096) ? std::min(4, K / 1024) : 1;
-  S = std::min(S, (int)std::max<int64_t>(1, AVSR_SKINNY_WS / (64 * (int64_t)N)));
+  int S = std::max((256 + nb - 1) / nb, (K + 1023) / 1024);
+  S = std::min(S, std::max(1, K / 256));
+  while (S > 1 && (int64_t)S * 64 * N + (int64_t)nb * S * 64 * 2 > AVSR_SKINNY_WS) --S;
   kchunk = ((K + S - 1) / S + 15) / 16 * 16;
   return (K + kchunk - 1) / kchunk;
 }
@@ -687,9 +808,29 @@ int skinny_launch(const DenseArgs& a, float* ws, hipStream_t st) {
   const int nb = (a.N + SK_NB - 1) / SK_NB;
   if (S > 1 && nb > AVSR_SKINNY_CNT) return AVSR_E_SHAPE;
   const dim3 g((unsigned)nb, (unsigned)S);
+  const int unr = nb * S > 256 ? 4 : 8;
+  if (a.ln_c1) {                       // LayerNorm prologue: fp32, every chunk one load batch
+    if (!(sizeof(T) == 4 && mma && kchunk <= SKM_WAVES * unr * 16 && !a.e.bwd && !a.e.preact &&
+          a.e.drop_p == 0.f && a.e.beta == 0.f && !a.e.atomic))
+      return AVSR_E_ARG;
+    if constexpr (sizeof(T) == 4) {
+      DenseArgs al = a;
+      al.lnst = S > 1 ? ws + (int64_t)S * a.M * a.N : nullptr;   // chunk statistics after the partials
+#define SKL_LN(T_) do { if (unr == 4) hipLaunchKernelGGL((skinny_mma_kernel<OutT, T_, 4, true>), g, dim3(64 * SKM_WAVES), 0, st, al, part, kchunk, cnt); \
+                        else hipLaunchKernelGGL((skinny_mma_kernel<OutT, T_, 8, true>), g, dim3(64 * SKM_WAVES), 0, st, al, part, kchunk, cnt); } while (0)
+      if (a.M <= 16) SKL_LN(1);
+      else if (a.M <= 32) SKL_LN(2);
+      else if (a.M <= 48) SKL_LN(3);
+      else SKL_LN(4);
+#undef SKL_LN
+      AVSR_CHECK_LAUNCH();
+      return 0;
+    }
+  }
   if constexpr (sizeof(T) == 4) {       // fp32: the matrix-core form (16-byte rows, 16-k groups)
     if (mma) {
-#define SKM(T_) hipLaunchKernelGGL((skinny_mma_kernel<OutT, T_>), g, dim3(64 * SKM_WAVES), 0, st, a, part, kchunk, cnt)
+#define SKM(T_) do { if (unr == 4) hipLaunchKernelGGL((skinny_mma_kernel<OutT, T_, 4>), g, dim3(64 * SKM_WAVES), 0, st, a, part, kchunk, cnt); \
+                      else hipLaunchKernelGGL((skinny_mma_kernel<OutT, T_, 8>), g, dim3(64 * SKM_WAVES), 0, st, a, part, kchunk, cnt); } while (0)
       if (a.M <= 16) SKM(1);
       else if (a.M <= 32) SKM(2);
       else if (a.M <= 48) SKM(3);
@@ -781,6 +922,8 @@ extern "C" int avsr_gemm(const avsr_gemm_params* p, void* stream) {
   a.sC = p->strideC; a.sR = p->strideR;
   a.stamp = p->stamp;
   a.cnt = nullptr; a.fC = nullptr; a.fldc = 0; a.falpha = 1.f; a.fbeta = 0.f;
+  a.ln_c1 = p->ln_c1; a.ln_eps = p->ln_eps; a.lnst = nullptr;
+  if (p->ln_c1 && (p->dtype != AVSR_F32 || p->M > 64 || splits > 1)) return AVSR_E_ARG;
   Epi& e = a.e;
   e.M = p->M; e.N = p->N; e.C = p->C; e.ldc = p->ldc;
   e.alpha = p->alpha; e.beta = p->beta; e.bias = p->bias;
@@ -807,6 +950,7 @@ extern "C" int avsr_gemm(const avsr_gemm_params* p, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   if (p->K == 0) return AVSR_E_SHAPE;
   int rc;
+  if (p->ln_c1 && (glds || slab || !skinny_ok(p, splits))) return AVSR_E_ARG;   // the prologue is the few-row kernel's
   if (!glds && !slab && skinny_ok(p, splits)) {
     float* sws = p->skinny_ws;          // optional K-split partials (AVSR_SKINNY_WS floats)
     if (p->dtype == AVSR_F32) return skinny_launch<float, float>(a, sws, st);

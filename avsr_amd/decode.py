@@ -30,6 +30,8 @@ import torch
 from . import ops
 
 LOGZERO = -10000000000.0
+# fp32 decode: LayerNorms folded into the linears they feed (the few-row kernel's LN prologue)
+FOLD_LN = True
 D_END = np.log(1 * np.exp(-10))          # end_detect's threshold (e2e_asr_common.py:18)
 
 
@@ -102,28 +104,42 @@ class BatchBeamSearch:
         x = eng._e(R, D)
         ops.embed_fwd(st["tok"], eng.w("decoder.embed.0.weight"), eng._pe, math.sqrt(D), x, 1, pe_row=pos)
         Tm = st["Tm"]
+        fold = st.get("fold")
         for i in range(eng.dl):
             p = f"decoder.decoders.{i}."
             sa, ca, ff = p + "self_attn.", p + "src_attn.", p + "feed_forward."
-            n1, _, _ = ops.layernorm_fwd(x, ar.master(p + "norm1.weight"), ar.master(p + "norm1.bias"), 1e-12)
-            qkv = ops.linear_fwd(n1, ar.span([sa + "linear_q.weight", sa + "linear_k.weight", sa + "linear_v.weight"]),
-                                 ar.span([sa + "linear_q.bias", sa + "linear_k.bias", sa + "linear_v.bias"], buf="master"))
+            if fold is not None:       # norm1 folded into the QKV linear (one launch)
+                Wg, bb, c1 = fold[i]["qkv"]
+                qkv = ops.linear_fwd(x, Wg, bb, ln=(c1, 1e-12))
+            else:
+                n1, _, _ = ops.layernorm_fwd(x, ar.master(p + "norm1.weight"), ar.master(p + "norm1.bias"), 1e-12)
+                qkv = ops.linear_fwd(n1, ar.span([sa + "linear_q.weight", sa + "linear_k.weight", sa + "linear_v.weight"]),
+                                     ar.span([sa + "linear_q.bias", sa + "linear_k.bias", sa + "linear_v.bias"],
+                                             buf="master"))
             kc, vc = cache[i, 0], cache[i, 1]               # (Lmax * R, D): rows step * R + r
             ops.beam_kv_put(qkv, kc, vc, pos, R, D)
             o1 = eng._e(R, D)
             ops.dec_attn(qkv[:, :D], kc, vc, o1, n=R, H=H, klen_max=st["Lmax"], k_bstride=0, v_bstride=0,
                          klen=st["klen_self"], kmap=anc)
             y1 = ops.linear_fwd(o1, eng.w(sa + "linear_out.weight"), ar.master(sa + "linear_out.bias"), res=x)
-            n2, _, _ = ops.layernorm_fwd(y1, ar.master(p + "norm2.weight"), ar.master(p + "norm2.bias"), 1e-12)
-            q2 = ops.linear_fwd(n2, eng.w(ca + "linear_q.weight"), ar.master(ca + "linear_q.bias"))
+            if fold is not None:
+                Wg, bb, c1 = fold[i]["q2"]
+                q2 = ops.linear_fwd(y1, Wg, bb, ln=(c1, 1e-12))
+            else:
+                n2, _, _ = ops.layernorm_fwd(y1, ar.master(p + "norm2.weight"), ar.master(p + "norm2.bias"), 1e-12)
+                q2 = ops.linear_fwd(n2, eng.w(ca + "linear_q.weight"), ar.master(ca + "linear_q.bias"))
             o2 = eng._e(R, D)
             kv = st["mem"][i]
             ops.dec_attn(q2, kv[:, :D], kv[:, D:], o2, n=R, H=H, klen_max=Tm, k_bstride=Tm * kv.stride(0),
                          v_bstride=Tm * kv.stride(0), kidx=st["uidx"], klen=st["klen_mem"],
-                         group=self.beam_size if self.beam_size <= 8 else 1)
+                         group=self.beam_size if self.beam_size <= 8 else 1, ksplit=2)
             y2 = ops.linear_fwd(o2, eng.w(ca + "linear_out.weight"), ar.master(ca + "linear_out.bias"), res=y1)
-            n3, _, _ = ops.layernorm_fwd(y2, ar.master(p + "norm3.weight"), ar.master(p + "norm3.bias"), 1e-12)
-            a = ops.linear_fwd(n3, eng.w(ff + "w_1.weight"), ar.master(ff + "w_1.bias"), act=ops.L.ACT_RELU)
+            if fold is not None:
+                Wg, bb, c1 = fold[i]["ff1"]
+                a = ops.linear_fwd(y2, Wg, bb, act=ops.L.ACT_RELU, ln=(c1, 1e-12))
+            else:
+                n3, _, _ = ops.layernorm_fwd(y2, ar.master(p + "norm3.weight"), ar.master(p + "norm3.bias"), 1e-12)
+                a = ops.linear_fwd(n3, eng.w(ff + "w_1.weight"), ar.master(ff + "w_1.bias"), act=ops.L.ACT_RELU)
             x = ops.linear_fwd(a, eng.w(ff + "w_2.weight"), ar.master(ff + "w_2.bias"), res=y2)
         yn, _, _ = ops.layernorm_fwd(x, ar.master("decoder.after_norm.weight"), ar.master("decoder.after_norm.bias"),
                                      1e-12)
@@ -133,6 +149,29 @@ class BatchBeamSearch:
         logp = torch.empty(R, eng.V, device=eng.device, dtype=torch.float32)
         # log-probs and the pre-beam (top-P decoder tokens per row) in one pass
         return ops.log_softmax_topk(logits, eng.V, logp, self.pre_beam_size, st["ids"])
+
+    def _fold_layernorms(self, eng):
+        """fp32 decode: each decoder layer's norm1 / norm2 / norm3 folded into the linear it feeds
+        (QKV, cross-attention query, FFN w_1): ops.fold_layernorm weights for the few-row kernel's
+        LayerNorm prologue (one launch instead of two per pair). Prepared per search (the weights may
+        have changed since the last one); None where the prologue does not apply (bf16, D > 1024)."""
+        if eng.dtype != torch.float32 or eng.dD > 1024 or eng.dD % 16:
+            return None
+        ar = eng.arena
+        out = []
+        for i in range(eng.dl):
+            p = f"decoder.decoders.{i}."
+            sa, ca, ff = p + "self_attn.", p + "src_attn.", p + "feed_forward."
+
+            def f(W, b, n):
+                return ops.fold_layernorm(W, b, ar.master(n + ".weight"), ar.master(n + ".bias"))
+            out.append(dict(
+                qkv=f(ar.span([sa + "linear_q.weight", sa + "linear_k.weight", sa + "linear_v.weight"]),
+                      ar.span([sa + "linear_q.bias", sa + "linear_k.bias", sa + "linear_v.bias"], buf="master"),
+                      p + "norm1"),
+                q2=f(eng.w(ca + "linear_q.weight"), ar.master(ca + "linear_q.bias"), p + "norm2"),
+                ff1=f(eng.w(ff + "w_1.weight"), ar.master(ff + "w_1.bias"), p + "norm3")))
+        return out
 
     def _step(self, eng, st, first, k):
         """one search step on the device (no host sync): decoder, pre-beam, CTC prefix scores,
@@ -236,7 +275,7 @@ class BatchBeamSearch:
             end_flag=torch.zeros(steps, R, **i32), end_score=torch.zeros(steps, R, **f32),
             end_dec=torch.zeros(steps, R, **f64), end_ctc=torch.zeros(steps, R, **f64),
             best_len=torch.full((U, Lmax + 3), float("-inf"), **f32), best_end=torch.full((U,), float("-inf"), **f32),
-            done=torch.zeros(U + 1, **i32))
+            done=torch.zeros(U + 1, **i32), fold=self._fold_layernorms(eng) if FOLD_LN else None)
         self._step(eng, st, True, 0)           # step 0: CTC state from scratch; reads ancestry 0, writes 1
         if steps > 1:
             graphs = self._capture(eng, st)

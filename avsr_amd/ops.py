@@ -66,10 +66,11 @@ def _skinny_ws(device):
 def gemm(A, B, C, *, M, N, K, a_kmajor, b_kmajor, lda, ldb, ldc, batch=1,
          strideA=0, strideB=0, strideC=0, alpha=1.0, beta=0.0, bias=None, act=L.ACT_NONE,
          epi_bwd=False, preact=None, res=None, ldr=None, strideR=0, gate=None, drop_p=0.0, seed=0,
-         splitk=1, ws=None, db=None, db_ws=None, skinny_split=None):
+         splitk=1, ws=None, db=None, db_ws=None, skinny_split=None, ln_c1=None, ln_eps=0.0):
     """Raw GEMM launch: C[b,m,n] = epi(alpha * sum_k A(b,m,k) B(b,n,k)). See avsr_hip.h.
     skinny_split: few-row launches (M <= 64) split K over skinny_splits(N, K) workgroup rows
-    (None: the module default SKINNY_SPLIT)."""
+    (None: the module default SKINNY_SPLIT). ln_c1 / ln_eps: LayerNorm prologue of the fp32
+    few-row kernel (A = LayerNorm input, B = gamma o W, ln_c1 = B's row sums)."""
     lib = L.load()
     assert A.is_cuda and B.is_cuda and C.is_cuda
     assert A.dtype == B.dtype, "A/B dtype mismatch"
@@ -105,6 +106,9 @@ def gemm(A, B, C, *, M, N, K, a_kmajor, b_kmajor, lda, ldb, ldc, batch=1,
         p.skinny_ws = _skinny_ws(A.device).data_ptr()   # K-split partials of the few-row vector-ALU path
     elif ws is not None and splitk > 1 and SLAB_FUSED_REDUCE:
         p.skinny_ws = _skinny_ws(A.device).data_ptr()   # arrival counters: in-kernel slab reduction
+    if ln_c1 is not None:
+        assert ln_c1.dtype == torch.float32 and ln_c1.numel() >= N and dt == L.AVSR_F32
+        p.ln_c1, p.ln_eps = ln_c1.data_ptr(), float(ln_eps)
     if db is not None:
         assert db.dtype == torch.float32 and db.numel() >= N and db_ws is not None and db_ws.dtype == torch.float32
         assert db_ws.numel() >= ((M + 63) // 64) * N
@@ -132,8 +136,10 @@ def gemm(A, B, C, *, M, N, K, a_kmajor, b_kmajor, lda, ldb, ldc, batch=1,
 # ---------------------------------------------------------------------------------------
 
 def linear_fwd(x, W, bias=None, *, act=L.ACT_NONE, preact=None, res=None, drop_p=0.0, seed=0, out=None,
-               skinny_split=None):
-    """y = dropout(act(x W^T + b)) + res ; optionally stores h = x W^T + b into `preact`."""
+               skinny_split=None, ln=None):
+    """y = dropout(act(x W^T + b)) + res ; optionally stores h = x W^T + b into `preact`.
+    ln = (c1, eps): x is the input of a LayerNorm folded into this linear (fold_layernorm):
+    y = act(LayerNorm(x) W0^T + b0) + res with W = gamma o W0, b = W0 beta + b0."""
     M, K = x.shape
     N = W.shape[0]
     assert W.shape[1] == K and x.stride(1) == 1 and W.stride(1) == 1
@@ -141,8 +147,18 @@ def linear_fwd(x, W, bias=None, *, act=L.ACT_NONE, preact=None, res=None, drop_p
         out = torch.empty(M, N, device=x.device, dtype=x.dtype)
     gemm(x, W, out, M=M, N=N, K=K, a_kmajor=True, b_kmajor=True, lda=x.stride(0), ldb=W.stride(0),
          ldc=out.stride(0), bias=bias, act=act, preact=preact, res=res,
-         ldr=None if res is None else res.stride(0), drop_p=drop_p, seed=seed, skinny_split=skinny_split)
+         ldr=None if res is None else res.stride(0), drop_p=drop_p, seed=seed, skinny_split=skinny_split,
+         ln_c1=None if ln is None else ln[0], ln_eps=0.0 if ln is None else ln[1])
     return out
+
+
+def fold_layernorm(W, b, gamma, beta):
+    """weights of LayerNorm(gamma, beta) followed by Linear(W, b) for linear_fwd(ln=...):
+    (gamma o W, W beta + b, row sums of gamma o W); the sums in fp64 (one-time weight preparation)"""
+    Wg = (W * gamma.unsqueeze(0)).contiguous()
+    bb = (W.double() @ beta.double() + (0 if b is None else b.double())).float()
+    c1 = Wg.double().sum(1).float()
+    return Wg, bb, c1
 
 
 def linear_dgrad(dy, W, *, gate=None, act=L.ACT_NONE, drop_p=0.0, seed=0, out=None, beta=0.0, db=None):
@@ -743,16 +759,33 @@ def log_softmax_rows(x, V, out):
     return out
 
 
+_DA_WS = {}
+
+
 def dec_attn(q, k, v, o, *, n, H, klen_max, k_bstride, v_bstride, klen=None, scale=0.125, kidx=None, kmap=None,
-             group=1):
+             group=1, ksplit=1):
     """one query per hypothesis: q/o rows i (ld = stride(0)), keys j of hypothesis i at
     k[b*k_bstride + j*k.stride(-2)] with b = kidx[i] (kidx None: b = i; bstride 0: shared keys);
     kmap (int32 [n][ldmap]): key j of hypothesis i is row kmap[i][j] of k instead; group: runs of
-    `group` hypotheses share their key block and klen (one read of each row for all of them)."""
+    `group` hypotheses share their key block and klen (one read of each row for all of them);
+    ksplit: up to ksplit workgroups per (group, head) over the keys, merged by the last to arrive
+    (per-stream partial buffer; the arrival counters of the few-row GEMM workspace)."""
+    ws = cnt = None
+    if ksplit > 1:
+        G = max(1, group)
+        slots = (n + G - 1) // G * H
+        assert slots <= SKINNY_CNT
+        key = (q.device, L.stream_ptr().value)
+        need = slots * ksplit * G * 66
+        ws = _DA_WS.get(key)
+        if ws is None or ws.numel() < need:
+            ws = _DA_WS[key] = torch.empty(need, device=q.device, dtype=torch.float32)
+        cnt = _skinny_ws(q.device)[SKINNY_WS:]
     _call("avsr_dec_attn", L.fill(L.DecAttnParams, dtype=dtype_code(q), n=n, H=H, klen_max=klen_max, scale=scale,
                                    q=q, ldq=q.stride(0), k=k, ldk=k.stride(-2), k_bstride=k_bstride, v=v,
                                    ldv=v.stride(-2), v_bstride=v_bstride, klen=klen, o=o, ldo=o.stride(0),
-                                   kidx=kidx, kmap=kmap, ldmap=0 if kmap is None else kmap.stride(0), group=group))
+                                   kidx=kidx, kmap=kmap, ldmap=0 if kmap is None else kmap.stride(0), group=group,
+                                   ksplit=ksplit, ws=ws, cnt=cnt))
     return o
 
 

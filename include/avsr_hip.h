@@ -94,6 +94,14 @@ typedef struct {
                                 with ws, both operands r-contiguous, fp32 C, plain epilogue): its
                                 counters let the last-arriving split of each output tile reduce
                                 the slabs in the GEMM itself (no separate reduction pass) */
+  const float* ln_c1;        /* optional LayerNorm prologue (fp32, M <= 64, K <= 1024, K % 16 == 0,
+                                unsplit): A holds the LayerNorm inputs x and B = gamma o W (W's
+                                columns scaled by the LayerNorm weight); per row the kernel takes
+                                mean and 1/sqrt(var + ln_eps) of x and computes
+                                C = epilogue(rstd * (x B^T - mean * ln_c1[n])) with ln_c1[n] =
+                                sum_k B[n][k] and bias = W beta + b — LayerNorm followed by the
+                                linear (decoder.py:98-134 norm1/2/3 + linear) in one launch */
+  float ln_eps;
 } avsr_gemm_params;
 #define AVSR_GEMM_COLSUM_WS(M, N) ((int64_t)(((M) + 63) / 64) * (N))
 /* slabs are AVSR_GEMM_SLAB_PAD floats apart beyond M*N: power-of-two slab strides put the
@@ -520,6 +528,13 @@ typedef struct {
                                  key block and klen (kidx / klen equal within a group, no kmap; the
                                  beams of one utterance over its memory): one workgroup reads each
                                  key / value row once for all of them */
+  int ksplit;                 /* >= 2: a workgroup row's keys split over up to ksplit workgroups
+                                 (min(ksplit, ceil(klen / 192)) of them: a function of the row's
+                                 klen only), each writing (max, sum, unnormalised o) partials to
+                                 ws; the last-arriving one (counter cnt[group][head], zeroed by
+                                 the caller once, left zero) merges them in split order. 0 / 1: none */
+  float* ws;                  /* ksplit >= 2: ceil(n / group) * H * ksplit * group * 66 floats */
+  unsigned* cnt;              /* ksplit >= 2: ceil(n / group) * H counters */
 } avsr_dec_attn_params;
 int avsr_dec_attn(const avsr_dec_attn_params* p, void* stream);
 

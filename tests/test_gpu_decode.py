@@ -173,33 +173,41 @@ def test_batched_decode_equals_per_utterance(g, model, beam):
         assert got[0][0].asdict()["yseq"] == g[f"yseq_b{beam}_0"].tolist()
 
 
-@pytest.mark.parametrize("G", [3, 5])
-def test_dec_attn_grouped_equals_single(G):
+@pytest.mark.parametrize("G,T,lens", [(3, 37, [37, 20, 5]), (5, 37, [37, 20, 5]), (5, 400, [400, 193, 150])])
+def test_dec_attn_grouped_equals_single(G, T, lens):
     """avsr_dec_attn with group = G (the beams of one utterance read each memory row once)
     equals the per-hypothesis launch bit for bit, with ragged key lengths per utterance, and
-    matches an fp64 softmax attention"""
+    matches an fp64 softmax attention; with ksplit = 2 (keys of rows >= 193 split over two
+    workgroups, merged by the last to arrive) grouped equals single too, and a row's result
+    does not depend on the other utterances in the launch"""
     from avsr_amd import ops
     dev = torch.device("cuda")
-    U, T, H = 3, 37, 4
+    U, H = 3, 4
     D = 64 * H
-    gen = torch.Generator().manual_seed(G)
+    gen = torch.Generator().manual_seed(G + T)
     mem = torch.randn(U * T, 2 * D, generator=gen).to(dev)
     q = torch.randn(U * G, D, generator=gen).to(dev)
     uidx = torch.arange(U * G, dtype=torch.int32).div(G, rounding_mode="floor").to(dev, torch.int32)
-    lens = [37, 20, 5]
     klen = torch.tensor([lens[u] for u in range(U) for _ in range(G)], dtype=torch.int32, device=dev)
-    outs = []
-    for grp in (1, G):
-        o = torch.empty(U * G, D, device=dev)
-        ops.dec_attn(q, mem[:, :D], mem[:, D:], o, n=U * G, H=H, klen_max=T, k_bstride=T * mem.stride(0),
-                     v_bstride=T * mem.stride(0), kidx=uidx, klen=klen, group=grp)
-        outs.append(o)
-    assert torch.equal(outs[0], outs[1])
     qd, md = q.double().cpu(), mem.double().cpu()
-    for i in range(U * G):
-        u = i // G
-        k = md[u * T:u * T + lens[u], :D].view(-1, H, 64)
-        v = md[u * T:u * T + lens[u], D:].view(-1, H, 64)
-        s = torch.einsum("hd,jhd->hj", qd[i].view(H, 64), k) * 0.125
-        ref = torch.einsum("hj,jhd->hd", torch.softmax(s, -1), v).reshape(D)
-        assert (outs[1][i].double().cpu() - ref).abs().max().item() < 1e-5
+    for ks in (1, 2):
+        outs = []
+        for grp in (1, G):
+            o = torch.empty(U * G, D, device=dev)
+            ops.dec_attn(q, mem[:, :D], mem[:, D:], o, n=U * G, H=H, klen_max=T, k_bstride=T * mem.stride(0),
+                         v_bstride=T * mem.stride(0), kidx=uidx, klen=klen, group=grp, ksplit=ks)
+            outs.append(o)
+        assert torch.equal(outs[0], outs[1])
+        # the last utterance alone (its own launch, smaller klen_max) gives the same rows
+        o1 = torch.empty(G, D, device=dev)
+        u = U - 1
+        ops.dec_attn(q[u * G:].contiguous(), mem[u * T:, :D], mem[u * T:, D:], o1, n=G, H=H, klen_max=lens[u],
+                     k_bstride=0, v_bstride=0, klen=klen[u * G:].contiguous(), group=G, ksplit=ks)
+        assert torch.equal(o1, outs[1][u * G:])
+        for i in range(U * G):
+            u = i // G
+            k = md[u * T:u * T + lens[u], :D].view(-1, H, 64)
+            v = md[u * T:u * T + lens[u], D:].view(-1, H, 64)
+            s = torch.einsum("hd,jhd->hj", qd[i].view(H, 64), k) * 0.125
+            ref = torch.einsum("hj,jhd->hd", torch.softmax(s, -1), v).reshape(D)
+            assert (outs[1][i].double().cpu() - ref).abs().max().item() < 1e-5

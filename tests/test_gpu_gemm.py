@@ -261,11 +261,11 @@ def test_skinny_k_split_rows_independent(dev, N, K, dtype):
     workgroup rows, fp32 partials reduced in a fixed order): S depends on dtype, N and K only, so
     every row equals the same row launched alone, bit for bit (batched beam search == per-utterance
     search relies on it); split and unsplit both match fp64. bf16 (vector-ALU kernel): >= 512
-    workgroups; fp32 (matrix-core kernel, 8 waves per workgroup): only K >= 4096 over < 128 column
-    blocks splits (the FFN w_2 shape)."""
+    workgroups; fp32 (matrix-core kernel, 8 waves per workgroup): >= 256 workgroups with K chunks of
+    256..1024."""
     S = ops.skinny_splits(N, K, dtype)
     if dtype == torch.float32:
-        assert S == (4 if (N, K) == (1024, 4096) else 1), (N, K, S)
+        assert S == {(1024, 4096): 4, (1024, 1024): 4, (4096, 1024): 1, (5056, 1024): 1, (256, 2048): 8}[(N, K)], (N, K, S)
     else:
         # the decoder's output layer (5056 columns) has no room for a split in AVSR_SKINNY_WS
         assert S == (1 if N == 5056 else {4096: 2}.get(N, S)) and (S > 1 or N == 5056), (N, K, S)
@@ -284,3 +284,30 @@ def test_skinny_k_split_rows_independent(dev, N, K, dtype):
     tol = 1e-6 if dtype == torch.float32 else 1e-2
     assert _rel(y, ref) < tol and _rel(y1, ref) < tol
     assert _rel(y, y1.double()) < (1e-6 if dtype == torch.float32 else 1e-2)
+
+
+@pytest.mark.parametrize("M,N,K", [(40, 3072, 1024), (10, 1024, 1024), (64, 4096, 1024), (1, 256, 256), (17, 100, 512),
+                                   (40, 1024, 1000 - 1000 % 16)])
+def test_skinny_layernorm_prologue(dev, M, N, K):
+    """LayerNorm folded into the following fp32 few-row linear (ops.fold_layernorm + the kernel's
+    LayerNorm prologue; the decoder's norm1/2/3 at decode time): vs LayerNorm then Linear in fp64,
+    inputs with a large common offset (the cancellation case of rstd * (x W'^T - mean * c1));
+    a row equals the same row launched alone, bit for bit."""
+    g = torch.Generator(device="cpu").manual_seed(M + N + K)
+    x = (torch.randn(M, K, generator=g) * 2 + 3).to(dev)
+    gam = (torch.rand(K, generator=g) + 0.5).to(dev)
+    bet = (torch.randn(K, generator=g) * 0.1).to(dev)
+    W = (torch.randn(N, K, generator=g) * K ** -0.5).to(dev)
+    b = torch.randn(N, generator=g).to(dev)
+    r = torch.randn(M, N, generator=g).to(dev)
+    Wg, bb, c1 = ops.fold_layernorm(W, b, gam, bet)
+    y = ops.linear_fwd(x, Wg, bb, act=L.ACT_RELU, res=r, ln=(c1, 1e-12))
+    y1 = ops.linear_fwd(x, Wg, bb, act=L.ACT_RELU, res=r, ln=(c1, 1e-12), skinny_split=False)
+    xd = x.double()
+    ln = (xd - xd.mean(1, keepdim=True)) / torch.sqrt(xd.var(1, unbiased=False, keepdim=True) + 1e-12)
+    ref = torch.relu((ln * gam.double() + bet.double()) @ W.double().t() + b.double()) + r.double()
+    assert _rel(y, ref) < 2e-6 and _rel(y1, ref) < 2e-6      # split (chunk statistics combined) / unsplit
+    for m in (0, M - 1):
+        one = ops.linear_fwd(x[m:m + 1].contiguous(), Wg, bb, act=L.ACT_RELU, res=r[m:m + 1].contiguous(),
+                             ln=(c1, 1e-12))
+        assert torch.equal(one[0], y[m]), m
