@@ -42,6 +42,7 @@ class GemmParams(ctypes.Structure):
         ("db_ws", _c_p),
         ("stamp", _c_p),
         ("skinny_ws", _c_p), ("ln_c1", _c_p), ("ln_eps", ctypes.c_float),
+        ("kv_k", _c_p), ("kv_v", _c_p), ("kv_pos", _c_p), ("kv_rows", _i),
     ]
 
 

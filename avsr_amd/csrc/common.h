@@ -26,15 +26,28 @@ struct alignas(16) v16 { uint32_t w[4]; };
 // hardware 2^x (v_exp_f32, ~1 ulp; no denormal-result fix-up): softmax / log-sum-exp inner loops
 AVSR_DEV float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
-AVSR_DEV float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+// Wave reductions on DPP row rotations (v_mov_b32_dpp row_ror: cross-lane moves inside each
+// 16-lane row, no LDS), then the four row results read as scalars (lanes 0 / 16 / 32 / 48) and
+// combined in a fixed order: the result is wave-uniform and deterministic. (A __shfl_xor
+// butterfly is six ds_bpermute round trips through the LDS unit on the reduction's dependent
+// chain.) Call in converged control flow, like the butterfly they replace.
+template <int R> AVSR_DEV float rorf(float x) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x120 + R, 0xf, 0xf, false));
 }
-AVSR_DEV float wave_max(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-  return v;
+template <int R> AVSR_DEV int rori(int x) { return __builtin_amdgcn_update_dpp(0, x, 0x120 + R, 0xf, 0xf, false); }
+AVSR_DEV float lanef(float x, int l) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), l)); }
+// sum over each 16-lane row (every lane of the row holds it; lanes may differ in the last bit)
+AVSR_DEV float row_sum16(float x) {
+  x += rorf<8>(x); x += rorf<4>(x); x += rorf<2>(x); x += rorf<1>(x);
+  return x;
+}
+AVSR_DEV float wave_sum(float x) {
+  x = row_sum16(x);
+  return (lanef(x, 0) + lanef(x, 16)) + (lanef(x, 32) + lanef(x, 48));
+}
+AVSR_DEV float wave_max(float x) {
+  x = fmaxf(x, rorf<8>(x)); x = fmaxf(x, rorf<4>(x)); x = fmaxf(x, rorf<2>(x)); x = fmaxf(x, rorf<1>(x));
+  return fmaxf(fmaxf(lanef(x, 0), lanef(x, 16)), fmaxf(lanef(x, 32), lanef(x, 48)));
 }
 
 // ---- counter-based dropout stream: keep(seed, idx) with P(keep) = 1 - p ------------

@@ -30,6 +30,24 @@ AVSR_DEV float lse2_fast(float a, float b) {
   return m + __logf(1.f + __expf(fminf(a, b) - m));
 }
 
+// Cross-lane reductions on DPP row rotations (common.h): the __shfl_xor butterflies they replace
+// are ds_bpermute round trips through the LDS unit (~2 us per block arg-max: the pre-beam's 7
+// rounds took 12 us of an 18 us kernel).
+// (value, index) arg-max over the wave, ties -> smaller index (a total order: exact, uniform)
+AVSR_DEV void dwave_argmax(float& v, int& i) {
+#define DA_STEP(R_) { const float ov = rorf<R_>(v); const int oi = rori<R_>(i); \
+                      if (ov > v || (ov == v && oi < i)) { v = ov; i = oi; } }
+  DA_STEP(8) DA_STEP(4) DA_STEP(2) DA_STEP(1)
+#undef DA_STEP
+  float bv = lanef(v, 0); int bi = __builtin_amdgcn_readlane(i, 0);
+#pragma unroll
+  for (int r = 1; r < 4; ++r) {
+    const float ov = lanef(v, 16 * r); const int oi = __builtin_amdgcn_readlane(i, 16 * r);
+    if (ov > bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
+  }
+  v = bv; i = bi;
+}
+
 AVSR_DEV float block_max256(float v, float* sh) {
   v = wave_max(v);
   if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
@@ -49,12 +67,7 @@ AVSR_DEV float block_sum256(float v, float* sh) {
 
 // (value, index) arg-max across the 256-thread block; ties -> smaller index
 AVSR_DEV void block_argmax256(float& v, int& i, float* shv, int* shi) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const float ov = __shfl_xor(v, o, 64);
-    const int oi = __shfl_xor(i, o, 64);
-    if (ov > v || (ov == v && oi < i)) { v = ov; i = oi; }
-  }
+  dwave_argmax(v, i);
   if ((threadIdx.x & 63) == 0) { shv[threadIdx.x >> 6] = v; shi[threadIdx.x >> 6] = i; }
   __syncthreads();
   v = shv[0]; i = shi[0];
@@ -154,8 +167,7 @@ __global__ __launch_bounds__(64 * DA_WAVES) void dec_attn_kernel(avsr_dec_attn_p
 #pragma unroll
       for (int g = 0; g < G; ++g) {
         float s = q[g][0] * k[u][0] + q[g][1] * k[u][1] + q[g][2] * k[u][2] + q[g][3] * k[u][3];
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1) s += __shfl_xor(s, o, 64);
+        s = row_sum16(s);               // over the key's 16 lanes (one DPP row)
         s *= p.scale;
         if (ok) {
           if ((lane & 15) == 0) sc[g * kpad + j] = s;

@@ -25,6 +25,7 @@ struct DenseArgs {
   float falpha, fbeta;
   const float* ln_c1; float ln_eps;   // skinny_mma_kernel LayerNorm prologue (avsr_gemm_params.ln_c1)
   float* lnst;                        // ... its per-chunk row statistics (split launches)
+  float* kvk; float* kvv; const int* kvpos; int kvrows;   // KV-cache append (avsr_gemm_params.kv_k)
 };
 
 template <typename T, typename OutT, int WM, int WN, bool AK, bool BK>
@@ -681,13 +682,20 @@ __global__ __launch_bounds__(64 * SKM_WAVES) void skinny_mma_kernel(DenseArgs a,
     mean = sm / (float)(kend - kbeg);
     m2 = sq;
   };
+  const int kvD = a.N / 3;
   auto epi = [&](int i, int m, int cl, float v) {
     if (fast) {                // epi_elems' arithmetic, operands already in registers
       float y = e.alpha * v;
       if (e.bias) y += pb[i];
       y = act_fwd_t<float>(e.act, y);
       if (e.res) y += pr[i];
-      ((OutT*)e.C)[(int64_t)m * e.ldc + cl] = from_f<OutT>(y);
+      if (a.kvk && cl >= kvD) {  // K / V columns: appended to the cache at this step's rows
+        const int64_t row = (int64_t)(*a.kvpos) * a.kvrows + m;
+        float* dst = cl < 2 * kvD ? a.kvk : a.kvv;
+        dst[row * kvD + (cl < 2 * kvD ? cl - kvD : cl - 2 * kvD)] = y;
+      } else {
+        ((OutT*)e.C)[(int64_t)m * e.ldc + cl] = from_f<OutT>(y);
+      }
     } else {
       epi_elems<float, OutT, 1>(a.e, m, cl, &v);
     }
@@ -809,6 +817,9 @@ int skinny_launch(const DenseArgs& a, float* ws, hipStream_t st) {
   if (S > 1 && nb > AVSR_SKINNY_CNT) return AVSR_E_SHAPE;
   const dim3 g((unsigned)nb, (unsigned)S);
   const int unr = nb * S > 256 ? 4 : 8;
+  if (a.kvk && !(sizeof(T) == 4 && mma && !a.e.bwd && !a.e.preact && a.e.drop_p == 0.f && a.e.beta == 0.f &&
+                 !a.e.atomic))
+    return AVSR_E_ARG;                   // the cache append is the matrix-core kernel's fast epilogue
   if (a.ln_c1) {                       // LayerNorm prologue: fp32, every chunk one load batch
     if (!(sizeof(T) == 4 && mma && kchunk <= SKM_WAVES * unr * 16 && !a.e.bwd && !a.e.preact &&
           a.e.drop_p == 0.f && a.e.beta == 0.f && !a.e.atomic))
@@ -923,6 +934,11 @@ extern "C" int avsr_gemm(const avsr_gemm_params* p, void* stream) {
   a.stamp = p->stamp;
   a.cnt = nullptr; a.fC = nullptr; a.fldc = 0; a.falpha = 1.f; a.fbeta = 0.f;
   a.ln_c1 = p->ln_c1; a.ln_eps = p->ln_eps; a.lnst = nullptr;
+  a.kvk = (float*)p->kv_k; a.kvv = (float*)p->kv_v; a.kvpos = p->kv_pos; a.kvrows = p->kv_rows;
+  if (p->kv_k && (p->dtype != AVSR_F32 || p->M > 64 || splits > 1 || (p->N % 3) || !p->kv_v || !p->kv_pos ||
+                  p->kv_rows < p->M))
+    return AVSR_E_ARG;
+  if (p->kv_k && (glds || slab || !skinny_ok(p, splits))) return AVSR_E_ARG;
   if (p->ln_c1 && (p->dtype != AVSR_F32 || p->M > 64 || splits > 1)) return AVSR_E_ARG;
   Epi& e = a.e;
   e.M = p->M; e.N = p->N; e.C = p->C; e.ldc = p->ldc;

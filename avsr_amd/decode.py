@@ -108,16 +108,16 @@ class BatchBeamSearch:
         for i in range(eng.dl):
             p = f"decoder.decoders.{i}."
             sa, ca, ff = p + "self_attn.", p + "src_attn.", p + "feed_forward."
-            if fold is not None:       # norm1 folded into the QKV linear (one launch)
+            kc, vc = cache[i, 0], cache[i, 1]               # (Lmax * R, D): rows step * R + r
+            if fold is not None:       # norm1 folded into the QKV linear, K / V appended to the cache (one launch)
                 Wg, bb, c1 = fold[i]["qkv"]
-                qkv = ops.linear_fwd(x, Wg, bb, ln=(c1, 1e-12))
+                qkv = ops.linear_fwd(x, Wg, bb, ln=(c1, 1e-12), kv=(kc, vc, pos, R))
             else:
                 n1, _, _ = ops.layernorm_fwd(x, ar.master(p + "norm1.weight"), ar.master(p + "norm1.bias"), 1e-12)
                 qkv = ops.linear_fwd(n1, ar.span([sa + "linear_q.weight", sa + "linear_k.weight", sa + "linear_v.weight"]),
                                      ar.span([sa + "linear_q.bias", sa + "linear_k.bias", sa + "linear_v.bias"],
                                              buf="master"))
-            kc, vc = cache[i, 0], cache[i, 1]               # (Lmax * R, D): rows step * R + r
-            ops.beam_kv_put(qkv, kc, vc, pos, R, D)
+                ops.beam_kv_put(qkv, kc, vc, pos, R, D)
             o1 = eng._e(R, D)
             ops.dec_attn(qkv[:, :D], kc, vc, o1, n=R, H=H, klen_max=st["Lmax"], k_bstride=0, v_bstride=0,
                          klen=st["klen_self"], kmap=anc)

@@ -66,7 +66,7 @@ def _skinny_ws(device):
 def gemm(A, B, C, *, M, N, K, a_kmajor, b_kmajor, lda, ldb, ldc, batch=1,
          strideA=0, strideB=0, strideC=0, alpha=1.0, beta=0.0, bias=None, act=L.ACT_NONE,
          epi_bwd=False, preact=None, res=None, ldr=None, strideR=0, gate=None, drop_p=0.0, seed=0,
-         splitk=1, ws=None, db=None, db_ws=None, skinny_split=None, ln_c1=None, ln_eps=0.0):
+         splitk=1, ws=None, db=None, db_ws=None, skinny_split=None, ln_c1=None, ln_eps=0.0, kv=None):
     """Raw GEMM launch: C[b,m,n] = epi(alpha * sum_k A(b,m,k) B(b,n,k)). See avsr_hip.h.
     skinny_split: few-row launches (M <= 64) split K over skinny_splits(N, K) workgroup rows
     (None: the module default SKINNY_SPLIT). ln_c1 / ln_eps: LayerNorm prologue of the fp32
@@ -109,6 +109,10 @@ def gemm(A, B, C, *, M, N, K, a_kmajor, b_kmajor, lda, ldb, ldc, batch=1,
     if ln_c1 is not None:
         assert ln_c1.dtype == torch.float32 and ln_c1.numel() >= N and dt == L.AVSR_F32
         p.ln_c1, p.ln_eps = ln_c1.data_ptr(), float(ln_eps)
+    if kv is not None:           # (k cache, v cache, device position, rows per step)
+        kc, vc, pos, rows = kv
+        assert kc.dtype == vc.dtype == torch.float32 and pos.dtype == torch.int32 and dt == L.AVSR_F32
+        p.kv_k, p.kv_v, p.kv_pos, p.kv_rows = kc.data_ptr(), vc.data_ptr(), pos.data_ptr(), int(rows)
     if db is not None:
         assert db.dtype == torch.float32 and db.numel() >= N and db_ws is not None and db_ws.dtype == torch.float32
         assert db_ws.numel() >= ((M + 63) // 64) * N
@@ -136,10 +140,12 @@ def gemm(A, B, C, *, M, N, K, a_kmajor, b_kmajor, lda, ldb, ldc, batch=1,
 # ---------------------------------------------------------------------------------------
 
 def linear_fwd(x, W, bias=None, *, act=L.ACT_NONE, preact=None, res=None, drop_p=0.0, seed=0, out=None,
-               skinny_split=None, ln=None):
+               skinny_split=None, ln=None, kv=None):
     """y = dropout(act(x W^T + b)) + res ; optionally stores h = x W^T + b into `preact`.
     ln = (c1, eps): x is the input of a LayerNorm folded into this linear (fold_layernorm):
-    y = act(LayerNorm(x) W0^T + b0) + res with W = gamma o W0, b = W0 beta + b0."""
+    y = act(LayerNorm(x) W0^T + b0) + res with W = gamma o W0, b = W0 beta + b0.
+    kv = (k_cache, v_cache, pos, rows): fused QKV projection whose K / V thirds are appended to the
+    caches at rows pos * rows + m (only the Q third is written to `out`)."""
     M, K = x.shape
     N = W.shape[0]
     assert W.shape[1] == K and x.stride(1) == 1 and W.stride(1) == 1
@@ -148,7 +154,7 @@ def linear_fwd(x, W, bias=None, *, act=L.ACT_NONE, preact=None, res=None, drop_p
     gemm(x, W, out, M=M, N=N, K=K, a_kmajor=True, b_kmajor=True, lda=x.stride(0), ldb=W.stride(0),
          ldc=out.stride(0), bias=bias, act=act, preact=preact, res=res,
          ldr=None if res is None else res.stride(0), drop_p=drop_p, seed=seed, skinny_split=skinny_split,
-         ln_c1=None if ln is None else ln[0], ln_eps=0.0 if ln is None else ln[1])
+         ln_c1=None if ln is None else ln[0], ln_eps=0.0 if ln is None else ln[1], kv=kv)
     return out
 
 

@@ -102,6 +102,14 @@ typedef struct {
                                 sum_k B[n][k] and bias = W beta + b — LayerNorm followed by the
                                 linear (decoder.py:98-134 norm1/2/3 + linear) in one launch */
   float ln_eps;
+  void* kv_k;                /* optional KV-cache append (fp32 few-row path, N % 3 == 0, D = N / 3):
+                                output columns [D, 2D) of row m go to kv_k row (*kv_pos * kv_rows +
+                                m) instead of C, columns [2D, 3D) to kv_v (the self-attention K / V
+                                cache of the device-side beam search; avsr_beam_kv_put fused into
+                                the QKV projection); columns [0, D) to C as usual */
+  void* kv_v;
+  const int* kv_pos;
+  int kv_rows;
 } avsr_gemm_params;
 #define AVSR_GEMM_COLSUM_WS(M, N) ((int64_t)(((M) + 63) / 64) * (N))
 /* slabs are AVSR_GEMM_SLAB_PAD floats apart beyond M*N: power-of-two slab strides put the

@@ -311,3 +311,33 @@ def test_skinny_layernorm_prologue(dev, M, N, K):
         one = ops.linear_fwd(x[m:m + 1].contiguous(), Wg, bb, act=L.ACT_RELU, res=r[m:m + 1].contiguous(),
                              ln=(c1, 1e-12))
         assert torch.equal(one[0], y[m]), m
+
+
+@pytest.mark.parametrize("ln", [False, True])
+def test_skinny_kv_cache_append(dev, ln):
+    """fused QKV projection of a decode step (kv=...): the Q third goes to the output, the K / V
+    thirds to the caches at rows pos * rows + m (pos read on the device), nothing else written;
+    equal bit for bit to the projection followed by the copy (avsr_beam_kv_put)."""
+    g = torch.Generator(device="cpu").manual_seed(11 + ln)
+    M, D, K, rows, Lmax = 40, 256, 512, 40, 6
+    x = (torch.randn(M, K, generator=g) + 1).to(dev)
+    W = (torch.randn(3 * D, K, generator=g) * K ** -0.5).to(dev)
+    b = torch.randn(3 * D, generator=g).to(dev)
+    lnarg = None
+    if ln:
+        W, b, c1 = ops.fold_layernorm(W, b, (torch.rand(K, generator=g) + 0.5).to(dev),
+                                      (torch.randn(K, generator=g) * 0.1).to(dev))
+        lnarg = (c1, 1e-12)
+    pos = torch.tensor([3], dtype=torch.int32, device=dev)
+    kc = torch.full((Lmax * rows, D), float("nan"), device=dev)
+    vc = torch.full((Lmax * rows, D), float("nan"), device=dev)
+    q = torch.full((M, 3 * D), float("nan"), device=dev)
+    ops.linear_fwd(x, W, b, out=q, ln=lnarg, kv=(kc, vc, pos, rows))
+    full = ops.linear_fwd(x, W, b, ln=lnarg)
+    kr, vr = torch.full_like(kc, float("nan")), torch.full_like(vc, float("nan"))
+    ops.beam_kv_put(full, kr, vr, pos, rows, D)
+    assert torch.equal(q[:, :D], full[:, :D])
+    assert torch.isnan(q[:, D:]).all()
+    assert torch.equal(kc[3 * rows:3 * rows + M], kr[3 * rows:3 * rows + M])
+    assert torch.equal(vc[3 * rows:3 * rows + M], vr[3 * rows:3 * rows + M])
+    assert torch.isnan(kc[:3 * rows]).all() and torch.isnan(kc[3 * rows + M:]).all()
