@@ -104,7 +104,7 @@ __global__ __launch_bounds__(CF::NTH, CF::MINB) void dense_glds_kernel(DenseArgs
 // from LDS, the others with sc1 loads), writes C = alpha*sum + beta*C — the arithmetic of
 // slab_reduce_kernel, which this replaces — and resets the counter (cdna_hip_programming.md
 // Guideline 16, counter form).
-template <class CF>
+template <class CF, bool FR = false>     // FR: the in-kernel slab reduction (its own register budget)
 __global__ __launch_bounds__(2 * CF::NTH, 1) void wgrad_dual_kernel(DenseArgs a, int tiles_m, int tiles_n) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   static_assert(CF::BM * (CF::BN + 4) * 4 <= 2 * CF::S * CF::STAGE, "reduction tile exceeds the two rings");
@@ -163,16 +163,18 @@ __global__ __launch_bounds__(2 * CF::NTH, 1) void wgrad_dual_kernel(DenseArgs a,
   __syncthreads();
   const bool slab = a.sSplit != 0;
   constexpr int Q = CF::BN / 4;                      // float4 per tile row
-  if (slab && a.cnt) {
+  if constexpr (FR) {
+    // 16-byte write-through (sc1) buffer stores / loads: the vector form of the agent-scope
+    // relaxed atomic store / load (global_store_dword ... sc1), one instruction per 4 columns
     float* W = (float*)a.e.C;                        // slab 0; split q's at W + q * sSplit
     const int64_t ldw = a.e.ldc;
+    const __amdgpu_buffer_rsrc_t rs = gemmg::make_rsrc(W, (uint32_t)((int64_t)a.splits * a.sSplit * 4));
     for (int c = threadIdx.x; c < CF::BM * Q; c += 2 * CF::NTH) {
       const int lr = c / Q, lc = (c % Q) * 4, row = m0 + lr, col = n0 + lc;
       if (row >= a.M || col >= a.N) continue;        // N % 4 == 0 in slab mode (host-checked)
       const f32x4 v = *(const f32x4*)(st + lr * LDR + lc);
-      float* o = W + sp * a.sSplit + (int64_t)row * ldw + col;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) __hip_atomic_store(o + q, v[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint32_t off = (uint32_t)((sp * a.sSplit + (int64_t)row * ldw + col) * 4);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i32, v), rs, off, 0, 16 /* sc1 */);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave: its partial is out
     __shared__ int last;
@@ -182,25 +184,58 @@ __global__ __launch_bounds__(2 * CF::NTH, 1) void wgrad_dual_kernel(DenseArgs a,
       last = __hip_atomic_fetch_add(&a.cnt[tile], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)a.splits - 1;
     __syncthreads();
     if (last) {
-      for (int c = threadIdx.x; c < CF::BM * Q; c += 2 * CF::NTH) {
-        const int lr = c / Q, lc = (c % Q) * 4, row = m0 + lr, col = n0 + lc;
-        if (row >= a.M || col >= a.N) continue;
-        const float* w = W + (int64_t)row * ldw + col;
-        const f32x4 own = *(const f32x4*)(st + lr * LDR + lc);
-        f32x4 sum;
-        for (int q = 0; q < a.splits; ++q) {
-          f32x4 v;
-          if (q == sp) v = own;
-          else {
+      // every load of the tail in flight at once (the tile's NI vectors per thread x the other
+      // splits, and C for beta), then the sums in split order
+      constexpr int NI = CF::BM * Q / (2 * CF::NTH), SMAX = 4;
+      static_assert(NI * 2 * CF::NTH == CF::BM * Q, "tile vectors per thread");
+      if (a.splits <= SMAX) {
+        f32x4 pv[NI][SMAX], cv[NI];
 #pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] = __hip_atomic_load(w + q * a.sSplit + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          }
-          if (q == 0) sum = v; else sum += v;
+        for (int i = 0; i < NI; ++i) {
+          const int c = threadIdx.x + i * 2 * CF::NTH;
+          const int lr = c / Q, lc = (c % Q) * 4, row = m0 + lr, col = n0 + lc;
+          const bool ok = row < a.M && col < a.N;
+          const int64_t w = (int64_t)row * ldw + col;
+#pragma unroll
+          for (int q = 0; q < SMAX; ++q)
+            if (ok && q < a.splits && q != sp)
+              pv[i][q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                             rs, (uint32_t)((q * a.sSplit + w) * 4), 0, 16 /* sc1 */));
+          if (ok && a.fbeta != 0.f) cv[i] = *(const f32x4*)(a.fC + (int64_t)row * a.fldc + col);
         }
-        float* o = a.fC + (int64_t)row * a.fldc + col;
-        f32x4 y = sum * a.falpha;
-        if (a.fbeta != 0.f) y += *(const f32x4*)o * a.fbeta;
-        *(f32x4*)o = y;
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+          const int c = threadIdx.x + i * 2 * CF::NTH;
+          const int lr = c / Q, lc = (c % Q) * 4, row = m0 + lr, col = n0 + lc;
+          if (row >= a.M || col >= a.N) continue;
+          const f32x4 own = *(const f32x4*)(st + lr * LDR + lc);
+          f32x4 sum = sp == 0 ? own : pv[i][0];
+#pragma unroll
+          for (int q = 1; q < SMAX; ++q)
+            if (q < a.splits) sum += (q == sp ? own : pv[i][q]);
+          f32x4 y = sum * a.falpha;
+          if (a.fbeta != 0.f) y += cv[i] * a.fbeta;
+          *(f32x4*)(a.fC + (int64_t)row * a.fldc + col) = y;
+        }
+      } else {
+        for (int c = threadIdx.x; c < CF::BM * Q; c += 2 * CF::NTH) {
+          const int lr = c / Q, lc = (c % Q) * 4, row = m0 + lr, col = n0 + lc;
+          if (row >= a.M || col >= a.N) continue;
+          const int64_t w = (int64_t)row * ldw + col;
+          const f32x4 own = *(const f32x4*)(st + lr * LDR + lc);
+          f32x4 sum;
+          for (int q = 0; q < a.splits; ++q) {
+            f32x4 v;
+            if (q == sp) v = own;
+            else v = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                         rs, (uint32_t)((q * a.sSplit + w) * 4), 0, 16 /* sc1 */));
+            if (q == 0) sum = v; else sum += v;
+          }
+          float* o = a.fC + (int64_t)row * a.fldc + col;
+          f32x4 y = sum * a.falpha;
+          if (a.fbeta != 0.f) y += *(const f32x4*)o * a.fbeta;
+          *(f32x4*)o = y;
+        }
       }
       if (threadIdx.x == 0) __hip_atomic_store(&a.cnt[tile], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
@@ -876,12 +911,17 @@ bool wgrad_dual_ok(const avsr_gemm_params* p, int splits, bool slab) {
          (p->ldc % 4) == 0 && avsr_aligned16(p->C);
 }
 
+template <class CF>
 int launch_wgrad_dual(const DenseArgs& a, hipStream_t st) {
-  const int tm = (a.M + CfgDual::BM - 1) / CfgDual::BM, tn = (a.N + CfgDual::BN - 1) / CfgDual::BN;
+  const int tm = (a.M + CF::BM - 1) / CF::BM, tn = (a.N + CF::BN - 1) / CF::BN;
   const long nwg = (long)tm * tn * a.splits;
   if (nwg > 0x7fffffffL) return AVSR_E_SHAPE;
-  hipLaunchKernelGGL((wgrad_dual_kernel<CfgDual>), dim3((unsigned)nwg), dim3(2 * CfgDual::NTH),
-                     2 * CfgDual::S * CfgDual::STAGE, st, a, tm, tn);
+  if (a.cnt)
+    hipLaunchKernelGGL((wgrad_dual_kernel<CF, true>), dim3((unsigned)nwg), dim3(2 * CF::NTH), 2 * CF::S * CF::STAGE,
+                       st, a, tm, tn);
+  else
+    hipLaunchKernelGGL((wgrad_dual_kernel<CF, false>), dim3((unsigned)nwg), dim3(2 * CF::NTH), 2 * CF::S * CF::STAGE,
+                       st, a, tm, tn);
   AVSR_CHECK_LAUNCH();
   return 0;
 }
@@ -974,12 +1014,13 @@ extern "C" int avsr_gemm(const avsr_gemm_params* p, void* stream) {
   }
   if (glds && wgrad_dual_ok(p, splits, slab)) {
     const int tiles = ((p->M + CfgDual::BM - 1) / CfgDual::BM) * ((p->N + CfgDual::BN - 1) / CfgDual::BN);
-    if (slab && p->skinny_ws && tiles <= AVSR_SKINNY_CNT) {   // in-kernel slab reduction (no slab_reduce pass)
+    if (slab && p->skinny_ws && tiles <= AVSR_SKINNY_CNT &&
+        (int64_t)splits * a.sSplit * 4 < (1ll << 31)) {   // in-kernel slab reduction (no slab_reduce pass)
       a.cnt = (unsigned*)(p->skinny_ws + AVSR_SKINNY_WS);
       a.fC = (float*)p->C; a.fldc = p->ldc; a.falpha = p->alpha; a.fbeta = p->beta;
-      return launch_wgrad_dual(a, st);
+      return launch_wgrad_dual<CfgDual>(a, st);
     }
-    rc = launch_wgrad_dual(a, st);
+    rc = launch_wgrad_dual<CfgDual>(a, st);
   }
   else if (glds) rc = p->c_f32 ? glds_by_layout<float>(p, a, st) : glds_by_layout<bf16>(p, a, st);
   else if (p->dtype == AVSR_F32) rc = by_tile<float, float>(p, a, st);

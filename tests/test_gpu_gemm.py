@@ -134,7 +134,8 @@ def test_gemm_layouts_bf16(dev, gemm_tile, a_kmajor, b_kmajor, M, N, K, splitk):
 
 
 @pytest.mark.parametrize("M,N,K,splitk", [(1024, 1024, 6000, 4), (3072, 1024, 6000, 1), (256, 384, 1000, 1),
-                                           (136, 200, 328, 1), (1024, 1024, 1000, 3), (640, 512, 64, 1)])
+                                           (136, 200, 328, 1), (1024, 1024, 1000, 3), (640, 512, 64, 1),
+                                           (1024, 1024, 6000, 1), (200, 136, 999, 1)])
 def test_wgrad_dual_kernel(dev, monkeypatch, M, N, K, splitk):
     """Weight-gradient GEMM dW[M][N] = beta*dW + alpha * dy^T x (both operands r-contiguous, the
     in-block split-K kernel: two wave groups per block over halves of the K range, one LDS
