@@ -106,7 +106,8 @@ def test_gemm_splitk(dev):
 
 
 @pytest.mark.parametrize("splitk", [0, 1, 3, 40])
-@pytest.mark.parametrize("case", [(40, 22, 22, 64, 64, 3, 1, 1), (30, 11, 11, 128, 256, 3, 2, 1)])
+@pytest.mark.parametrize("case", [(40, 22, 22, 64, 64, 3, 1, 1), (30, 11, 11, 128, 256, 3, 2, 1),
+                                  (12, 88, 88, 8, 64, 7, 2, 3)])     # stem geometry
 def test_wgrad_slab_accumulates(dev, case, splitk):
     """Split-K weight gradient through the fp32 slab workspace (+ chunked reduce) matches the
     atomic path and torch, accumulates into a non-zero dw, and tolerates a 4-byte-aligned dw view."""
