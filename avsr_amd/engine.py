@@ -151,7 +151,8 @@ class Engine:
         self._pinned = [(None, None)] * 4
         self._pin_next = 0
         import os
-        self.side = torch.cuda.Stream(device=self.device) if self.device.type == "cuda" else None
+        self.side = (torch.cuda.Stream(device=self.device)
+                     if self.device.type == "cuda" and os.environ.get("AVSR_SIDE_STREAM", "1") != "0" else None)
         # reused events: a stream wait binds the record that precedes it
         self._side_ev = [torch.cuda.Event() for _ in range(8)] if self.side is not None else []
         self._side_i = 0
