@@ -368,6 +368,12 @@ __global__ __launch_bounds__(256) void log_softmax_topk_kernel(int V, int K, con
   // index asc) -- the order row_topk's insertion lists produce, so the ids are the same; a
   // round is one register scan plus a block arg-max (the unrolled 24 x 16 insertion network
   // with its divergent swaps took ~30 us per call)
+  // Each wave first takes the top-K of its own elements (rounds of wave arg-max, DPP only, no
+  // barrier); the block's top-K is among those 4K candidates, which wave 0 then ranks the same way
+  // (one barrier instead of two per round).
+  __shared__ float cv[4 * KMAX];
+  __shared__ int ci[4 * KMAX];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   float pv = INFINITY;
   int pi = -1;
   for (int rr = 0; rr < K; ++rr) {
@@ -378,8 +384,21 @@ __global__ __launch_bounds__(256) void log_softmax_topk_kernel(int V, int K, con
       const bool below = c < V && (v[q] < pv || (v[q] == pv && c > pi));
       if (below && (v[q] > bv || bi == 0x7fffffff)) { bv = v[q]; bi = c; }
     }
-    block_argmax256(bv, bi, shv, shi);
-    if (threadIdx.x == 0) ids[(int64_t)blockIdx.x * K + rr] = bi;
+    dwave_argmax(bv, bi);
+    if (lane == 0) { cv[wv * KMAX + rr] = bv; ci[wv * KMAX + rr] = bi; }
+    pv = bv; pi = bi;
+  }
+  __syncthreads();
+  if (wv != 0) return;
+  const bool have = lane < 4 * KMAX && (lane % KMAX) < K;
+  const float mv = have ? cv[lane] : -INFINITY;
+  const int mi = have ? ci[lane] : 0x7fffffff;
+  pv = INFINITY; pi = -1;
+  for (int rr = 0; rr < K; ++rr) {
+    const bool below = have && mi != 0x7fffffff && (mv < pv || (mv == pv && mi > pi));
+    float bv = below ? mv : -INFINITY; int bi = below ? mi : 0x7fffffff;
+    dwave_argmax(bv, bi);
+    if (lane == 0) ids[(int64_t)blockIdx.x * K + rr] = bi;
     pv = bv; pi = bi;
   }
 }

@@ -500,20 +500,21 @@ def gpu_bench(args):
             traffic = rec["traffic_bytes"]
 
     # per-modality-variant step time (outside the timed region; every rank forced alike)
+    # back-to-back steps of one variant, like the timed loop (no synchronisation between them:
+    # a synchronised step also pays the pipeline refill); the median of the last three intervals
     variant_ms = {}
     for name, forced in (("none", None), ("audio_off", "audio_off"), ("video_off", "video_off")):
         eng.force_modality = (forced,)
-        per = []
-        for _ in range(3):
-            if world > 1:
-                dist.barrier()
-            torch.cuda.synchronize()
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        evs = [torch.cuda.Event(enable_timing=True) for _ in range(5)]
+        evs[0].record()
+        for j in range(4):
             step(variant=True)
-            e1.record()
-            torch.cuda.synchronize()
-            per.append(e0.elapsed_time(e1))
+            evs[j + 1].record()
+        torch.cuda.synchronize()
+        per = [evs[j].elapsed_time(evs[j + 1]) for j in range(1, 4)]
         variant_ms[name] = round(sorted(per)[1], 2)
     eng.force_modality = None
     exp_ms = expected_step_ms(variant_ms, world)
@@ -567,7 +568,7 @@ def gpu_bench(args):
                               "value_expected": round(B * T * world / exp_ms * 1e3, 2),
                               "value_seeded_draw": round(args.steps * B * T * world / raw_ms * 1e3, 2),
                               "seeded_draw_counts": {k: raw.count(k) for k in MODALITY_P},
-                              "note": "median of 3 forced steps per variant; value_expected weights them with "
+                              "note": "median of 3 back-to-back forced steps per variant (after one lead-in step); value_expected weights them with "
                                       "the reference's draw probabilities (avhubert.py:476-482), slowest rank "
                                       "bounding a step for N > 1; value_seeded_draw: the same K steps under one "
                                       "numpy draw (seed --seed) instead of the stratified schedule"},
