@@ -201,7 +201,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
       st[r] = ok ? st[r] * sl2 : -INFINITY;
       mt = fmaxf(mt, st[r]);
     }
-    mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+    mt = xor32_max(mt);
     const float mn = fmaxf(m, mt);
     const float alpha = mn == -INFINITY ? 1.f : exp2f(m - mn);
     float ps = 0.f;
@@ -211,7 +211,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
       ps += p;
       st[r] = p;
     }
-    ps += __shfl_xor(ps, 32, 64);
+    ps = xor32_sum(ps);
     lsum = lsum * alpha + ps;
     m = mn;
 #pragma unroll
@@ -503,7 +503,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
       s0[r] = x0; s1[r] = x1;
       mt = fmaxf(mt, fmaxf(x0, x1));
     }
-    mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+    mt = xor32_max(mt);
     const float mn = fmaxf(m, mt);
     const float mb = mn == -INFINITY ? 0.f : mn;
     const float alpha = exp2f(m - mb);
@@ -514,7 +514,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
       ps += p0 + p1;
       s0[r] = p0; s1[r] = p1;
     }
-    ps += __shfl_xor(ps, 32, 64);
+    ps = xor32_sum(ps);
     lsum = lsum * alpha + ps;
     m = mn;
 #pragma unroll
@@ -915,10 +915,14 @@ __global__ __launch_bounds__(768) void attn_fwd_kernel(AttnArgs a) {
           st[r] = ok ? st[r] : -INFINITY;
         }
       }
-      float mt = st[0];
+      float mx[8];
 #pragma unroll
-      for (int r = 1; r < 16; ++r) mt = fmaxf(mt, st[r]);
-      mt = fmaxf(mt, __shfl_xor(mt, 32, 64)) * sl2;
+      for (int r = 0; r < 8; ++r) mx[r] = fmaxf(st[r], st[r + 8]);
+#pragma unroll
+      for (int w2 = 4; w2 > 0; w2 >>= 1)
+#pragma unroll
+        for (int r = 0; r < w2; ++r) mx[r] = fmaxf(mx[r], mx[r + w2]);
+      float mt = xor32_max(mx[0]) * sl2;
       // a query with no visible key so far keeps mb = -inf (exponent reference 0) and
       // contributes exp2(-inf) = 0; the MFMAs below run for the whole wave
       const bool grow = mt > mb + 8.f;
@@ -930,11 +934,16 @@ __global__ __launch_bounds__(768) void attn_fwd_kernel(AttnArgs a) {
         for (int r = 0; r < 16; ++r) { o0[r] *= alpha; o1[r] *= alpha; }
       }
       const float mbu = mb == -INFINITY ? 0.f : mb;
+      float ts[8];
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        st[r] = fexp2(fmaf(st[r], sl2, -mbu));     // masked keys: exp2(-inf) = 0
-        lsum += st[r];
-      }
+      for (int r = 0; r < 16; ++r) st[r] = fexp2(fmaf(st[r], sl2, -mbu));     // masked keys: exp2(-inf) = 0
+#pragma unroll
+      for (int r = 0; r < 8; ++r) ts[r] = st[r] + st[r + 8];
+#pragma unroll
+      for (int w2 = 4; w2 > 0; w2 >>= 1)
+#pragma unroll
+        for (int r = 0; r < w2; ++r) ts[r] += ts[r + w2];
+      lsum += ts[0];
       if (a.drop_p > 0.f) drop_tile_sel(st, rowG + (uint32_t)(t * 16) * GOLD, drop, hh);
       const bf16x8 pa = accb(st, 0), pb = accb(st, 1);
       o0 = mfma32(rdT(Vs, t * 32, 0, l), pa, o0);
@@ -944,7 +953,7 @@ __global__ __launch_bounds__(768) void attn_fwd_kernel(AttnArgs a) {
     }
   }
   if (q0 < a.Lq) {
-    lsum += __shfl_xor(lsum, 32, 64);
+    lsum = xor32_sum(lsum);
     if (hh == 0 && qi < a.Lq)
       a.lse[(int64_t)bh * a.Lq + qi] = lsum > 0.f ? (mb + log2f(lsum)) * LN2 : -INFINITY;
   }
@@ -1369,10 +1378,15 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_kernel(AttnArgs a, int nqb) {
         s1[r] = k0 + 32 + qrow(r, hh) < klen ? s1[r] : -INFINITY;
       }
     }
-    float mt = fmaxf(s0[0], s1[0]);
+    // balanced trees (the 16-deep max / add chains were on the tile's dependent path)
+    float mx[16];
 #pragma unroll
-    for (int r = 1; r < 16; ++r) mt = fmaxf(mt, fmaxf(s0[r], s1[r]));
-    mt = fmaxf(mt, __shfl_xor(mt, 32, 64)) * sl2;
+    for (int r = 0; r < 16; ++r) mx[r] = fmaxf(s0[r], s1[r]);
+#pragma unroll
+    for (int w2 = 8; w2 > 0; w2 >>= 1)
+#pragma unroll
+      for (int r = 0; r < w2; ++r) mx[r] = fmaxf(mx[r], mx[r + w2]);
+    float mt = xor32_max(mx[0]) * sl2;
     const bool grow = mt > mb + 8.f;
     if (__any(grow)) {
       const float alpha = grow ? (mb == -INFINITY ? 0.f : fexp2(mb - mt)) : 1.f;
@@ -1382,12 +1396,18 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_kernel(AttnArgs a, int nqb) {
       for (int r = 0; r < 16; ++r) { o0[r] *= alpha; o1[r] *= alpha; }
     }
     const float mbu = mb == -INFINITY ? 0.f : mb;
+    float ts[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       s0[r] = fexp2(fmaf(s0[r], sl2, -mbu));
       s1[r] = fexp2(fmaf(s1[r], sl2, -mbu));
-      lsum += s0[r] + s1[r];
+      ts[r] = s0[r] + s1[r];
     }
+#pragma unroll
+    for (int w2 = 8; w2 > 0; w2 >>= 1)
+#pragma unroll
+      for (int r = 0; r < w2; ++r) ts[r] += ts[r + w2];
+    lsum += ts[0];
     if (a.drop_p > 0.f) {
       drop_tile_sel(s0, rowG + (uint32_t)(k0 >> 1) * GOLD, drop, hh);
       drop_tile_sel(s1, rowG + (uint32_t)((k0 + 32) >> 1) * GOLD, drop, hh);
@@ -1403,7 +1423,7 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_kernel(AttnArgs a, int nqb) {
     o1 = mfma32(ldT(Vs, 48, fo, 1), p1b, o1);
     cs = next_stage(cs);
   }
-  lsum += __shfl_xor(lsum, 32, 64);
+  lsum = xor32_sum(lsum);
   if (hh == 0 && qi < a.Lq) a.lse[(int64_t)bh * a.Lq + qi] = lsum > 0.f ? (mb + log2f(lsum)) * LN2 : -INFINITY;
   __syncthreads();                           // the ring is free: reuse it as the store slabs
   const float inv = lsum > 0.f ? (a.drop_p > 0.f ? drop.scale : 1.f) / lsum : 0.f;
@@ -1450,7 +1470,7 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_dq_kernel(AttnArgs a, int nqb
   for (int s = 0; s < 4; ++s)
 #pragma unroll
     for (int j = 0; j < 8; ++j) dsum = fmaf((float)of[s][j], (float)ov[s][j], dsum);
-  dsum += __shfl_xor(dsum, 32, 64);
+  dsum = xor32_sum(dsum);
   if (hh == 0 && qok) a.delta[bhq] = dsum;
   const float lq = qok ? lq0 * LOG2E : 0.f;
   const float dl = qok ? dsum : 0.f;

@@ -46,6 +46,17 @@ AVSR_DEV float wave_sum(float x) {
   x = row_sum16(x);
   return (lanef(x, 0) + lanef(x, 16)) + (lanef(x, 32) + lanef(x, 48));
 }
+// max / sum with the lane 32 apart (the two halves of a wave): v_permlane32_swap (gfx950) hands
+// every lane both x[l mod 32] and x[32 + l mod 32] without an LDS round trip (ds_bpermute);
+// the sum is lo + hi in every lane (the __shfl_xor form gave hi + lo in the upper half: equal)
+AVSR_DEV float xor32_max(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+AVSR_DEV float xor32_sum(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
 AVSR_DEV float wave_max(float x) {
   x = fmaxf(x, rorf<8>(x)); x = fmaxf(x, rorf<4>(x)); x = fmaxf(x, rorf<2>(x)); x = fmaxf(x, rorf<1>(x));
   return fmaxf(fmaxf(lanef(x, 0), lanef(x, 16)), fmaxf(lanef(x, 32), lanef(x, 48)));
