@@ -330,9 +330,12 @@ using Cfg192x256 = gemmg::GCfg<2, 4, 3, 2, 2>;   // 192x256, 8 waves (96x64 each
 using Cfg192s3 = gemmg::GCfg<2, 2, 3, 2, 3>;     // 192x128, 4 waves, 3 stages (120 KiB)
 using Cfg192w8 = gemmg::GCfg<2, 4, 3, 1, 2>;     // 192x128, 8 waves (96x32 each), 2 stages (80 KiB)
 using Cfg192w8s3 = gemmg::GCfg<2, 4, 3, 1, 3>;   // 192x128, 8 waves, 3 stages (120 KiB)
+using Cfg64 = gemmg::GCfg<2, 2, 1, 1, 2>;        // 64x64, 4 waves (32x32 each), 2 stages (32 KiB)
 
 // tile choice: AVSR_GEMM_TILE=128|256|256x128|128x256 forces one (benchmarks); otherwise the
 // configuration with the fewest block rounds x per-tile work (wave quantisation over 256 CUs)
+bool getenv_flag(const char* name);
+
 int tile_cfg(const avsr_gemm_params* p, int splits) {
   const char* e = getenv("AVSR_GEMM_TILE");
   const int forced = !e ? -1 : !strcmp(e, "128") ? 0 : !strcmp(e, "256") ? 1 : !strcmp(e, "256x128") ? 2
@@ -340,7 +343,7 @@ int tile_cfg(const avsr_gemm_params* p, int splits) {
                    : !strcmp(e, "128w8s3") ? 6 : !strcmp(e, "128w8s4") ? 7 : !strcmp(e, "pp") ? 8
                    : !strcmp(e, "96") ? 9 : !strcmp(e, "128x64") ? 10 : !strcmp(e, "192") ? 11
                    : !strcmp(e, "192x256") ? 12 : !strcmp(e, "192s3") ? 13 : !strcmp(e, "192w8") ? 14
-                   : !strcmp(e, "192w8s3") ? 15 : -1;
+                   : !strcmp(e, "192w8s3") ? 15 : !strcmp(e, "64") ? 16 : -1;
   if (forced >= 0) return forced;
   // 128x128 at two blocks per CU is the default (tools/gemm_table.py, profiles/r02_gemm_table.*:
   // the 256x256 ping-pong core loses 8-36 % at M = 6000, the 3-stage / 8-wave variants are
@@ -360,6 +363,14 @@ int tile_cfg(const avsr_gemm_params* p, int splits) {
     // the other's LDS-DMA issue) and 3 stages: -10..-15 % vs 128x128 (profiles/r03_gemm_table_192w8.txt)
     if (t192 > 128 && t192 <= 256) return 15;
   }
+  // grids of fewer 128x128 tiles than CUs (the teacher-forced decoder: M = 16 x 41 rows, N = 1024:
+  // 48 tiles) leave most of the chip idle: 64x64 tiles (4x the workgroups, several per CU)
+  {
+    const long tiles_z = (long)p->batch * splits;
+    const long t128 = (long)((p->M + 127) / 128) * ((p->N + 127) / 128) * tiles_z;
+    const long t64 = (long)((p->M + 63) / 64) * ((p->N + 63) / 64) * tiles_z;
+    if (t128 < 256 && t64 >= 2 * t128 && !getenv_flag("AVSR_GEMM_NO64")) return 16;
+  }
   return 0;
 }
 
@@ -376,6 +387,7 @@ int cfg_bm(int cfg, bool ak) {
     case 8: return gemmpp::BM;
     case 9: return ak ? Cfg96::BM : Cfg128::BM;   // as launch_cfg
     case 10: return Cfg128x64::BM;
+    case 16: return Cfg64::BM;
     case 11: return ak ? Cfg192::BM : Cfg128::BM;
     case 12: return ak ? Cfg192x256::BM : Cfg128::BM;
     case 13: return ak ? Cfg192s3::BM : Cfg128::BM;
@@ -400,6 +412,7 @@ int launch_cfg(int cfg, const DenseArgs& a, int batch, hipStream_t st) {
       if constexpr (AK) return launch_glds<OutT, AK, BK, Cfg96>(a, batch, st);   // r-contiguous A needs BM % 64 == 0
       else return launch_glds<OutT, AK, BK, Cfg128>(a, batch, st);
     case 10: return launch_glds<OutT, AK, BK, Cfg128x64>(a, batch, st);
+    case 16: return launch_glds<OutT, AK, BK, Cfg64>(a, batch, st);
     case 11:   // BM = 192: r-contiguous A needs BM % 64 == 0 (weight-grads stay on 128x128)
       if constexpr (AK) return launch_glds<OutT, AK, BK, Cfg192>(a, batch, st);
       else return launch_glds<OutT, AK, BK, Cfg128>(a, batch, st);

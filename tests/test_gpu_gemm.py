@@ -93,7 +93,7 @@ def _ref_gemm(A, B, a_kmajor, b_kmajor):
     return Af @ Bf.t()
 
 
-@pytest.fixture(params=["auto", "128", "256", "256x128", "128x256", "128s3", "128w8s3", "pp", "192", "192x256"])
+@pytest.fixture(params=["auto", "128", "256", "256x128", "128x256", "128s3", "128w8s3", "pp", "192", "192x256", "64"])
 def gemm_tile(request, monkeypatch):
     """forces each LDS-DMA tile configuration (AVSR_GEMM_TILE, read per launch by avsr_gemm)"""
     if request.param != "auto":
