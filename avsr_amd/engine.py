@@ -151,6 +151,7 @@ class Engine:
         self._pinned = [(None, None)] * 4
         self._pin_next = 0
         import os
+        self._nbt = None
         self.side = (torch.cuda.Stream(device=self.device)
                      if self.device.type == "cuda" and os.environ.get("AVSR_SIDE_STREAM", "1") != "0" else None)
         # reused events: a stream wait binds the record that precedes it
@@ -481,6 +482,14 @@ class Engine:
     def _geom(self, nimg, hin, cin, cout, k, s):
         return ops.ConvGeom(nimg, hin, hin, cin, cout, k, k, (s, s), (k // 2, k // 2))
 
+    def _count_bn(self, bn):
+        """BatchNorm num_batches_tracked += 1: collected and applied by one multi-tensor add at the
+        end of the ResNet forward (20 one-element kernel launches on the forward's chain before)"""
+        if self._nbt is not None:
+            self._nbt.append(bn.num_batches_tracked)
+        else:
+            bn.num_batches_tracked.add_(1)
+
     def _conv_bn(self, g, x, wname, bnprefix, train):
         """conv (implicit GEMM) + BN statistics (fused in the conv epilogue) + BN finalize."""
         h = self._e(g.out_pixels, g.cout)
@@ -491,7 +500,7 @@ class Engine:
             ops.conv_fwd(g, x, self.w(wname), h, part)
             ops.bn_finalize(st, gam, bet, bn.running_mean, bn.running_var, partials=part, training=True,
                             momentum=bn.momentum, eps=bn.eps)
-            bn.num_batches_tracked.add_(1)
+            self._count_bn(bn)
         else:
             ops.conv_fwd(g, x, self.w(wname), h)
             ops.bn_finalize(st, gam, bet, bn.running_mean, bn.running_var, training=False, eps=bn.eps)
@@ -534,7 +543,8 @@ class Engine:
         if train:
             ops.bn_finalize(st0, gam, bet, bn.running_mean, bn.running_var, partials=part, training=True,
                             momentum=bn.momentum, eps=bn.eps)
-            bn.num_batches_tracked.add_(1)
+            self._nbt = []
+            self._count_bn(bn)
         else:
             ops.bn_finalize(st0, gam, bet, bn.running_mean, bn.running_var, training=False, eps=bn.eps)
         x = self._e(N * 22 * 22, 64)
@@ -569,6 +579,9 @@ class Engine:
             hw = ho
         feat = self._e(N, 512)
         ops.avgpool_fwd(x, N, hw * hw, 512, feat)
+        if self._nbt:
+            torch._foreach_add_(self._nbt, 1)
+        self._nbt = None
         if save:
             ctx.update(blocks=blocks, hw_last=hw, feat=feat)
         return feat, ctx
