@@ -21,6 +21,6 @@ done
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/dp -o run -- python3 tools/decode_c5.py split > $O/dprof.log 2>&1 || { echo dprof failed; tail -20 $O/dprof.log; exit 1; }
 rm -f $O/dp/run_kernel_trace.csv
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 bench.py --steps 4 --warmup 2 --quick --no-cpu-baseline --force-modality none > $O/prof.log 2>&1 || { echo prof failed; tail -20 $O/prof.log; exit 1; }
-timeout -k 10 60 python tools/profsum.py $O/prof/run_kernel_trace.csv 4 60 > $O/steps.txt 2>&1 || { echo profsum failed; exit 1; }
+timeout -k 10 60 python tools/profsum.py $O/prof/run_kernel_trace.csv 4 60 --skip 12 > $O/steps.txt 2>&1 || { echo profsum failed; exit 1; }
 rm -rf $O/prof/*/ 2>/dev/null
 echo rc=0

@@ -29,8 +29,8 @@ rows = sorted(load_rows(path), key=lambda r: int(r["Start_Timestamp"]))
 ends = [i for i, r in enumerate(rows) if "adamw_kernel" in r["Kernel_Name"]]
 # two adamw launches (decay / no-decay segments) per step
 ends = ends[1::2]
-# --skip S: leave out the last S steps (bench --quick appends 9 per-variant steps: none x3,
-# audio_off x3, video_off x3; the forced timed steps are the 3 before them)
+# --skip S: leave out the last S steps (bench --quick appends 12 per-variant steps: none x4,
+# audio_off x4, video_off x4, one lead-in + 3 timed each; the forced timed steps are the 4 before them)
 skip = int(sys.argv[sys.argv.index("--skip") + 1]) if "--skip" in sys.argv else 0
 if skip:
     ends = ends[:-skip]

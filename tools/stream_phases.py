@@ -1,15 +1,19 @@
 """Per-step phase timeline of a rocprofv3 kernel trace: for each training step (delimited by
 the AdamW launches) the forward / backward / optimizer spans, per-stream busy time inside each
 span, and the union busy time (GPU idle = span - union).
-usage: python tools/stream_phases.py run_kernel_trace.csv [last_steps]"""
+usage: python tools/stream_phases.py run_kernel_trace.csv [last_steps] [--skip S]
+(--skip S: leave out the last S steps, as in tools/profsum.py)"""
 import csv
 import sys
 from collections import defaultdict
 
 rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
-last = int(sys.argv[2]) if len(sys.argv) > 2 else 3
+last = int(sys.argv[2]) if len(sys.argv) > 2 and sys.argv[2] != "--skip" else 3
+skip = int(sys.argv[sys.argv.index("--skip") + 1]) if "--skip" in sys.argv else 0
 ad = [i for i, r in enumerate(rows) if "adamw_kernel" in r["Kernel_Name"]]
 ends = ad[1::2]                  # decay + no-decay launch per step: the second closes a step
+if skip:
+    ends = ends[:-skip]
 steps = list(zip(ends[:-1], ends[1:]))[-last:]
 
 
