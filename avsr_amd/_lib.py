@@ -103,7 +103,7 @@ class StemPoolParams(ctypes.Structure):
         ("h", _c_p), ("scale", _c_p), ("shift", _c_p), ("prelu", _c_p), ("y", _c_p), ("argmax", _c_p),
         ("dy", _c_p), ("dz", _c_p), ("mean", _c_p), ("invstd", _c_p),
         ("sums", _c_p), ("dprelu", _c_p), ("dgamma", _c_p), ("dbeta", _c_p), ("ws", _c_p),
-        ("hmax", _c_p), ("dh", _c_p),
+        ("hmax", _c_p), ("dh", _c_p), ("m_total", _i64),
     ]
 
 

@@ -690,7 +690,7 @@ __global__ __launch_bounds__(256) void stem_bwd_apply_kernel(avsr_stem_pool_para
   const int64_t nv = (int64_t)p.nimg * p.H * p.W * cpv, stride = (int64_t)gridDim.x * 256;
   const int64_t t0 = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int cv = (int)(t0 % cpv), c0 = cv * VE;
-  const float invM = 1.f / ((float)p.nimg * p.H * p.W);
+  const float invM = 1.f / (p.m_total > 0 ? (float)p.m_total : (float)p.nimg * p.H * p.W);
   float ka[VE], kb[VE], kc[VE], km[VE];
 #pragma unroll
   for (int j = 0; j < VE; ++j) {
@@ -758,7 +758,7 @@ __global__ __launch_bounds__(256) void stem_bwd_apply2_kernel(avsr_stem_pool_par
   const int64_t nv = (int64_t)p.nimg * p.Ho * p.Wo * cpv, stride = (int64_t)gridDim.x * 256;
   const int64_t t0 = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int cv = (int)(t0 % cpv), c0 = cv * VE;
-  const float invM = 1.f / ((float)p.nimg * p.H * p.W);
+  const float invM = 1.f / (p.m_total > 0 ? (float)p.m_total : (float)p.nimg * p.H * p.W);
   float ka[VE], kb[VE], kc[VE], km[VE];
 #pragma unroll
   for (int j = 0; j < VE; ++j) {

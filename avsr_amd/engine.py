@@ -658,11 +658,16 @@ class Engine:
                 else:
                     ops.conv_bwd_data(blk["gd"], dhd, self.w(p + "downsample.0.weight"), dx, beta=1.0)
             dout = dx
-        # stem: BN/PReLU reduction on the pooled grid, then the argmax-routed apply
+        # stem: BN/PReLU reduction on the pooled grid, then the argmax-routed apply and the
+        # weight-grad (pipelining the two over frame ranges on two streams measured no gain: both
+        # slow down together, profiles/r04_stem_pipeline_ab.txt)
         dh0 = self._e(N * 44 * 44, 64)
-        ops.stem_pool_bwd(dout, ctx["am"], ctx["hmax"], ctx["h0"], N, 44, 44, ctx["st0"],
-                          self.arena.master(R + "frontend3D.2.weight"), dh0, dprelu=self.g(R + "frontend3D.2.weight"),
-                          dgamma=self.g(R + "frontend3D.1.weight"), dbeta=self.g(R + "frontend3D.1.bias"), reduced=red)
+        dzp, sums = ops.stem_pool_bwd_reduce(dout, ctx["hmax"], N, 44, 44, ctx["st0"],
+                                             self.arena.master(R + "frontend3D.2.weight"),
+                                             dprelu=self.g(R + "frontend3D.2.weight"),
+                                             dgamma=self.g(R + "frontend3D.1.weight"),
+                                             dbeta=self.g(R + "frontend3D.1.bias"), reduced=red)
+        ops.stem_pool_bwd_apply(dzp, ctx["am"], ctx["h0"], N, 44, 44, ctx["st0"], sums, dh0)
         gp = self._z(64, 7, 7, 8, dtype=torch.float32)
         ops.conv_bwd_weight(ctx["gs"], ctx["xp"], dh0, gp)
         ops.stem_wgrad_unpack(gp, self.g(R + "frontend3D.0.weight"))

@@ -451,18 +451,30 @@ def stem_pool_bwd(dy, argmax, hmax, h, nimg, H, W, st, prelu, dh, *, dzp=None, s
     """Backward through max-pool, PReLU and BN of the stem: writes dh (grad of the conv output).
     The BN/PReLU reduction runs on the pooled grid (h = hmax); `reduced` = (ws, tiles) when a
     data-grad BN epilogue already stored the pooled dz in dy and wrote the partials."""
-    C = h.shape[-1]
-    Ho, Wo = (H + 1) // 2, (W + 1) // 2
-    Mo = nimg * Ho * Wo
+    dzp, sums = stem_pool_bwd_reduce(dy, hmax, nimg, H, W, st, prelu, dzp=dzp, sums=sums, dprelu=dprelu,
+                                     dgamma=dgamma, dbeta=dbeta, reduced=reduced)
+    return stem_pool_bwd_apply(dzp, argmax, h, nimg, H, W, st, sums, dh)
+
+
+def stem_pool_bwd_reduce(dy, hmax, nimg, H, W, st, prelu, *, dzp=None, sums=None, dprelu=None, dgamma=None,
+                         dbeta=None, reduced=None):
+    """the stem's BN/PReLU backward reduction over the pooled grid: (pooled dz, sums)"""
+    C = hmax.shape[-1]
+    Mo = nimg * ((H + 1) // 2) * ((W + 1) // 2)
     if reduced is None:
-        dzp, sums = bn_act_bwd_reduce(dy.view(Mo, C), hmax.view(Mo, C), st, prelu, dz=dzp, sums=sums,
-                                      dprelu=dprelu, dgamma=dgamma, dbeta=dbeta)
-    else:
-        dzp = dy
-        sums = bn_bwd_finalize(reduced[0], reduced[1], C, sums=sums, dprelu=dprelu, dgamma=dgamma, dbeta=dbeta)
+        return bn_act_bwd_reduce(dy.view(Mo, C), hmax.view(Mo, C), st, prelu, dz=dzp, sums=sums,
+                                 dprelu=dprelu, dgamma=dgamma, dbeta=dbeta)
+    return dy, bn_bwd_finalize(reduced[0], reduced[1], C, sums=sums, dprelu=dprelu, dgamma=dgamma, dbeta=dbeta)
+
+
+def stem_pool_bwd_apply(dzp, argmax, h, nimg, H, W, st, sums, dh, m_total=0):
+    """dh of `nimg` images from their pooled dz / argmax (views starting at the first of them);
+    m_total: the pixel count the BN statistics cover when this is a range of the batch"""
+    C = h.shape[-1]
     _call("avsr_stem_pool_bwd_apply", L.fill(L.StemPoolParams, dtype=dtype_code(h), nimg=nimg, H=H, W=W, C=C,
-                                              Ho=Ho, Wo=Wo, h=h, scale=st.scale, argmax=argmax, dz=dzp,
-                                              mean=st.mean, invstd=st.invstd, sums=sums, dh=dh))
+                                              Ho=(H + 1) // 2, Wo=(W + 1) // 2, h=h, scale=st.scale, argmax=argmax,
+                                              dz=dzp, mean=st.mean, invstd=st.invstd, sums=sums, dh=dh,
+                                              m_total=int(m_total)))
     return dh
 
 

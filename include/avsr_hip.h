@@ -276,7 +276,7 @@ int avsr_bn_bwd_apply(const avsr_bn_act_params* p, void* stream);
  * data-grad BN epilogue) over the POOLED grid with h = hmax, dy = pooled gradient, giving the
  * pooled dz and the sums over input pixels (dz vanishes off the argmax positions);
  * bwd_apply: dh[n][h][w][c] = scale*(dz - S0/M - xhat*S1/M), dz routed back through the
- * argmax (M = nimg*H*W). */
+ * argmax (M = m_total, or nimg*H*W). */
 typedef struct {
   int dtype, nimg, H, W, C, Ho, Wo;
   const void* h; const float* scale; const float* shift; const float* prelu;
@@ -287,6 +287,9 @@ typedef struct {
   float* ws;
   void* hmax;                                      /* fwd output [n][Ho][Wo][C] (optional) */
   void* dh;                                        /* bwd_apply output [n][H][W][C] */
+  int64_t m_total;                                 /* bwd_apply: pixels M the BN statistics
+                                                      cover (0: nimg*H*W); a launch over a range
+                                                      of images passes the whole batch's M */
 } avsr_stem_pool_params;
 int avsr_stem_pool_fwd(const avsr_stem_pool_params* p, void* stream);
 int avsr_stem_pool_bwd_apply(const avsr_stem_pool_params* p, void* stream);

@@ -207,6 +207,21 @@ def test_stem_bwd_apply_block_kernel(dev, dtype, monkeypatch, n, H, W):
     assert _rel(out[0][0], out[1][0]) < (1e-6 if dtype == torch.float32 else 8e-3)
     for g0, g1 in zip(out[0][1], out[1][1]):
         assert torch.equal(g0, g1)
+    # the engine's pipelined stem backward: one reduction, then the apply over image ranges
+    # (m_total = the whole batch's pixels) -> the same dh bit for bit
+    monkeypatch.delenv("AVSR_STEM_APPLY_PIXEL")
+    dzp, sums = ops.stem_pool_bwd_reduce(dy, hmax, n, H, W, st, a, dgamma=torch.zeros(C, device=dev),
+                                         dbeta=torch.zeros(C, device=dev), dprelu=torch.zeros(C, device=dev))
+    dzp = dzp.view(n, Ho, Wo, C)
+    dh_full = ops.stem_pool_bwd_apply(dzp, am, hd, n, H, W, st, sums, torch.full_like(hd, float("nan")))
+    dh_rng = torch.full_like(hd, float("nan"))
+    for f0, f1 in ((0, 1), (1, n // 2 + 1), (n // 2 + 1, n)):
+        if f1 > f0:
+            ops.stem_pool_bwd_apply(dzp[f0:], am[f0:], hd[f0:], f1 - f0, H, W, st, sums, dh_rng[f0:],
+                                    m_total=n * H * W)
+    torch.cuda.synchronize()
+    assert torch.equal(dh_full, dh_rng)
+    assert torch.equal(dh_full, out[1][0])
 
 
 BNR_CASES = [
