@@ -26,8 +26,29 @@ constexpr int SC_ND = SC_CW / 2 + 1;       // pixel pairs staged per input row (
 constexpr int SC_K = 288;
 constexpr int SC_ROWB = 2 * SC_CW * 2;     // one staged input row, both copies (384 B)
 constexpr int SC_SLOT = SC_ROWS * SC_ROWB; // one frame's band (4,992 B)
-constexpr int SC_LDS = 5 * SC_SLOT;        // ring of the 5 frames a step reads (24,960 B)
+constexpr int SC_LDS = 5 * SC_SLOT + 64;   // ring of the 5 frames a step reads (24,960 B) + the dropped columns' overrun
 constexpr int SC_BLOCKS_PER_CU = 2;
+
+typedef int v2i32 __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) void sc_lds_t;
+
+// B fragment i of a step: two 8-byte LDS reads at the lane's window base + the fragment's
+// compile-time offset (fragment i = pixel row i / 3 of the wave, 16-column block i % 3), as
+// inline asm: two ds_read_b64 (2 cycles each) with the offset in the instruction, which the
+// compiler would otherwise pair into ds_read2_b64 (8 cycles). The compiler does not see these
+// LDS reads, so the consumer waits with sc_lgkm_wait (which also pins the registers).
+template <int I>
+AVSR_DEV bf16x8 sc_frag(uint32_t a) {
+  constexpr int off = 2 * (I / 3) * (2 * 2 * 96) + 64 * (I % 3);
+  union { uint2 u[2]; bf16x8 h; } x;
+  asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(x.u[0]) : "v"(a), "i"(off));
+  asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(x.u[1]) : "v"(a), "i"(off + 8));
+  return x.h;
+}
+template <int N>
+AVSR_DEV void sc_lgkm_wait(bf16x8 (&b)[6]) {
+  asm volatile("s_waitcnt lgkmcnt(%6)" : "+v"(b[0]), "+v"(b[1]), "+v"(b[2]), "+v"(b[3]), "+v"(b[4]), "+v"(b[5]) : "n"(N));
+}
 
 AVSR_DEV uint32_t pack_bf16(float a, float b) {
   union { bf16 h[2]; uint32_t u; } v;
@@ -104,35 +125,53 @@ __global__ __launch_bounds__(256, SC_BLOCKS_PER_CU) void stem_conv_kernel(
 #pragma unroll
     for (int j = 0; j < 2; ++j)
       wr[ks][j] = *(const bf16x8*)(wk + (wn * 32 + j * 16 + (lane & 15)) * SC_K + ks * 32 + (lane >> 4) * 8);
-  // this lane's pixel (B column) in each of the wave's 6 pixel fragments
-  int pbase[6];
+  // this lane's pixel (B column) in each of the wave's 6 pixel fragments: fragment i is pixel
+  // (ob, ow) = (2wm + i/3, 16(i%3) + l), l = lane & 15 (3 fragments = one 48-wide row), so its
+  // LDS window is the lane's base pbase0 plus a compile-time offset (LDS instruction offset
+  // field, no per-fragment address VALU). Columns 44..47 (fragments 2 and 5, l >= 12) are
+  // computed from whatever follows the row in LDS (in range; out of the allocation reads as 0)
+  // and dropped.
+  const int l16 = lane & 15;
+  const int pbase0 = 4 * wm * SC_ROWB + (l16 & 1) * (SC_CW * 2) + 4 * l16 - 4 * (l16 & 1);
+  const bool tail_ok = l16 < 12;                         // fragments 2 and 5: ow = 32 + l < 44
+  const uint32_t sbase = (uint32_t)(uintptr_t)(sc_lds_t*)smem;
   bool pvalid[6];
 #pragma unroll
-  for (int i = 0; i < 6; ++i) {
-    const int v = wm * 96 + i * 16 + (lane & 15);
-    const int ob = v / SC_VW, ow = v - ob * SC_VW;
-    const int owc = min(ow, 43), cp = owc & 1, j0 = 2 * owc - 2 * cp;
-    pvalid[i] = ow < 44;
-    pbase[i] = 2 * ob * SC_ROWB + cp * (SC_CW * 2) + j0 * 2;
-  }
+  for (int i = 0; i < 6; ++i) pvalid[i] = i % 3 != 2 || tail_ok;
   float shift[8], s1[8], s2[8], cnt = 0.f;               // this lane's 8 channels: shifted sums
   float pv_count = 0.f;
 #pragma unroll
   for (int i = 0; i < 6; ++i) pv_count += pvalid[i] ? 1.f : 0.f;
 #pragma unroll
   for (int q = 0; q < 8; ++q) shift[q] = s1[q] = s2[q] = 0.f;
+  // the ring's first 5 frames: every load issued before the first store (one latency)
   if (t0 < t1) {
-    for (int f = t0 - 2; f <= t0 + 2; ++f) {
-      StageRegs g;
-      stem_stage_load(g, rs, b, T, f, ir0, tid);
-      stem_stage_store(g, smem, f, tid);
-    }
+    StageRegs p[5];
+#pragma unroll
+    for (int f = 0; f < 5; ++f) stem_stage_load(p[f], rs, b, T, t0 - 2 + f, ir0, tid);
+#pragma unroll
+    for (int f = 0; f < 5; ++f) stem_stage_store(p[f], smem, t0 - 2 + f, tid);
   }
+  // frames t + 3 and t + 4 stay in flight in registers (two sets, alternating): a frame's loads
+  // are issued two steps before it is stored into the ring. Loads past the clip return zeros
+  // (range check) and are issued unconditionally, and the output goes out through buffer
+  // stores with out-of-range offsets for the dropped columns, so the step has no divergent
+  // memory operations and the ring store waits only for its own frame's loads
+  StageRegs sa, sb;
+  stem_stage_load(sb, rs, b, T, t0 + 3, ir0, tid);
   __syncthreads();
   const int g0 = lane >> 4;
-  for (int t = t0; t < t1; ++t) {
-    StageRegs nxt;                                        // frame t + 3: loads in flight during the MFMAs
-    if (t + 1 < t1) stem_stage_load(nxt, rs, b, T, t + 3, ir0, tid);
+  int ooff[6][2];                                         // byte offsets in the band (OOB: dropped)
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    const int v = wm * 96 + i * 16 + (lane & 15);
+    const int ob = v / SC_VW, ow = v - ob * SC_VW;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      ooff[i][j] = pvalid[i] ? ((ob * 44 + ow) * 64 + wn * 32 + j * 16 + 4 * g0) * 2 : (int)0x80000000u;
+  }
+  auto step = [&](int t, StageRegs& ld, const StageRegs& st) {
+    stem_stage_load(ld, rs, b, T, t + 4, ir0, tid);       // frame t + 4: stored at the end of step t + 1
     f32x4 acc[6][2];
 #pragma unroll
     for (int i = 0; i < 6; ++i)
@@ -140,49 +179,47 @@ __global__ __launch_bounds__(256, SC_BLOCKS_PER_CU) void stem_conv_kernel(
       for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     // B fragments of K-step ks (the lane's 8 k = group 4ks + g0 of its pixel), double-buffered:
     // step ks + 1's reads are issued before step ks's MFMAs
+    // k group g = 4ks + g0 -> (frame dt, row kh) = divmod(g, 7), from compile-time 4ks / 7 and
+    // 4ks % 7 (group 35 has zero weights: its window is any in-range row)
+    const int t5 = (t + 8) % 5;
     auto rdB = [&](int ks, bf16x8 (&xb)[6]) {
-      const int g = 4 * ks + g0;
-      const int dt = g < 35 ? g / 7 : 0, kh = g < 35 ? g - 7 * (g / 7) : 0;
-      const int roff = ((t + dt - 2 + 10) % 5) * SC_SLOT + kh * SC_ROWB;
-#pragma unroll
-      for (int i = 0; i < 6; ++i) {
-        const int o1 = pbase[i] + roff;
-        int o2 = o1 + 8;
-        asm volatile("" : "+v"(o2));                      // two ds_read_b64 (2 cycles each), not one ds_read2_b64 (8)
-        union { uint2 u[2]; bf16x8 hh; } x;
-        x.u[0] = *(const uint2*)(smem + o1);
-        x.u[1] = *(const uint2*)(smem + o2);
-        xb[i] = x.hh;
-      }
+      const int q7 = (4 * ks) / 7, r7 = (4 * ks) % 7;
+      const int c = g0 >= 7 - r7 ? 1 : 0;
+      const int dt = q7 + c, kh = r7 + g0 - 7 * c;
+      int slot = t5 + dt;
+      slot = slot >= 5 ? slot - 5 : slot;
+      slot = slot >= 5 ? slot - 5 : slot;
+      const uint32_t a = sbase + (uint32_t)(pbase0 + slot * SC_SLOT + kh * SC_ROWB);
+      xb[0] = sc_frag<0>(a); xb[1] = sc_frag<1>(a); xb[2] = sc_frag<2>(a);
+      xb[3] = sc_frag<3>(a); xb[4] = sc_frag<4>(a); xb[5] = sc_frag<5>(a);
     };
-    bf16x8 bcur[6], bnx[6];
-    rdB(0, bcur);
+    bf16x8 bb[2][6];                                      // ping-pong by k-step parity (no register copies)
+    rdB(0, bb[0]);
 #pragma unroll
     for (int ks = 0; ks < SC_K / 32; ++ks) {
-      if (ks + 1 < SC_K / 32) rdB(ks + 1, bnx);
+      if (ks + 1 < SC_K / 32) {
+        rdB(ks + 1, bb[(ks + 1) & 1]);
+        sc_lgkm_wait<12>(bb[ks & 1]);                      // step ks's reads are done, step ks + 1's fly
+      } else {
+        sc_lgkm_wait<0>(bb[ks & 1]);
+      }
 #pragma unroll
       for (int i = 0; i < 6; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = mfma16(wr[ks][j], bcur[i], acc[i][j]);
-#pragma unroll
-      for (int i = 0; i < 6; ++i) bcur[i] = bnx[i];
+        for (int j = 0; j < 2; ++j) acc[i][j] = mfma16(wr[ks][j], bb[ks & 1][i], acc[i][j]);
     }
     // output: lane holds channels co0 .. co0+3 of pixel (ob, ow) in tile (i, j)
     const int n = b * T + t;
-    bf16* out = h + ((int64_t)n * 44 * 44 + (int64_t)oh0 * 44) * 64;
+    const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
+        h + ((int64_t)n * 44 * 44 + (int64_t)oh0 * 44) * 64, (short)0, SC_R * 44 * 64 * 2, 0x00020000);
 #pragma unroll
-    for (int i = 0; i < 6; ++i) {
-      if (!pvalid[i]) continue;
-      const int v = wm * 96 + i * 16 + (lane & 15);
-      const int ob = v / SC_VW, ow = v - ob * SC_VW;
+    for (int i = 0; i < 6; ++i)
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
-        const int co0 = wn * 32 + j * 16 + 4 * g0;
-        union { bf16x4 v4; uint2 u; } o;
+        union { bf16x4 v4; v2i32 u; } o;
         o.v4 = bf16x4{(bf16)acc[i][j][0], (bf16)acc[i][j][1], (bf16)acc[i][j][2], (bf16)acc[i][j][3]};
-        *(uint2*)(out + (ob * 44 + ow) * 64 + co0) = o.u;
+        __builtin_amdgcn_raw_buffer_store_b64(o.u, ro, (uint32_t)ooff[i][j], 0, 0);
       }
-    }
     if (stats != nullptr) {   // per-lane shifted sums of the lane's 8 channels (no cross-lane work per step)
       if (t == t0) {
 #pragma unroll
@@ -192,7 +229,8 @@ __global__ __launch_bounds__(256, SC_BLOCKS_PER_CU) void stem_conv_kernel(
       for (int q = 0; q < 8; ++q)
 #pragma unroll
         for (int i = 0; i < 6; ++i) {
-          const float x = pvalid[i] ? acc[i][q >> 2][q & 3] - shift[q] : 0.f;
+          const float d = acc[i][q >> 2][q & 3] - shift[q];
+          const float x = i % 3 != 2 ? d : (tail_ok ? d : 0.f);
           s1[q] += x;
           s2[q] = fmaf(x, x, s2[q]);
         }
@@ -200,9 +238,13 @@ __global__ __launch_bounds__(256, SC_BLOCKS_PER_CU) void stem_conv_kernel(
     }
     __syncthreads();                                      // every wave is done with frame t - 2's slot
     if (t + 1 < t1) {
-      stem_stage_store(nxt, smem, t + 3, tid);
+      stem_stage_store(st, smem, t + 3, tid);
       __syncthreads();
     }
+  };
+  for (int t = t0; t < t1; t += 2) {
+    step(t, sa, sb);
+    if (t + 1 < t1) step(t + 1, sb, sa);
   }
   if (stats != nullptr) {
     // per lane (count, mean, M2) from the shifted sums, Chan-merged over the 16 pixel lanes of

@@ -12,6 +12,7 @@ for prog in ${PROGS:-attn resnet gemm}; do
     resnet) CMD="python3 tools/resnet_bench.py 1";;
     gemm) CMD="python3 tools/gemm_sq.py ${GEMM_CFGS:-128}";;
     wgrad) CMD="python3 tools/wgrad_kb.py";;
+    stem) CMD="python3 tools/stem_kbench.py 5";;
   esac
   for pass in A B; do
     if [ $pass = A ]; then P="$PA"; else P="$PB"; fi
