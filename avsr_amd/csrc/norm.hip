@@ -615,19 +615,22 @@ __global__ __launch_bounds__(256) void stem_pool_fwd_kernel(avsr_stem_pool_param
 // visits its taps in row-major order with the strict '>' (same maximum, same argmax on ties).
 // Grid-stride with the channel group fixed (per-channel coefficients loaded once).
 template <typename T>
-__global__ __launch_bounds__(256) void stem_pool_fwd2_kernel(avsr_stem_pool_params p) {
+__global__ __launch_bounds__(256) void stem_pool_fwd2_kernel(avsr_stem_pool_params p, FastDiv fbwo, FastDiv fbho) {
   constexpr int VE = VecW<T>::VE;
-  const int cpv = p.C / VE;
+  const int cpv = p.C / VE, cshift = 31 - __builtin_clz(cpv);
   const int bho = p.Ho >> 1, bwo = p.Wo >> 1;
-  const int64_t nv = (int64_t)p.nimg * bho * bwo * cpv, stride = (int64_t)gridDim.x * 256;
-  const int64_t t0 = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const int cv = (int)(t0 % cpv), c0 = cv * VE;
+  // 32-bit indices with multiply-shift divisions (the launcher checks nv < 2^31)
+  const uint32_t nv = (uint32_t)p.nimg * bho * bwo * cpv, stride = gridDim.x * 256u;
+  const uint32_t t0 = blockIdx.x * 256u + threadIdx.x;
+  const int cv = (int)(t0 & (cpv - 1)), c0 = cv * VE;
   float sc[VE], sh[VE], pw[VE];
   chan_load(p.scale, c0, sc); chan_load(p.shift, c0, sh); chan_load(p.prelu, c0, pw);
-  for (int64_t v = t0; v < nv; v += stride) {
-    const int64_t blk = v / cpv;
-    const int bw = (int)(blk % bwo), bh = (int)((blk / bwo) % bho);
-    const int64_t n = blk / ((int64_t)bwo * bho);
+  for (uint32_t v = t0; v < nv; v += stride) {
+    const uint32_t blk = v >> cshift, q = fdiv(blk, fbwo);
+    const int bw = (int)(blk - q * fbwo.d);
+    const uint32_t nq = fdiv(q, fbho);
+    const int bh = (int)(q - nq * fbho.d);
+    const int64_t n = nq;
     const int ih0 = 4 * bh - 1, iw0 = 4 * bw - 1;        // patch origin (may be -1)
     const T* base = (const T*)p.h + n * p.H * p.W * p.C + c0;
     float best[4][VE], bhv[4][VE];
@@ -751,13 +754,16 @@ __global__ __launch_bounds__(256) void stem_bwd_apply_kernel(avsr_stem_pool_para
 // for four outputs (2.25 window gathers per pixel otherwise), with no per-pixel divisions and
 // every load of the block issued together. Windows are added in the per-pixel kernel's order
 // (bit-identical).
-template <typename T>
-__global__ __launch_bounds__(256) void stem_bwd_apply2_kernel(avsr_stem_pool_params p) {
+template <typename T, int U>
+__global__ __launch_bounds__(256) void stem_bwd_apply2_kernel(avsr_stem_pool_params p, FastDiv fwo, FastDiv fho) {
   constexpr int VE = VecW<T>::VE;
-  const int cpv = p.C / VE;
-  const int64_t nv = (int64_t)p.nimg * p.Ho * p.Wo * cpv, stride = (int64_t)gridDim.x * 256;
-  const int64_t t0 = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const int cv = (int)(t0 % cpv), c0 = cv * VE;
+  const int cpv = p.C / VE, cshift = 31 - __builtin_clz(cpv);
+  // 32-bit indices with multiply-shift divisions (the launcher checks nv < 2^31; the int64
+  // divisions they replace were ~1/3 of this HBM-bound pass, 900 -> 737 us at C2). U blocks per
+  // iteration with every load issued first (U = 2 needs 198 VGPRs: 2 waves per SIMD instead of 3)
+  const uint32_t nv = (uint32_t)p.nimg * p.Ho * p.Wo * cpv, stride = gridDim.x * 256u;
+  const uint32_t t0 = blockIdx.x * 256u + threadIdx.x;
+  const int cv = (int)(t0 & (cpv - 1)), c0 = cv * VE;
   const float invM = 1.f / (p.m_total > 0 ? (float)p.m_total : (float)p.nimg * p.H * p.W);
   float ka[VE], kb[VE], kc[VE], km[VE];
 #pragma unroll
@@ -766,50 +772,57 @@ __global__ __launch_bounds__(256) void stem_bwd_apply2_kernel(avsr_stem_pool_par
     const float s0 = p.sums[c * 3 + 0] * invM, s1 = p.sums[c * 3 + 1] * invM;
     ka[j] = p.scale[c]; kb[j] = -p.scale[c] * s1 * p.invstd[c]; kc[j] = -p.scale[c] * s0; km[j] = p.mean[c];
   }
-  for (int64_t v = t0; v < nv; v += stride) {
-    const int64_t blk = v / cpv;                       // (n, oh, ow)
-    const int ow = (int)(blk % p.Wo), oh = (int)((blk / p.Wo) % p.Ho);
-    const int64_t n = blk / ((int64_t)p.Wo * p.Ho);
-    // windows w = (oh + a, ow + b), a, b in {0, 1}; out-of-range windows contribute nothing
-    float g[4][VE];
-    uint8_t am[4][VE];
-    bool wok[4];
+  for (uint32_t v0 = t0; v0 < nv; v0 += U * stride) {
+    float g[U][4][VE], h[U][4][VE];
+    uint8_t am[U][4][VE];
+    bool wok[U][4], ok[U];
+    uint32_t hb[U];                                    // vector index of pixel (2oh, 2ow)
 #pragma unroll
-    for (int w = 0; w < 4; ++w) {
-      const int wa = w >> 1, wb = w & 1;
-      wok[w] = oh + wa < p.Ho && ow + wb < p.Wo;
-      const int64_t ov = ((n * p.Ho + min(oh + wa, p.Ho - 1)) * p.Wo + min(ow + wb, p.Wo - 1)) * cpv + cv;
-      ldv((const T*)p.dz + ov * VE, g[w]);
-      if constexpr (VE == 8) *(uint2*)am[w] = *(const uint2*)(p.argmax + ov * VE);
-      else *(uint32_t*)am[w] = *(const uint32_t*)(p.argmax + ov * VE);
-    }
-    float h[4][VE];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int ih = 2 * oh + (q >> 1), iw = 2 * ow + (q & 1);
-      ldv((const T*)p.h + (((n * p.H + ih) * p.W + iw) * cpv + cv) * VE, h[q]);
-    }
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int dy = q >> 1, dx = q & 1;
-      float d[VE];
-#pragma unroll
-      for (int j = 0; j < VE; ++j) d[j] = 0.f;
-      // pixel (2oh+dy, 2ow+dx) sits at window-local position (dy+1, dx+1) of window (oh, ow)
-      // and at (dy-1, dx+1), (dy+1, dx-1), (dy-1, dx-1) of the others (rows: 3 per window)
+    for (int u = 0; u < U; ++u) {
+      const uint32_t v = v0 + u * stride;
+      ok[u] = v < nv;
+      const uint32_t blk = (ok[u] ? v : v0) >> cshift;   // (n, oh, ow)
+      const uint32_t q = fdiv(blk, fwo), n = fdiv(q, fho);
+      const int ow = (int)(blk - q * fwo.d), oh = (int)(q - n * fho.d);
+      // windows w = (oh + a, ow + b), a, b in {0, 1}; out-of-range windows contribute nothing
 #pragma unroll
       for (int w = 0; w < 4; ++w) {
         const int wa = w >> 1, wb = w & 1;
-        if ((wa && !dy) || (wb && !dx)) continue;      // the pixel is not in that window
-        const uint8_t want = (uint8_t)((dy - 2 * wa + 1) * 3 + (dx - 2 * wb + 1));
-#pragma unroll
-        for (int j = 0; j < VE; ++j) d[j] += (wok[w] && am[w][j] == want) ? g[w][j] : 0.f;
+        wok[u][w] = oh + wa < p.Ho && ow + wb < p.Wo;
+        const uint32_t ov = ((n * p.Ho + min(oh + wa, p.Ho - 1)) * p.Wo + min(ow + wb, p.Wo - 1)) * cpv + cv;
+        ldv((const T*)p.dz + (int64_t)ov * VE, g[u][w]);
+        if constexpr (VE == 8) *(uint2*)am[u][w] = *(const uint2*)(p.argmax + (int64_t)ov * VE);
+        else *(uint32_t*)am[u][w] = *(const uint32_t*)(p.argmax + (int64_t)ov * VE);
       }
-      float o[VE];
+      hb[u] = ((n * p.H + 2 * oh) * p.W + 2 * ow) * cpv + cv;
 #pragma unroll
-      for (int j = 0; j < VE; ++j) o[j] = ka[j] * d[j] + kb[j] * (h[q][j] - km[j]) + kc[j];
-      const int ih = 2 * oh + dy, iw = 2 * ow + dx;
-      stv((T*)p.dh + (((n * p.H + ih) * p.W + iw) * cpv + cv) * VE, o);
+      for (int qd = 0; qd < 4; ++qd)
+        ldv((const T*)p.h + (int64_t)(hb[u] + ((qd >> 1) * p.W + (qd & 1)) * cpv) * VE, h[u][qd]);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (!ok[u]) break;
+#pragma unroll
+      for (int qd = 0; qd < 4; ++qd) {
+        const int dy = qd >> 1, dx = qd & 1;
+        float d[VE];
+#pragma unroll
+        for (int j = 0; j < VE; ++j) d[j] = 0.f;
+        // pixel (2oh+dy, 2ow+dx) sits at window-local position (dy+1, dx+1) of window (oh, ow)
+        // and at (dy-1, dx+1), (dy+1, dx-1), (dy-1, dx-1) of the others (rows: 3 per window)
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+          const int wa = w >> 1, wb = w & 1;
+          if ((wa && !dy) || (wb && !dx)) continue;      // the pixel is not in that window
+          const uint8_t want = (uint8_t)((dy - 2 * wa + 1) * 3 + (dx - 2 * wb + 1));
+#pragma unroll
+          for (int j = 0; j < VE; ++j) d[j] += (wok[u][w] && am[u][w][j] == want) ? g[u][w][j] : 0.f;
+        }
+        float o[VE];
+#pragma unroll
+        for (int j = 0; j < VE; ++j) o[j] = ka[j] * d[j] + kb[j] * (h[u][qd][j] - km[j]) + kc[j];
+        stv((T*)p.dh + (int64_t)(hb[u] + (dy * p.W + dx) * cpv) * VE, o);
+      }
     }
   }
 }
@@ -964,9 +977,12 @@ extern "C" int avsr_stem_pool_fwd(const avsr_stem_pool_params* p, void* stream) 
   const char* pp = getenv("AVSR_STEM_APPLY_PIXEL");   // A/B: the per-pixel kernels
   if (p->H == 2 * p->Ho && p->W == 2 * p->Wo && !(p->Ho & 1) && !(p->Wo & 1) && !(pp && pp[0] == '1') &&
       256 % (p->C / ve) == 0) {
-    const int g2 = bn_grid((int64_t)p->nimg * (p->Ho / 2) * (p->Wo / 2) * p->C / ve, p->C / ve);
-    if (p->dtype == AVSR_BF16) hipLaunchKernelGGL(stem_pool_fwd2_kernel<bf16>, dim3(g2), dim3(256), 0, (hipStream_t)stream, *p);
-    else hipLaunchKernelGGL(stem_pool_fwd2_kernel<float>, dim3(g2), dim3(256), 0, (hipStream_t)stream, *p);
+    const int64_t nv2 = (int64_t)p->nimg * (p->Ho / 2) * (p->Wo / 2) * p->C / ve;
+    if (nv2 >= (1ll << 31)) return AVSR_E_SHAPE;
+    const int g2 = bn_grid(nv2, p->C / ve);
+    const FastDiv fbwo = make_fastdiv(p->Wo / 2), fbho = make_fastdiv(p->Ho / 2);
+    if (p->dtype == AVSR_BF16) hipLaunchKernelGGL(stem_pool_fwd2_kernel<bf16>, dim3(g2), dim3(256), 0, (hipStream_t)stream, *p, fbwo, fbho);
+    else hipLaunchKernelGGL(stem_pool_fwd2_kernel<float>, dim3(g2), dim3(256), 0, (hipStream_t)stream, *p, fbwo, fbho);
     AVSR_CHECK_LAUNCH();
     return 0;
   }
@@ -988,9 +1004,12 @@ extern "C" int avsr_stem_pool_bwd_apply(const avsr_stem_pool_params* p, void* st
   const char* pp = getenv("AVSR_STEM_APPLY_PIXEL");   // A/B: the per-pixel kernel
   const bool per_pixel = pp && pp[0] == '1';
   if (!(p->H & 1) && !(p->W & 1) && !per_pixel) {     // 2x2-block kernel (same result)
-    const int g2 = bn_grid((int64_t)p->nimg * p->Ho * p->Wo * p->C / ve, p->C / ve);
-    if (p->dtype == AVSR_BF16) hipLaunchKernelGGL(stem_bwd_apply2_kernel<bf16>, dim3(g2), dim3(256), 0, (hipStream_t)stream, *p);
-    else hipLaunchKernelGGL(stem_bwd_apply2_kernel<float>, dim3(g2), dim3(256), 0, (hipStream_t)stream, *p);
+    const int64_t nv2 = (int64_t)p->nimg * p->Ho * p->Wo * p->C / ve;
+    if (nv2 >= (1ll << 31) || (int64_t)p->nimg * p->H * p->W * p->C / ve >= (1ll << 31)) return AVSR_E_SHAPE;
+    const int g2 = bn_grid(nv2, p->C / ve);
+    const FastDiv fwo = make_fastdiv(p->Wo), fho = make_fastdiv(p->Ho);
+    if (p->dtype == AVSR_BF16) hipLaunchKernelGGL((stem_bwd_apply2_kernel<bf16, 1>), dim3(g2), dim3(256), 0, (hipStream_t)stream, *p, fwo, fho);
+    else hipLaunchKernelGGL((stem_bwd_apply2_kernel<float, 1>), dim3(g2), dim3(256), 0, (hipStream_t)stream, *p, fwo, fho);
     AVSR_CHECK_LAUNCH();
     return 0;
   }
