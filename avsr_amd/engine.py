@@ -522,14 +522,16 @@ class Engine:
                   and vid.numel() * vid.element_size() < ops.STEM_DIRECT_MAX_BYTES)
         # the packed 8-channel input: the general conv's operand, and the stem weight-grad's. With
         # the direct conv only the weight-grad (end of the backward) reads it: packed on the side
-        # stream, off the forward's serial chain (joined with the CTC branch at the forward's end)
+        # stream after the ResNet forward (beside the encoder's GEMMs rather than the HBM-heavy
+        # stem conv), off the forward's serial chain (joined with the CTC branch at its end)
         xp = None
+        side_pack = False
         if not direct:
             xp = self._e(N, 88, 88, 8)
             ops.stem_pack(vid, xp)
         elif save:
             xp = self._e(N, 88, 88, 8)
-            self._on_side(lambda: ops.stem_pack(vid, xp), vid, xp)
+            side_pack = True
         if direct:      # bf16: the stem conv reads the video itself (stem.hip, K = 288 instead of 392)
             wk = self._e(64, ops.STEM_K)
             ops.stem_wpack2(self.arena.master(R + "frontend3D.0.weight"), wk)
@@ -579,6 +581,8 @@ class Engine:
             hw = ho
         feat = self._e(N, 512)
         ops.avgpool_fwd(x, N, hw * hw, 512, feat)
+        if side_pack:
+            self._on_side(lambda: ops.stem_pack(vid, xp), vid, xp)
         if self._nbt:
             torch._foreach_add_(self._nbt, 1)
         self._nbt = None
