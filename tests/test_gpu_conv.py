@@ -195,12 +195,13 @@ def test_conv_stats_at_192_eligible_shape(dev, dtype):
     assert _rel(var, yf.var(0, unbiased=False)) < 1e-3
 
 
-def test_stem_conv_direct(dev):
+@pytest.mark.parametrize("B,T", [(2, 7), (1, 375)])
+def test_stem_conv_direct(dev, B, T):
     """stem Conv3d (k 5x7x7, stride 1x2x2, pad 2x3x3) straight from the fp32 video
     (stem.hip, K = 288 grouped (frame, row) x 8 columns) vs fp64 conv3d on the same
-    bf16-rounded operands; BN partial statistics combine to the batch moments. T = 7 so
-    that frames outside the clip (time padding) are hit at both ends."""
-    B, T = 2, 7
+    bf16-rounded operands; BN partial statistics combine to the batch moments. T = 7: frames
+    outside the clip (time padding) are hit at both ends by one run; T = 375: 23 runs of 17
+    frames per band, the last one a single frame (the ring's frames loaded ahead of a run's end)."""
     g = torch.Generator().manual_seed(11)
     video = torch.randn(B, 1, T, 88, 88, generator=g)
     w = torch.randn(64, 1, 5, 7, 7, generator=g) * 0.05
