@@ -43,6 +43,7 @@ class GemmParams(ctypes.Structure):
         ("stamp", _c_p),
         ("skinny_ws", _c_p), ("ln_c1", _c_p), ("ln_eps", ctypes.c_float),
         ("kv_k", _c_p), ("kv_v", _c_p), ("kv_pos", _c_p), ("kv_rows", _i),
+        ("slab_cnt", _c_p),
     ]
 
 
@@ -245,6 +246,8 @@ class VideoNormParams(ctypes.Structure):
 
 SYMBOLS = {
     "avsr_version": ([], ctypes.c_char_p),
+    "avsr_set_option": ([_i, _i64], _i),
+    "avsr_get_option": ([_i], _i64),
     "avsr_gemm": ([ctypes.POINTER(GemmParams), _c_p], _i),
     "avsr_gemm_skinny_splits": ([_i, _i, _i], _i),
     "avsr_conv_fwd": ([ctypes.POINTER(ConvParams), _c_p], _i),
@@ -338,6 +341,28 @@ def load():
 def check(rc, op):
     if rc != 0:
         raise AvsrLibError(f"{op} failed with code {rc}")
+
+
+# kernel-selection options (avsr_hip.h AVSR_OPT_*, AVSR_TILE_*): A/B tools and variant tests
+OPTIONS = {"gemm_tile": 0, "attn_sq_fwd": 1, "attn_sq_bwd": 2, "wgrad_dual": 3, "conv_192": 4, "conv_s2phase": 5,
+           "conv_patch": 6, "conv_wpatch": 7, "stem_pool_2x2": 8}
+TILES = ["128", "256", "256x128", "128x256", "128s3", "128s4", "128w8s3", "128w8s4", "pp", "96", "128x64", "192",
+         "192x256", "192s3", "192w8", "192w8s3", "64"]
+
+
+def set_option(name, value):
+    """avsr_set_option by name; gemm_tile takes a tile name (TILES) or None / "auto"; returns
+    the previous value"""
+    if name == "gemm_tile" and not isinstance(value, int):
+        value = 0 if value in (None, "auto") else TILES.index(value) + 1
+    lib = load()
+    prev = get_option(name)
+    check(lib.avsr_set_option(OPTIONS[name], int(value)), f"avsr_set_option({name}, {value})")
+    return prev
+
+
+def get_option(name):
+    return int(load().avsr_get_option(OPTIONS[name]))
 
 
 _raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)

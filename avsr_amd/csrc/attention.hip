@@ -1659,12 +1659,9 @@ extern "C" int avsr_debug_attn_stamps(unsigned long long* buf) {
   return (int)hipMemcpyToSymbol(HIP_SYMBOL(res::g_stamps), &buf, sizeof(buf));
 }
 
-// query-tiled streamed kernels for the encoder's self-attention (AVSR_ATTN_SQ=0: the resident
-// kernels, A/B runs)
-static bool sq_enabled() {
-  const char* e = getenv("AVSR_ATTN_SQ");
-  return !(e && e[0] == '0');
-}
+// query-tiled streamed kernels for the encoder's self-attention (AVSR_OPT_ATTN_SQ_FWD = 0: the
+// resident kernels, A/B runs)
+static bool sq_enabled() { return avsr_opt(AVSR_OPT_ATTN_SQ_FWD) != 0; }
 
 extern "C" int avsr_attn_fwd(const avsr_attn_params* p, void* stream) {
   int rc = check(p);
@@ -1702,8 +1699,7 @@ extern "C" int avsr_attn_fwd(const avsr_attn_params* p, void* stream) {
 // faster (C2 with dropout 93.7 vs 101.5 us), but inside the training step, beside the weight-
 // gradient GEMMs of the side stream, it took 144 vs 100 us per layer (profiles/r04_*)
 static bool sq_bwd(const avsr_attn_params* p) {
-  const char* e = getenv("AVSR_ATTN_SQ_BWD");
-  const bool force = e && e[0] == '1';
+  const bool force = avsr_opt(AVSR_OPT_ATTN_SQ_BWD) != 0;
   return p->dtype == AVSR_BF16 && !p->causal && p->Lq >= 128 && p->Lk >= 128 && res::small_index(p) && sq_enabled() &&
          (force || p->Lq > res::MAXR || p->Lk > res::MAXR);
 }

@@ -202,6 +202,9 @@ AVSR_DEV f32x16 mfma32(const bf16x8& a, const bf16x8& b, const f32x16& c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
 
+// kernel-selection options (avsr_set_option, version.hip); the library reads no environment
+int64_t avsr_opt(int option);
+
 #define AVSR_CHECK_LAUNCH() do { hipError_t e_ = hipGetLastError(); if (e_ != hipSuccess) return (int)e_; } while (0)
 
 static inline int avsr_aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }

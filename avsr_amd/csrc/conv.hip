@@ -429,11 +429,9 @@ static bool conv_glds_enabled() { return true; }
 
 // 192x128 for the k-major-A directions (forward, data-grad) where it still runs >= 2 blocks per
 // CU and its rounds carry no more work than 128x128's (the dense rule, gemm.hip tile_cfg):
-// ResNet stages 2-3 at C2; AVSR_CONV_192=0 disables it (A/B)
+// ResNet stages 2-3 at C2 (video fwd 9.09 -> 8.83 ms, bwd 17.13 -> 16.84, profiles/r02_resnet_c192_ab.txt)
 static bool conv192(int M, int N, int groups) {
-  if (N <= 64 || M <= 64 || !conv_glds_enabled()) return false;
-  const char* e = getenv("AVSR_CONV_192");
-  if (e && e[0] == '0') return false;
+  if (N <= 64 || M <= 64 || !conv_glds_enabled() || !avsr_opt(AVSR_OPT_CONV_192)) return false;
   const long tn = (long)((N + 127) / 128) * groups;
   const long n128 = ((long)((M + 127) / 128) * tn + 255) / 256, n192 = ((long)((M + 191) / 192) * tn + 255) / 256;
   return n192 >= 2 && 3 * n192 * 50 <= 2 * n128 * 51;
@@ -568,8 +566,7 @@ static void s2_classes(const avsr_conv_params* p, S2Class (&c)[4]) {
 
 // the parity-class path: bf16 buffer-DMA loaders (tap-uniform K-tiles), one group, stride 2
 static bool s2_phase(const avsr_conv_params* p) {
-  const char* e = getenv("AVSR_CONV_S2PHASE");
-  if (e && e[0] == '0') return false;
+  if (!avsr_opt(AVSR_OPT_CONV_S2PHASE)) return false;
   if (p->sh != 2 || p->sw != 2 || p->groups != 1 || p->dtype != AVSR_BF16 || !conv_glds_enabled()) return false;
   if (p->cout % 64) return false;
   ConvArgs t;
@@ -933,11 +930,9 @@ __global__ __launch_bounds__(256) void wpatch_reduce_kernel(float* __restrict__ 
 }
 
 // the patch-resident weight-grad applies: bf16, slab workspace, automatic split, 3x3 / stride 1
-// / pad 1, one group, the stage-1 (22 x 22, 64 -> 64) or stage-2 (11 x 11, 128 -> 128) geometry;
-// AVSR_CONV_WPATCH=0 keeps the general kernel (A/B comparisons)
+// / pad 1, one group, the stage-1 (22 x 22, 64 -> 64) or stage-2 (11 x 11, 128 -> 128) geometry
 static bool wpatch_ok(const avsr_conv_params* p) {
-  const char* env = getenv("AVSR_CONV_WPATCH");
-  if ((env && env[0] == '0') || p->dtype != AVSR_BF16 || !conv_glds_enabled() || p->groups != 1 || p->splitk > 0)
+  if (!avsr_opt(AVSR_OPT_CONV_WPATCH) || p->dtype != AVSR_BF16 || !conv_glds_enabled() || p->groups != 1 || p->splitk > 0)
     return false;
   if (p->kh != 3 || p->kw != 3 || p->sh != 1 || p->sw != 1 || p->ph != 1 || p->pw != 1) return false;
   if (p->cin != p->cout || p->ldx != p->cin || p->ldy != p->cout || p->hin != p->hout || p->win != p->wout) return false;
@@ -974,10 +969,9 @@ static int wpatch_launch(const avsr_conv_params* p, hipStream_t st) {
   return wpatch_launch_g<WPStage2>(p, st);
 }
 
-// AVSR_CONV_PATCH=0 keeps the general kernel (A/B comparisons)
+// the patch-resident stage-1 kernel applies (bf16, 3x3 / stride 1 / pad 1, 64 -> 64 channels)
 static bool patch_ok(const avsr_conv_params* p, const ConvArgs& a) {
-  const char* env = getenv("AVSR_CONV_PATCH");
-  if ((env && env[0] == '0') || p->dtype != AVSR_BF16 || !conv_glds_enabled() || !a.a_bytes || p->groups != 1) return false;
+  if (!avsr_opt(AVSR_OPT_CONV_PATCH) || p->dtype != AVSR_BF16 || !conv_glds_enabled() || !a.a_bytes || p->groups != 1) return false;
   if (p->kh != 3 || p->kw != 3 || p->sh != 1 || p->sw != 1 || p->ph != 1 || p->pw != 1) return false;
   if (p->cin != 64 || p->cout != 64 || p->ldx != 64 || p->ldy != 64) return false;
   if (p->hin != p->hout || p->win != p->wout) return false;

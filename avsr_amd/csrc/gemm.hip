@@ -332,18 +332,11 @@ using Cfg192w8 = gemmg::GCfg<2, 4, 3, 1, 2>;     // 192x128, 8 waves (96x32 each
 using Cfg192w8s3 = gemmg::GCfg<2, 4, 3, 1, 3>;   // 192x128, 8 waves, 3 stages (120 KiB)
 using Cfg64 = gemmg::GCfg<2, 2, 1, 1, 2>;        // 64x64, 4 waves (32x32 each), 2 stages (32 KiB)
 
-// tile choice: AVSR_GEMM_TILE=128|256|256x128|128x256 forces one (benchmarks); otherwise the
-// configuration with the fewest block rounds x per-tile work (wave quantisation over 256 CUs)
-bool getenv_flag(const char* name);
-
+// tile choice: AVSR_OPT_GEMM_TILE = k + 1 forces configuration k (AVSR_TILE_*, benchmarks);
+// otherwise the configuration with the fewest block rounds x per-tile work (wave quantisation
+// over 256 CUs)
 int tile_cfg(const avsr_gemm_params* p, int splits) {
-  const char* e = getenv("AVSR_GEMM_TILE");
-  const int forced = !e ? -1 : !strcmp(e, "128") ? 0 : !strcmp(e, "256") ? 1 : !strcmp(e, "256x128") ? 2
-                   : !strcmp(e, "128x256") ? 3 : !strcmp(e, "128s3") ? 4 : !strcmp(e, "128s4") ? 5
-                   : !strcmp(e, "128w8s3") ? 6 : !strcmp(e, "128w8s4") ? 7 : !strcmp(e, "pp") ? 8
-                   : !strcmp(e, "96") ? 9 : !strcmp(e, "128x64") ? 10 : !strcmp(e, "192") ? 11
-                   : !strcmp(e, "192x256") ? 12 : !strcmp(e, "192s3") ? 13 : !strcmp(e, "192w8") ? 14
-                   : !strcmp(e, "192w8s3") ? 15 : !strcmp(e, "64") ? 16 : -1;
+  const int forced = (int)avsr_opt(AVSR_OPT_GEMM_TILE) - 1;
   if (forced >= 0) return forced;
   // 128x128 at two blocks per CU is the default (tools/gemm_table.py, profiles/r02_gemm_table.*:
   // the 256x256 ping-pong core loses 8-36 % at M = 6000, the 3-stage / 8-wave variants are
@@ -369,7 +362,7 @@ int tile_cfg(const avsr_gemm_params* p, int splits) {
     const long tiles_z = (long)p->batch * splits;
     const long t128 = (long)((p->M + 127) / 128) * ((p->N + 127) / 128) * tiles_z;
     const long t64 = (long)((p->M + 63) / 64) * ((p->N + 63) / 64) * tiles_z;
-    if (t128 < 256 && t64 >= 2 * t128 && !getenv_flag("AVSR_GEMM_NO64")) return 16;
+    if (t128 < 256 && t64 >= 2 * t128) return 16;
   }
   return 0;
 }
@@ -471,11 +464,6 @@ int by_tile(const avsr_gemm_params* p, const DenseArgs& a, hipStream_t st) {
   if (p->N <= 64) return by_layout<T, OutT, 4, 1>(p, a, st);
   if (p->M <= 64) return by_layout<T, OutT, 1, 4>(p, a, st);
   return by_layout<T, OutT, 2, 2>(p, a, st);
-}
-
-bool getenv_flag(const char* name) {
-  const char* e = getenv(name);
-  return e && e[0] == '1';
 }
 
 // ---------------------------------------------------------------- skinny (M <= 64) linears
@@ -851,7 +839,7 @@ int skinny_mma_splits(int N, int K, int& kchunk) {
 }
 
 bool skinny_mma_ok(const DenseArgs& a) {
-  return a.K % 16 == 0 && a.lda % 4 == 0 && a.ldb % 4 == 0 && !getenv_flag("AVSR_SKINNY_VALU");
+  return a.K % 16 == 0 && a.lda % 4 == 0 && a.ldb % 4 == 0;
 }
 
 template <typename T, typename OutT>
@@ -915,10 +903,9 @@ int skinny_launch(const DenseArgs& a, float* ws, hipStream_t st) {
 using CfgDual = gemmg::GCfg<2, 2, 2, 2, 2>;       // per wave group of wgrad_dual_kernel (8 waves, 128 KiB)
 
 // weight-gradient shape (dy^T x: both operands r-contiguous, fp32 C, plain epilogue, one batch):
-// the in-block split-K kernel (AVSR_WGRAD_DUAL=0 keeps the 4-wave core: A/B runs)
+// the in-block split-K kernel (AVSR_OPT_WGRAD_DUAL = 0 keeps the 4-wave core: A/B runs)
 bool wgrad_dual_ok(const avsr_gemm_params* p, int splits, bool slab) {
-  const char* e = getenv("AVSR_WGRAD_DUAL");
-  const bool off = e && e[0] == '0';
+  const bool off = avsr_opt(AVSR_OPT_WGRAD_DUAL) == 0;
   return !off && !p->a_kmajor && !p->b_kmajor && p->c_f32 && p->batch == 1 && (splits == 1 || slab) && !p->bias &&
          !p->act && !p->preact && !p->res && !p->gate && p->drop_p == 0.f && !p->epi_bwd && !p->db &&
          (p->ldc % 4) == 0 && avsr_aligned16(p->C);
@@ -1027,9 +1014,9 @@ extern "C" int avsr_gemm(const avsr_gemm_params* p, void* stream) {
   }
   if (glds && wgrad_dual_ok(p, splits, slab)) {
     const int tiles = ((p->M + CfgDual::BM - 1) / CfgDual::BM) * ((p->N + CfgDual::BN - 1) / CfgDual::BN);
-    if (slab && p->skinny_ws && tiles <= AVSR_SKINNY_CNT &&
+    if (slab && p->slab_cnt && tiles <= AVSR_SLAB_CNT &&
         (int64_t)splits * a.sSplit * 4 < (1ll << 31)) {   // in-kernel slab reduction (no slab_reduce pass)
-      a.cnt = (unsigned*)(p->skinny_ws + AVSR_SKINNY_WS);
+      a.cnt = p->slab_cnt;
       a.fC = (float*)p->C; a.fldc = p->ldc; a.falpha = p->alpha; a.fbeta = p->beta;
       return launch_wgrad_dual<CfgDual>(a, st);
     }
@@ -1058,6 +1045,6 @@ extern "C" int avsr_gemm(const avsr_gemm_params* p, void* stream) {
 extern "C" int avsr_gemm_skinny_splits(int dtype, int N, int K) {
   if (N <= 0 || K <= 0) return 1;
   int kchunk;
-  if (dtype == AVSR_F32 && K % 16 == 0 && !getenv_flag("AVSR_SKINNY_VALU")) return skinny_mma_splits(N, K, kchunk);
+  if (dtype == AVSR_F32 && K % 16 == 0) return skinny_mma_splits(N, K, kchunk);
   return skinny_splits(N, K, kchunk);
 }

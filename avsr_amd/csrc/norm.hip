@@ -181,18 +181,11 @@ __global__ __launch_bounds__(64 * W) void ln_bwd_kernel(LnArgs a) {
   }
 }
 
-// LayerNorm backward launch shape: AVSR_LN_BWD = "W,R" (waves per block, rows in flight per
-// wave) for experiments. Default 4,1: in isolation (tools/ln_bench.py) 6000 x 1024 takes
-// 18.3-20.1 us with 4-8 waves (2 waves: 26 us; 16 waves: 38 us), 8-16 waves lose 2x at N = 2048,
-// and in the step 4,1 beats 2,x and 8,x by 0.5-1 % (profiles/r02_ln_bwd_shape_ab.txt)
-static void ln_bwd_shape(int& W, int& R) {
-  W = 4; R = 1;
-  const char* e = getenv("AVSR_LN_BWD");
-  const char* comma = e ? strchr(e, ',') : nullptr;
-  if (comma) { W = atoi(e); R = atoi(comma + 1); }
-  if (W != 2 && W != 4 && W != 8 && W != 16) W = 8;
-  if (R != 1 && R != 2) R = 2;
-}
+// LayerNorm backward launch shape: 4 waves per block, one row in flight per wave. In isolation
+// 6000 x 1024 takes 18.3-20.1 us with 4-8 waves (2 waves: 26 us; 16 waves: 38 us), 8-16 waves
+// lose 2x at N = 2048, and in the step 4,1 beats 2,x and 8,x by 0.5-1 %
+// (profiles/r02_ln_bwd_shape_ab.txt)
+static void ln_bwd_shape(int& W, int& R) { W = 4; R = 1; }
 
 static int ln_bwd_blocks() { return AVSR_LN_BLOCKS; }
 
@@ -974,8 +967,7 @@ extern "C" int avsr_stem_pool_fwd(const avsr_stem_pool_params* p, void* stream) 
   const int ve = p->dtype == AVSR_BF16 ? 8 : 4;
   if (p->C % ve) return AVSR_E_SHAPE;
   if (p->nimg > 65535) return AVSR_E_SHAPE;
-  const char* pp = getenv("AVSR_STEM_APPLY_PIXEL");   // A/B: the per-pixel kernels
-  if (p->H == 2 * p->Ho && p->W == 2 * p->Wo && !(p->Ho & 1) && !(p->Wo & 1) && !(pp && pp[0] == '1') &&
+  if (p->H == 2 * p->Ho && p->W == 2 * p->Wo && !(p->Ho & 1) && !(p->Wo & 1) && avsr_opt(AVSR_OPT_STEM_POOL_2X2) &&
       256 % (p->C / ve) == 0) {
     const int64_t nv2 = (int64_t)p->nimg * (p->Ho / 2) * (p->Wo / 2) * p->C / ve;
     if (nv2 >= (1ll << 31)) return AVSR_E_SHAPE;
@@ -1001,9 +993,7 @@ extern "C" int avsr_stem_pool_bwd_apply(const avsr_stem_pool_params* p, void* st
   if (256 % (p->C / ve)) return AVSR_E_SHAPE;
   if ((int64_t)p->nimg * p->H * p->W >= (1ll << 31)) return AVSR_E_SHAPE;
   if (p->Ho != (p->H + 1) / 2 || p->Wo != (p->W + 1) / 2) return AVSR_E_SHAPE;
-  const char* pp = getenv("AVSR_STEM_APPLY_PIXEL");   // A/B: the per-pixel kernel
-  const bool per_pixel = pp && pp[0] == '1';
-  if (!(p->H & 1) && !(p->W & 1) && !per_pixel) {     // 2x2-block kernel (same result)
+  if (!(p->H & 1) && !(p->W & 1) && avsr_opt(AVSR_OPT_STEM_POOL_2X2)) {     // 2x2-block kernel (same result)
     const int64_t nv2 = (int64_t)p->nimg * p->Ho * p->Wo * p->C / ve;
     if (nv2 >= (1ll << 31) || (int64_t)p->nimg * p->H * p->W * p->C / ve >= (1ll << 31)) return AVSR_E_SHAPE;
     const int g2 = bn_grid(nv2, p->C / ve);

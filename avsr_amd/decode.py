@@ -67,6 +67,17 @@ def end_detect(ended_hyps, i, M=3, D_end=D_END):
     return count == M
 
 
+_CAPTURE_STREAMS = {}
+
+
+def _capture_stream(dev):
+    """one graph-capture stream per device for every search (its workspaces are reused)"""
+    s = _CAPTURE_STREAMS.get(dev)
+    if s is None:
+        s = _CAPTURE_STREAMS[dev] = torch.cuda.Stream(device=dev)
+    return s
+
+
 class BatchBeamSearch:
     """Beam search over one utterance with the decoder + CTC prefix scorers of an E2E model
     running on its HIP engine."""
@@ -91,6 +102,12 @@ class BatchBeamSearch:
 
     def __call__(self, x, maxlenratio: float = 0.0, minlenratio: float = 0.0):
         return self.forward(x, maxlenratio, minlenratio)
+
+    def _cross_group(self, Tm):
+        """hypotheses of one utterance per cross-attention workgroup: the beam, while its
+        [beam][Tm] scores fit the grouped kernel's LDS (about 2.7 k frames at beam 5)"""
+        G = self.beam_size if self.beam_size <= 8 else 1
+        return G if ops.dec_attn_group_fits(Tm, G) else 1
 
     # ----------------------------------------------------------------------- decoder step
     def _decoder_step(self, eng, st):
@@ -132,7 +149,7 @@ class BatchBeamSearch:
             kv = st["mem"][i]
             ops.dec_attn(q2, kv[:, :D], kv[:, D:], o2, n=R, H=H, klen_max=Tm, k_bstride=Tm * kv.stride(0),
                          v_bstride=Tm * kv.stride(0), kidx=st["uidx"], klen=st["klen_mem"],
-                         group=self.beam_size if self.beam_size <= 8 else 1, ksplit=2)
+                         group=self._cross_group(Tm), ksplit=2)
             y2 = ops.linear_fwd(o2, eng.w(ca + "linear_out.weight"), ar.master(ca + "linear_out.bias"), res=y1)
             if fold is not None:
                 Wg, bb, c1 = fold[i]["ff1"]
@@ -288,11 +305,17 @@ class BatchBeamSearch:
         return self._collect(st, xs, maxlenratio, minlenratio)
 
     def _capture(self, eng, st):
-        """two graphs of the generic step (k = 0, 1): capture records, it does not run"""
+        """two graphs of the generic step (k = 0, 1): capture records, it does not run. The
+        capture stream is one long-lived stream per device, and its workspaces (split-K arrival
+        counters, which must start at zero, and the dec_attn partials) are created eagerly
+        before the capture: a zero-fill recorded inside graph 0 would never run before graph 1's
+        first replay."""
         dev = eng.device
         graphs = []
-        s = torch.cuda.Stream(device=dev)
+        s = _capture_stream(dev)
         s.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(s):
+            ops.reserve_stream_workspaces(dev, ops.dec_attn_ws_floats(st["R"], eng.dH, self._cross_group(st["Tm"]), 2))
         for k in (0, 1):
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, stream=s):

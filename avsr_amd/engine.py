@@ -49,6 +49,10 @@ _STEM_DIRECT = True
 # encoder residual-branch dropout backward (+ bias gradient) fused into the LayerNorm backward
 # that produces its input gradient
 _LN_EW_FUSE = True
+# weight-gradients, the forward's CTC branch and the gradient clear on a second stream beside the
+# data-gradient chain (off: in line on the step stream; 54.3 vs 51.0 ms per video-on step,
+# profiles/r04_side_stream_ab.txt)
+SIDE_STREAM = True
 
 
 _STEP_STREAMS = {}
@@ -80,10 +84,10 @@ def wgrad_splitk(M, N, K):
     blocks. The library runs weight-gradients as 8-wave blocks that already split their K range
     between two wave groups (gemm.hip wgrad_dual_kernel, one block per CU), so the block grid is
     split only when the 128x128 tiles fill less than half the chip (out-proj 1024x1024: 64 tiles
-    x 4), through a slab workspace (no atomics). AVSR_WGRAD_DUAL=0 (A/B): the 4-wave core at two
-    blocks per CU with its 512-block target."""
+    x 4), through a slab workspace (no atomics). With the library option wgrad_dual = 0 (A/B):
+    the 4-wave core at two blocks per CU with its 512-block target."""
     tiles = ((N + 127) // 128) * ((K + 127) // 128)
-    if os.environ.get("AVSR_WGRAD_DUAL", "1") == "0":
+    if ops.L.get_option("wgrad_dual") == 0:
         return 1 if tiles > 256 else max(1, min(16, 512 // max(tiles, 1), M // 512))
     return 1 if tiles >= 128 else max(1, min(16, 256 // max(tiles, 1), M // 1024))
 
@@ -150,10 +154,9 @@ class Engine:
         self.capture = None          # tests: a dict receives the last forward's enc / logits / batch
         self._pinned = [(None, None)] * 4
         self._pin_next = 0
-        import os
         self._nbt = None
         self.side = (torch.cuda.Stream(device=self.device)
-                     if self.device.type == "cuda" and os.environ.get("AVSR_SIDE_STREAM", "1") != "0" else None)
+                     if self.device.type == "cuda" and SIDE_STREAM else None)
         # reused events: a stream wait binds the record that precedes it
         self._side_ev = [torch.cuda.Event() for _ in range(8)] if self.side is not None else []
         self._side_i = 0
@@ -1123,6 +1126,9 @@ class Engine:
     def encoder_backward(self, ectx, denc):
         """encoder-only backward (the reference call form model.encoder(...) trained alone,
         surface._EncoderStep) with backward()'s data-parallel hooks and finalise batching"""
+        # as in backward(): the side stream's work from the forward (the bf16 stem's packed
+        # input for its weight-grad, a zero_grad_async clear) must land before the first write
+        self.join_side()
         if self.before_backward is not None:
             self.before_backward()
         prev = ops.colsum_defer(_COLSUM_DEFER)

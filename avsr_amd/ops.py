@@ -53,14 +53,55 @@ def skinny_splits(N, K, dtype=torch.float32):
     return int(L.load().avsr_gemm_skinny_splits(code, int(N), int(K)))
 
 
+def _norm_dev(device):
+    """workspace-cache key of a device: always with its index"""
+    device = torch.device(device)
+    return device if device.index is not None else torch.device(device.type, torch.cuda.current_device())
+
+
 def _skinny_ws(device):
     """per (device, stream) partial-sum workspace of the few-row GEMM path: launches on one
-    stream run in order, so one buffer per stream is never read and written at once"""
+    stream run in order, so one buffer per stream is never read and written at once. Its
+    arrival counters must start at zero: a stream that will be captured into a graph gets its
+    workspace from reserve_stream_workspaces() BEFORE the capture (a zero-fill recorded inside
+    a capture only runs when that graph is replayed)."""
+    device = _norm_dev(device)
     key = (device, L.stream_ptr().value)
     ws = _SKINNY_WS.get(key)
     if ws is None:
+        if torch.cuda.is_current_stream_capturing():
+            raise L.AvsrLibError("few-row GEMM workspace first requested inside a graph capture: call "
+                                 "ops.reserve_stream_workspaces() on the capture stream before capturing")
         ws = _SKINNY_WS[key] = torch.zeros(SKINNY_WS + SKINNY_CNT, device=device, dtype=torch.float32)
     return ws
+
+
+_SLAB_CNT = {}
+SLAB_CNT = 4096            # AVSR_SLAB_CNT
+
+
+def _slab_cnt(device):
+    """per (device, stream) zeroed arrival counters of the slab split-K weight-gradients (every
+    launch leaves them zero; launches on one stream run in order)"""
+    key = (_norm_dev(device), L.stream_ptr().value)
+    c = _SLAB_CNT.get(key)
+    if c is None:
+        if torch.cuda.is_current_stream_capturing():
+            raise L.AvsrLibError("slab counters first requested inside a graph capture")
+        c = _SLAB_CNT[key] = torch.zeros(SLAB_CNT, device=key[0], dtype=torch.int32)
+    return c
+
+
+def reserve_stream_workspaces(device, dec_attn_floats=0):
+    """create (zeroed) the current stream's few-row GEMM workspace and size its dec_attn
+    partial buffer to at least `dec_attn_floats`, eagerly — call outside any graph capture"""
+    assert not torch.cuda.is_current_stream_capturing()
+    device = _norm_dev(device)
+    _skinny_ws(device)
+    key = (device, L.stream_ptr().value)
+    ws = _DA_WS.get(key)
+    if dec_attn_floats and (ws is None or ws.numel() < dec_attn_floats):
+        _DA_WS[key] = torch.empty(dec_attn_floats, device=device, dtype=torch.float32)
 
 
 def gemm(A, B, C, *, M, N, K, a_kmajor, b_kmajor, lda, ldb, ldc, batch=1,
@@ -105,7 +146,7 @@ def gemm(A, B, C, *, M, N, K, a_kmajor, b_kmajor, lda, ldb, ldc, batch=1,
     if (SKINNY_SPLIT if skinny_split is None else skinny_split) and M <= 64 and splitk <= 1:
         p.skinny_ws = _skinny_ws(A.device).data_ptr()   # K-split partials of the few-row vector-ALU path
     elif ws is not None and splitk > 1 and SLAB_FUSED_REDUCE:
-        p.skinny_ws = _skinny_ws(A.device).data_ptr()   # arrival counters: in-kernel slab reduction
+        p.slab_cnt = _slab_cnt(A.device).data_ptr()     # arrival counters: in-kernel slab reduction
     if ln_c1 is not None:
         assert ln_c1.dtype == torch.float32 and ln_c1.numel() >= N and dt == L.AVSR_F32
         p.ln_c1, p.ln_eps = ln_c1.data_ptr(), float(ln_eps)
@@ -778,6 +819,20 @@ def log_softmax_rows(x, V, out):
 
 
 _DA_WS = {}
+DA_WAVES = 8               # waves per dec_attn workgroup (decode.hip)
+
+
+def dec_attn_group_fits(klen_max, group):
+    """the grouped dec_attn keeps [group][klen_max rounded to 4] scores plus [8][group][64]
+    partials in 64 KiB of LDS (decode.hip avsr_dec_attn); beyond that the kernel refuses"""
+    kpad = (int(klen_max) + 3) & ~3
+    return (group * kpad + DA_WAVES * group * 64) * 4 <= 64 * 1024
+
+
+def dec_attn_ws_floats(n, H, group, ksplit):
+    """fp32 partials the key-split dec_attn needs for n hypotheses in runs of `group`"""
+    G = max(1, group)
+    return (n + G - 1) // G * H * ksplit * G * 66 if ksplit > 1 else 0
 
 
 def dec_attn(q, k, v, o, *, n, H, klen_max, k_bstride, v_bstride, klen=None, scale=0.125, kidx=None, kmap=None,
@@ -789,14 +844,19 @@ def dec_attn(q, k, v, o, *, n, H, klen_max, k_bstride, v_bstride, klen=None, sca
     ksplit: up to ksplit workgroups per (group, head) over the keys, merged by the last to arrive
     (per-stream partial buffer; the arrival counters of the few-row GEMM workspace)."""
     ws = cnt = None
+    if group > 1 and not dec_attn_group_fits(klen_max, group):
+        group = 1          # the grouped kernel's [group][klen] scores would not fit its 64 KiB of LDS
     if ksplit > 1:
         G = max(1, group)
         slots = (n + G - 1) // G * H
         assert slots <= SKINNY_CNT
-        key = (q.device, L.stream_ptr().value)
-        need = slots * ksplit * G * 66
+        key = (_norm_dev(q.device), L.stream_ptr().value)
+        need = dec_attn_ws_floats(n, H, group, ksplit)
         ws = _DA_WS.get(key)
         if ws is None or ws.numel() < need:
+            if torch.cuda.is_current_stream_capturing():
+                raise L.AvsrLibError("dec_attn workspace first sized inside a graph capture: call "
+                                     "ops.reserve_stream_workspaces() on the capture stream before capturing")
             ws = _DA_WS[key] = torch.empty(need, device=q.device, dtype=torch.float32)
         cnt = _skinny_ws(q.device)[SKINNY_WS:]
     _call("avsr_dec_attn", L.fill(L.DecAttnParams, dtype=dtype_code(q), n=n, H=H, klen_max=klen_max, scale=scale,

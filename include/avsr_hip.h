@@ -34,6 +34,56 @@ enum { AVSR_E_SHAPE = 1001, AVSR_E_ALIGN = 1002, AVSR_E_DTYPE = 1003, AVSR_E_ARG
 const char* avsr_version(void);
 
 /* ------------------------------------------------------------------------------------
+ * Process-wide kernel-selection options. These are the only switches that change which
+ * kernel an entry point launches; the library reads no environment variables. Every option
+ * defaults to the measured production choice (value in brackets); the others exist for A/B
+ * measurements (tools/) and the tests that pin each variant. Set them between launches, not
+ * while another host thread is enqueueing work. Results of the variants are identical
+ * unless an option says otherwise.
+ *   AVSR_OPT_GEMM_TILE      [0]  0: automatic tile choice (gemm.hip tile_cfg); k + 1 forces
+ *                                 tile configuration k (AVSR_TILE_* below) on the bf16 core
+ *   AVSR_OPT_ATTN_SQ_FWD    [1]  1: query-tiled streamed self-attention forward for bf16,
+ *                                 L >= 128; 0: the resident-K/V kernel (same rows to 1e-2)
+ *   AVSR_OPT_ATTN_SQ_BWD    [0]  1: query-tiled backward also where the resident backward
+ *                                 applies (L <= 384); 0: resident up to 384 frames
+ *   AVSR_OPT_WGRAD_DUAL     [1]  1: two-wave-group weight-gradient kernel (fp32 C, both
+ *                                 operands r-contiguous); 0: the 4-wave core
+ *   AVSR_OPT_CONV_192       [1]  1: 192x128 tiles for conv fwd / data-grad where they still
+ *                                 run >= 2 blocks per CU; 0: 128x128 (bit-identical)
+ *   AVSR_OPT_CONV_S2PHASE   [1]  1: stride-2 data-grads as four parity-class GEMMs; 0: one
+ *                                 col2im GEMM over all taps (bit-identical)
+ *   AVSR_OPT_CONV_PATCH     [1]  1: patch-resident 3x3 kernel for 64-channel stride-1 fwd /
+ *                                 data-grad; 0: the general implicit GEMM (bit-identical)
+ *   AVSR_OPT_CONV_WPATCH    [1]  1: patch-resident weight-grad (stage 1 / 2 geometries); 0:
+ *                                 the general split-K weight-grad (fp32 re-association)
+ *   AVSR_OPT_STEM_POOL_2X2  [1]  1: stem max-pool forward / backward apply over 2x2 output
+ *                                 blocks; 0: one output pixel per thread (bit-identical)
+ * avsr_set_option returns 0, or AVSR_E_ARG for an unknown option or a value out of range;
+ * avsr_get_option returns the value, or -1 for an unknown option.
+ * ------------------------------------------------------------------------------------ */
+enum {
+  AVSR_OPT_GEMM_TILE = 0,
+  AVSR_OPT_ATTN_SQ_FWD = 1,
+  AVSR_OPT_ATTN_SQ_BWD = 2,
+  AVSR_OPT_WGRAD_DUAL = 3,
+  AVSR_OPT_CONV_192 = 4,
+  AVSR_OPT_CONV_S2PHASE = 5,
+  AVSR_OPT_CONV_PATCH = 6,
+  AVSR_OPT_CONV_WPATCH = 7,
+  AVSR_OPT_STEM_POOL_2X2 = 8,
+  AVSR_OPT_COUNT = 9
+};
+/* tile configurations of the bf16 GEMM core (AVSR_OPT_GEMM_TILE = k + 1) */
+enum {
+  AVSR_TILE_128 = 0, AVSR_TILE_256 = 1, AVSR_TILE_256x128 = 2, AVSR_TILE_128x256 = 3, AVSR_TILE_128s3 = 4,
+  AVSR_TILE_128s4 = 5, AVSR_TILE_128w8s3 = 6, AVSR_TILE_128w8s4 = 7, AVSR_TILE_PP = 8, AVSR_TILE_96 = 9,
+  AVSR_TILE_128x64 = 10, AVSR_TILE_192 = 11, AVSR_TILE_192x256 = 12, AVSR_TILE_192s3 = 13, AVSR_TILE_192w8 = 14,
+  AVSR_TILE_192w8s3 = 15, AVSR_TILE_64 = 16, AVSR_TILE_COUNT = 17
+};
+int avsr_set_option(int option, int64_t value);
+int64_t avsr_get_option(int option);
+
+/* ------------------------------------------------------------------------------------
  * GEMM with fused epilogue, fp32 accumulate: v_mfma_f32_16x16x32_bf16 on the LDS-DMA core
  * (128x128 / 192x128 tiles, bf16), v_mfma_f32_32x32x16_bf16 on the register-staged core
  * (fp32 parity mode: bf16 hi/lo split; shapes under 128 rows / columns).
@@ -89,11 +139,7 @@ typedef struct {
                                 partials, then AVSR_SKINNY_CNT uint32 arrival counters that the
                                 caller zeroes once (every launch leaves them zero); the last
                                 workgroup of a column block adds the partials in a fixed order
-                                and runs the epilogue. NULL: one workgroup row.
-                                Also used by the slab split-K weight-gradient path (splitk > 1
-                                with ws, both operands r-contiguous, fp32 C, plain epilogue): its
-                                counters let the last-arriving split of each output tile reduce
-                                the slabs in the GEMM itself (no separate reduction pass) */
+                                and runs the epilogue. NULL: one workgroup row. */
   const float* ln_c1;        /* optional LayerNorm prologue (fp32, M <= 64, K <= 1024, K % 16 == 0,
                                 unsplit): A holds the LayerNorm inputs x and B = gamma o W (W's
                                 columns scaled by the LayerNorm weight); per row the kernel takes
@@ -110,6 +156,13 @@ typedef struct {
   void* kv_v;
   const int* kv_pos;
   int kv_rows;
+  unsigned* slab_cnt;        /* optional, AVSR_SLAB_CNT uint32 arrival counters for the slab split-K
+                                weight-gradient path (splitk > 1 with ws, both operands r-contiguous,
+                                fp32 C, plain epilogue): the last-arriving split of each output
+                                tile reduces the slabs inside the GEMM (no separate reduction pass).
+                                The caller zeroes them once; every launch leaves them zero. Launches
+                                that share a counter buffer must be ordered (one stream). NULL: a
+                                separate reduction pass. */
 } avsr_gemm_params;
 #define AVSR_GEMM_COLSUM_WS(M, N) ((int64_t)(((M) + 63) / 64) * (N))
 /* slabs are AVSR_GEMM_SLAB_PAD floats apart beyond M*N: power-of-two slab strides put the
@@ -118,6 +171,7 @@ typedef struct {
 #define AVSR_GEMM_SLAB_PAD 1088
 #define AVSR_SKINNY_WS (1 << 19)
 #define AVSR_SKINNY_CNT 4096
+#define AVSR_SLAB_CNT 4096
 #define AVSR_SKINNY_WS_BYTES ((int64_t)AVSR_SKINNY_WS * 4 + AVSR_SKINNY_CNT * 4)
 #define AVSR_GEMM_SLAB_WS(batch, splitk, M, N) ((int64_t)(batch) * (splitk) * ((int64_t)(M) * (N) + AVSR_GEMM_SLAB_PAD))
 

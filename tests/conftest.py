@@ -21,3 +21,18 @@ def dev():
     from avsr_amd import _lib
     _lib.load()
     return torch.device("cuda:0")
+
+
+@pytest.fixture
+def lib_opt():
+    """set a library kernel-selection option (avsr_set_option) for one test; restored after"""
+    from avsr_amd import _lib
+    saved = {}
+
+    def set_(name, value):
+        prev = _lib.set_option(name, value)
+        saved.setdefault(name, prev)
+
+    yield set_
+    for name, value in saved.items():
+        _lib.set_option(name, value)

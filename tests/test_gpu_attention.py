@@ -185,7 +185,7 @@ def test_attention_dropout_bf16(dev):
 
 
 @pytest.mark.parametrize("B,H,L,klen", [(2, 16, 375, [375, 301]), (3, 2, 200, [200, 129, 64])])
-def test_attention_sq_matches_resident(dev, monkeypatch, B, H, L, klen):
+def test_attention_sq_matches_resident(dev, monkeypatch, B, H, L, klen, lib_opt):
     """The query-tiled forward (K/V streamed through the LDS-DMA ring, sq::attn_fwd_kernel)
     against the resident-K/V forward on the same bf16 inputs with dropout: the same dropout
     mask (zero pattern of P' through one-hot V rows is covered by test_attention_dropout_bf16;
@@ -205,14 +205,14 @@ def test_attention_sq_matches_resident(dev, monkeypatch, B, H, L, klen):
     o1, l1 = run()
     o1b, l1b = run()
     assert torch.equal(o1, o1b) and torch.equal(l1, l1b)
-    monkeypatch.setenv("AVSR_ATTN_SQ", "0")
+    lib_opt("attn_sq_fwd", 0)
     o0, l0 = run()
     assert _rel(o1, o0) < 1e-2
     assert (l1 - l0).abs().max().item() < 1e-4
 
 
 @pytest.mark.parametrize("B,H,L,klen", [(2, 16, 375, [375, 301]), (3, 2, 200, [200, 129, 64])])
-def test_attention_sq_backward_matches_resident(dev, monkeypatch, B, H, L, klen):
+def test_attention_sq_backward_matches_resident(dev, monkeypatch, B, H, L, klen, lib_opt):
     """The query-tiled backward (dQ kernel computing delta, then dK / dV streaming Q, dO, lse,
     delta; the default only past 384 frames) against the resident backward on the same bf16
     inputs with dropout: dQ / dK / dV agree to bf16 rounding."""
@@ -236,7 +236,7 @@ def test_attention_sq_backward_matches_resident(dev, monkeypatch, B, H, L, klen)
                      drop_p=0.1, seed=5, dq=dq)
         return dq, dk, dv
     ref = bwd()
-    monkeypatch.setenv("AVSR_ATTN_SQ_BWD", "1")
+    lib_opt("attn_sq_bwd", 1)
     got = bwd()
     again = bwd()
     for a_, b_, c_ in zip(got, ref, again):

@@ -140,7 +140,7 @@ S2_CASES = [(5, 22, 22, 64, 128, 3, 2, 1), (5, 11, 11, 128, 256, 3, 2, 1), (7, 6
 
 @pytest.mark.parametrize("beta", [0.0, 1.0])
 @pytest.mark.parametrize("case", S2_CASES)
-def test_stride2_dgrad_parity_classes_match_full(dev, case, beta, monkeypatch):
+def test_stride2_dgrad_parity_classes_match_full(dev, case, beta, monkeypatch, lib_opt):
     """The stride-2 data-grad split into input-pixel parity classes (conv.hip s2_launch) adds
     the same non-zero products in the same order as the full col2im GEMM: bit-identical."""
     n, h, w, cin, cout, k, s, p = case
@@ -152,7 +152,7 @@ def test_stride2_dgrad_parity_classes_match_full(dev, case, beta, monkeypatch):
     old = torch.randn(n, h, w, cin, generator=g).to(dev, bf)
     outs = []
     for mode in ("1", "0"):
-        monkeypatch.setenv("AVSR_CONV_S2PHASE", mode)
+        lib_opt("conv_s2phase", int(mode))
         dx = old.clone()
         ops.conv_bwd_data(geom, dy, wd, dx, beta=beta)
         outs.append(dx)
@@ -230,7 +230,7 @@ def test_stem_conv_direct(dev, B, T):
 
 @pytest.mark.parametrize("hw,c", [(22, 64), (11, 128)])
 @pytest.mark.parametrize("nimg", [1, 37, 600])
-def test_wgrad_patch_matches_general(dev, nimg, hw, c, monkeypatch):
+def test_wgrad_patch_matches_general(dev, nimg, hw, c, monkeypatch, lib_opt):
     """Patch-resident weight-grad of the stage-1 / stage-2 3x3 convolutions (persistent blocks,
     per-block slabs, ordered reduce) vs the general implicit-GEMM weight-grad and fp64 torch;
     blocks without tiles (nimg = 1), accumulation into a non-zero dw, run-to-run bit-identical."""
@@ -246,7 +246,7 @@ def test_wgrad_patch_matches_general(dev, nimg, hw, c, monkeypatch):
     dw1b = init.clone()
     ops.conv_bwd_weight(geom, xd, dy, dw1b)
     assert torch.equal(dw1, dw1b)
-    monkeypatch.setenv("AVSR_CONV_WPATCH", "0")
+    lib_opt("conv_wpatch", 0)
     dw2 = init.clone()
     ops.conv_bwd_weight(geom, xd, dy, dw2)
     assert _rel(dw1 - init, dw2 - init) < 1e-4

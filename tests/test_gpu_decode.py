@@ -211,3 +211,54 @@ def test_dec_attn_grouped_equals_single(G, T, lens):
             s = torch.einsum("hd,jhd->hj", qd[i].view(H, 64), k) * 0.125
             ref = torch.einsum("hj,jhd->hd", torch.softmax(s, -1), v).reshape(D)
             assert (outs[1][i].double().cpu() - ref).abs().max().item() < 1e-5
+
+
+def test_dec_attn_group_beyond_lds_limit_falls_back():
+    """a cross-attention memory longer than the grouped kernel's LDS bound (about 2.7 k frames
+    at group 5) runs ungrouped instead of raising, with the same rows bit for bit"""
+    dev = torch.device("cuda")
+    G, T, H = 5, 3000, 4
+    D = 64 * H
+    assert not ops.dec_attn_group_fits(T, G) and ops.dec_attn_group_fits(T, 1)
+    gen = torch.Generator().manual_seed(11)
+    mem = torch.randn(T, 2 * D, generator=gen).to(dev)
+    q = torch.randn(G, D, generator=gen).to(dev)
+    klen = torch.tensor([T, 2999, 1500, 7, 2800], dtype=torch.int32, device=dev)
+    for ks in (1, 2):
+        outs = []
+        for grp in (1, G):
+            o = torch.empty(G, D, device=dev)
+            ops.dec_attn(q, mem[:, :D], mem[:, D:], o, n=G, H=H, klen_max=T, k_bstride=0, v_bstride=0, klen=klen,
+                         group=grp, ksplit=ks)
+            outs.append(o)
+        assert torch.equal(outs[0], outs[1])
+    qd, md = q.double().cpu(), mem.double().cpu()
+    for i in range(G):
+        n = int(klen[i])
+        s = torch.einsum("hd,jhd->hj", qd[i].view(H, 64), md[:n, :D].view(-1, H, 64)) * 0.125
+        ref = torch.einsum("hj,jhd->hd", torch.softmax(s, -1), md[:n, D:].view(-1, H, 64)).reshape(D)
+        assert (outs[1][i].double().cpu() - ref).abs().max().item() < 1e-5
+
+
+def test_decode_graph_workspaces_zeroed_before_capture(g, model):
+    """the captured decode step's split-K arrival counters live in the capture stream's
+    workspace; it is created (zeroed) eagerly before capture, so a first replay of graph 1 on
+    recycled allocator memory full of garbage still decodes the reference's hypotheses, and
+    the counters are back at zero afterwards"""
+    from avsr_amd import decode as Dm
+    dev = torch.device("cuda")
+    for s in list(Dm._CAPTURE_STREAMS.values()):         # force a fresh capture stream + workspaces
+        for key in [k for k in ops._SKINNY_WS if k[1] == s.cuda_stream]:
+            del ops._SKINNY_WS[key]
+    Dm._CAPTURE_STREAMS.clear()
+    torch.cuda.synchronize()
+    junk = torch.full((1 << 26,), -1, dtype=torch.int32, device=dev)      # 256 MiB of 0xFFFFFFFF
+    del junk                                                                  # back to the caching allocator
+    bs = get_beam_search_decoder(model.avsr, TOKENS, ctc_weight=0.1, beam_size=3)
+    got = bs.decode_batch([torch.from_numpy(g["dec_enc_0"]).cuda(), torch.from_numpy(g["dec_enc_1"]).cuda()])
+    assert got[0][0].asdict()["yseq"] == g["yseq_b3_0"].tolist()
+    assert got[1][0].asdict()["yseq"] == g["yseq_b3_1"].tolist()
+    s = Dm._CAPTURE_STREAMS[dev]
+    ws = ops._SKINNY_WS[(ops._norm_dev(dev), s.cuda_stream)]
+    torch.cuda.synchronize()
+    assert int(ws[ops.SKINNY_WS:].view(torch.int32).abs().sum()) == 0

@@ -94,10 +94,9 @@ def _ref_gemm(A, B, a_kmajor, b_kmajor):
 
 
 @pytest.fixture(params=["auto", "128", "256", "256x128", "128x256", "128s3", "128w8s3", "pp", "192", "192x256", "64"])
-def gemm_tile(request, monkeypatch):
-    """forces each LDS-DMA tile configuration (AVSR_GEMM_TILE, read per launch by avsr_gemm)"""
-    if request.param != "auto":
-        monkeypatch.setenv("AVSR_GEMM_TILE", request.param)
+def gemm_tile(request, lib_opt):
+    """forces each LDS-DMA tile configuration (library option gemm_tile, read per launch by avsr_gemm)"""
+    lib_opt("gemm_tile", request.param)
     return request.param
 
 
@@ -136,12 +135,12 @@ def test_gemm_layouts_bf16(dev, gemm_tile, a_kmajor, b_kmajor, M, N, K, splitk):
 @pytest.mark.parametrize("M,N,K,splitk", [(1024, 1024, 6000, 4), (3072, 1024, 6000, 1), (256, 384, 1000, 1),
                                            (136, 200, 328, 1), (1024, 1024, 1000, 3), (640, 512, 64, 1),
                                            (1024, 1024, 6000, 1), (200, 136, 999, 1)])
-def test_wgrad_dual_kernel(dev, monkeypatch, M, N, K, splitk):
+def test_wgrad_dual_kernel(dev, monkeypatch, M, N, K, splitk, lib_opt):
     """Weight-gradient GEMM dW[M][N] = beta*dW + alpha * dy^T x (both operands r-contiguous, the
     in-block split-K kernel: two wave groups per block over halves of the K range, one LDS
     reduction; with splitk > 1 also split over blocks into slabs): vs fp64, ragged K (a group
     whose last tile is empty), ragged M / N edges, beta accumulation; bit-identical run to run;
-    and within fp32 re-association of the 4-wave core (AVSR_WGRAD_DUAL=0)."""
+    and within fp32 re-association of the 4-wave core (library option wgrad_dual = 0)."""
     g = torch.Generator().manual_seed(M + N + K)
     dy = torch.randn(K, M, generator=g).to(dev, torch.bfloat16)
     x = torch.randn(K, N, generator=g).to(dev, torch.bfloat16)
@@ -162,7 +161,7 @@ def test_wgrad_dual_kernel(dev, monkeypatch, M, N, K, splitk):
         monkeypatch.setattr(ops, "SLAB_FUSED_REDUCE", False)
         assert torch.equal(run(), a)
         monkeypatch.setattr(ops, "SLAB_FUSED_REDUCE", True)
-    monkeypatch.setenv("AVSR_WGRAD_DUAL", "0")
+    lib_opt("wgrad_dual", 0)
     c = run()
     assert _rel(a, c.double()) < 1e-5 * (K ** 0.5)
 
@@ -203,7 +202,7 @@ def test_dgrad_fused_bias_grad(dev, gemm_tile, M, N, K):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("tile", ["192", "192x256", "256x128", "pp"])
-def test_tile_configs_bit_identical(dev, monkeypatch, tile):
+def test_tile_configs_bit_identical(dev, monkeypatch, tile, lib_opt):
     """Every tile configuration accumulates each output over the same K order (64-deep K-tiles,
     the same 16x16x32 MFMA sequence), so the fused-epilogue results must equal the 128x128
     tile's bit for bit: FFN1-style forward (bias, GELU, pre-activation store, residual,
@@ -225,9 +224,9 @@ def test_tile_configs_bit_identical(dev, monkeypatch, tile):
         torch.cuda.synchronize()
         return y, h, dx, db
 
-    monkeypatch.setenv("AVSR_GEMM_TILE", "128")
+    lib_opt("gemm_tile", "128")
     ref = run()
-    monkeypatch.setenv("AVSR_GEMM_TILE", tile)
+    lib_opt("gemm_tile", tile)
     got = run()
     for a_, b_, name in zip(got[:3], ref[:3], ("y", "preact", "dx")):
         assert torch.equal(a_, b_), (tile, name, (a_.float() - b_.float()).abs().max().item())

@@ -171,7 +171,7 @@ def test_stem_pool(dev, dtype):
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("n,H,W", [(6, 44, 44), (3, 12, 16), (3, 10, 14), (2, 9, 7)])
-def test_stem_bwd_apply_block_kernel(dev, dtype, monkeypatch, n, H, W):
+def test_stem_bwd_apply_block_kernel(dev, dtype, monkeypatch, n, H, W, lib_opt):
     """the 2x2-block stem backward apply (even H, W) reproduces the per-pixel kernel (same windows,
     same addition order; the final fma contraction may differ: 1e-6 relative); odd sizes take
     the per-pixel kernel either way"""
@@ -185,7 +185,7 @@ def test_stem_bwd_apply_block_kernel(dev, dtype, monkeypatch, n, H, W):
     Ho, Wo = (H + 1) // 2, (W + 1) // 2
     fw = []
     for pix in ("1", "0"):          # forward: 2x2 output blocks (even Ho, Wo) vs per-output windows
-        monkeypatch.setenv("AVSR_STEM_APPLY_PIXEL", pix)
+        lib_opt("stem_pool_2x2", 1 - int(pix))
         y = torch.full((n, Ho, Wo, C), float("nan"), device=dev, dtype=dtype)
         am = torch.full((n, Ho, Wo, C), 255, device=dev, dtype=torch.uint8)
         hmax = torch.full((n, Ho, Wo, C), float("nan"), device=dev, dtype=dtype)
@@ -198,7 +198,7 @@ def test_stem_bwd_apply_block_kernel(dev, dtype, monkeypatch, n, H, W):
     dy = torch.randn(n, Ho, Wo, C, generator=g).to(dev, dtype)
     out = []
     for pix in ("1", "0"):
-        monkeypatch.setenv("AVSR_STEM_APPLY_PIXEL", pix)
+        lib_opt("stem_pool_2x2", 1 - int(pix))
         dh = torch.full_like(hd, float("nan"))
         grads = [torch.zeros(C, device=dev) for _ in range(3)]
         ops.stem_pool_bwd(dy, am, hmax, hd, n, H, W, st, a, dh, dgamma=grads[0], dbeta=grads[1], dprelu=grads[2])
@@ -209,7 +209,7 @@ def test_stem_bwd_apply_block_kernel(dev, dtype, monkeypatch, n, H, W):
         assert torch.equal(g0, g1)
     # the engine's pipelined stem backward: one reduction, then the apply over image ranges
     # (m_total = the whole batch's pixels) -> the same dh bit for bit
-    monkeypatch.delenv("AVSR_STEM_APPLY_PIXEL")
+    lib_opt("stem_pool_2x2", 1)
     dzp, sums = ops.stem_pool_bwd_reduce(dy, hmax, n, H, W, st, a, dgamma=torch.zeros(C, device=dev),
                                          dbeta=torch.zeros(C, device=dev), dprelu=torch.zeros(C, device=dev))
     dzp = dzp.view(n, Ho, Wo, C)
@@ -302,8 +302,8 @@ def test_avgpool(dev):
 
 
 @pytest.mark.parametrize("case", [(140, 22, 128, 128, 3, 1, 1, "identity"), (150, 22, 128, 128, 3, 1, 1, "plain")])
-def test_conv_192_tiles_match_128(dev, monkeypatch, case):
-    """the 192x128 row tiles of the forward / data-grad convolutions (AVSR_CONV_192, chosen for
+def test_conv_192_tiles_match_128(dev, monkeypatch, case, lib_opt):
+    """the 192x128 row tiles of the forward / data-grad convolutions (library option conv_192, chosen for
     the large-M ResNet stages) against 128x128: identical stored outputs (same K order), BN
     partial statistics and fused BN-backward sums equal up to the per-tile grouping (1e-5)."""
     n, hw, cin, cout, k, s, p, mode = case
@@ -322,7 +322,7 @@ def test_conv_192_tiles_match_128(dev, monkeypatch, case):
     a = (0.25 + 0.05 * torch.randn(cin, generator=g)).to(dev)
     out = {}
     for flag in ("0", "1"):
-        monkeypatch.setenv("AVSR_CONV_192", flag)
+        lib_opt("conv_192", int(flag))
         y = torch.empty(geom.out_pixels, cout, device=dev, dtype=bf)
         part = torch.empty(cout, ops.conv_stat_tiles(geom, ops.dtype_code(x)), 3, device=dev)
         ops.conv_fwd(geom, x, w, y, stats=part)
@@ -342,8 +342,8 @@ def test_conv_192_tiles_match_128(dev, monkeypatch, case):
 
 
 @pytest.mark.parametrize("case", [(40, 22, 64, 64, 3, 1, 1, "identity"), (33, 22, 64, 64, 3, 1, 1, "plain")])
-def test_conv_patch_matches_general(dev, monkeypatch, case):
-    """the patch-resident 3x3 stride-1 kernel (AVSR_CONV_PATCH, ResNet stage 1: one LDS image of
+def test_conv_patch_matches_general(dev, monkeypatch, case, lib_opt):
+    """the patch-resident 3x3 stride-1 kernel (library option conv_patch, ResNet stage 1: one LDS image of
     the padded input patch per 256-pixel block) against the general implicit-GEMM kernel:
     same tiles, same K order -> bit-identical forward outputs, BN partial statistics, data-grads
     with the fused BN-backward epilogue and their column sums, and plain data-grads
@@ -366,7 +366,7 @@ def test_conv_patch_matches_general(dev, monkeypatch, case):
     a = (0.25 + 0.05 * torch.randn(cin, generator=g)).to(dev)
     out = {}
     for flag in ("0", "1"):
-        monkeypatch.setenv("AVSR_CONV_PATCH", flag)
+        lib_opt("conv_patch", int(flag))
         y = torch.empty(geom.out_pixels, cout, device=dev, dtype=bf)
         part = torch.empty(cout, ops.conv_stat_tiles(geom, ops.dtype_code(x)), 3, device=dev)
         ops.conv_fwd(geom, x, w, y, stats=part)

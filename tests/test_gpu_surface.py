@@ -68,6 +68,41 @@ def test_encoder_submodule_train_backward(g):
     assert params["avsr.ctc.ctc_lo.weight"].grad.abs().max().item() == 0.0
 
 
+def test_encoder_submodule_bf16_direct_stem_backward(g):
+    """the bf16 encoder step (direct stem conv: its weight-grad input is packed on the side
+    stream after the forward) after a gradient clear queued on the side stream: encoder_backward
+    joins the side stream first, so two identical steps give identical gradients and the stem /
+    ResNet gradients follow the fp32 engine to bf16 accuracy"""
+    from avsr_amd import engine as E
+    assert E._STEM_DIRECT
+    b = _batch(g)
+    mask = torch.arange(b["videos"].shape[2]).unsqueeze(0) < b["video_lengths"].unsqueeze(1)
+    w = torch.randn(2, b["videos"].shape[2], TINY_CONFIG["hidden_size"], generator=torch.Generator().manual_seed(7))
+    grads = {}
+    for dt in (torch.float32, torch.bfloat16, torch.bfloat16):
+        m = _model(g, dt).train()
+        eng = m.avsr.engine()
+        runs = []
+        for _ in range(2):
+            eng.zero_grad_async()
+            out = m.avsr.encoder(input_features=b["audios"].cuda(), attention_mask=mask.cuda(), video=b["videos"].cuda())
+            (out.last_hidden_state.float() * w.cuda()).sum().backward()
+            torch.cuda.synchronize()
+            runs.append({k: p.grad.detach().clone() for k, p in m.named_parameters()
+                         if k.startswith("avsr.encoder.feature_extractor_video") and p.grad is not None})
+        assert all(torch.equal(runs[0][k], runs[1][k]) for k in runs[0]), "step-to-step gradient difference"
+        grads.setdefault(dt, []).append(runs[0])
+    ref, b16 = grads[torch.float32][0], grads[torch.bfloat16]
+    assert all(torch.equal(b16[0][k], b16[1][k]) for k in ref)
+    stem = [k for k in ref if "frontend3D.0.weight" in k]
+    assert stem, sorted(ref)[:5]
+    for k in ref:
+        r = ref[k].double().norm().item()
+        if r < 1e-6:
+            continue
+        assert abs(b16[0][k].double().norm().item() - r) <= 6e-2 * r, k
+
+
 def test_decoder_api_matches_oracle(g):
     m = _model(g).eval()
     cfg = tiny_cfg()

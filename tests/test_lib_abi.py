@@ -57,3 +57,47 @@ def test_conv_stat_tiles_per_dtype():
     # N <= 64 (stage 1): 256-row tiles on both paths
     g3 = ops.ConvGeom(6000, 22, 22, 64, 64, 3, 3, (1, 1), (1, 1))
     assert ops.conv_stat_tiles(g3, L.AVSR_BF16) == ops.conv_stat_tiles(g3, L.AVSR_F32) == -(-6000 * 484 // 256)
+
+
+def _header_option_defaults():
+    """{AVSR_OPT_name: default} from the bracketed defaults in avsr_hip.h's option table"""
+    src = open(os.path.join(ROOT, "include", "avsr_hip.h")).read()
+    return {m.group(1): int(m.group(2)) for m in re.finditer(r"\*\s+(AVSR_OPT_[A-Z0-9_]+)\s+\[(-?\d+)\]", src)}
+
+
+def test_kernel_options_declared_and_defaulted():
+    """every kernel-selection knob is a declared option (avsr_set_option / avsr_get_option) with
+    the default the header documents; Python's name table covers them all"""
+    lib = L.load()
+    doc = _header_option_defaults()
+    src = open(os.path.join(ROOT, "include", "avsr_hip.h")).read()
+    ids = {m.group(1): int(m.group(2)) for m in re.finditer(r"\b(AVSR_OPT_[A-Z0-9_]+)\s*=\s*(\d+)", src)}
+    count = ids.pop("AVSR_OPT_COUNT")
+    assert set(doc) == set(ids) and len(ids) == count == len(L.OPTIONS)
+    for name, i in ids.items():
+        assert lib.avsr_get_option(i) == doc[name], name
+        assert L.OPTIONS[name[len("AVSR_OPT_"):].lower()] == i
+    assert lib.avsr_get_option(count) == -1 and lib.avsr_get_option(-1) == -1
+
+
+def test_set_option_roundtrip_and_range():
+    lib = L.load()
+    assert lib.avsr_set_option(L.OPTIONS["attn_sq_bwd"], 2) == 1004          # AVSR_E_ARG: out of range
+    assert lib.avsr_set_option(99, 0) == 1004                                  # unknown option
+    prev = L.set_option("gemm_tile", "192")
+    try:
+        assert L.get_option("gemm_tile") == L.TILES.index("192") + 1
+        assert lib.avsr_set_option(L.OPTIONS["gemm_tile"], len(L.TILES) + 1) == 1004
+    finally:
+        L.set_option("gemm_tile", prev)
+    assert L.get_option("gemm_tile") == 0
+
+
+def test_library_reads_no_environment():
+    """kernel selection does not depend on process environment: no getenv in the sources, and
+    the built library imports no getenv"""
+    for f in glob.glob(os.path.join(ROOT, "avsr_amd", "csrc", "*")):
+        assert "getenv" not in open(f).read(), f
+    import subprocess
+    out = subprocess.run(["nm", "-D", "--undefined-only", L.LIB_PATH], capture_output=True, text=True).stdout
+    assert "getenv" not in out
