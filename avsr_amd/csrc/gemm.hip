@@ -616,8 +616,11 @@ __global__ __launch_bounds__(256) void skinny_kernel(DenseArgs a, float* part, i
 // LNP (LayerNorm prologue, a.ln_c1): the batch holds whole rows of the chunk, so each row's chunk
 // mean and M2 (two passes over the registers, partials over the 4 lanes of a row and the 8 waves in
 // a fixed order) come for free; split launches hand them over with the partial sums (a.lnst) and
-// the last arriver combines them (Chan et al.'s pairwise formula, split order); the MFMAs run on the
-// raw x against gamma o W, and the epilogue applies rstd * (acc - mean * c1[n]).
+// the last arriver combines them (Chan et al.'s pairwise formula, split order); the MFMAs run on
+// x - s against gamma o W, with s = x[m][0] a per-row shift every chunk knows, and the epilogue
+// applies rstd * (acc - (mean - s) * c1[n]): without the shift a row whose |mean| is large next to
+// its spread would subtract two large terms (acc ~ mean * c1) and lose the digits the reference's
+// normalise-then-project keeps.
 constexpr int SKM_WAVES = 8;
 template <typename OutT, int MT, int UNR, bool LNP = false>
 __global__ __launch_bounds__(64 * SKM_WAVES) void skinny_mma_kernel(DenseArgs a, float* part, int kchunk, unsigned* cnt) {
@@ -668,6 +671,9 @@ __global__ __launch_bounds__(64 * SKM_WAVES) void skinny_mma_kernel(DenseArgs a,
       for (int t = 0; t < MT; ++t) x[u][t] = (ok && rok[t]) ? *(const f32x4*)(Ar[t] + k) : f32x4{0.f, 0.f, 0.f, 0.f};
     }
     if constexpr (LNP) {       // the batch holds the chunk's rows: chunk mean and M2 per row
+      float sft[MT];
+#pragma unroll
+      for (int t = 0; t < MT; ++t) sft[t] = ((const float*)a.A)[(int64_t)min(16 * t + c, a.M - 1) * a.lda];
       const float inv_n = 1.f / (float)(kend - kbeg);
 #pragma unroll
       for (int t = 0; t < MT; ++t) {
@@ -696,6 +702,12 @@ __global__ __launch_bounds__(64 * SKM_WAVES) void skinny_mma_kernel(DenseArgs a,
         s2 += __shfl_xor(s2, 32, 64);
         if (g == 0) st2[w][16 * t + c] = s2;
       }
+#pragma unroll
+      for (int u = 0; u < UNR; ++u)     // (loads past the chunk are 0 against b = 0: still 0)
+#pragma unroll
+        for (int t = 0; t < MT; ++t)
+#pragma unroll
+          for (int e2 = 0; e2 < 4; ++e2) x[u][t][e2] -= sft[t];
     }
 #pragma unroll
     for (int u = 0; u < UNR; ++u)
@@ -748,7 +760,8 @@ __global__ __launch_bounds__(64 * SKM_WAVES) void skinny_mma_kernel(DenseArgs a,
         if constexpr (LNP) {
           float mean, m2;
           chunk_stats(m, mean, m2);
-          v = (1.f / sqrtf(m2 / (float)a.K + a.ln_eps)) * (v - mean * a.ln_c1[cl]);
+          const float s = ((const float*)a.A)[(int64_t)m * a.lda];
+          v = (1.f / sqrtf(m2 / (float)a.K + a.ln_eps)) * (v - (mean - s) * a.ln_c1[cl]);
         }
         epi(i, m, cl, v);
       }
@@ -807,7 +820,7 @@ __global__ __launch_bounds__(64 * SKM_WAVES) void skinny_mma_kernel(DenseArgs a,
       const float* pp = part + (int64_t)m * a.N + cl;
       float v = __hip_atomic_load(pp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       for (int q = 1; q < S; ++q) v += __hip_atomic_load(pp + q * MN, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if constexpr (LNP) v = rrstd[m] * (v - rmean[m] * a.ln_c1[cl]);
+      if constexpr (LNP) v = rrstd[m] * (v - (rmean[m] - ((const float*)a.A)[(int64_t)m * a.lda]) * a.ln_c1[cl]);
       epi(i, m, cl, v);
     }
   }

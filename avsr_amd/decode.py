@@ -20,6 +20,14 @@ once per utterance (the reference recomputes them every step), the self-attentio
 earlier positions are cached instead of the layer outputs they are computed from (rows of
 step j at cache row j*R + r, reached through each hypothesis's ancestry table instead of
 being copied on every reorder), and finished hypotheses stay in the batch as dead rows.
+
+The two ends of the CTC-weight range are the configurations the reference builds with one
+scorer (a scorer of weight 0 is dropped, beam_search.py:69-73): ctc_weight = 0 searches on the
+decoder alone (no partial scorer, so no pre-beam: every token of every row is a candidate);
+ctc_weight = 1 on the CTC prefix scorer alone over the full vocabulary (pre_beam_score_key None,
+no decoder step at all): psi of every token in chunks of 64, then the row's top int(1.5*beam)
+tokens by psi (a superset of every token the flat top-beam can pick from that row, since the row
+offset is common) get their CTC states.
 """
 import math
 from typing import Any, Dict, List, NamedTuple, Union
@@ -94,11 +102,15 @@ class BatchBeamSearch:
         self.pre_beam_size = int(pre_beam_ratio * beam_size)
         self.w_dec = float(weights.get("decoder", 0.0))
         self.w_ctc = float(weights.get("ctc", 0.0))
-        if self.w_ctc == 0.0 or self.w_dec == 0.0:
-            raise NotImplementedError("the HIP beam search implements the joint decoder+CTC configuration "
-                                      "(0 < ctc_weight < 1) that get_beam_search_decoder builds")
-        if pre_beam_score_key != "decoder" or not (self.pre_beam_size < vocab_size):
-            raise NotImplementedError("pre-beam on the decoder score is the configuration the reference uses")
+        self.use_dec, self.use_ctc = self.w_dec != 0.0, self.w_ctc != 0.0
+        if not (self.use_dec or self.use_ctc):
+            raise NotImplementedError("no scorer with a non-zero weight")
+        if self.use_ctc and pre_beam_score_key is not None and pre_beam_score_key != "decoder":
+            raise NotImplementedError(f"pre-beam on {pre_beam_score_key!r}: the reference builds 'decoder' or None")
+        if self.use_ctc and not self.use_dec and pre_beam_score_key == "decoder":
+            raise KeyError("decoder is not a scorer (weight 0): pre_beam_score_key must be None")   # beam_search.py:92-97
+        if self.use_ctc and self.use_dec and (pre_beam_score_key is None or not self.pre_beam_size < vocab_size):
+            raise NotImplementedError("the joint search pre-beams on the decoder score, as the reference configures it")
 
     def __call__(self, x, maxlenratio: float = 0.0, minlenratio: float = 0.0):
         return self.forward(x, maxlenratio, minlenratio)
@@ -190,6 +202,18 @@ class BatchBeamSearch:
                 ff1=f(eng.w(ff + "w_1.weight"), ar.master(ff + "w_1.bias"), p + "norm3")))
         return out
 
+    def _ctc_full_vocab(self, st, r_prev):
+        """ctc_weight = 1: psi of every token (chunks of 64 ids through the prefix kernel), then
+        the row's top-P tokens by psi into st["ids"] (the kernel's psi of a token does not depend
+        on the other ids of its launch)"""
+        R, V = st["R"], self.n_vocab
+        kw = dict(n=R, out_len=0, out_len_dev=st["pos"], blank=self.blank, eos=self.eos, uidx=st["uidx"], tlen=st["tlen"])
+        pf = st["psi_full"]
+        for c in range(st["vchunks"].shape[0]):
+            ops.ctc_prefix(st["logp"], r_prev, st["tok"], st["vchunks"][c], st["r_scr"], st["psi_c"], **kw)
+            pf[:, c * 64:(c + 1) * 64].copy_(st["psi_c"][:, :64])
+        ops.row_topk(pf, V, self.pre_beam_size, st["ids"])
+
     def _step(self, eng, st, first, k):
         """one search step on the device (no host sync): decoder, pre-beam, CTC prefix scores,
         per-utterance beam selection, bookkeeping, state reorder. k = 0 / 1 picks the ancestry
@@ -197,10 +221,14 @@ class BatchBeamSearch:
         R, P, beam = st["R"], self.pre_beam_size, self.beam_size
         st["anc_in"] = st["anc"][k]
         ops.beam_step_prep(R, st["pos"], st["anc"][k], st["klen_self"])
-        dec = self._decoder_step(eng, st)      # also writes the pre-beam ids
-        ops.ctc_prefix(st["logp"], None if first else st["r_prev"][k], st["tok"], st["ids"], st["r_new"], st["psi"],
-                       n=R, out_len=0, out_len_dev=st["pos"], blank=self.blank, eos=self.eos, uidx=st["uidx"],
-                       tlen=st["tlen"])
+        # decoder log-probs + the pre-beam ids; without a decoder scorer its score is 0
+        dec = self._decoder_step(eng, st) if self.use_dec else st["dec0"]
+        if self.use_ctc:
+            r_prev = None if first else st["r_prev"][k]
+            if not self.use_dec:
+                self._ctc_full_vocab(st, r_prev)
+            ops.ctc_prefix(st["logp"], r_prev, st["tok"], st["ids"], st["r_new"], st["psi"], n=R, out_len=0,
+                           out_len_dev=st["pos"], blank=self.blank, eos=self.eos, uidx=st["uidx"], tlen=st["tlen"])
         out = st["out"]
         ops.beam_select(dec, self.n_vocab, st["ids"], st["psi"], st["s_prev"], st["score"], out, n=R, beam=beam,
                         blank=self.blank, eos=self.eos, w_dec=self.w_dec, w_ctc=self.w_ctc, seg=st["seg"])
@@ -214,8 +242,9 @@ class BatchBeamSearch:
         Lm, Tm = st["Lmax"], st["Tm"]
         ops.gather_rows(st["anc"][k], st["anc"][1 - k], st["src"][:R], groups=1, n=R, row_bytes=Lm * 4,
                         src_gstride=0, src_rstride=Lm * 4, dst_gstride=0, dst_rstride=Lm * 4)
-        ops.gather_rows(st["r_new"], st["r_prev"][1 - k], st["src"][R:], groups=1, n=R, row_bytes=Tm * 2 * 4,
-                        src_gstride=0, src_rstride=Tm * 2 * 4, dst_gstride=0, dst_rstride=Tm * 2 * 4)
+        if self.use_ctc:
+            ops.gather_rows(st["r_new"], st["r_prev"][1 - k], st["src"][R:], groups=1, n=R, row_bytes=Tm * 2 * 4,
+                            src_gstride=0, src_rstride=Tm * 2 * 4, dst_gstride=0, dst_rstride=Tm * 2 * 4)
 
     # ----------------------------------------------------------------------- search
     def forward(self, x, maxlenratio: float = 0.0, minlenratio: float = 0.0) -> List[Hypothesis]:
@@ -292,7 +321,18 @@ class BatchBeamSearch:
             end_flag=torch.zeros(steps, R, **i32), end_score=torch.zeros(steps, R, **f32),
             end_dec=torch.zeros(steps, R, **f64), end_ctc=torch.zeros(steps, R, **f64),
             best_len=torch.full((U, Lmax + 3), float("-inf"), **f32), best_end=torch.full((U,), float("-inf"), **f32),
-            done=torch.zeros(U + 1, **i32), fold=self._fold_layernorms(eng) if FOLD_LN else None)
+            done=torch.zeros(U + 1, **i32), fold=self._fold_layernorms(eng) if FOLD_LN and self.use_dec else None)
+        if not self.use_ctc:
+            st["psi"].zero_()                 # w_ctc = 0 multiplies it: keep it finite
+        if not self.use_dec:
+            st["dec0"] = torch.zeros(R, eng.V, **f32)
+            nch = -(-self.n_vocab // 64)
+            ids = torch.arange(nch * 64, dtype=torch.int32)
+            ids[ids >= self.n_vocab] = self.blank          # padding ids: blank (psi = LOGZERO)
+            st["vchunks"] = ids.view(nch, 1, 64).expand(nch, R, 64).contiguous().to(dev)
+            st["psi_c"] = torch.empty(R, 65, **f32)
+            st["r_scr"] = torch.empty(R, 64, Tm, 2, **f32)
+            st["psi_full"] = torch.empty(R, nch * 64, **f32)
         self._step(eng, st, True, 0)           # step 0: CTC state from scratch; reads ancestry 0, writes 1
         if steps > 1:
             graphs = self._capture(eng, st)
@@ -345,7 +385,7 @@ class BatchBeamSearch:
                     h = int(bp_prev[j, h])
                 yseq = [self.sos] + toks[::-1] + ([self.eos] if flag[i, r] == 2 else [])
                 ended[r // beam].append(self._make_hyp(dict(yseq=yseq, score=float(esc[i, r]), dec=float(edec[i, r]),
-                                                            ctc=float(ectc[i, r]))))
+                                                            ctc=float(ectc[i, r])), self.use_dec, self.use_ctc))
         results = []
         for u in range(U):
             nbest = sorted(ended[u], key=lambda h: float(h.score), reverse=True)
@@ -355,12 +395,15 @@ class BatchBeamSearch:
         return results
 
     @staticmethod
-    def _make_hyp(hyp):
+    def _make_hyp(hyp, use_dec=True, use_ctc=True):
+        """the reference's Hypothesis: scores of the scorers in the search only"""
+        scores = {}
+        if use_dec:
+            scores["decoder"] = torch.tensor(hyp["dec"], dtype=torch.float32)
+        if use_ctc:
+            scores["ctc"] = torch.tensor(hyp["ctc"], dtype=torch.float32)
         return Hypothesis(yseq=torch.tensor(hyp["yseq"], dtype=torch.int64),
-                          score=torch.tensor(hyp["score"], dtype=torch.float32),
-                          scores={"decoder": torch.tensor(hyp["dec"], dtype=torch.float32),
-                                  "ctc": torch.tensor(hyp["ctc"], dtype=torch.float32)},
-                          states={})
+                          score=torch.tensor(hyp["score"], dtype=torch.float32), scores=scores, states={})
 
 
 def get_beam_search_decoder(model, token_list, ctc_weight=0.1, beam_size=3):

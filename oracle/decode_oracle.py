@@ -12,6 +12,9 @@ ctc_weight, length_bonus 0 and lm None => both dropped, pre_beam_score_key "deco
   Decoder.batch_score / forward_one_step               src/nets/backend/transformer/decoder.py:153-227
 The decoder is evaluated without a cache (full causal recompute of the prefix), which is
 the same function of the prefix as the reference's output cache.
+ctc_weight 0 / 1 are the one-scorer searches the reference builds (a scorer of weight 0 is
+dropped, beam_search.py:69-73): the decoder alone (no partial scorer => no pre-beam,
+:96-100), or the CTC prefix scorer alone over the full vocabulary (pre_beam_score_key None).
 """
 from dataclasses import dataclass, field
 from typing import Dict, List
@@ -96,34 +99,44 @@ def beam_search(sd, cfg, x, ctc_logp, beam_size, ctc_weight=0.1, maxlenratio=0.0
     sos = eos = V - 1
     blank = 0
     w_dec, w_ctc = 1.0 - ctc_weight, ctc_weight
+    use_dec, use_ctc = w_dec != 0.0, w_ctc != 0.0
     pre_beam = int(1.5 * beam_size)
     T = x.shape[0]
     # beam_search.py:349-354
     maxlen = T if maxlenratio == 0 else (-int(maxlenratio) if maxlenratio < 0 else max(1, int(maxlenratio * T)))
-    running = [Hyp([sos], 0.0, {"decoder": 0.0, "ctc": 0.0}, None, 0.0)]
+    running = [Hyp([sos], 0.0, {k: 0.0 for k, u in (("decoder", use_dec), ("ctc", use_ctc)) if u}, None, 0.0)]
     ended = []
     for i in range(maxlen):
         n = len(running)
         ys = torch.tensor([h.yseq for h in running])
-        with torch.no_grad():
-            dec = decoder_one_step(sd, cfg, ys, x.unsqueeze(0).expand(n, -1, -1))   # (n, V)
-        weighted = w_dec * dec
-        ids = torch.topk(dec, pre_beam, dim=-1)[1]
-        states = [None if h.ctc_r is None else (h.ctc_r, h.ctc_s) for h in running]
-        ctc_sc, r_new, log_psi = ctc_prefix_scores(ctc_logp, [h.yseq for h in running], states, ids, blank, eos)
-        weighted = weighted + w_ctc * ctc_sc
+        weighted = torch.zeros(n, V, dtype=ctc_logp.dtype)
+        if use_dec:
+            with torch.no_grad():
+                dec = decoder_one_step(sd, cfg, ys, x.unsqueeze(0).expand(n, -1, -1))   # (n, V)
+            weighted = weighted + w_dec * dec
+        if use_ctc:
+            # pre-beam on the decoder score in the joint search; the full vocabulary without it
+            ids = torch.topk(dec, pre_beam, dim=-1)[1] if use_dec else torch.arange(V).expand(n, V)
+            states = [None if h.ctc_r is None else (h.ctc_r, h.ctc_s) for h in running]
+            ctc_sc, r_new, log_psi = ctc_prefix_scores(ctc_logp, [h.yseq for h in running], states, ids, blank, eos)
+            weighted = weighted + w_ctc * ctc_sc
         weighted = weighted + torch.tensor([h.score for h in running], dtype=weighted.dtype).unsqueeze(1)
         top = weighted.view(-1).topk(beam_size)[1]
         best = []
         for flat in top.tolist():
             p, tok = flat // V, flat % V
             h = running[p]
+            sc = {}
+            if use_dec:
+                sc["decoder"] = h.scores["decoder"] + float(dec[p, tok])
+            if not use_ctc:
+                best.append(Hyp(h.yseq + [tok], float(weighted[p, tok]), sc, None, 0.0))
+                continue
             pos = (ids[p] == tok).nonzero()
             col = int(pos[0, 0]) if len(pos) else P_LAST(ids)   # scoring_idmap -1 => index -1
-            best.append(Hyp(h.yseq + [tok], float(weighted[p, tok]),
-                            {"decoder": h.scores["decoder"] + float(dec[p, tok]),
-                             "ctc": h.scores["ctc"] + float(ctc_sc[p, tok])},
-                            r_new[:, :, p, col].clone(), float(log_psi[p, tok])))
+            sc["ctc"] = h.scores["ctc"] + float(ctc_sc[p, tok])
+            best.append(Hyp(h.yseq + [tok], float(weighted[p, tok]), sc, r_new[:, :, p, col].clone(),
+                            float(log_psi[p, tok])))
         if i == maxlen - 1:
             best = [Hyp(h.yseq + [eos], h.score, h.scores, h.ctc_r, h.ctc_s) for h in best]
         running = []

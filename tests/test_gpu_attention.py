@@ -242,3 +242,125 @@ def test_attention_sq_backward_matches_resident(dev, monkeypatch, B, H, L, klen,
     for a_, b_, c_ in zip(got, ref, again):
         assert torch.equal(a_, c_)
         assert _rel(a_, b_) < 2e-2
+
+
+# ---------------------------------------------------------------------------------------------
+# Dropout mask identity (verdict r4 item 2): the kept / dropped pattern of every (query, key)
+# pair is recovered exactly from each kernel that applies or regenerates it, and must be the
+# same bit for bit. With Q.K = 0 for every pair (Q and K in orthogonal halves of the head
+# dimension, or zero) the probabilities are uniform over the allowed keys, so
+#  - forward: V rows one-hot over a chunk of 64 keys -> O[i, t] != 0 iff pair (i, c + t) kept;
+#  - dK/dV kernel: dO rows one-hot over a chunk of 64 queries -> dV[j, t] != 0 iff (c + t, j) kept;
+#  - dQ and dK: V = dO = ones gives dS_ij = P (64 m_ij / (1 - p) - delta_i); with Q one-hot over
+#    a 32-query chunk in dims 0-31 and K one-hot over a 32-key chunk in dims 32-63,
+#    dQ[i, 32 + t] = s dS_{i, c + t} and dK[j, t] = s dS_{c + t, j}; dS + P delta is 64P / (1 - p)
+#    when kept and 0 when dropped (a gap of ~70P against bf16 rounding of < P).
+# ---------------------------------------------------------------------------------------------
+MASK_CASES = [
+    # name, B, H, Lq, Lk, klen, causal: the C2 encoder self-attention, and the teacher-forced
+    # decoder's causal self-attention and source attention at C2 (16 x 41 labels, 375 frames)
+    ("enc_c2", 16, 16, 375, 375, [375, 301] * 8, False),
+    ("dec_self", 16, 16, 41, 41, None, True),
+    ("dec_src", 16, 16, 41, 375, [375, 301] * 8, False),
+]
+
+
+def _allowed(dev, B, H, Lq, Lk, klen, causal):
+    m = torch.ones(B, 1, Lq, Lk, dtype=torch.bool, device=dev)
+    if klen is not None:
+        m &= (torch.arange(Lk, device=dev)[None, :] < torch.tensor(klen, device=dev)[:, None])[:, None, None, :]
+    if causal:
+        m &= torch.tril(torch.ones(Lq, Lk, dtype=torch.bool, device=dev))[None, None]
+    return m.expand(B, H, Lq, Lk)
+
+
+def _onehot_rows(rows, H, L, c, n, col0, dev, dt):
+    """rows x (H*64) zeros with row c+t of every clip holding 1 at column h*64 + col0 + t (t < n)"""
+    x = torch.zeros(rows // L, L, H, 64, device=dev, dtype=dt)
+    if n > 0:
+        x[:, c:c + n, :, col0:col0 + n] = torch.eye(n, device=dev, dtype=dt)[None, :, None, :]
+    return x.view(rows, H * 64)
+
+
+def _masks(dev, dt, B, H, Lq, Lk, klen, causal, p, seed):
+    """(forward mask, dV mask, dQ mask, dK mask) recovered from the kernels the current library
+    options select, each restricted to the allowed pairs"""
+    D = H * 64
+    kl = None if klen is None else torch.tensor(klen, dtype=torch.int32, device=dev)
+    kw = dict(B=B, H=H, Lq=Lq, Lk=Lk, klen=kl, causal=causal, scale=0.125, drop_p=p, seed=seed)
+    allowed = _allowed(dev, B, H, Lq, Lk, klen, causal)
+    lse = torch.empty(B, H, Lq, device=dev)
+    zq, zk = torch.zeros(B * Lq, D, device=dev, dtype=dt), torch.zeros(B * Lk, D, device=dev, dtype=dt)
+
+    def bwd(dout, q, k, v, o):
+        dk = torch.empty(B * Lk, D, device=dev, dtype=dt)
+        dv = torch.empty(B * Lk, D, device=dev, dtype=dt)
+        delta = torch.empty(B, H, Lq, device=dev)
+        if dt == torch.bfloat16:
+            dq = torch.empty(B * Lq, D, device=dev, dtype=dt)
+            ops.attn_bwd(dout, q, k, v, o, lse, None, dk, dv, delta, dq=dq, **kw)
+        else:
+            dq = torch.zeros(B * Lq, D, device=dev)
+            ops.attn_bwd(dout, q, k, v, o, lse, dq, dk, dv, delta, **kw)
+        return dq, dk, dv
+
+    fwd = torch.zeros(B, H, Lq, Lk, dtype=torch.bool, device=dev)
+    for c in range(0, Lk, 64):
+        n = min(64, Lk - c)
+        o = torch.empty(B * Lq, D, device=dev, dtype=dt)
+        ops.attn_fwd(zq, zk, _onehot_rows(B * Lk, H, Lk, c, n, 0, dev, dt), o, lse, **kw)
+        fwd[..., c:c + n] = o.view(B, Lq, H, 64)[..., :n].permute(0, 2, 1, 3) != 0
+    o = torch.empty(B * Lq, D, device=dev, dtype=dt)
+    ops.attn_fwd(zq, zk, zk, o, lse, **kw)
+    dvm = torch.zeros_like(fwd)
+    for c in range(0, Lq, 64):
+        n = min(64, Lq - c)
+        _, _, dv = bwd(_onehot_rows(B * Lq, H, Lq, c, n, 0, dev, dt), zq, zk, zk, o)
+        dvm[:, :, c:c + n, :] = dv.view(B, Lk, H, 64)[..., :n].permute(0, 2, 3, 1) != 0
+    nkeys = allowed.sum(-1, keepdim=True).double()                  # uniform P = 1 / nkeys
+    ones_q, ones_k = torch.ones(B * Lq, D, device=dev, dtype=dt), torch.ones(B * Lk, D, device=dev, dtype=dt)
+    dqm, dkm = torch.zeros_like(fwd), torch.zeros_like(fwd)
+    for r in range(max(-(-Lq // 32), -(-Lk // 32))):
+        cq, ck = 32 * r, 32 * r
+        nq, nk = max(0, min(32, Lq - cq)), max(0, min(32, Lk - ck))
+        q = _onehot_rows(B * Lq, H, Lq, cq, nq, 0, dev, dt)
+        k = _onehot_rows(B * Lk, H, Lk, ck, nk, 32, dev, dt)
+        ob = torch.empty(B * Lq, D, device=dev, dtype=dt)
+        ops.attn_fwd(q, k, ones_k, ob, lse, **kw)
+        dq, dk, _ = bwd(ones_q, q, k, ones_k, ob)
+        delta = ob.double().view(B, Lq, H, 64).sum(-1).permute(0, 2, 1)[..., None]     # (B, H, Lq, 1)
+        pd = delta / nkeys                                                             # P * delta
+        thr = 32.0 / (1 - p) / nkeys                                                   # P * 32 / (1 - p)
+        if nk:
+            ds = dq.double().view(B, Lq, H, 64)[..., 32:32 + nk].permute(0, 2, 1, 3) / 0.125
+            dqm[..., ck:ck + nk] = ds + pd > thr
+        if nq:
+            ds = dk.double().view(B, Lk, H, 64)[..., :nq].permute(0, 2, 3, 1) / 0.125    # (B, H, nq, Lk)
+            dkm[:, :, cq:cq + nq, :] = ds + pd[:, :, cq:cq + nq] > thr[:, :, cq:cq + nq]
+    return tuple(m & allowed for m in (fwd, dvm, dqm, dkm)), allowed
+
+
+@pytest.mark.parametrize("case", MASK_CASES, ids=[c[0] for c in MASK_CASES])
+def test_attention_dropout_mask_bitexact(dev, lib_opt, case):
+    """every attention kernel of the training step applies or regenerates exactly the same
+    dropout mask: the query-tiled and resident forwards, the resident and query-tiled backward
+    (dK/dV and dQ kernels), bf16 and the fp32 parity kernels — torch.equal on the recovered
+    kept / dropped pattern of every allowed (query, key) pair"""
+    name, B, H, Lq, Lk, klen, causal = case
+    p, seed = 0.1, 0x5EED + Lq
+    bf = torch.bfloat16
+    runs = {}
+    for fwd_sq in (1, 0):
+        for bwd_sq in (0, 1):
+            lib_opt("attn_sq_fwd", fwd_sq)
+            lib_opt("attn_sq_bwd", bwd_sq)
+            runs[f"bf16 fwd_sq={fwd_sq} bwd_sq={bwd_sq}"], allowed = _masks(dev, bf, B, H, Lq, Lk, klen, causal, p, seed)
+    lib_opt("attn_sq_fwd", 1)
+    lib_opt("attn_sq_bwd", 0)
+    runs["fp32"], _ = _masks(dev, torch.float32, B, H, Lq, Lk, klen, causal, p, seed)
+    ref = runs["bf16 fwd_sq=1 bwd_sq=0"][0]          # the production forward's mask
+    frac = ref.sum().item() / allowed.sum().item()
+    assert 0.88 < frac < 0.92, frac                  # keep probability 1 - p
+    for label, masks in runs.items():
+        for kind, m in zip(("fwd", "dV", "dQ", "dK"), masks):
+            assert torch.equal(m, ref), (label, kind, (m ^ ref).sum().item())

@@ -262,3 +262,29 @@ def test_decode_graph_workspaces_zeroed_before_capture(g, model):
     ws = ops._SKINNY_WS[(ops._norm_dev(dev), s.cuda_stream)]
     torch.cuda.synchronize()
     assert int(ws[ops.SKINNY_WS:].view(torch.int32).abs().sum()) == 0
+
+
+@pytest.mark.parametrize("w", [0.0, 1.0])
+@pytest.mark.parametrize("beam", [1, 3])
+def test_one_scorer_searches_match_reference(g, model, w, beam):
+    """ctc_weight = 0 (decoder alone, no pre-beam) and ctc_weight = 1 (CTC prefix scorer alone
+    over the full vocabulary, no decoder step) reproduce every hypothesis the reference returns
+    (tests/golden/avsr_ctcw.npz from make_golden_ctcw.py): token sequences in order, total and
+    per-scorer scores; batched over both clips = per clip"""
+    import os
+    c = np.load(os.path.join(os.path.dirname(__file__), "golden", "avsr_ctcw.npz"))
+    bs = get_beam_search_decoder(model.avsr, TOKENS, ctc_weight=w, beam_size=beam)
+    xs = [torch.from_numpy(g[f"dec_enc_{b}"]).cuda() for b in range(2)]
+    batched = bs.decode_batch(xs)
+    scorer = "decoder" if w == 0.0 else "ctc"
+    for b in range(2):
+        key = f"w{w:g}_b{beam}_{b}"
+        lens = c[key + "_len"]
+        ys = [y.tolist() for y in np.split(c[key + "_yseq"], np.cumsum(lens)[:-1])]
+        hyps = [h.asdict() for h in bs(xs[b])]
+        assert [h["yseq"] for h in hyps] == ys
+        assert set(hyps[0]["scores"]) == {scorer}
+        for h, s, s1 in zip(hyps, c[key + "_score"], c[key + "_" + scorer]):
+            assert abs(h["score"] - s) <= 1e-4 * abs(s)
+            assert abs(h["scores"][scorer] - s1) <= 1e-4 * abs(s1)
+        assert [h.asdict()["yseq"] for h in batched[b]] == ys

@@ -286,15 +286,17 @@ def test_skinny_k_split_rows_independent(dev, N, K, dtype):
     assert _rel(y, y1.double()) < (1e-6 if dtype == torch.float32 else 1e-2)
 
 
-@pytest.mark.parametrize("M,N,K", [(40, 3072, 1024), (10, 1024, 1024), (64, 4096, 1024), (1, 256, 256), (17, 100, 512),
-                                   (40, 1024, 1000 - 1000 % 16)])
-def test_skinny_layernorm_prologue(dev, M, N, K):
+@pytest.mark.parametrize("M,N,K,off", [(40, 3072, 1024, 3.0), (10, 1024, 1024, 3.0), (64, 4096, 1024, 3.0),
+                                       (1, 256, 256, 3.0), (17, 100, 512, 3.0), (40, 1024, 1000 - 1000 % 16, 3.0),
+                                       (40, 1024, 1024, 100.0), (5, 256, 256, -300.0)])
+def test_skinny_layernorm_prologue(dev, M, N, K, off):
     """LayerNorm folded into the following fp32 few-row linear (ops.fold_layernorm + the kernel's
     LayerNorm prologue; the decoder's norm1/2/3 at decode time): vs LayerNorm then Linear in fp64,
-    inputs with a large common offset (the cancellation case of rstd * (x W'^T - mean * c1));
-    a row equals the same row launched alone, bit for bit."""
+    inputs with a common offset up to 150x their spread (the cancellation case of
+    rstd * (x W'^T - mean * c1), removed by the kernel's per-row shift); a row equals the same
+    row launched alone, bit for bit."""
     g = torch.Generator(device="cpu").manual_seed(M + N + K)
-    x = (torch.randn(M, K, generator=g) * 2 + 3).to(dev)
+    x = (torch.randn(M, K, generator=g) * 2 + off).to(dev)
     gam = (torch.rand(K, generator=g) + 0.5).to(dev)
     bet = (torch.randn(K, generator=g) * 0.1).to(dev)
     W = (torch.randn(N, K, generator=g) * K ** -0.5).to(dev)

@@ -1,5 +1,7 @@
 """Pin the CPU oracle (oracle/avsr_oracle.py) to the golden vectors the reference itself
 produced (tests/golden/make_golden.py). CPU only."""
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -85,3 +87,30 @@ def test_beam_search_oracle(g, b, beam):
     assert hyps[0].yseq == g[f"yseq_b{beam}_{b}"].tolist()
     ref = float(g[f"score_b{beam}_{b}"][0])
     assert abs(hyps[0].score - ref) <= 1e-4 * abs(ref)
+
+
+def _ctcw_hyps(c, key):
+    """every hypothesis the reference returned for avsr_ctcw.npz entry `key`"""
+    lens = c[key + "_len"]
+    ys = np.split(c[key + "_yseq"], np.cumsum(lens)[:-1])
+    return [y.tolist() for y in ys], c[key + "_score"]
+
+
+@pytest.mark.parametrize("w", [0.0, 1.0])
+@pytest.mark.parametrize("beam", [1, 3])
+@pytest.mark.parametrize("b", [0, 1])
+def test_beam_search_oracle_one_scorer(g, w, beam, b):
+    """the oracle's decoder-only (ctc_weight 0) and CTC-only full-vocabulary (ctc_weight 1)
+    searches return the reference's hypotheses (tests/golden/make_golden_ctcw.py): every token
+    sequence in order, scores to 1e-5"""
+    from oracle import decode_oracle as D
+    c = np.load(os.path.join(os.path.dirname(__file__), "golden", "avsr_ctcw.npz"))
+    sd = O.to_torch_state(golden_state(g))
+    x = torch.from_numpy(g[f"dec_enc_{b}"])
+    ctc_logp = torch.from_numpy(g[f"ctc_logp_{b}"])[0]
+    hyps = D.beam_search(sd, tiny_cfg(), x, ctc_logp, beam, ctc_weight=w)
+    ys, scores = _ctcw_hyps(c, f"w{w:g}_b{beam}_{b}")
+    assert [h.yseq for h in hyps] == ys
+    for h, s in zip(hyps, scores):
+        assert abs(h.score - s) <= 1e-5 * abs(s)
+    assert set(hyps[0].scores) == ({"decoder"} if w == 0.0 else {"ctc"})
