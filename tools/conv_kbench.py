@@ -9,7 +9,7 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
-from avsr_amd import ops  # noqa: E402
+from avsr_amd import _lib as L, ops  # noqa: E402
 
 reps = int(sys.argv[1]) if len(sys.argv) > 1 else 10
 dev = torch.device("cuda")
@@ -72,13 +72,13 @@ a = torch.full((64,), 0.25, device=dev)
 dw = torch.zeros(64, 3, 3, 64, device=dev)
 p1 = torch.empty(64, ops.conv_stat_tiles(geom, ops.dtype_code(x)), 3, device=dev)
 for flag in ("0", "1"):
-    os.environ["AVSR_CONV_PATCH"] = flag
+    L.set_option("conv_patch", int(flag))
     res[f"s1_fwd_patch{flag}"] = timed(lambda: ops.conv_fwd(geom, x, w, y, p1))
     res[f"s1_dgrad_bnr_patch{flag}"] = timed(lambda: ops.conv_bwd_data_bnr(geom, dy, w, dx, hh, st, a, beta=0.0))
     res[f"s1_dgrad_bnr_id_patch{flag}"] = timed(lambda: ops.conv_bwd_data_bnr(geom, dy, w, dx, hh, st, a, res=x,
                                                                              beta=1.0))
 for flag in ("0", "1"):
-    os.environ["AVSR_CONV_WPATCH"] = flag
+    L.set_option("conv_wpatch", int(flag))
     res[f"s1_wgrad_wpatch{flag}"] = timed(lambda: ops.conv_bwd_weight(geom, x, dy, dw))
 # stage 2: 11 x 11 x 128, 3x3 stride 1
 geom2 = ops.ConvGeom(N, 11, 11, 128, 128, 3, 3, (1, 1), (1, 1))
@@ -87,7 +87,7 @@ x2 = torch.randn(M2, 128, generator=g).to(dev, bf)
 dy2 = torch.randn(M2, 128, generator=g).to(dev, bf)
 dw2 = torch.zeros(128, 3, 3, 128, device=dev)
 for flag in ("0", "1"):
-    os.environ["AVSR_CONV_WPATCH"] = flag
+    L.set_option("conv_wpatch", int(flag))
     res[f"s2_wgrad_wpatch{flag}"] = timed(lambda: ops.conv_bwd_weight(geom2, x2, dy2, dw2))
 # stage-2 forward / data-grad (general implicit-GEMM kernels), for the fwd vs dgrad gap
 w2 = (torch.randn(128, 3, 3, 128, generator=g) * 0.03).to(dev, bf)

@@ -10,6 +10,7 @@ M, N, K = (int(a) for a in sys.argv[1:4])
 kind = sys.argv[4] if len(sys.argv) > 4 else "fwd"
 reps = int(sys.argv[5]) if len(sys.argv) > 5 else 20
 dev = torch.device("cuda")
+ops.L.set_option("gemm_tile", os.environ.get("GEMM_TILE", "auto"))
 x = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
 W = torch.randn(N, K, device=dev, dtype=torch.bfloat16)
 dy = torch.randn(M, N, device=dev, dtype=torch.bfloat16)
@@ -23,4 +24,4 @@ fn = {"fwd": lambda: ops.linear_fwd(x, W),
 for _ in range(reps):
     fn()
 torch.cuda.synchronize()
-print("done", M, N, K, kind, os.environ.get("AVSR_GEMM_TILE", "auto"))
+print("done", M, N, K, kind, os.environ.get("GEMM_TILE", "auto"))

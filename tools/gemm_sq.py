@@ -1,5 +1,5 @@
 """bf16 GEMM cores on square and encoder shapes (random [-1,1) operands, HIP-graph timed):
-AVSR_GEMM_TILE in {auto, 128, pp, 256}. usage: python tools/gemm_sq.py [cfg,cfg,...]"""
+library option gemm_tile in {auto, 128, pp, 256}. usage: python tools/gemm_sq.py [cfg,cfg,...]"""
 import os
 import sys
 
@@ -19,8 +19,8 @@ for M, N, K in shapes:
     fl = 2.0 * M * N * K
     line = f"M{M:5d} N{N:5d} K{K:5d}"
     for c in cfgs:
-        os.environ["AVSR_GEMM_TILE"] = c
+        ops.L.set_option("gemm_tile", c)
         us = timed(lambda: ops.linear_fwd(x, W), n=5 if M > 4096 else 10)
         line += f"  {c}: {us:8.1f}us {fl / us / 1e6:6.0f}TF"
-    os.environ.pop("AVSR_GEMM_TILE", None)
+    ops.L.set_option("gemm_tile", "auto")
     print(line, flush=True)

@@ -1,6 +1,6 @@
 """Per-shape table of the encoder GEMMs at C2 (M = B*T = 6000 tokens, d = 1024, F = 4096):
 QKV, out-proj, FFN1, FFN2 x forward / data-grad / weight-grad, each under every GEMM tile
-configuration (AVSR_GEMM_TILE), with the engine's own split-K choice for weight-grads.
+configuration (library option gemm_tile), with the engine's own split-K choice for weight-grads.
 Launches are captured in a HIP graph (device time only). Prints a table and writes JSON.
 
   python tools/gemm_table.py [out.json] [cfg,cfg,...]
@@ -74,9 +74,9 @@ def main():
                 rec.update(M=N, N=K, K=M)
             for c in cfgs:
                 if c == "auto":
-                    os.environ.pop("AVSR_GEMM_TILE", None)
+                    ops.L.set_option("gemm_tile", "auto")
                 else:
-                    os.environ["AVSR_GEMM_TILE"] = c
+                    ops.L.set_option("gemm_tile", c)
                 try:
                     us = timed(fn)
                 except Exception as e:          # a config may refuse a shape
@@ -84,7 +84,7 @@ def main():
                     continue
                 rec["us"][c] = round(us, 2)
                 rec["tflops"][c] = round(fl / us / 1e6, 1)
-            os.environ.pop("AVSR_GEMM_TILE", None)
+            ops.L.set_option("gemm_tile", "auto")
             best = max(rec["tflops"], key=rec["tflops"].get)
             rec["best"] = best
             rec["best_frac"] = round(rec["tflops"][best] / PEAK, 4)

@@ -8,7 +8,7 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
-from avsr_amd import engine as E  # noqa: E402
+from avsr_amd import _lib as L, engine as E  # noqa: E402
 from avsr_amd.avhubert_avsr_model import AVHubertAVSR  # noqa: E402
 from avsr_amd.configuration_avhubert_avsr import AVHubertAVSRConfig  # noqa: E402
 from bench import synthetic_batch  # noqa: E402
@@ -39,7 +39,7 @@ def once(fuse):
     return ev[0].elapsed_time(ev[1]), ev[1].elapsed_time(ev[2])
 
 
-# variants: (label, BN fusion, AVSR_CONV_S2PHASE)
+# variants: (label, BN fusion, library option conv_s2phase)
 mode = sys.argv[2] if len(sys.argv) > 2 else "fuse"
 variants = [("fuse=1", True, "1"), ("fuse=0", False, "1")] if mode == "fuse" else \
     [("c192=1", True, "1", "1"), ("c192=0", True, "1", "0")] if mode == "c192" else \
@@ -49,9 +49,9 @@ variants = [("fuse=1", True, "1"), ("fuse=0", False, "1")] if mode == "fuse" els
 
 
 def run(var):
-    os.environ["AVSR_CONV_S2PHASE"] = var[2]
-    os.environ["AVSR_CONV_192"] = var[3] if len(var) > 3 else "1"
-    os.environ["AVSR_CONV_PATCH"] = var[4] if len(var) > 4 else "1"
+    L.set_option("conv_s2phase", int(var[2]))
+    L.set_option("conv_192", int(var[3]) if len(var) > 3 else 1)
+    L.set_option("conv_patch", int(var[4]) if len(var) > 4 else 1)
     E._STEM_DIRECT = var[5] if len(var) > 5 else True
     return once(var[1])
 
