@@ -687,27 +687,25 @@ __global__ __launch_bounds__(PCfg::NTH, 2) void conv_patch_kernel(ConvArgs a, Pa
     const int kh = kt / 3, kw = kt - 3 * kh;
     return pg.sign * ((kh - 1) * pg.Wp + (kw - 1));
   };
-  PatchFrags<LB> cur, nxt;
-  cur.load(patch, row, toff(0), ring, 0, lane);
+  // two fragment sets in fixed roles (k-step 0 / 1 of a tap): no register copies (gemm_glds.h)
+  static_assert(KS == 2, "the fragment sets alternate over two k-steps per K-tile");
+  PatchFrags<LB> f0, f1;
+  f0.load(patch, row, toff(0), ring, 0, lane);
   int cs = 0;
   for (int kt = 0; kt < NK; ++kt) {
     const int ns = cs + 1 == S ? 0 : cs + 1;
-#pragma unroll
-    for (int s = 0; s < KS; ++s) {
-      if (s + 1 < KS) {
-        nxt.load(patch, row, toff(kt), ring + cs * PATCH_SB, s + 1, lane);
-      } else if (kt + 1 < NK) {
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        if (kt + S - 1 < NK) gemmg::wait_vmcnt<GLB * (S - 2)>();
-        else gemmg::wait_vmcnt<0>();
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-        if (kt + S < NK) lb.issue(ring + cs * PATCH_SB, (kt + S) * GBK, wave);
-        nxt.load(patch, row, toff(kt + 1), ring + ns * PATCH_SB, 0, lane);
-      }
-      cur.mma(acc);
-      cur = nxt;
+    f1.load(patch, row, toff(kt), ring + cs * PATCH_SB, 1, lane);
+    f0.mma(acc);
+    if (kt + 1 < NK) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (kt + S - 1 < NK) gemmg::wait_vmcnt<GLB * (S - 2)>();
+      else gemmg::wait_vmcnt<0>();
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (kt + S < NK) lb.issue(ring + cs * PATCH_SB, (kt + S) * GBK, wave);
+      f0.load(patch, row, toff(kt + 1), ring + ns * PATCH_SB, 0, lane);
     }
+    f1.mma(acc);
     cs = ns;
   }
   __syncthreads();

@@ -331,6 +331,7 @@ using Cfg192s3 = gemmg::GCfg<2, 2, 3, 2, 3>;     // 192x128, 4 waves, 3 stages (
 using Cfg192w8 = gemmg::GCfg<2, 4, 3, 1, 2>;     // 192x128, 8 waves (96x32 each), 2 stages (80 KiB)
 using Cfg192w8s3 = gemmg::GCfg<2, 4, 3, 1, 3>;   // 192x128, 8 waves, 3 stages (120 KiB)
 using Cfg64 = gemmg::GCfg<2, 2, 1, 1, 2>;        // 64x64, 4 waves (32x32 each), 2 stages (32 KiB)
+using Cfg192w8s4 = gemmg::GCfg<2, 4, 3, 1, 4>;   // 192x128, 8 waves, 4 stages (160 KiB: 3 K-tiles in flight)
 
 // tile choice: AVSR_OPT_GEMM_TILE = k + 1 forces configuration k (AVSR_TILE_*, benchmarks);
 // otherwise the configuration with the fewest block rounds x per-tile work (wave quantisation
@@ -386,6 +387,7 @@ int cfg_bm(int cfg, bool ak) {
     case 13: return ak ? Cfg192s3::BM : Cfg128::BM;
     case 14: return ak ? Cfg192w8::BM : Cfg128::BM;
     case 15: return ak ? Cfg192w8s3::BM : Cfg128::BM;
+    case 17: return ak ? Cfg192w8s4::BM : Cfg128::BM;
     default: return Cfg128::BM;
   }
 }
@@ -420,6 +422,9 @@ int launch_cfg(int cfg, const DenseArgs& a, int batch, hipStream_t st) {
       else return launch_glds<OutT, AK, BK, Cfg128>(a, batch, st);
     case 15:
       if constexpr (AK) return launch_glds<OutT, AK, BK, Cfg192w8s3>(a, batch, st);
+      else return launch_glds<OutT, AK, BK, Cfg128>(a, batch, st);
+    case 17:
+      if constexpr (AK) return launch_glds<OutT, AK, BK, Cfg192w8s4>(a, batch, st);
       else return launch_glds<OutT, AK, BK, Cfg128>(a, batch, st);
     default: return launch_glds<OutT, AK, BK, Cfg128>(a, batch, st);
   }
@@ -616,11 +621,12 @@ __global__ __launch_bounds__(256) void skinny_kernel(DenseArgs a, float* part, i
 // LNP (LayerNorm prologue, a.ln_c1): the batch holds whole rows of the chunk, so each row's chunk
 // mean and M2 (two passes over the registers, partials over the 4 lanes of a row and the 8 waves in
 // a fixed order) come for free; split launches hand them over with the partial sums (a.lnst) and
-// the last arriver combines them (Chan et al.'s pairwise formula, split order); the MFMAs run on
-// x - s against gamma o W, with s = x[m][0] a per-row shift every chunk knows, and the epilogue
-// applies rstd * (acc - (mean - s) * c1[n]): without the shift a row whose |mean| is large next to
-// its spread would subtract two large terms (acc ~ mean * c1) and lose the digits the reference's
-// normalise-then-project keeps.
+// the last arriver combines them (Chan et al.'s pairwise formula, split order). Everything runs on
+// x' = x - s with s = x[m][0], a per-row shift every chunk knows (x - s is exact in fp32 for values
+// within a factor 2): the statistics give mean' = mean - s, the MFMAs x' against gamma o W, and the
+// epilogue applies rstd * (acc - mean' * c1[n]). Without the shift a row whose |mean| is large next
+// to its spread would subtract two large terms (acc ~ mean * c1) and lose the digits the
+// reference's normalise-then-project keeps.
 constexpr int SKM_WAVES = 8;
 template <typename OutT, int MT, int UNR, bool LNP = false>
 __global__ __launch_bounds__(64 * SKM_WAVES) void skinny_mma_kernel(DenseArgs a, float* part, int kchunk, unsigned* cnt) {
@@ -670,10 +676,18 @@ __global__ __launch_bounds__(64 * SKM_WAVES) void skinny_mma_kernel(DenseArgs a,
 #pragma unroll
       for (int t = 0; t < MT; ++t) x[u][t] = (ok && rok[t]) ? *(const f32x4*)(Ar[t] + k) : f32x4{0.f, 0.f, 0.f, 0.f};
     }
-    if constexpr (LNP) {       // the batch holds the chunk's rows: chunk mean and M2 per row
+    if constexpr (LNP) {       // the batch holds the chunk's rows: chunk mean and M2 per row of x - s
       float sft[MT];
 #pragma unroll
       for (int t = 0; t < MT; ++t) sft[t] = ((const float*)a.A)[(int64_t)min(16 * t + c, a.M - 1) * a.lda];
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {   // loads past the chunk stay 0 (they meet b = 0 and no statistic)
+        const bool ok = q0 + NW * u < ng;
+#pragma unroll
+        for (int t = 0; t < MT; ++t)
+#pragma unroll
+          for (int e2 = 0; e2 < 4; ++e2) x[u][t][e2] = ok ? x[u][t][e2] - sft[t] : 0.f;
+      }
       const float inv_n = 1.f / (float)(kend - kbeg);
 #pragma unroll
       for (int t = 0; t < MT; ++t) {
@@ -702,12 +716,6 @@ __global__ __launch_bounds__(64 * SKM_WAVES) void skinny_mma_kernel(DenseArgs a,
         s2 += __shfl_xor(s2, 32, 64);
         if (g == 0) st2[w][16 * t + c] = s2;
       }
-#pragma unroll
-      for (int u = 0; u < UNR; ++u)     // (loads past the chunk are 0 against b = 0: still 0)
-#pragma unroll
-        for (int t = 0; t < MT; ++t)
-#pragma unroll
-          for (int e2 = 0; e2 < 4; ++e2) x[u][t][e2] -= sft[t];
     }
 #pragma unroll
     for (int u = 0; u < UNR; ++u)
@@ -760,8 +768,7 @@ __global__ __launch_bounds__(64 * SKM_WAVES) void skinny_mma_kernel(DenseArgs a,
         if constexpr (LNP) {
           float mean, m2;
           chunk_stats(m, mean, m2);
-          const float s = ((const float*)a.A)[(int64_t)m * a.lda];
-          v = (1.f / sqrtf(m2 / (float)a.K + a.ln_eps)) * (v - (mean - s) * a.ln_c1[cl]);
+          v = (1.f / sqrtf(m2 / (float)a.K + a.ln_eps)) * (v - mean * a.ln_c1[cl]);
         }
         epi(i, m, cl, v);
       }
@@ -820,7 +827,7 @@ __global__ __launch_bounds__(64 * SKM_WAVES) void skinny_mma_kernel(DenseArgs a,
       const float* pp = part + (int64_t)m * a.N + cl;
       float v = __hip_atomic_load(pp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       for (int q = 1; q < S; ++q) v += __hip_atomic_load(pp + q * MN, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if constexpr (LNP) v = rrstd[m] * (v - (rmean[m] - ((const float*)a.A)[(int64_t)m * a.lda]) * a.ln_c1[cl]);
+      if constexpr (LNP) v = rrstd[m] * (v - rmean[m] * a.ln_c1[cl]);
       epi(i, m, cl, v);
     }
   }

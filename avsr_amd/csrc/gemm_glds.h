@@ -270,31 +270,31 @@ AVSR_DEV void mainloop_glds(const LA& la, const LB& lb, int kbeg, int nk, f32x4 
   else wait_vmcnt<0>();
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
-  Frags<CF, LA::KMAJ, LB::KMAJ> cur, nxt;
-  cur.load(smem, 0, wm, wn, lane);
+  // two fragment sets in fixed roles (KS == 2): f0 holds k-step 0 of a tile, f1 k-step 1, so the
+  // register double-buffer needs no copies (a `cur = nxt` rotation compiled to 16 v_mov_b64 per
+  // k-step on the 96x32 wave tile)
+  static_assert(KS == 2, "the fragment sets alternate over two k-steps per K-tile");
+  Frags<CF, LA::KMAJ, LB::KMAJ> f0, f1;
+  f0.load(smem, 0, wm, wn, lane);
   int cs = 0;                       // stage of tile kt
   for (int kt = 0; kt < nk; ++kt) {
     const char* stage = smem + cs * CF::STAGE;
     const int ns = cs + 1 == S ? 0 : cs + 1;
-#pragma unroll
-    for (int s = 0; s < KS; ++s) {
-      if (s + 1 < KS) {
-        nxt.load(stage, s + 1, wm, wn, lane);
-      } else if (kt + 1 < nk) {
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        wait_tiles_ahead<CF>(kt + S - 1 < nk);
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-        if (kt + S < nk) {
-          char* st = smem + cs * CF::STAGE;
-          la.issue(st, kbeg + (kt + S) * GBK, wave);
-          lb.issue(st + CF::SA, kbeg + (kt + S) * GBK, wave);
-        }
-        nxt.load(smem + ns * CF::STAGE, 0, wm, wn, lane);
+    f1.load(stage, 1, wm, wn, lane);
+    f0.mma(acc);
+    if (kt + 1 < nk) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      wait_tiles_ahead<CF>(kt + S - 1 < nk);
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (kt + S < nk) {
+        char* st = smem + cs * CF::STAGE;
+        la.issue(st, kbeg + (kt + S) * GBK, wave);
+        lb.issue(st + CF::SA, kbeg + (kt + S) * GBK, wave);
       }
-      cur.mma(acc);
-      cur = nxt;
+      f0.load(smem + ns * CF::STAGE, 0, wm, wn, lane);
     }
+    f1.mma(acc);
     cs = ns;
   }
   __syncthreads();

@@ -93,11 +93,13 @@ def _slab_cnt(device):
 
 
 def reserve_stream_workspaces(device, dec_attn_floats=0):
-    """create (zeroed) the current stream's few-row GEMM workspace and size its dec_attn
-    partial buffer to at least `dec_attn_floats`, eagerly — call outside any graph capture"""
+    """create (zeroed) the current stream's few-row GEMM workspace and slab split-K counters and
+    size its dec_attn partial buffer to at least `dec_attn_floats`, eagerly — call outside any
+    graph capture, on the stream that will be captured"""
     assert not torch.cuda.is_current_stream_capturing()
     device = _norm_dev(device)
     _skinny_ws(device)
+    _slab_cnt(device)
     key = (device, L.stream_ptr().value)
     ws = _DA_WS.get(key)
     if dec_attn_floats and (ws is None or ws.numel() < dec_attn_floats):

@@ -492,10 +492,13 @@ def gpu_bench(args):
     achieved = flops / (avg_ms * 1e-3) / 1e12 if avg_ms > 0 else 0.0
     # FLOPs the timed steps performed (video_off steps skip the ResNet backward)
     fpf = sum(model_flops_per_frame(cfg, T, L, d or "none") for d in timed_drops) / max(1, len(timed_drops))
-    traffic = None      # HBM bytes per launch from the committed PMC passes (tools/pmc_traffic.py)
-    tp = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if os.path.exists(tp):
-        rec = json.load(open(tp))
+    # HBM bytes per launch from the committed PMC passes of the current GEMM core (tools/pmc_traffic.py
+    # via tools/gpu_counters.sh): the newest profiles/r*_pmc_traffic.json
+    traffic, traffic_src = None, None
+    cands = sorted(f for f in os.listdir(os.path.join(ROOT, "profiles")) if f.endswith("_pmc_traffic.json"))
+    if cands:
+        traffic_src = "profiles/" + cands[-1]
+        rec = json.load(open(os.path.join(ROOT, traffic_src)))
         if rec.get("shape") == [M, N_, K_]:
             traffic = rec["traffic_bytes"]
 
@@ -555,7 +558,7 @@ def gpu_bench(args):
         "roofline": {"bound": "mfma", "kernel": f"dense_glds_kernel bf16 (encoder FFN1 fwd {M}x{N_}x{K_})",
                      "achieved": round(achieved, 1), "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": round(achieved / BF16_PEAK_TFLOPS, 4), "traffic": traffic,
-                     "traffic_unit": "bytes/launch (rocprofv3 FETCH_SIZEx2+WRITE_SIZE, profiles/pmc_traffic.json)",
+                     "traffic_unit": f"bytes/launch (rocprofv3 FETCH_SIZEx2+WRITE_SIZE, {traffic_src})",
                      "algorithmic_flops_per_launch": flops, "launches": nl,
                      "avg_launch_ms": round(avg_ms, 4), "median_launch_ms": round(med_ms, 4),
                      "timing": "in-kernel s_memrealtime stamps (first workgroup start -> last workgroup end)",

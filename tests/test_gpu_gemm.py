@@ -343,3 +343,29 @@ def test_skinny_kv_cache_append(dev, ln):
     assert torch.equal(kc[3 * rows:3 * rows + M], kr[3 * rows:3 * rows + M])
     assert torch.equal(vc[3 * rows:3 * rows + M], vr[3 * rows:3 * rows + M])
     assert torch.isnan(kc[:3 * rows]).all() and torch.isnan(kc[3 * rows + M:]).all()
+
+
+@pytest.mark.parametrize("M,N,K", [(20, 768, 256), (40, 1024, 1024), (17, 256, 512)])
+def test_skinny_layernorm_prologue_every_row_alone(dev, M, N, K):
+    """batch invariance of the folded-LayerNorm few-row linear for EVERY row: each row of an
+    M-row launch (row tiles of 16: the row's lane position differs between the launches) equals
+    the same row launched alone, bit for bit, with and without the fused K/V-cache append"""
+    g = torch.Generator(device="cpu").manual_seed(M * 7 + N + K)
+    x = (torch.randn(M, K, generator=g) * 1.5 + torch.randn(M, 1, generator=g) * 4).to(dev)
+    W = (torch.randn(N, K, generator=g) * K ** -0.5).to(dev)
+    b = torch.randn(N, generator=g).to(dev)
+    Wg, bb, c1 = ops.fold_layernorm(W, b, (torch.rand(K, generator=g) + 0.5).to(dev),
+                                    (torch.randn(K, generator=g) * 0.1).to(dev))
+    y = ops.linear_fwd(x, Wg, bb, ln=(c1, 1e-12))
+    for m in range(M):
+        one = ops.linear_fwd(x[m:m + 1].contiguous(), Wg, bb, ln=(c1, 1e-12))
+        assert torch.equal(one[0], y[m]), m
+    if N % 3 == 0:
+        D = N // 3
+        pos = torch.tensor([1], dtype=torch.int32, device=dev)
+        kc = torch.zeros(2 * M, D, device=dev); vc = torch.zeros(2 * M, D, device=dev)
+        q = ops.linear_fwd(x, Wg, bb, ln=(c1, 1e-12), kv=(kc, vc, pos, M))
+        for m in range(M):
+            k1 = torch.zeros(2, D, device=dev); v1 = torch.zeros(2, D, device=dev)
+            q1 = ops.linear_fwd(x[m:m + 1].contiguous(), Wg, bb, ln=(c1, 1e-12), kv=(k1, v1, pos, 1))
+            assert torch.equal(q1[0, :D], q[m, :D]) and torch.equal(k1[1], kc[M + m]) and torch.equal(v1[1], vc[M + m]), m

@@ -26,6 +26,7 @@ def timed(fn, n=10, reps=5):
     torch.cuda.synchronize()
     s = torch.cuda.Stream()
     with torch.cuda.stream(s):
+        ops.reserve_stream_workspaces(dev)      # zeroed split-K counters exist before the capture
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g, stream=s):
             for _ in range(n):
@@ -67,6 +68,12 @@ def main():
         ops_ = {"fwd": lambda: ops.linear_fwd(x, W),
                 "dgrad": lambda: ops.linear_dgrad(dy, W),
                 "wgrad": lambda: wgrad(dy, x, dW)}
+        if name == "ffn1" and os.environ.get("GEMM_TABLE_PROBE", "1") == "1":
+            # the bench roofline probe: FFN1 forward with its full epilogue (bias, GELU, pre-activation
+            # store, dropout); not counted in the layer totals below
+            bias = torch.zeros(N, device=dev)
+            h = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+            ops_["probe"] = lambda: ops.linear_fwd(x, W, bias, act=1, preact=h, drop_p=0.1, seed=7)
         for op, fn in ops_.items():
             rec = {"layer": name, "op": op, "M": M, "N": N if op != "dgrad" else K, "K": K if op != "dgrad" else N,
                    "gflop": round(fl / 1e9, 2), "us": {}, "tflops": {}}
@@ -92,9 +99,10 @@ def main():
             print(f"{name:5s} {op:5s} M{rec['M']:5d} N{rec['N']:5d} K{rec['K']:5d} " +
                   " ".join(f"{c}:{rec['us'].get(c, float('nan')):7.1f}us/{rec['tflops'].get(c, 0):5.0f}" for c in cfgs) +
                   f"  best {best} {rec['best_frac']:.3f}", flush=True)
-    tot_auto = sum(r["us"].get("auto", 0) for r in rows)
-    tot_best = sum(min(r["us"].values()) for r in rows)
-    fl_all = sum(r["gflop"] for r in rows) * 1e9
+    layer = [r for r in rows if r["op"] != "probe"]
+    tot_auto = sum(r["us"].get("auto", 0) for r in layer)
+    tot_best = sum(min(r["us"].values()) for r in layer)
+    fl_all = sum(r["gflop"] for r in layer) * 1e9
     print(f"one encoder layer, 12 GEMMs: auto {tot_auto:.0f} us ({fl_all / tot_auto / 1e6:.0f} TF/s), "
           f"best-per-shape {tot_best:.0f} us ({fl_all / tot_best / 1e6:.0f} TF/s)", flush=True)
     if out:

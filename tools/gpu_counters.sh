@@ -28,5 +28,6 @@ for prog in ${PROGS:-probe wgrad attn stem cwgrad step}; do
   done
   timeout -k 10 60 python tools/pmc_sum.py $O/sq_$prog.json $O/${prog}A/run_counter_collection.csv $O/${prog}B/run_counter_collection.csv > $O/sq_$prog.txt 2>&1 || { echo "sum $prog failed"; exit 1; }
   echo "== $prog"; head -12 $O/sq_$prog.txt
+  [ $prog = step ] && rm -rf $O/${prog}A $O/${prog}B     # the per-dispatch step CSVs exceed what gpurun copies back
 done
 echo rc=0

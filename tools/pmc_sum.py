@@ -1,6 +1,6 @@
 """Sum rocprofv3 --pmc counters per kernel (name pattern groups) from *_counter_collection.csv
 files. usage: python tools/pmc_sum.py out.json csv [csv ...]
-Derived: mfma_busy = SQ_VALU_MFMA_BUSY_CYCLES / SQ_BUSY_CYCLES per the kernel's dispatches;
+Derived: mfma_util = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 XCDs x 1024 SIMDs);
 valu/mfma/lds instruction ratios; LDS bank-conflict share of LDS-array cycles."""
 import csv
 import json
@@ -38,9 +38,9 @@ res = {}
 for k, c in acc.items():
     d = dict(c)
     d["dispatches"] = len(disp[k])
-    if c.get("SQ_BUSY_CYCLES"):
-        if "SQ_VALU_MFMA_BUSY_CYCLES" in c:
-            d["mfma_busy_frac"] = round(c["SQ_VALU_MFMA_BUSY_CYCLES"] / c["SQ_BUSY_CYCLES"], 4)
+    if c.get("GRBM_GUI_ACTIVE") and "SQ_VALU_MFMA_BUSY_CYCLES" in c:
+        # MFMA pipe busy share of the SIMD cycles: GRBM_GUI_ACTIVE sums the 8 XCDs' cycle counts
+        d["mfma_util"] = round(c["SQ_VALU_MFMA_BUSY_CYCLES"] / (c["GRBM_GUI_ACTIVE"] / 8 * 1024), 4)
     if c.get("SQ_INSTS_MFMA"):
         for x in ("SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_INSTS_VMEM", "SQ_INSTS_SALU"):
             if x in c:
@@ -54,9 +54,9 @@ for k, c in acc.items():
                 d[x.lower() + "_frac"] = round(c[x] / c["SQ_WAVE_CYCLES"], 4)
     res[k] = d
 json.dump(res, open(out, "w"), indent=1, sort_keys=True)
-for k in sorted(res, key=lambda k: -res[k].get("SQ_BUSY_CYCLES", 0))[:30]:
+for k in sorted(res, key=lambda k: -res[k].get("GRBM_GUI_ACTIVE", 0))[:30]:
     d = res[k]
-    print(f"{k[:60]:60s} n={d['dispatches']:4d} mfma_busy={d.get('mfma_busy_frac', '-')} "
+    print(f"{k[:60]:60s} n={d['dispatches']:4d} mfma_util={d.get('mfma_util', '-')} "
           f"valu/mfma={d.get('valu_per_mfma', '-')} lds/mfma={d.get('lds_per_mfma', '-')} "
           f"ldsconf={d.get('lds_conflict_frac', '-')} wait={d.get('sq_wait_any_frac', '-')} "
           f"waitinst={d.get('sq_wait_inst_any_frac', '-')}")
