@@ -80,40 +80,39 @@ AVSR_DEV uint32_t mix32_lo(uint32_t pre, uint32_t lo) { return fmix32((lo * 0x9E
 AVSR_DEV uint32_t mix32(uint64_t seed, uint64_t idx) {
   return mix32_lo(mix32_hi(seed, (uint32_t)(idx >> 32)), (uint32_t)idx);
 }
-// dropout over an index space of `total` elements: when every index fits in 32 bits (a
-// kernel-uniform test, e.g. B*H*Lq*Lk = 36 M for the C2 encoder attention) the high-word mix
-// is a constant and each element costs one finaliser; same mask as drop_scale
-struct DropTile {
-  uint32_t pre, thr; float keep_scale; bool small;
-  AVSR_DEV DropTile(float p, uint64_t seed, uint64_t total) {
-    thr = (uint32_t)(p * 4294967296.0f);
-    keep_scale = 1.0f / (1.0f - p);
-    small = total <= 0x100000000ull;
-    pre = mix32_hi(seed, 0u);
-  }
-  AVSR_DEV float scale(uint64_t seed, uint64_t idx) const {
-    const uint32_t h = small ? mix32_lo(pre, (uint32_t)idx) : mix32(seed, idx);
-    return h >= thr ? keep_scale : 0.0f;
-  }
-};
+// Elementwise dropout (GEMM epilogues, ew_bwd / dropout_fwd, the LayerNorm backward's fused
+// ew_bwd): element idx reads the 16-bit half (idx & 1) of the hash of PAIR idx >> 1 — one
+// finaliser per two elements, the scheme of the attention kernels' AttnDrop — and is dropped iff
+// that half < thr = round(p * 65536) (p_eff within 8e-6 of p); kept values are scaled by
+// 65536 / (65536 - thr), so E[mask] = 1 exactly. Every site evaluates this same function of
+// (seed, idx): masks are recomputed, never stored.
+AVSR_DEV uint32_t drop_thr16(float p) { return (uint32_t)(p * 65536.f + 0.5f); }
+AVSR_DEV float drop_keep_scale(uint32_t thr) { return thr < 65536u ? 65536.f / (float)(65536u - thr) : 0.f; }
+AVSR_DEV uint32_t drop_half(uint32_t h, bool odd) { return odd ? (h >> 16) : (h & 0xFFFFu); }
 
 AVSR_DEV float drop_scale(float p, uint64_t seed, uint64_t idx) {
-  // returns 0 for dropped, 1/(1-p) for kept
-  uint32_t thr = (uint32_t)(p * 4294967296.0f);
-  return mix32(seed, idx) >= thr ? 1.0f / (1.0f - p) : 0.0f;
+  // returns 0 for dropped, 65536 / (65536 - thr) for kept
+  const uint32_t thr = drop_thr16(p);
+  return drop_half(mix32(seed, idx >> 1), idx & 1) >= thr ? drop_keep_scale(thr) : 0.0f;
 }
 
-// drop_scale over indices d0 .. d0+7, multiplied into v: when the 8 indices share their high
-// word the mix32_hi finaliser is computed once (same mask as drop_scale element by element)
+// drop_scale over indices d0 .. d0+7, multiplied into v: for even d0 the 4 pairs are hashed once
+// each, with the high-word finaliser shared when they have one high word (same mask as
+// drop_scale element by element)
 AVSR_DEV void drop8(float p, uint64_t seed, uint64_t d0, float* v) {
-  const uint32_t thr = (uint32_t)(p * 4294967296.0f);
-  const float ks = 1.0f / (1.0f - p);
-  const uint32_t lo = (uint32_t)d0;
-  if (lo <= 0xFFFFFFF8u) {
-    const uint32_t pre = mix32_hi(seed, (uint32_t)(d0 >> 32));
+  const uint32_t thr = drop_thr16(p);
+  const float ks = drop_keep_scale(thr);
+  const uint64_t p0 = d0 >> 1;
+  const uint32_t lo = (uint32_t)p0;
+  if (!(d0 & 1) && lo <= 0xFFFFFFFCu) {
+    const uint32_t pre = mix32_hi(seed, (uint32_t)(p0 >> 32));
     const uint32_t g0 = lo * 0x9E3779B1u;
 #pragma unroll
-    for (int q = 0; q < 8; ++q) v[q] *= fmix32((g0 + (uint32_t)q * 0x9E3779B1u) ^ pre) >= thr ? ks : 0.0f;
+    for (int q = 0; q < 4; ++q) {
+      const uint32_t h = fmix32((g0 + (uint32_t)q * 0x9E3779B1u) ^ pre);
+      v[2 * q] *= (h & 0xFFFFu) >= thr ? ks : 0.0f;
+      v[2 * q + 1] *= (h >> 16) >= thr ? ks : 0.0f;
+    }
   } else {
 #pragma unroll
     for (int q = 0; q < 8; ++q) v[q] *= drop_scale(p, seed, d0 + q);

@@ -885,10 +885,11 @@ int skinny_launch(const DenseArgs& a, float* ws, hipStream_t st) {
       al.lnst = S > 1 ? ws + (int64_t)S * a.M * a.N : nullptr;   // chunk statistics after the partials
 #define SKL_LN(T_) do { if (unr == 4) hipLaunchKernelGGL((skinny_mma_kernel<OutT, T_, 4, true>), g, dim3(64 * SKM_WAVES), 0, st, al, part, kchunk, cnt); \
                         else hipLaunchKernelGGL((skinny_mma_kernel<OutT, T_, 8, true>), g, dim3(64 * SKM_WAVES), 0, st, al, part, kchunk, cnt); } while (0)
-      if (a.M <= 16) SKL_LN(1);
-      else if (a.M <= 32) SKL_LN(2);
-      else if (a.M <= 48) SKL_LN(3);
-      else SKL_LN(4);
+      // one row-tile count for every M: the per-row statistics / shift / epilogue arithmetic of the
+      // MT = 1..3 instantiations compiled to different roundings (a row's result then depended on
+      // how many rows shared the launch: batched decode != per-utterance by 1e-5, and
+      // test_skinny_layernorm_prologue_every_row_alone failed); MT = 4 for all is batch-invariant
+      SKL_LN(4);
 #undef SKL_LN
       AVSR_CHECK_LAUNCH();
       return 0;

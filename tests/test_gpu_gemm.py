@@ -369,3 +369,17 @@ def test_skinny_layernorm_prologue_every_row_alone(dev, M, N, K):
             k1 = torch.zeros(2, D, device=dev); v1 = torch.zeros(2, D, device=dev)
             q1 = ops.linear_fwd(x[m:m + 1].contiguous(), Wg, bb, ln=(c1, 1e-12), kv=(k1, v1, pos, 1))
             assert torch.equal(q1[0, :D], q[m, :D]) and torch.equal(k1[1], kc[M + m]) and torch.equal(v1[1], vc[M + m]), m
+
+
+@pytest.mark.parametrize("M,N,K", [(20, 768, 256), (40, 1024, 1024), (17, 256, 512)])
+def test_skinny_every_row_alone(dev, M, N, K):
+    """the plain fp32 few-row linear (no LayerNorm prologue): every row of an M-row launch equals
+    the same row launched alone, bit for bit"""
+    g = torch.Generator(device="cpu").manual_seed(M * 5 + N + K)
+    x = (torch.randn(M, K, generator=g) + 3).to(dev)
+    W = (torch.randn(N, K, generator=g) * K ** -0.5).to(dev)
+    b = torch.randn(N, generator=g).to(dev)
+    y = ops.linear_fwd(x, W, b)
+    for m in range(M):
+        one = ops.linear_fwd(x[m:m + 1].contiguous(), W, b)
+        assert torch.equal(one[0], y[m]), m
