@@ -336,6 +336,12 @@ using Cfg192w8s4 = gemmg::GCfg<2, 4, 3, 1, 4>;   // 192x128, 8 waves, 4 stages (
 // tile choice: AVSR_OPT_GEMM_TILE = k + 1 forces configuration k (AVSR_TILE_*, benchmarks);
 // otherwise the configuration with the fewest block rounds x per-tile work (wave quantisation
 // over 256 CUs)
+#ifndef AVSR_AB_FWD2      // A/B builds only (tools/build_variant.py): tile of the multi-round shapes
+#define AVSR_AB_FWD2 11
+#endif
+#ifndef AVSR_AB_ROUND1    // ... and of the one-round (N = 1024) shapes
+#define AVSR_AB_ROUND1 15
+#endif
 int tile_cfg(const avsr_gemm_params* p, int splits) {
   const int forced = (int)avsr_opt(AVSR_OPT_GEMM_TILE) - 1;
   if (forced >= 0) return forced;
@@ -351,11 +357,11 @@ int tile_cfg(const avsr_gemm_params* p, int splits) {
     const long t128 = (long)((p->M + 127) / 128) * ((p->N + 127) / 128) * tiles_z;
     const long t192 = (long)((p->M + 191) / 192) * ((p->N + 127) / 128) * tiles_z;
     const long n128 = (t128 + 255) / 256, n192 = (t192 + 255) / 256;   // blocks on the busiest CU
-    if (n192 >= 2 && 3 * n192 * 50 <= 2 * n128 * 51) return 11;      // 1.5 n192 <= 1.02 n128
+    if (n192 >= 2 && 3 * n192 * 50 <= 2 * n128 * 51) return AVSR_AB_FWD2;      // 1.5 n192 <= 1.02 n128
     // one round of 192-row tiles that fills at least half the chip (the M = 6000, N = 1024
     // encoder GEMMs: 256 tiles): one block per CU, so 8 waves (two per SIMD, one's MFMAs cover
     // the other's LDS-DMA issue) and 3 stages: -10..-15 % vs 128x128 (profiles/r03_gemm_table_192w8.txt)
-    if (t192 > 128 && t192 <= 256) return 15;
+    if (t192 > 128 && t192 <= 256) return AVSR_AB_ROUND1;
   }
   // grids of fewer 128x128 tiles than CUs (the teacher-forced decoder: M = 16 x 41 rows, N = 1024:
   // 48 tiles) leave most of the chip idle: 64x64 tiles (4x the workgroups, several per CU)

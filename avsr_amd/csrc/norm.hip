@@ -159,7 +159,7 @@ __global__ __launch_bounds__(64 * W) void ln_bwd_kernel(LnArgs a) {
   }
   if (!a.dgamma) return;
   // per-block column partials (the block's waves summed in LDS) -> ws[block][2 or 3][N]
-  extern __shared__ float red[];                 // [W][N]
+  extern __shared__ __attribute__((aligned(16))) float red[];   // [W][N]
   const int w = threadIdx.x >> 6;
   const int nq = a.db ? 3 : 2;
   for (int q = 0; q < nq; ++q) {
@@ -167,9 +167,16 @@ __global__ __launch_bounds__(64 * W) void ln_bwd_kernel(LnArgs a) {
 #pragma unroll
     for (int i = 0; i < VPL; ++i) {
       const int c = (lane + i * 64) * VE;
-      if (c < a.N)
+      if (c < a.N) {
+        // 16-byte stores of the lane's VE consecutive columns (scalar stores at a VE-float lane
+        // stride were 4-8-way bank conflicts: 78 % of the kernel's LDS cycles, profiles/r05_sq_counters.txt)
+        float* dst = red + w * a.N + c;
 #pragma unroll
-        for (int j = 0; j < VE; ++j) red[w * a.N + c + j] = q == 0 ? dg[i][j] : (q == 1 ? db[i][j] : gb[i][j]);
+        for (int j = 0; j < VE; j += 4)
+          *(f32x4*)(dst + j) = q == 0 ? f32x4{dg[i][j], dg[i][j + 1], dg[i][j + 2], dg[i][j + 3]}
+                             : q == 1 ? f32x4{db[i][j], db[i][j + 1], db[i][j + 2], db[i][j + 3]}
+                                      : f32x4{gb[i][j], gb[i][j + 1], gb[i][j + 2], gb[i][j + 3]};
+      }
     }
     __syncthreads();
     for (int c = threadIdx.x; c < a.N; c += 64 * W) {
