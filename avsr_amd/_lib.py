@@ -116,6 +116,7 @@ class AttnParams(ctypes.Structure):
         ("drop_p", _f), ("seed", ctypes.c_uint64),
         ("dout", _c_p), ("lddo", _i64), ("delta", _c_p), ("dq", _c_p), ("lddq", _i64),
         ("dk", _c_p), ("lddk", _i64), ("dv", _c_p), ("lddv", _i64), ("dq_out", _c_p), ("lddq_out", _i64),
+        ("db", _c_p), ("db_ws", _c_p),
     ]
 
 

@@ -117,6 +117,7 @@ struct AttnArgs {
   void* o; int64_t ldo; float* lse; const int* klen; int causal; float drop_p; uint64_t seed;
   const void* dout; int64_t lddo; float* delta; float* dq; int64_t lddq;
   void* dk; int64_t lddk; void* dv; int64_t lddv;
+  float* db_ws;                 // per-utterance q/k/v bias-gradient partials [B][3][H][64] or null
 };
 
 template <typename T> struct L {
@@ -147,6 +148,15 @@ AVSR_DEV void store_t(const f32x16& x0, const f32x16& x1, float mul, float* st, 
       stv(out + (int64_t)i * ld + cb + e, v);
     }
   }
+}
+
+// column sums of the wave's 32 x 64 slab (rows < nvalid) as store_t stored them (rounded to
+// T); lane l returns column l. Read after store_t by the same wave (LDS order), no barrier
+template <typename T> AVSR_DEV float slab_colsum(const float* st, int nvalid) {
+  const int l = threadIdx.x & 63, n = nvalid < 32 ? nvalid : 32;
+  float s = 0.f;
+  for (int i = 0; i < n; ++i) s += (float)from_f<T>(st[i * 65 + l]);
+  return s;
 }
 
 template <typename T>
@@ -1095,12 +1105,29 @@ __global__ __launch_bounds__(NT) void attn_bwd_dkdv_kernel(AttnArgs a) {
     }
   }
   __syncthreads();
+  // fused k / v bias gradients: each wave's column sums of what it stores, then wave 0 adds the
+  // waves' partials in wave order (the launch has one workgroup per (b, h) and every wave holds
+  // keys < Lk, so every wave reaches every barrier)
+  float* part = (float*)sm + (nthr >> 6) * 32 * 65;
   if (kb0 < a.Lk) {
     float* scr = (float*)sm + w * 32 * 65;
     bf16* DK = (bf16*)a.dk + ((int64_t)b * a.Lk + kb0) * a.lddk + h * DH;
     store_t<bf16>(dk0, dk1, a.scale, scr, DK, a.lddk, a.Lk - kb0);
+    if (a.db_ws) part[w * 128 + l] = slab_colsum<bf16>(scr, a.Lk - kb0);
     bf16* DV = (bf16*)a.dv + ((int64_t)b * a.Lk + kb0) * a.lddv + h * DH;
     store_t<bf16>(dv0, dv1, dscale, scr, DV, a.lddv, a.Lk - kb0);
+    if (a.db_ws) part[w * 128 + 64 + l] = slab_colsum<bf16>(scr, a.Lk - kb0);
+  }
+  if (a.db_ws) {
+    __syncthreads();
+    if (w == 0) {
+      const int nw = min(nthr >> 6, (a.Lk + 31) >> 5);
+      float sk = 0.f, sv = 0.f;
+      for (int i = 0; i < nw; ++i) { sk += part[i * 128 + l]; sv += part[i * 128 + 64 + l]; }
+      float* o = a.db_ws + (int64_t)b * 3 * a.H * DH + h * DH + l;
+      o[a.H * DH] = sk;
+      o[2 * a.H * DH] = sv;
+    }
   }
 }
 
@@ -1177,9 +1204,20 @@ __global__ __launch_bounds__(768) void attn_bwd_dq_kernel(AttnArgs a, OutT* dq, 
     }
   }
   __syncthreads();
+  float* part = (float*)sm + (nthr >> 6) * 32 * 65;
   if (q0 < a.Lq) {
     OutT* DQ = dq + ((int64_t)b * a.Lq + q0) * lddq + h * DH;
     store_t<OutT>(dq0, dq1, a.scale, (float*)sm + w * 32 * 65, DQ, lddq, a.Lq - q0);
+    if (a.db_ws) part[w * 64 + l] = slab_colsum<OutT>((float*)sm + w * 32 * 65, a.Lq - q0);
+  }
+  if (a.db_ws) {                  // fused q bias gradient (as in the dK/dV kernel)
+    __syncthreads();
+    if (w == 0) {
+      const int nw = min(nthr >> 6, (a.Lq + 31) >> 5);
+      float sq = 0.f;
+      for (int i = 0; i < nw; ++i) sq += part[i * 64 + l];
+      a.db_ws[(int64_t)b * 3 * a.H * DH + h * DH + l] = sq;
+    }
   }
 }
 
@@ -1640,6 +1678,7 @@ AttnArgs args(const avsr_attn_params* p) {
   a.o = p->o; a.ldo = p->ldo; a.lse = p->lse; a.klen = p->klen; a.causal = p->causal;
   a.drop_p = p->drop_p; a.seed = p->seed; a.dout = p->dout; a.lddo = p->lddo; a.delta = p->delta;
   a.dq = p->dq; a.lddq = p->lddq; a.dk = p->dk; a.lddk = p->lddk; a.dv = p->dv; a.lddv = p->lddv;
+  a.db_ws = nullptr;            // set per kernel path by avsr_attn_bwd
   return a;
 }
 
@@ -1720,12 +1759,9 @@ extern "C" int avsr_attn_bwd_prep(const avsr_attn_params* p, void* stream) {
   return 0;
 }
 
-extern "C" int avsr_attn_bwd(const avsr_attn_params* p, void* stream) {
-  int rc = check(p);
-  if (rc) return rc;
-  if (p->B * p->H == 0 || p->Lk == 0) return 0;
+// the backward kernels of one call; fused = the q/k/v bias partials were written by them
+static int attn_bwd_kernels(const avsr_attn_params* p, hipStream_t st, bool& fused) {
   AttnArgs a = args(p);
-  hipStream_t st = (hipStream_t)stream;
   dim3 grid((p->Lk + 127) / 128, p->B * p->H);
   if (p->dtype == AVSR_BF16) {
     if (p->dq_out && (p->lddq_out % 8 || !avsr_aligned16(p->dq_out))) return AVSR_E_ALIGN;
@@ -1748,14 +1784,17 @@ extern "C" int avsr_attn_bwd(const avsr_attn_params* p, void* stream) {
     if (resident_bwd(p)) {
       // dK/dV: 12 waves (3 per SIMD; a few registers spill to scratch, measured 5 % faster than
       // 8 spill-free waves at 2 per SIMD)
+      // (one workgroup per (b, h): grid.y = 1 for L <= 384) with the fused bias-gradient partials
       const int nwk = std::min(res::nwaves(p->Lk), 12), nwq = res::nwaves(p->Lq);
+      a.db_ws = p->db ? p->db_ws : nullptr;
+      fused = p->db != nullptr;
       const size_t ldk = std::max(res::img_lds(p->Lq) + (size_t)2 * ((p->Lq + 31) & ~31) * sizeof(float),
-                                  res::slab_lds(nwk));
+                                  res::slab_lds(nwk) + (size_t)nwk * 128 * sizeof(float));
       const dim3 gk(p->B * p->H, (p->Lk + 32 * nwk - 1) / (32 * nwk));
       res::allow_lds(res::attn_bwd_dkdv_kernel<768>);
       hipLaunchKernelGGL(res::attn_bwd_dkdv_kernel<768>, gk, dim3(64 * nwk), ldk, st, a);
       AVSR_CHECK_LAUNCH();
-      const size_t ldq = std::max(res::img_lds(p->Lk), res::slab_lds(nwq));
+      const size_t ldq = std::max(res::img_lds(p->Lk), res::slab_lds(nwq) + (size_t)nwq * 64 * sizeof(float));
       dim3 gq(p->B * p->H, (p->Lq + 32 * nwq - 1) / (32 * nwq));
       if (p->dq_out) {
         res::allow_lds(res::attn_bwd_dq_kernel<bf16>);
@@ -1777,4 +1816,49 @@ extern "C" int avsr_attn_bwd(const avsr_attn_params* p, void* stream) {
   }
   AVSR_CHECK_LAUNCH();
   return 0;
+}
+
+// column sums per utterance of the stored dQ / dK / dV (the paths whose kernels do not write the
+// bias partials themselves): ws[b][s][c], thread = one of the 3 * HD columns, rows in order
+template <typename TQ, typename T>
+__global__ __launch_bounds__(256) void attn_db_kernel(const TQ* dq, int64_t lddq, const T* dk, int64_t lddk, const T* dv,
+                                                      int64_t lddv, int Lq, int Lk, int HD, float* ws) {
+  const int b = blockIdx.y, col = blockIdx.x * 256 + threadIdx.x;
+  if (col >= 3 * HD) return;
+  const int s = col / HD, c = col % HD;
+  float acc = 0.f;
+  if (s == 0) {
+    for (int i = 0; i < Lq; ++i) acc += (float)dq[((int64_t)b * Lq + i) * lddq + c];
+  } else {
+    const T* x = s == 1 ? dk : dv;
+    const int64_t ld = s == 1 ? lddk : lddv;
+    for (int i = 0; i < Lk; ++i) acc += (float)x[((int64_t)b * Lk + i) * ld + c];
+  }
+  ws[(int64_t)b * 3 * HD + col] = acc;
+}
+
+extern "C" int avsr_attn_bwd(const avsr_attn_params* p, void* stream) {
+  int rc = check(p);
+  if (rc) return rc;
+  if (p->db && !p->db_ws) return AVSR_E_ARG;
+  if (p->B * p->H == 0 || p->Lk == 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  bool fused = false;
+  rc = attn_bwd_kernels(p, st, fused);
+  if (rc || !p->db) return rc;
+  const int HD = p->H * DH;
+  if (!fused) {
+    const dim3 g((3 * HD + 255) / 256, p->B);
+    if (p->dtype == AVSR_BF16 && p->dq_out)
+      hipLaunchKernelGGL((attn_db_kernel<bf16, bf16>), g, dim3(256), 0, st, (const bf16*)p->dq_out, p->lddq_out,
+                         (const bf16*)p->dk, p->lddk, (const bf16*)p->dv, p->lddv, p->Lq, p->Lk, HD, p->db_ws);
+    else if (p->dtype == AVSR_BF16)
+      hipLaunchKernelGGL((attn_db_kernel<float, bf16>), g, dim3(256), 0, st, (const float*)p->dq, p->lddq,
+                         (const bf16*)p->dk, p->lddk, (const bf16*)p->dv, p->lddv, p->Lq, p->Lk, HD, p->db_ws);
+    else
+      hipLaunchKernelGGL((attn_db_kernel<float, float>), g, dim3(256), 0, st, (const float*)p->dq, p->lddq,
+                         (const float*)p->dk, p->lddk, (const float*)p->dv, p->lddv, p->Lq, p->Lk, HD, p->db_ws);
+    AVSR_CHECK_LAUNCH();
+  }
+  return colsum_launch(p->db_ws, p->B, (int64_t)3 * HD, 3 * HD, p->db, 0, nullptr, st);
 }

@@ -42,6 +42,11 @@ _DB_FUSE = True
 _COLSUM_DEFER = True
 # bias gradients of operands only the side stream's weight-grads read run on the side stream
 _SIDE_BIAS = True
+# encoder q/k/v bias gradients written by the attention backward (avsr_attn_params.db) instead of
+# a column-sum pass over dqkv on the side stream: off — the fused form adds ~1 us per layer to the
+# data-gradient chain and removes ~27 us of side-stream work, and the step got 1 % slower
+# (131.2 vs 132.8 k AV-frames/s, 3 interleaved pairs, profiles/r05_attn_db_ab.txt)
+_ATTN_DB = False
 # the CTC branch of the forward runs on the side stream beside the decoder forward
 _CTC_SIDE = True
 # bf16 stem conv straight from the video (stem.hip) instead of pack + general implicit GEMM
@@ -836,14 +841,19 @@ class Engine:
         dqkv = self._e(M, 3 * D)
         dq32 = self._dq32(M, D)
         delta = self._e(B, H, T, dtype=torch.float32)
-        ops.attn_bwd(do, qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:], lc["o"], lc["lse"], dq32, dqkv[:, D:2 * D],
-                     dqkv[:, 2 * D:], delta, B=B, H=H, Lq=T, Lk=T, klen=klen, scale=0.125, drop_p=lc["p_att"],
-                     seed=lc["sd_att"], dq=None if dq32 is not None else dqkv[:, :D])
-        if dq32 is not None:
-            ops.cast(dq32, dqkv[:, :D])
         names_b = [a + "q_proj.bias", a + "k_proj.bias", a + "v_proj.bias"]
         names_w = [a + "q_proj.weight", a + "k_proj.weight", a + "v_proj.weight"]
-        self._bias_grad_side(dqkv, self.arena.span(names_b, buf="g"))
+        db_qkv = self.arena.span(names_b, buf="g")
+        # the q/k/v bias gradients (column sums of dqkv) come out of the attention backward's
+        # store epilogues (bf16) instead of a pass over dqkv
+        ops.attn_bwd(do, qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:], lc["o"], lc["lse"], dq32, dqkv[:, D:2 * D],
+                     dqkv[:, 2 * D:], delta, B=B, H=H, Lq=T, Lk=T, klen=klen, scale=0.125, drop_p=lc["p_att"],
+                     seed=lc["sd_att"], dq=None if dq32 is not None else dqkv[:, :D],
+                     db=db_qkv if _ATTN_DB else None)
+        if dq32 is not None:
+            ops.cast(dq32, dqkv[:, :D])
+        if not _ATTN_DB:
+            self._bias_grad_side(dqkv, db_qkv)
         self._wgrad(dqkv, lc["ln1"], self.arena.span(names_w, buf="g"))
         dln1 = ops.linear_dgrad(dqkv, self.arena.span(names_w))
         ew = self._ew_next(i - 1, lc_prev, M) if lc_prev is not None else None

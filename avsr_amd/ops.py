@@ -551,9 +551,11 @@ def attn_fwd(q, k, v, o, lse, *, B, H, Lq, Lk, klen=None, causal=False, scale=0.
 
 
 def attn_bwd(dout, q, k, v, o, lse, dq32, dk, dv, delta, *, B, H, Lq, Lk, klen=None, causal=False,
-             scale=0.125, drop_p=0.0, seed=0, dq=None):
+             scale=0.125, drop_p=0.0, seed=0, dq=None, db=None):
     """dq32: fp32 accumulator (zeroed by the caller), or None with dq (bf16 only): dQ written
-    straight into dq in the activation dtype. dk/dv in the activation dtype."""
+    straight into dq in the activation dtype. dk/dv in the activation dtype. db (fp32, 3*H*64):
+    += the column sums of the stored dQ | dK | dV (the fused q/k/v bias gradients), finalised
+    through the column-sum path (deferred within a training step's backward)."""
     p = _attn_params(q, k, v, o, B, H, Lq, Lk, lse, klen, causal, scale, drop_p, seed)
     p.dout, p.lddo = dout.data_ptr(), dout.stride(0)
     p.delta = delta.data_ptr()
@@ -564,6 +566,11 @@ def attn_bwd(dout, q, k, v, o, lse, dq32, dk, dv, delta, *, B, H, Lq, Lk, klen=N
         p.dq, p.lddq = dq32.data_ptr(), dq32.stride(0)
     p.dk, p.lddk = dk.data_ptr(), dk.stride(0)
     p.dv, p.lddv = dv.data_ptr(), dv.stride(0)
+    ws = None
+    if db is not None:
+        assert db.dtype == torch.float32 and db.is_contiguous() and db.numel() == 3 * H * 64
+        ws = _colsum_ws(B * 3 * H * 64, dk.device)                  # AVSR_ATTN_DB_WS(B, H)
+        p.db, p.db_ws = db.data_ptr(), ws.data_ptr()
     _call("avsr_attn_bwd_prep", p)
     _call("avsr_attn_bwd", p)
 

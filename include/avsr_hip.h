@@ -388,7 +388,15 @@ typedef struct {
   /* bf16 only: if non-NULL, dQ is written here in the activation dtype (dq unused);
    * otherwise bf16 writes dq (fp32) with plain stores (= accumulate onto a zeroed buffer) */
   void* dq_out; int64_t lddq_out;
+  /* optional (backward): db[s*H*64 + h*64 + d] += column sums over all B*L rows of the dQ
+   * (s = 0), dK (s = 1), dV (s = 2) values as stored (bf16-rounded in bf16) — the fused q/k/v
+   * projection bias gradients. db_ws: AVSR_ATTN_DB_WS(B, H) floats of per-utterance partials,
+   * finalised through the column-sum path (deferred like avsr_gemm db: keep it alive until the
+   * flush). The resident bf16 kernels sum them in their store epilogues; other paths run one
+   * extra pass over dq/dk/dv. NULL: off. */
+  float* db; float* db_ws;
 } avsr_attn_params;
+#define AVSR_ATTN_DB_WS(B, H) ((int64_t)(B) * 3 * (H) * 64)
 /* diagnostic (not product path): per-workgroup s_memrealtime stamps of the resident attention
  * forward into buf[6 * workgroups] (start, first K/V round, compute done, end, HW_ID, XCC_ID);
  * buf = NULL turns them off */

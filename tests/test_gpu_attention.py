@@ -364,3 +364,40 @@ def test_attention_dropout_mask_bitexact(dev, lib_opt, case):
     for label, masks in runs.items():
         for kind, m in zip(("fwd", "dV", "dQ", "dK"), masks):
             assert torch.equal(m, ref), (label, kind, (m ^ ref).sum().item())
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("case", CASES)
+def test_attention_bias_grad(dev, dtype, case):
+    """avsr_attn_params.db: += the column sums of the dQ | dK | dV the backward stores (the fused
+    q/k/v bias gradients; the resident bf16 kernels sum them in their store epilogues, the other
+    paths in a pass over the outputs) — against fp64 sums of the stored tensors, dropout on"""
+    B, H, Lq, Lk, klen, causal = case
+    D = H * 64
+    g = torch.Generator().manual_seed(B * 7 + Lk)
+    q = torch.randn(B * Lq, D, generator=g).to(dev, dtype)
+    kv = torch.randn(B * Lk, 2 * D, generator=g).to(dev, dtype)
+    k, v = kv[:, :D], kv[:, D:]
+    o = torch.empty(B * Lq, D, device=dev, dtype=dtype)
+    lse = torch.empty(B, H, Lq, device=dev)
+    kl = None if klen is None else torch.tensor(klen, dtype=torch.int32, device=dev)
+    kw = dict(B=B, H=H, Lq=Lq, Lk=Lk, klen=kl, causal=causal, scale=0.125, drop_p=0.1, seed=99)
+    ops.attn_fwd(q, k, v, o, lse, **kw)
+    dout = torch.randn(B * Lq, D, generator=g).to(dev, dtype)
+    dk = torch.empty(B * Lk, D, device=dev, dtype=dtype)
+    dv = torch.empty(B * Lk, D, device=dev, dtype=dtype)
+    delta = torch.empty(B, H, Lq, device=dev)
+    modes = ["f32"] + (["bf16"] if dtype == torch.bfloat16 else [])
+    for mode in modes:
+        db0 = torch.randn(3 * D, generator=g).to(dev)
+        db = db0.clone()
+        if mode == "bf16":
+            dq = torch.empty(B * Lq, D, device=dev, dtype=dtype)
+            ops.attn_bwd(dout, q, k, v, o, lse, None, dk, dv, delta, dq=dq, db=db, **kw)
+        else:
+            dq = torch.zeros(B * Lq, D, device=dev)
+            ops.attn_bwd(dout, q, k, v, o, lse, dq, dk, dv, delta, db=db, **kw)
+        want = torch.cat([t.double().sum(0) for t in (dq, dk, dv)]).cpu()
+        mag = torch.cat([t.double().abs().sum(0) for t in (dq, dk, dv)]).cpu()
+        got = (db.double() - db0.double()).cpu()
+        assert ((got - want).abs() <= 2e-6 * mag + 1e-5).all(), (mode, (got - want).abs().max().item())

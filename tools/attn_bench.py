@@ -35,3 +35,12 @@ for p in (0.0, 0.1):
                                 drop_p=p, seed=3, dq=dq))
     print(f"drop {p}: fwd {f * 1e3:.1f} us ({fl / f / 1e9:.0f} TF/s)  bwd(prep+dkdv+dq) {g * 1e3:.1f} us "
           f"({2.5 * fl / g / 1e9:.0f} TF/s)", flush=True)
+db = torch.zeros(3 * H * D, device=dev)
+for p in (0.0, 0.1):
+    g0 = tm(lambda: ops.attn_bwd(do, q, k, v, o, lse, None, dk, dv, delta, B=B, H=H, Lq=L, Lk=L, klen=klen,
+                                 drop_p=p, seed=3, dq=dq))
+    g1 = tm(lambda: ops.attn_bwd(do, q, k, v, o, lse, None, dk, dv, delta, B=B, H=H, Lq=L, Lk=L, klen=klen,
+                                 drop_p=p, seed=3, dq=dq, db=db))
+    g2 = tm(lambda: ops.ew_bwd(qkv, db=db))
+    print(f"drop {p}: bwd {g0 * 1e3:.1f} us, with fused q/k/v bias grads {g1 * 1e3:.1f} us; "
+          f"separate column-sum pass over dqkv {g2 * 1e3:.1f} us", flush=True)
