@@ -277,7 +277,7 @@ SYMBOLS = {
     "avsr_lsm_bwd": ([ctypes.POINTER(XentParams), _c_p], _i),
     "avsr_ctc_fwd": ([ctypes.POINTER(CtcParams), _c_p], _i),
     "avsr_ctc_bwd": ([ctypes.POINTER(CtcParams), _c_p], _i),
-    "avsr_loss_finalize": ([_i, _c_p, _i, _c_p, _c_p, _f, _c_p, _c_p], _i),
+    "avsr_loss_finalize": ([_i, _c_p, _i, _c_p, _c_p, _f, _i, _c_p, _c_p], _i),
     "avsr_ew_bwd": ([ctypes.POINTER(EwParams), _c_p], _i),
     "avsr_colsum_defer": ([_i], _i),
     "avsr_colsum_flush": ([_c_p], _i),

@@ -110,6 +110,11 @@ class Arena:
             mod._parameters[attr] = newp
             self.params[n] = newp
         self.grad_views = {n: self._logical(self.grad, self.meta[n]) for n in self.order if n not in frozen}
+        # LayerDrop (engine): per encoder layer its arena ranges, and the layers a backward has
+        # touched since the last gradient clear (the others have no gradient: the optimizer skips
+        # them as torch.optim.AdamW skips parameters whose grad is None)
+        self.ld_ranges = None
+        self.ld_touched = set()
         self.attach_grads(zero=False)
         self.sync_shadow()
 
@@ -219,6 +224,17 @@ class Arena:
     def zero_grad(self):
         self.grad.zero_()
         self.attach_grads(zero=False)
+        self.ld_touched.clear()
+
+    def ranges_of(self, prefix):
+        """merged [start, end) arena ranges of the parameters whose names start with prefix"""
+        out = []
+        for s, e in sorted((m["off"], m["off"] + m["numel"]) for n, m in self.meta.items() if n.startswith(prefix)):
+            if out and s <= out[-1][1]:
+                out[-1] = (out[-1][0], max(out[-1][1], e))
+            else:
+                out.append((s, e))
+        return out
 
     def init_optimizer(self):
         if self.exp_avg is None:

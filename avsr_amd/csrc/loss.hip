@@ -296,7 +296,7 @@ __global__ __launch_bounds__(256) void ctc_bwd_kernel(avsr_ctc_params p) {
 }
 
 __global__ void loss_finalize_kernel(int B, const float* nll, int rows, const float* row_loss,
-                                     const int* row_correct, float mtl, float* out) {
+                                     const int* row_correct, float mtl, int per_token, float* out) {
   __shared__ float sh[4];
   float a = 0.f, c = 0.f, n = 0.f, v = 0.f;
   for (int i = threadIdx.x; i < B; i += 256) a += nll[i];
@@ -306,7 +306,7 @@ __global__ void loss_finalize_kernel(int B, const float* nll, int rows, const fl
   }
   a = block_sum(a, sh); c = block_sum(c, sh); n = block_sum(n, sh); v = block_sum(v, sh);
   if (threadIdx.x == 0) {
-    const float lc = a / (float)B, la = c / (float)B;
+    const float lc = a / (float)B, la = c / (per_token ? fmaxf(v, 1.f) : (float)B);
     out[0] = mtl * lc + (1.f - mtl) * la;
     out[1] = lc; out[2] = la; out[3] = v > 0.f ? n / v : 0.f;
   }
@@ -361,9 +361,10 @@ extern "C" int avsr_ctc_bwd(const avsr_ctc_params* p, void* stream) {
 }
 
 extern "C" int avsr_loss_finalize(int B, const float* nll, int rows, const float* row_loss, const int* row_correct,
-                                  float mtlalpha, float* out, void* stream) {
+                                  float mtlalpha, int att_per_token, float* out, void* stream) {
+  if (att_per_token && !row_correct) return AVSR_E_ARG;
   hipLaunchKernelGGL(loss_finalize_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, B, nll, rows, row_loss,
-                     row_correct, mtlalpha, out);
+                     row_correct, mtlalpha, att_per_token, out);
   AVSR_CHECK_LAUNCH();
   return 0;
 }

@@ -146,12 +146,13 @@ class Engine:
         assert self.D // self.H == 64 and self.dD // self.dH == 64, "kernels use head dim 64"
         assert cfg.adim == self.D == self.dD, "proj_decoder (adim != ddim) not on the hot path"
         # configuration the reference reads but the engine does not implement: refuse loudly
-        if getattr(cfg, "layerdrop", 0.0):
-            raise NotImplementedError("layerdrop > 0 (avhubert.py:710-712) is not implemented by the engine")
-        if getattr(cfg, "transformer_length_normalized_loss", False):
-            raise NotImplementedError("transformer_length_normalized_loss=True is not implemented by the engine")
-        if getattr(cfg, "modality_fuse", "concat") != "concat":
-            raise NotImplementedError("modality_fuse='add' is not implemented by the engine")
+        # LayerDrop (avhubert.py:709-712): training skips encoder layer i when its draw is below it
+        self.layerdrop = float(getattr(cfg, "layerdrop", 0.0) or 0.0)
+        # LabelSmoothingLoss(normalize_length) (label_smoothing_loss.py:61): / tokens instead of / B
+        self.len_norm = bool(getattr(cfg, "transformer_length_normalized_loss", False))
+        if getattr(cfg, "modality_fuse", "concat") not in ("concat", "add"):
+            raise ValueError(f"unknown modality_fuse {cfg.modality_fuse!r}")
+        self.fuse_add = getattr(cfg, "modality_fuse", "concat") == "add"
         if getattr(cfg, "modality", "av") not in ("av", "audio", "video"):
             raise ValueError(f"unknown modality {cfg.modality!r}")
         self.last_modality = None
@@ -227,6 +228,8 @@ class Engine:
             pre = f"encoder.encoder.layers.{i}."
             offs = [m["off"] for n, m in self.arena.meta.items() if n.startswith(pre) and d0 <= m["off"] < d1]
             self._layer_decay_off.append(min(offs) if offs else d1)
+        if self.layerdrop > 0:      # the optimizer skips the layers no backward touched (grad None)
+            self.arena.ld_ranges = [self.arena.ranges_of(f"encoder.encoder.layers.{i}.") for i in range(self.nl)]
         self.shell = shell
         self.step_count = 0
         self._pe = positional_encoding(max(512, 64), self.dD, self.device)
@@ -347,6 +350,7 @@ class Engine:
         g = self.arena.grad
         self._on_side(lambda: g.zero_(), g)
         self.arena.attach_grads(zero=False)
+        self.arena.ld_touched.clear()
 
     def join_side(self):
         """make the current stream wait for every weight gradient issued so far"""
@@ -712,29 +716,40 @@ class Engine:
         M, D = B * T, self.D
         EN = "encoder."
         ctx = {"B": B, "T": T, "modality": modality}
-        # audio / video frontends -> concat buffer [M][2D] (audio | video)
-        fcat = self._e(M, 2 * D)
+        # audio / video frontends -> concat buffer [M][2D] (audio | video), or with
+        # modality_fuse 'add' the sum [M][D] (avhubert.py:486-489: the video projection adds the
+        # audio features as its residual)
+        add = self.fuse_add
+        fcat = self._e(M, D if add else 2 * D)
+        fa = self._e(M, D) if add else fcat[:, :D]
         ain = self._e(M, cfg.audio_feat_dim)
         ops.audio_pack(audios.contiguous(), ain)
         if modality == "audio_off":
-            fcat[:, :D].zero_()
+            fa.zero_()
         else:
             ops.linear_fwd(ain, self.w(EN + "feature_extractor_audio.proj.weight"),
-                           self.arena.master(EN + "feature_extractor_audio.proj.bias"), out=fcat[:, :D])
+                           self.arena.master(EN + "feature_extractor_audio.proj.bias"), out=fa)
         # video_off: the ResNet gradient is exactly zero (avhubert.py:480), so nothing of its
         # forward is kept for a backward (no packed stem input, no pooled-grid argmax values);
         # the forward itself still runs for the BatchNorm running statistics, as in the reference
         feat, vctx = self.video_fwd(videos, train, save and modality != "video_off")
         if modality == "video_off":
-            fcat[:, D:].zero_()
+            if add:
+                fcat.copy_(fa)
+            else:
+                fcat[:, D:].zero_()
         else:
             ops.linear_fwd(feat, self.w(EN + "feature_extractor_video.proj.weight"),
-                           self.arena.master(EN + "feature_extractor_video.proj.bias"), out=fcat[:, D:])
+                           self.arena.master(EN + "feature_extractor_video.proj.bias"),
+                           res=fa if add and modality != "audio_off" else None, out=fcat if add else fcat[:, D:])
         ln0, m0, r0 = self._ln(fcat, EN + "layer_norm", 1e-5)
         sd_in = seeds.next()
         p_in = cfg.dropout_input if train else 0.0
-        x = ops.linear_fwd(ln0, self.w(EN + "post_extract_proj.weight"), self.arena.master(EN + "post_extract_proj.bias"),
-                           drop_p=p_in, seed=sd_in)
+        if add:        # embed dim = encoder dim: no post_extract_proj (avhubert.py:229-233)
+            x = ops.dropout_fwd(ln0, self._e(M, D), p_in, sd_in) if p_in > 0 else ln0.clone()
+        else:
+            x = ops.linear_fwd(ln0, self.w(EN + "post_extract_proj.weight"),
+                               self.arena.master(EN + "post_extract_proj.bias"), drop_p=p_in, seed=sd_in)
         if not bt["full"]:
             ops.mask_rows(x, B, T, bt["lens"])
         klen = None if bt["full"] else bt["lens"]
@@ -759,7 +774,15 @@ class Engine:
                        norm=norm, pre=pre, sd_pc=sd_pc, p_h=p_h, vctx=vctx, feat=feat, klen=klen)
         x = y
         layers = []
+        # LayerDrop: one torch.rand([]) (CPU generator) per layer on every call, train or eval, as
+        # the reference draws them (avhubert.py:709-712); training skips a layer whose draw is below
+        # cfg.layerdrop (its context is None, the backward passes the gradient through)
+        draws = [float(torch.rand([])) for _ in range(self.nl)]
         for i in range(self.nl):
+            if train and draws[i] < self.layerdrop:
+                if save:
+                    layers.append(None)
+                continue
             x, lc = self._enc_layer_fwd(i, x, B, T, klen, train, save, seeds)
             if save:
                 layers.append(lc)
@@ -801,7 +824,7 @@ class Engine:
                             drop_p=p_h, seed=sd_f)
         lc = None
         if save:
-            lc = dict(x=x, ln1=ln1, m1=m1, r1=r1, qkv=qkv, o=o, lse=lse, sd_att=sd_att, p_att=p_att, sd_o=sd_o, p_h=p_h,
+            lc = dict(i=i, x=x, ln1=ln1, m1=m1, r1=r1, qkv=qkv, o=o, lse=lse, sd_att=sd_att, p_att=p_att, sd_o=sd_o, p_h=p_h,
                       x1=x1, ln2=ln2, m2=m2, r2=r2, h=h, act=act, sd_a=sd_a, p_a=p_a, sd_f=sd_f)
         return x2, lc
 
@@ -856,7 +879,7 @@ class Engine:
             self._bias_grad_side(dqkv, db_qkv)
         self._wgrad(dqkv, lc["ln1"], self.arena.span(names_w, buf="g"))
         dln1 = ops.linear_dgrad(dqkv, self.arena.span(names_w))
-        ew = self._ew_next(i - 1, lc_prev, M) if lc_prev is not None else None
+        ew = self._ew_next(lc_prev["i"], lc_prev, M) if lc_prev is not None else None
         dx = self._ln_bwd(dln1, lc["x"], p + "layer_norm", lc["m1"], lc["r1"], dres=dx1, dx=dx1, ew=ew)
         return dx, (ew[0] if ew is not None else None)
 
@@ -867,15 +890,19 @@ class Engine:
         EN = "encoder."
         E = "encoder.encoder."
         layers = ctx["layers"]
-        ew = self._ew_next(self.nl - 1, layers[-1], M) if self.nl else None
+        ex = [i for i in range(self.nl) if layers[i] is not None]       # layers LayerDrop kept
+        self.arena.ld_touched.update(ex)
+        ew = self._ew_next(ex[-1], layers[ex[-1]], M) if ex else None
         dx = self._ln_bwd(dout, ctx["x_last"], E + "layer_norm", ctx["mf"], ctx["rf"], ew=ew)
         g2 = ew[0] if ew is not None else None
         for i in reversed(range(self.nl)):
-            self._side_layer(True)
-            dx, g2 = self._enc_layer_bwd(i, layers[i], dx, B, T, ctx["klen"], g2=g2,
-                                         lc_prev=layers[i - 1] if i > 0 else None)
-            self._side_layer(False)
-            ops.colsum_flush()                      # this layer's bias / LayerNorm gradients
+            if layers[i] is not None:
+                j = ex.index(i)
+                self._side_layer(True)
+                dx, g2 = self._enc_layer_bwd(i, layers[i], dx, B, T, ctx["klen"], g2=g2,
+                                             lc_prev=layers[ex[j - 1]] if j > 0 else None)
+                self._side_layer(False)
+                ops.colsum_flush()                  # this layer's bias / LayerNorm gradients
             if self.on_grad_ready is not None:      # layers >= i (and everything after them) final
                 self.on_grad_ready(self._layer_decay_off[i])   # (the reducer also waits for the side stream)
         # pos-conv block: x0 = drop(x + gelu(conv(x) + b))
@@ -896,17 +923,23 @@ class Engine:
             ops.mask_rows(dx, B, T, ctx["klen"])
         # post_extract_proj (+ dropout_input)
         gi = gp
-        ops.ew_bwd(dx, out=gi, drop_p=ctx["p_in"], seed=ctx["sd_in"], db=self.g(EN + "post_extract_proj.bias"))
-        self._wgrad(gi, ctx["ln0"], self.g(EN + "post_extract_proj.weight"))
-        dln0 = ops.linear_dgrad(gi, self.w(EN + "post_extract_proj.weight"))
+        if self.fuse_add:
+            ops.ew_bwd(dx, out=gi, drop_p=ctx["p_in"], seed=ctx["sd_in"])
+            dln0 = gi
+        else:
+            ops.ew_bwd(dx, out=gi, drop_p=ctx["p_in"], seed=ctx["sd_in"], db=self.g(EN + "post_extract_proj.bias"))
+            self._wgrad(gi, ctx["ln0"], self.g(EN + "post_extract_proj.weight"))
+            dln0 = ops.linear_dgrad(gi, self.w(EN + "post_extract_proj.weight"))
         dfcat = self._ln_bwd(dln0, ctx["fcat"], EN + "layer_norm", ctx["m0"], ctx["r0"])
         fgm = cfg.feature_grad_mult            # GradMultiply (avhubert.py:173-182) on both frontends
+        # 'add': both streams receive the sum's gradient; 'concat': each its half
+        da_all, dv_all = (dfcat, dfcat) if self.fuse_add else (dfcat[:, :D], dfcat[:, D:])
         if ctx["modality"] != "audio_off":
-            da = dfcat[:, :D]
+            da = da_all
             self._bias_grad(da, self.g(EN + "feature_extractor_audio.proj.bias"), alpha=fgm)
             self._wgrad(da, ctx["ain"], self.g(EN + "feature_extractor_audio.proj.weight"), alpha=fgm)
         if ctx["modality"] != "video_off":
-            dv = dfcat[:, D:]
+            dv = dv_all
             self._bias_grad(dv, self.g(EN + "feature_extractor_video.proj.bias"), alpha=fgm)
             self._wgrad(dv, ctx["feat"], self.g(EN + "feature_extractor_video.proj.weight"), alpha=fgm)
             dfeat = self._e(M, 512)
@@ -1099,7 +1132,7 @@ class Engine:
         rcorr = self._e(R, dtype=torch.int32)
         ops.lsm_fwd(dlog, self.V, bt["ys_out"], cfg.lsm_weight, dlse, rloss, rcorr)
         out4 = self._e(4, dtype=torch.float32)
-        ops.loss_finalize(B, nll, rloss, rcorr, cfg.mtlalpha, out4)
+        ops.loss_finalize(B, nll, rloss, rcorr, cfg.mtlalpha, out4, att_per_token=self.len_norm)
         if self.capture is not None:
             self.capture.update(enc=enc, clog=clog, dlog=dlog, bt=bt)
         ctx = None
@@ -1159,7 +1192,11 @@ class Engine:
         # attention loss -> decoder
         dl = ctx["dlog"]
         ddl = self._e(dl.shape[0], self.Vp)
-        ops.lsm_bwd(dl, self.V, bt["ys_out"], cfg.lsm_weight, ctx["dlse"], d_att, 1.0 / B, ddl)
+        if self.len_norm:      # / the number of target tokens (device count, no host sync)
+            d_att = d_att / (bt["ys_out"] != -1).sum().clamp_min(1).to(torch.float32)
+            ops.lsm_bwd(dl, self.V, bt["ys_out"], cfg.lsm_weight, ctx["dlse"], d_att, 1.0, ddl)
+        else:
+            ops.lsm_bwd(dl, self.V, bt["ys_out"], cfg.lsm_weight, ctx["dlse"], d_att, 1.0 / B, ddl)
         denc = self._e(M, self.D)
         # CTC -> denc (first write), then decoder adds
         dcl = self._e(M, self.Vp)

@@ -617,9 +617,12 @@ def ctc_bwd(p, dloss, coef, dx):
     return dx
 
 
-def loss_finalize(B, nll, row_loss, row_correct, mtlalpha, out):
+def loss_finalize(B, nll, row_loss, row_correct, mtlalpha, out, att_per_token=False):
+    """att_per_token: the attention loss divides by the number of target tokens
+    (transformer_length_normalized_loss) instead of B"""
     L.check(L.load().avsr_loss_finalize(B, nll.data_ptr(), row_loss.shape[0], row_loss.data_ptr(),
-                                        _p(row_correct), mtlalpha, out.data_ptr(), L.stream_ptr()),
+                                        _p(row_correct), mtlalpha, int(bool(att_per_token)), out.data_ptr(),
+                                        L.stream_ptr()),
             "avsr_loss_finalize")
     return out
 

@@ -31,6 +31,7 @@ class FusedAdamW:
         self.lr, self.betas, self.eps, self.wd, self.max_norm = lr, betas, eps, weight_decay, max_grad_norm
         self.schedule = schedule
         self.step_count = 0
+        self.layer_steps = None      # LayerDrop: per encoder layer, the steps that updated it
         self._sumsq = torch.zeros(1, device=arena.device)
         self._sumsq_ws = torch.empty(ops.SUMSQ_WS, device=arena.device)
 
@@ -56,26 +57,64 @@ class FusedAdamW:
         if self.max_norm and self.max_norm > 0 and not sumsq_ready:
             self.grad_sumsq()
 
-        def launch(s, e, wd):
+        def launch(s, e, wd, step):
             ops.adamw(a.data[s:e], a.grad[s:e], a.exp_avg[s:e], a.exp_avg_sq[s:e], lr=lr, beta1=self.betas[0],
-                      beta2=self.betas[1], eps=self.eps, weight_decay=wd, step=self.step_count,
+                      beta2=self.betas[1], eps=self.eps, weight_decay=wd, step=step,
                       shadow=None if a.shadow is None else a.shadow[s:e],
                       sumsq_buf=self._sumsq if self.max_norm else None, max_norm=self.max_norm or 1.0,
                       grad_scale=grad_scale)
 
+        if a.ld_ranges is not None:
+            if self.layer_steps is None:
+                self.layer_steps = [self.step_count - 1] * len(a.ld_ranges)
+            for i in a.ld_touched:
+                self.layer_steps[i] += 1
         for (s, e), wd in (((d0, d1), self.wd), ((n0, n1), 0.0)):
-            if e > s:
-                launch(s, e, wd)
+            for ps, pe, step in self._pieces(s, e):
+                if step is not None:
+                    launch(ps, pe, wd, step)
         if zero_grad:
             a.zero_grad()
         return lr
+
+    def _pieces(self, s, e):
+        """[s, e) as (start, end, step) launches: without LayerDrop one piece at the global step;
+        with it, each encoder layer's ranges at that layer's own step count, or step None (no
+        launch) for a layer no backward touched since the last gradient clear — torch.optim.AdamW
+        skips a parameter whose grad is None (no decay, no moment update, its own step count)"""
+        a = self.arena
+        if a.ld_ranges is None or e <= s:
+            return [(s, e, self.step_count)] if e > s else []
+        cuts = []
+        for i, rs in enumerate(a.ld_ranges):
+            st = self.layer_steps[i] if i in a.ld_touched else None
+            for r0, r1 in rs:
+                lo, hi = max(r0, s), min(r1, e)
+                if lo < hi:
+                    cuts.append((lo, hi, st))
+        out, pos = [], s
+        for lo, hi, st in sorted(cuts):
+            if pos < lo:
+                out.append((pos, lo, self.step_count))
+            out.append((lo, hi, st))
+            pos = hi
+        if pos < e:
+            out.append((pos, e, self.step_count))
+        merged = []
+        for p in out:
+            if merged and merged[-1][2] == p[2] and merged[-1][1] == p[0]:
+                merged[-1] = (merged[-1][0], p[1], p[2])
+            else:
+                merged.append(p)
+        return merged
 
     # ------------------------------------------------------------------ checkpoint / resume
     def state_dict(self):
         """optimizer state for resume (script/train.py:280-287,310-314): step count and the
         arena-layout moments (tensors only: loadable with torch.load(weights_only=True))."""
         a = self.arena
-        return {"step": self.step_count, "exp_avg": a.exp_avg.detach().clone(),
+        extra = {} if self.layer_steps is None else {"layer_steps": torch.tensor(self.layer_steps)}
+        return {"step": self.step_count, **extra, "exp_avg": a.exp_avg.detach().clone(),
                 "exp_avg_sq": a.exp_avg_sq.detach().clone(),
                 "hyper": {"lr": self.lr, "betas": list(self.betas), "eps": self.eps, "weight_decay": self.wd,
                           "max_grad_norm": self.max_norm}}
@@ -87,6 +126,8 @@ class FusedAdamW:
         a.exp_avg.copy_(sd["exp_avg"])
         a.exp_avg_sq.copy_(sd["exp_avg_sq"])
         self.step_count = int(sd["step"])
+        if "layer_steps" in sd:
+            self.layer_steps = [int(v) for v in sd["layer_steps"]]
 
 
 class ArenaAdamW(torch.optim.Optimizer):

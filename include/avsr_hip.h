@@ -418,7 +418,9 @@ int avsr_attn_bwd(const avsr_attn_params* p, void* stream);
  *   state occupancies gamma[b][t][s] = P(path at state s at t | x) (0 if infeasible)
  * avsr_ctc_bwd:   dx[b,t,k] = (*dloss * coef) * (softmax_t(k) - sum_{s: ext_s = k} gamma_t(s))
  *   for t < in_len[b] (0 otherwise and for infeasible utterances)
- * avsr_loss_finalize: loss_ctc = sum nll / B, loss_att = sum row_loss / B,
+ * avsr_loss_finalize: loss_ctc = sum nll / B, loss_att = sum row_loss / B (att_per_token = 0) or
+ *   / the number of target tokens, i.e. rows with row_correct >= 0 (att_per_token = 1:
+ *   transformer_length_normalized_loss, label_smoothing_loss.py:61; needs row_correct),
  *   loss = mtl*ctc + (1-mtl)*att, acc = correct / valid  (e2e_asr_avhubert.py:150-159)
  *   out[4] = {loss, loss_ctc, loss_att, acc}, all on device (no host sync)
  * ------------------------------------------------------------------------------------ */
@@ -450,7 +452,7 @@ int avsr_ctc_fwd(const avsr_ctc_params* p, void* stream);
 int avsr_ctc_bwd(const avsr_ctc_params* p, void* stream);
 
 int avsr_loss_finalize(int B, const float* nll, int rows, const float* row_loss, const int* row_correct,
-                       float mtlalpha, float* out, void* stream);
+                       float mtlalpha, int att_per_token, float* out, void* stream);
 
 /* ------------------------------------------------------------------------------------
  * Elementwise / data-movement kernels around the GEMMs.

@@ -109,3 +109,25 @@ def endbeam_state(g, off):
     st["avsr.decoder.output_layer.bias"] = st["avsr.decoder.output_layer.bias"].copy()
     st["avsr.decoder.output_layer.bias"][5048] += np.float32(off)
     return st
+
+
+# ------------------------------------------------------------------ config-option variants
+GOLDEN_CFGVAR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "avsr_cfgvar.npz")
+# the reference config options of tests/golden/make_golden_cfgvar.py (tiny config, dropouts 0)
+CFGVAR = {"add": dict(modality_fuse="add"), "lnorm": dict(transformer_length_normalized_loss=True),
+          "ldrop": dict(layerdrop=0.5)}
+LDROP_SEED = 1
+
+
+def load_cfgvar():
+    return dict(np.load(GOLDEN_CFGVAR, allow_pickle=False))
+
+
+def cfgvar_state(gv, name, seed=0):
+    shapes = {k: tuple(int(x) for x in s.split(",") if x)
+              for k, s in zip(gv[f"{name}_param_keys"], gv[f"{name}_param_shapes"])}
+    return {k: gen_tensor(k, s, seed) for k, s in shapes.items()}
+
+
+def cfgvar_oracle_cfg(name):
+    return O.OracleConfig.from_dict({**TINY_CONFIG, **CFGVAR[name]})
