@@ -58,6 +58,9 @@ _LN_EW_FUSE = True
 # data-gradient chain (off: in line on the step stream; 54.3 vs 51.0 ms per video-on step,
 # profiles/r04_side_stream_ab.txt)
 SIDE_STREAM = True
+# single process: the optimizer's gradient-norm pass over everything but the ResNet frontend runs
+# on the side stream beside the ResNet backward (bench.py wires Engine.pre_video_grads)
+EARLY_NORM = True
 
 
 _STEP_STREAMS = {}
@@ -219,6 +222,7 @@ class Engine:
         # of a training forward, before_backward() / on_grad_ready(offset) / after_backward()
         # around the backward (offset: the decay segment is final from there on)
         self.on_grad_ready = None
+        self.pre_video_grads = None   # callable: see _grads_before_video
         self.before_forward = None
         self.before_backward = None
         self.after_backward = None
@@ -945,8 +949,19 @@ class Engine:
             dfeat = self._e(M, 512)
             ops.gemm(dv, self.w(EN + "feature_extractor_video.proj.weight"), dfeat, M=M, N=512, K=D, a_kmajor=True,
                      b_kmajor=False, lda=dv.stride(0), ldb=512, ldc=512, alpha=fgm)
+            self._grads_before_video()
             self.video_bwd(ctx["vctx"], dfeat)
+        else:
+            self._grads_before_video()
         self.join_side()
+
+    def _grads_before_video(self):
+        """every gradient but the ResNet frontend's is final here: pre_video_grads (e.g.
+        FusedAdamW.early_sumsq, single process) runs on the side stream beside the ResNet backward
+        instead of in the step's serial tail"""
+        if self.pre_video_grads is not None:
+            ops.colsum_flush()          # the deferred bias / LayerNorm finalise passes first
+            self._on_side(self.pre_video_grads)
 
     # ============================================================================ decoder
     def decoder_fwd(self, enc, bt, train, save, seeds):

@@ -34,10 +34,40 @@ class FusedAdamW:
         self.layer_steps = None      # LayerDrop: per encoder layer, the steps that updated it
         self._sumsq = torch.zeros(1, device=arena.device)
         self._sumsq_ws = torch.empty(ops.SUMSQ_WS, device=arena.device)
+        self._early = False
+        # gradients the backward finalises last (the ResNet frontend, resnet.py): early_sumsq()
+        # sums the others beforehand, grad_sumsq() then adds these
+        d0, _ = arena.segments["decay"]
+        _, n1 = arena.segments["no_decay"]
+        late = [(max(s, d0), min(e, n1)) for s, e in arena.ranges_of("encoder.feature_extractor_video.resnet.")]
+        self._late = [(s, e) for s, e in late if s < e]
+        self._early_ranges, pos = [], d0
+        for s, e in self._late:
+            if pos < s:
+                self._early_ranges.append((pos, s))
+            pos = max(pos, e)
+        if pos < n1:
+            self._early_ranges.append((pos, n1))
+
+    def early_sumsq(self):
+        """sum of squares of every trainable gradient outside the ResNet frontend (current stream;
+        the engine calls it on its side stream once those gradients are final — single process
+        only: under DDP the norm must follow the all-reduce)"""
+        a = self.arena
+        self._sumsq.zero_()
+        for s, e in self._early_ranges:
+            ops.sumsq(a.grad[s:e], self._sumsq, self._sumsq_ws)
+        self._early = True
 
     def grad_sumsq(self):
-        """sum of squared gradients over the trainable segments (device scalar, no sync)"""
+        """sum of squared gradients over the trainable segments (device scalar, no sync); after
+        early_sumsq() only the ResNet frontend's ranges are left to add"""
         a = self.arena
+        if self._early:
+            self._early = False
+            for s, e in self._late:
+                ops.sumsq(a.grad[s:e], self._sumsq, self._sumsq_ws)
+            return self._sumsq
         d0, _ = a.segments["decay"]
         _, n1 = a.segments["no_decay"]
         self._sumsq.zero_()

@@ -391,6 +391,9 @@ def gpu_bench(args):
     # average is folded into the AdamW kernel (average=False, grad_scale below)
     ddp = parallel.ArenaDDP(model, average=False, compress=args.grad_compress)
     opt = FusedAdamW(arena, lr=1e-4, weight_decay=0.005, max_grad_norm=1.0)
+    from avsr_amd import engine as _engine
+    if world == 1 and _engine.EARLY_NORM:   # gradient norm of all but the ResNet beside the ResNet backward
+        eng.pre_video_grads = opt.early_sumsq
 
     B, T, L = args.batch, args.seq, args.labels
     v, a, lens, lab = synthetic_batch(B, T, L, seed=args.seed + rank)

@@ -117,3 +117,20 @@ def test_layerdrop_optimizer_skips_dropped_layers(gv, batch):
         # as in test_gpu_surface.py), which an Adam step passes on element by element
         assert d < (1e-2 if ".resnet." in k else 2e-3), (k, d)
     assert opt.layer_steps == [1, 1]
+
+
+def test_early_gradient_norm_matches_full(gv, batch):
+    """FusedAdamW.early_sumsq on the engine's side stream before the ResNet backward plus the
+    ResNet ranges at step time == the one-pass gradient norm (fp32 sums, tolerance 1e-6)"""
+    m = _model(gv, "add").train()
+    eng = m.avsr.engine()
+    opt = FusedAdamW(eng.arena, max_grad_norm=1.0)
+    eng.pre_video_grads = opt.early_sumsq
+    eng.arena.zero_grad()
+    out = m(**batch)
+    out.loss.backward()
+    assert opt._early
+    split = opt.grad_sumsq().item()
+    full = opt.grad_sumsq().item()
+    assert not opt._early and full > 0
+    assert abs(split - full) <= 1e-6 * full, (split, full)
