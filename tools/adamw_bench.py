@@ -49,3 +49,23 @@ us = tm(lambda: ops.adamw(p, g, m, v, lr=1e-4, beta1=0.9, beta2=0.999, eps=1e-8,
 print(f"adamw fresh tensors:                           {us:8.1f} us  {30 * n / us / 1e6:.2f} TB/s")
 us = tm(lambda: m.copy_(p))
 print(f"fp32 copy (torch):                             {us:8.1f} us  {8 * n / us / 1e6:.2f} TB/s")
+# where does the arena's extra time come from: one launch over the arena's own buffers, and fresh
+# tensors with each arena buffer swapped in
+model = AVHubertAVSR(AVHubertAVSRConfig(odim=5049)).train()
+model.setup_engine(dev, torch.bfloat16)
+ar = model.avsr.engine().arena
+ar.init_optimizer()
+ar.grad.normal_()
+arr = {"p": ar.data[d0:n1], "g": ar.grad[d0:n1], "m": ar.exp_avg[d0:n1], "v": ar.exp_avg_sq[d0:n1], "sh": ar.shadow[d0:n1]}
+fresh = {"p": p, "g": g, "m": m, "v": v, "sh": sh}
+
+
+def run(src):
+    t = {k: (arr if k in src else fresh)[k] for k in fresh}
+    return tm(lambda: ops.adamw(t["p"], t["g"], t["m"], t["v"], lr=1e-4, beta1=0.9, beta2=0.999, eps=1e-8,
+                                weight_decay=0.005, step=3, shadow=t["sh"], sumsq_buf=ss, max_norm=1.0))
+
+
+for src in ((), ("p", "g", "m", "v", "sh"), ("p",), ("g",), ("m",), ("v",), ("sh",)):
+    us = run(src)
+    print(f"arena buffers {','.join(src) or '-':14s}: {us:8.1f} us  {30 * n / us / 1e6:.2f} TB/s")
