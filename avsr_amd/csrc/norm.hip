@@ -469,25 +469,39 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(BnArgs a) {
   block_chan_partial<VE>(s3, lds, cpv, wsb + 3 * a.C);
 }
 
-// ws[nb][4][C] -> ws2[slices][4][C]: block (channel group of 64, slice); each wave takes every
-// 4th block row of the slice, lanes = channels (256-byte coalesced reads)
-__global__ __launch_bounds__(256) void bn_ws_fold_kernel(const float* ws, int nb, int C, int per, float* ws2) {
-  __shared__ float red[4][4][64];
+// ws[nb][4][C] -> ws2[slices][4][C]: block (channel group of 64, slice) of 8 waves; each wave
+// takes every 8th block row of the slice, four rows per iteration (16 independent 256-byte
+// coalesced loads in flight per lane: the fold is a latency-bound walk over up to ~90 rows per
+// slice, 27 us per call at one row per iteration and 4 waves)
+constexpr int BN_FOLD_W = 8;
+__global__ __launch_bounds__(64 * BN_FOLD_W) void bn_ws_fold_kernel(const float* ws, int nb, int C, int per, float* ws2) {
+  __shared__ float red[BN_FOLD_W][4][64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + lane, sl = blockIdx.y;
   const int b0 = sl * per, b1 = min(nb, b0 + per);
-  float s[4] = {0.f, 0.f, 0.f, 0.f};
-  if (c < C)
-    for (int b = b0 + wave; b < b1; b += 4)
+  float s[4][4] = {};
+  if (c < C) {
+    int b = b0 + wave;
+    for (; b + 3 * BN_FOLD_W < b1; b += 4 * BN_FOLD_W)
 #pragma unroll
-      for (int q = 0; q < 4; ++q) s[q] += ws[((int64_t)b * 4 + q) * C + c];
+      for (int u = 0; u < 4; ++u)
 #pragma unroll
-  for (int q = 0; q < 4; ++q) red[wave][q][lane] = s[q];
+        for (int q = 0; q < 4; ++q) s[u][q] += ws[((int64_t)(b + u * BN_FOLD_W) * 4 + q) * C + c];
+    for (; b < b1; b += BN_FOLD_W)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) s[0][q] += ws[((int64_t)b * 4 + q) * C + c];
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) red[wave][q][lane] = (s[0][q] + s[1][q]) + (s[2][q] + s[3][q]);
   __syncthreads();
   if (wave == 0 && c < C)
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
-      ws2[((int64_t)sl * 4 + q) * C + c] = red[0][q][lane] + red[1][q][lane] + red[2][q][lane] + red[3][q][lane];
+    for (int q = 0; q < 4; ++q) {
+      float t = 0.f;
+#pragma unroll
+      for (int w = 0; w < BN_FOLD_W; ++w) t += red[w][q][lane];
+      ws2[((int64_t)sl * 4 + q) * C + c] = t;
+    }
 }
 
 template <typename T>
@@ -946,8 +960,8 @@ extern "C" int avsr_bn_bwd_finalize(const avsr_bn_act_params* p, int tiles, void
     constexpr int SL = 128;
     const int per = (tiles + SL - 1) / SL;
     float* ws2 = p->ws + (int64_t)tiles * 4 * p->C;
-    hipLaunchKernelGGL(bn_ws_fold_kernel, dim3((p->C + 63) / 64, SL), dim3(256), 0, st, (const float*)p->ws, tiles,
-                       p->C, per, ws2);
+    hipLaunchKernelGGL(bn_ws_fold_kernel, dim3((p->C + 63) / 64, SL), dim3(64 * BN_FOLD_W), 0, st, (const float*)p->ws,
+                       tiles, p->C, per, ws2);
     ws = ws2; nb = SL;
   }
   hipLaunchKernelGGL(bn_grad_finalize_kernel, dim3(p->C), dim3(256), 0, st, ws, nb, p->C, p->sums, p->dbeta,

@@ -384,3 +384,21 @@ def test_conv_patch_matches_general(dev, monkeypatch, case, lib_opt):
     wr = w.double().permute(0, 3, 1, 2)
     ref = torch.nn.functional.conv2d(xr, wr, padding=1).permute(0, 2, 3, 1).reshape(M, cout)
     assert _rel(out["1"][0], ref) < 2e-2
+
+
+@pytest.mark.parametrize("tiles,C", [(257, 64), (3000, 64), (11337, 128), (1000, 200)])
+def test_bn_finalize_fold_matches_fp64(dev, tiles, C):
+    """avsr_bn_bwd_finalize over > 256 partial rows (the 128-slice fold, 8 waves x 4 rows in
+    flight) vs fp64 column sums of the partials, and the parameter-gradient accumulation"""
+    g = torch.Generator().manual_seed(tiles + C)
+    part = torch.randn(tiles, 4, C, generator=g)
+    ws = torch.zeros(ops.bn_fin_ws(tiles, C), device=dev)
+    ws[:tiles * 4 * C] = part.reshape(-1).to(dev)
+    db, dg, dp = (torch.full((C,), 0.5, device=dev) for _ in range(3))
+    sums = ops.bn_bwd_finalize(ws, tiles, C, dbeta=db, dgamma=dg, dprelu=dp)
+    want = part.double().sum(0)                                   # (4, C)
+    got = torch.stack([sums.view(C, 3)[:, 0], sums.view(C, 3)[:, 1], sums.view(C, 3)[:, 2]]).double().cpu()
+    scale = part.double().abs().sum(0)
+    assert ((got - want[:3]).abs() <= 1e-5 * scale[:3] + 1e-6).all()
+    for t, q in ((db, 0), (dg, 1), (dp, 3)):
+        assert ((t.double().cpu() - 0.5 - want[q]).abs() <= 1e-5 * scale[q] + 1e-5).all(), q
