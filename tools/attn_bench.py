@@ -1,5 +1,6 @@
 """Encoder self-attention fwd / bwd timing at C2 (B=16, H=16, L=375, dh=64), with and without
-probability dropout. usage: python tools/attn_bench.py"""
+probability dropout; with `db` also the fused q/k/v bias-gradient variant of the backward against
+the separate column-sum pass. usage: python tools/attn_bench.py [db]"""
 import os
 import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -36,7 +37,7 @@ for p in (0.0, 0.1):
     print(f"drop {p}: fwd {f * 1e3:.1f} us ({fl / f / 1e9:.0f} TF/s)  bwd(prep+dkdv+dq) {g * 1e3:.1f} us "
           f"({2.5 * fl / g / 1e9:.0f} TF/s)", flush=True)
 db = torch.zeros(3 * H * D, device=dev)
-for p in (0.0, 0.1):
+for p in ((0.0, 0.1) if "db" in sys.argv[1:] else ()):   # `python tools/attn_bench.py db`
     g0 = tm(lambda: ops.attn_bwd(do, q, k, v, o, lse, None, dk, dv, delta, B=B, H=H, Lq=L, Lk=L, klen=klen,
                                  drop_p=p, seed=3, dq=dq))
     g1 = tm(lambda: ops.attn_bwd(do, q, k, v, o, lse, None, dk, dv, delta, B=B, H=H, Lq=L, Lk=L, klen=klen,
