@@ -52,7 +52,9 @@ for a, b in steps:
     # backward starts at the first kernel named *bwd* / dgrad after the loss kernels: use the
     # CTC backward (loss.hip ctc_bwd_kernel) as the boundary (it runs right after the forward)
     cut = next((i for i, r in enumerate(seg) if "ctc_bwd" in r["Kernel_Name"] or "lsm_bwd" in r["Kernel_Name"]), None)
-    opt = next((i for i, r in enumerate(seg) if "sumsq_kernel" in r["Kernel_Name"]), len(seg) - 2)
+    # optimizer: from the LAST gradient-norm pass of the step (the early one, engine.EARLY_NORM, runs
+    # on the side stream inside the backward)
+    opt = max((i for i, r in enumerate(seg) if "sumsq_kernel" in r["Kernel_Name"]), default=len(seg) - 2)
     print(f"step ({len(seg)} kernels)")
     phase(seg[:cut], "forward")
     phase(seg[cut:opt], "backward")
