@@ -331,6 +331,7 @@ using Cfg192s3 = gemmg::GCfg<2, 2, 3, 2, 3>;     // 192x128, 4 waves, 3 stages (
 using Cfg192w8 = gemmg::GCfg<2, 4, 3, 1, 2>;     // 192x128, 8 waves (96x32 each), 2 stages (80 KiB)
 using Cfg192w8s3 = gemmg::GCfg<2, 4, 3, 1, 3>;   // 192x128, 8 waves, 3 stages (120 KiB)
 using Cfg64 = gemmg::GCfg<2, 2, 1, 1, 2>;        // 64x64, 4 waves (32x32 each), 2 stages (32 KiB)
+using Cfg64s4 = gemmg::GCfg<2, 2, 1, 1, 4>;      // 64x64, 4 stages (64 KiB: 3 K-tiles in flight)
 using Cfg192w8s4 = gemmg::GCfg<2, 4, 3, 1, 4>;   // 192x128, 8 waves, 4 stages (160 KiB: 3 K-tiles in flight)
 
 // tile choice: AVSR_OPT_GEMM_TILE = k + 1 forces configuration k (AVSR_TILE_*, benchmarks);
@@ -369,7 +370,11 @@ int tile_cfg(const avsr_gemm_params* p, int splits) {
     const long tiles_z = (long)p->batch * splits;
     const long t128 = (long)((p->M + 127) / 128) * ((p->N + 127) / 128) * tiles_z;
     const long t64 = (long)((p->M + 63) / 64) * ((p->N + 63) / 64) * tiles_z;
-    if (t128 < 256 && t64 >= 2 * t128) return 16;
+    // with at most one 64x64 block per CU and a long K (>= 32 K-tiles) the K loop is DMA-latency
+    // bound: 4 stages keep 3 K-tiles in flight (decoder K = 3072 / 5056 GEMMs 26 -> 20 us,
+    // 41 -> 30 us; with 2+ blocks per CU or K = 1024 the 2-stage tile stays ahead,
+    // profiles/r05_dec_gemm_stages.txt)
+    if (t128 < 256 && t64 >= 2 * t128) return (t64 <= 256 && p->K >= 2048) ? 18 : 16;
   }
   return 0;
 }
@@ -388,6 +393,7 @@ int cfg_bm(int cfg, bool ak) {
     case 9: return ak ? Cfg96::BM : Cfg128::BM;   // as launch_cfg
     case 10: return Cfg128x64::BM;
     case 16: return Cfg64::BM;
+    case 18: return Cfg64s4::BM;
     case 11: return ak ? Cfg192::BM : Cfg128::BM;
     case 12: return ak ? Cfg192x256::BM : Cfg128::BM;
     case 13: return ak ? Cfg192s3::BM : Cfg128::BM;
@@ -414,6 +420,7 @@ int launch_cfg(int cfg, const DenseArgs& a, int batch, hipStream_t st) {
       else return launch_glds<OutT, AK, BK, Cfg128>(a, batch, st);
     case 10: return launch_glds<OutT, AK, BK, Cfg128x64>(a, batch, st);
     case 16: return launch_glds<OutT, AK, BK, Cfg64>(a, batch, st);
+    case 18: return launch_glds<OutT, AK, BK, Cfg64s4>(a, batch, st);
     case 11:   // BM = 192: r-contiguous A needs BM % 64 == 0 (weight-grads stay on 128x128)
       if constexpr (AK) return launch_glds<OutT, AK, BK, Cfg192>(a, batch, st);
       else return launch_glds<OutT, AK, BK, Cfg128>(a, batch, st);

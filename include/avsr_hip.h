@@ -78,7 +78,7 @@ enum {
   AVSR_TILE_128 = 0, AVSR_TILE_256 = 1, AVSR_TILE_256x128 = 2, AVSR_TILE_128x256 = 3, AVSR_TILE_128s3 = 4,
   AVSR_TILE_128s4 = 5, AVSR_TILE_128w8s3 = 6, AVSR_TILE_128w8s4 = 7, AVSR_TILE_PP = 8, AVSR_TILE_96 = 9,
   AVSR_TILE_128x64 = 10, AVSR_TILE_192 = 11, AVSR_TILE_192x256 = 12, AVSR_TILE_192s3 = 13, AVSR_TILE_192w8 = 14,
-  AVSR_TILE_192w8s3 = 15, AVSR_TILE_64 = 16, AVSR_TILE_192w8s4 = 17, AVSR_TILE_COUNT = 18
+  AVSR_TILE_192w8s3 = 15, AVSR_TILE_64 = 16, AVSR_TILE_192w8s4 = 17, AVSR_TILE_64s4 = 18, AVSR_TILE_COUNT = 19
 };
 int avsr_set_option(int option, int64_t value);
 int64_t avsr_get_option(int option);

@@ -201,7 +201,7 @@ def test_dgrad_fused_bias_grad(dev, gemm_tile, M, N, K):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("tile", ["192", "192x256", "256x128", "pp"])
+@pytest.mark.parametrize("tile", ["192", "192x256", "256x128", "pp", "64", "64s4"])
 def test_tile_configs_bit_identical(dev, monkeypatch, tile, lib_opt):
     """Every tile configuration accumulates each output over the same K order (64-deep K-tiles,
     the same 16x16x32 MFMA sequence), so the fused-epilogue results must equal the 128x128

@@ -4,7 +4,7 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 O=gpurun_out/${1:-ab}; mkdir -p $O
-for rep in 1 2; do
+for rep in ${REPS:-1 2}; do
   for v in $(echo ${2:-base} | tr , ' '); do
     if [ $v = base ]; then unset AVSR_LIB_PATH_AB; else export AVSR_LIB_PATH_AB=ab/$v/libavsr_hip.so; fi
     timeout -k 10 300 python -u bench.py --steps 12 --warmup 3 --quick --no-cpu-baseline --no-decode > $O/$v.$rep.log 2>&1 || { echo "$v failed"; tail -5 $O/$v.$rep.log; exit 1; }
