@@ -4,8 +4,25 @@ weight_decay 0.005 on all but biases / LayerNorm weights, max_grad_norm 1.0, lin
 warm-up then linear decay). One sumsq launch + one AdamW launch per segment, no host sync:
 the clip coefficient is computed on the device from the gradient norm."""
 import torch
+import torch.distributed as dist
 
 from . import ops
+
+
+def union_touched(touched, n, device=None):
+    """LayerDrop under data parallelism: the encoder layers some rank's backward touched. The
+    all-reduce hands every rank the average gradient, so a layer kept on any rank has a gradient
+    everywhere and every rank must update it (a per-rank skip would let the replicas drift). One
+    MAX all-reduce of an n-flag vector and a host read (one sync per step, LayerDrop + DDP only);
+    single process: the local set."""
+    if not (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1):
+        return set(touched)
+    dev = device if dist.get_backend() == "nccl" else torch.device("cpu")
+    m = torch.zeros(n, dtype=torch.int32, device=dev)
+    if touched:
+        m[list(touched)] = 1
+    dist.all_reduce(m, op=dist.ReduceOp.MAX)
+    return set(torch.nonzero(m).flatten().tolist())
 
 
 class LinearWarmupDecay:
@@ -97,7 +114,8 @@ class FusedAdamW:
         if a.ld_ranges is not None:
             if self.layer_steps is None:
                 self.layer_steps = [self.step_count - 1] * len(a.ld_ranges)
-            for i in a.ld_touched:
+            self._touched = union_touched(a.ld_touched, len(a.ld_ranges), a.device)
+            for i in self._touched:
                 self.layer_steps[i] += 1
         for (s, e), wd in (((d0, d1), self.wd), ((n0, n1), 0.0)):
             for ps, pe, step in self._pieces(s, e):
@@ -117,7 +135,7 @@ class FusedAdamW:
             return [(s, e, self.step_count)] if e > s else []
         cuts = []
         for i, rs in enumerate(a.ld_ranges):
-            st = self.layer_steps[i] if i in a.ld_touched else None
+            st = self.layer_steps[i] if i in self._touched else None
             for r0, r1 in rs:
                 lo, hi = max(r0, s), min(r1, e)
                 if lo < hi:

@@ -115,3 +115,31 @@ def test_grad_reducer_bf16_compression_world2():
     for rank, err, differs in res:
         assert err < 2 ** -7, (rank, err)
         assert differs, rank
+
+
+def _ld_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    try:
+        from avsr_amd.optim import union_touched
+        parallel.init_from_env(backend="gloo")
+        local = {0, 3} if rank == 0 else {3, 5}         # LayerDrop kept different layers per rank
+        q.put((rank, sorted(union_touched(local, 8))))
+        dist.destroy_process_group()
+    except Exception as e:                              # pragma: no cover - reported to the parent
+        q.put((rank, repr(e)))
+
+
+def test_layerdrop_touched_union_world2():
+    """LayerDrop + DDP: every rank updates the layers that ANY rank's backward touched (the
+    all-reduced gradient is nonzero there on every rank), so the replicas stay identical"""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_ld_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    out = dict(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+    assert out == {0: [0, 3, 5], 1: [0, 3, 5]}, out
