@@ -469,39 +469,29 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(BnArgs a) {
   block_chan_partial<VE>(s3, lds, cpv, wsb + 3 * a.C);
 }
 
-// ws[nb][4][C] -> ws2[slices][4][C]: block (channel group of 64, slice) of 8 waves; each wave
-// takes every 8th block row of the slice, four rows per iteration (16 independent 256-byte
-// coalesced loads in flight per lane: the fold is a latency-bound walk over up to ~90 rows per
-// slice, 27 us per call at one row per iteration and 4 waves)
-constexpr int BN_FOLD_W = 8;
-__global__ __launch_bounds__(64 * BN_FOLD_W) void bn_ws_fold_kernel(const float* ws, int nb, int C, int per, float* ws2) {
-  __shared__ float red[BN_FOLD_W][4][64];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + lane, sl = blockIdx.y;
-  const int b0 = sl * per, b1 = min(nb, b0 + per);
+// ws[nb][4][C] -> ws2[slices][4][C]: one wave per (channel group of 64, slice of BN_FOLD_PER
+// block rows), four rows per iteration (16 independent 256-byte coalesced loads in flight per
+// lane), no LDS. Single-wave blocks: the fold runs on the main stream while the side stream's
+// persistent weight-gradient blocks (conv_wgrad_patch, one 4-wave block per CU with up to 152 KB
+// of LDS) hold every CU, and the former 8-wave / 8 KB-LDS blocks found no room beside them
+// (6 us alone, 180 us in the step: they waited for the weight-gradient tail).
+constexpr int BN_FOLD_PER = 16;
+__global__ __launch_bounds__(64) void bn_ws_fold_kernel(const float* ws, int nb, int C, float* ws2) {
+  const int c = blockIdx.x * 64 + threadIdx.x, sl = blockIdx.y;
+  const int b0 = sl * BN_FOLD_PER, b1 = min(nb, b0 + BN_FOLD_PER);
+  if (c >= C) return;
   float s[4][4] = {};
-  if (c < C) {
-    int b = b0 + wave;
-    for (; b + 3 * BN_FOLD_W < b1; b += 4 * BN_FOLD_W)
+  int b = b0;
+  for (; b + 3 < b1; b += 4)
 #pragma unroll
-      for (int u = 0; u < 4; ++u)
+    for (int u = 0; u < 4; ++u)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) s[u][q] += ws[((int64_t)(b + u * BN_FOLD_W) * 4 + q) * C + c];
-    for (; b < b1; b += BN_FOLD_W)
+      for (int q = 0; q < 4; ++q) s[u][q] += ws[((int64_t)(b + u) * 4 + q) * C + c];
+  for (; b < b1; ++b)
 #pragma unroll
-      for (int q = 0; q < 4; ++q) s[0][q] += ws[((int64_t)b * 4 + q) * C + c];
-  }
+    for (int q = 0; q < 4; ++q) s[0][q] += ws[((int64_t)b * 4 + q) * C + c];
 #pragma unroll
-  for (int q = 0; q < 4; ++q) red[wave][q][lane] = (s[0][q] + s[1][q]) + (s[2][q] + s[3][q]);
-  __syncthreads();
-  if (wave == 0 && c < C)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      float t = 0.f;
-#pragma unroll
-      for (int w = 0; w < BN_FOLD_W; ++w) t += red[w][q][lane];
-      ws2[((int64_t)sl * 4 + q) * C + c] = t;
-    }
+  for (int q = 0; q < 4; ++q) ws2[((int64_t)sl * 4 + q) * C + c] = (s[0][q] + s[1][q]) + (s[2][q] + s[3][q]);
 }
 
 template <typename T>
@@ -949,19 +939,19 @@ extern "C" int avsr_bn_act_bwd_reduce(const avsr_bn_act_params* p, void* stream)
 }
 
 // ws[tiles][4][C] (from the reduce kernel or a data-grad BN epilogue) -> sums + parameter
-// grads. More than 256 partial rows are first folded into 128 slices, stored after the
-// partials (ws holds AVSR_BN_FIN_WS(tiles, C) floats).
+// grads. More than 256 partial rows are first folded into ceil(tiles / 16) slices, stored after
+// the partials (ws holds AVSR_BN_FIN_WS(tiles, C) floats).
 extern "C" int avsr_bn_bwd_finalize(const avsr_bn_act_params* p, int tiles, void* stream) {
   if (!p || !p->ws || p->C <= 0 || tiles <= 0) return AVSR_E_ARG;
   const float* ws = p->ws;
   int nb = tiles;
   hipStream_t st = (hipStream_t)stream;
   if (tiles > 256) {
-    constexpr int SL = 128;
-    const int per = (tiles + SL - 1) / SL;
+    const int SL = (tiles + BN_FOLD_PER - 1) / BN_FOLD_PER;
+    if (SL > 65535) return AVSR_E_SHAPE;
     float* ws2 = p->ws + (int64_t)tiles * 4 * p->C;
-    hipLaunchKernelGGL(bn_ws_fold_kernel, dim3((p->C + 63) / 64, SL), dim3(64 * BN_FOLD_W), 0, st, (const float*)p->ws,
-                       tiles, p->C, per, ws2);
+    hipLaunchKernelGGL(bn_ws_fold_kernel, dim3((p->C + 63) / 64, SL), dim3(64), 0, st, (const float*)p->ws, tiles,
+                       p->C, ws2);
     ws = ws2; nb = SL;
   }
   hipLaunchKernelGGL(bn_grad_finalize_kernel, dim3(p->C), dim3(256), 0, st, ws, nb, p->C, p->sums, p->dbeta,

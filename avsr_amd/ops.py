@@ -316,7 +316,7 @@ def conv_bwd_data(g, dy, w, dx, alpha=1.0, beta=0.0):
 
 def bn_fin_ws(tiles, C):
     """floats of a BN-backward partials workspace (AVSR_BN_FIN_WS)"""
-    return (tiles + (128 if tiles > 256 else 0)) * 4 * C
+    return (tiles + ((tiles + 15) // 16 if tiles > 256 else 0)) * 4 * C
 
 
 def conv_bwd_data_bnr(g, dy, w, dx, h, st, prelu, *, res=None, st2=None, alpha=1.0, beta=0.0):

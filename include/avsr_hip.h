@@ -314,7 +314,7 @@ typedef struct {
   float* ws;                                       /* bwd_reduce workspace >= AVSR_BN_WS(C) floats */
 } avsr_bn_act_params;
 /* partial sums of `tiles` row blocks [tiles][4][C] plus the fold area finalize uses */
-#define AVSR_BN_FIN_WS(tiles, C) (((int64_t)(tiles) + ((tiles) > 256 ? 128 : 0)) * 4 * (C))
+#define AVSR_BN_FIN_WS(tiles, C) (((int64_t)(tiles) + ((tiles) > 256 ? ((tiles) + 15) / 16 : 0)) * 4 * (C))
 #define AVSR_BN_WS(C) AVSR_BN_FIN_WS(2048, C)
 int avsr_bn_act_fwd(const avsr_bn_act_params* p, void* stream);
 /* reduce + finalize (sums, dgamma/dbeta, dprelu) */

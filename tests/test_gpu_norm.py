@@ -388,8 +388,8 @@ def test_conv_patch_matches_general(dev, monkeypatch, case, lib_opt):
 
 @pytest.mark.parametrize("tiles,C", [(257, 64), (3000, 64), (11337, 128), (1000, 200)])
 def test_bn_finalize_fold_matches_fp64(dev, tiles, C):
-    """avsr_bn_bwd_finalize over > 256 partial rows (the 128-slice fold, 8 waves x 4 rows in
-    flight) vs fp64 column sums of the partials, and the parameter-gradient accumulation"""
+    """avsr_bn_bwd_finalize over > 256 partial rows (the fold into ceil(tiles / 16) slices,
+    one wave per slice and 64 channels) vs fp64 column sums of the partials, and the parameter-gradient accumulation"""
     g = torch.Generator().manual_seed(tiles + C)
     part = torch.randn(tiles, 4, C, generator=g)
     ws = torch.zeros(ops.bn_fin_ws(tiles, C), device=dev)
