@@ -346,7 +346,8 @@ def check(rc, op):
 
 # kernel-selection options (avsr_hip.h AVSR_OPT_*, AVSR_TILE_*): A/B tools and variant tests
 OPTIONS = {"gemm_tile": 0, "attn_sq_fwd": 1, "attn_sq_bwd": 2, "wgrad_dual": 3, "conv_192": 4, "conv_s2phase": 5,
-           "conv_patch": 6, "conv_wpatch": 7, "stem_pool_2x2": 8}
+           "conv_patch": 6, "conv_wpatch": 7, "stem_pool_2x2": 8,
+           "stem_wpatch": 9}
 TILES = ["128", "256", "256x128", "128x256", "128s3", "128s4", "128w8s3", "128w8s4", "pp", "96", "128x64", "192",
          "192x256", "192s3", "192w8", "192w8s3", "64", "192w8s4", "64s4"]
 

@@ -967,6 +967,196 @@ static int wpatch_launch(const avsr_conv_params* p, hipStream_t st) {
   return wpatch_launch_g<WPStage2>(p, st);
 }
 
+// ---------------------------------------------------------------- patch-resident stem weight-grad
+// The stem conv's weight-gradient (Conv3d 1 -> 64, 5 x 7 x 7, stride (1, 2, 2), pad (2, 3, 3)) on
+// the packed input xp [N][88][88][8] (the 5 frames t-2 .. t+2 of each pixel in channels 0-4,
+// zeros after; ops.stem_pack): gp[co][kh][kw][c] += sum_p dy[p][co] * xp[p's image][2oy+kh-3]
+// [2ox+kw-3][c] over the N x 44 x 44 output pixels. The general implicit GEMM computes an im2col
+// address per 16-byte DMA slot and amortises its 256-column tiles over only 64 output channels
+// (VALU-bound, MFMA busy 0.28: profiles/r05_stem_wgrad_counters.txt). Here persistent blocks
+// (one per CU) walk tiles of 4 output rows of one image, 48 columns wide (44 real; the other dy
+// rows are DMA zeros). Per tile the dy rows and the zero-padded 13 x 103 input patch (16 bytes
+// per pixel) are DMA'd into LDS once, three buffers deep, and every tap of every pixel is an
+// offset into the patch. A k-step's 32 pixels are a 4-row x 8-column block (dy rows stored in
+// that order), so every LDS address of the main loop is a per-lane base fixed for the kernel plus
+// a compile-time offset (no address arithmetic per k-step), and the DMA offsets are per-lane
+// constants plus a per-tile scalar. The 64 x 392 gradient block stays in registers: columns are
+// pairs of taps (t, t+1) x 8 channels (16 per MFMA tile; 25 pairs, the 49th tap's partner a
+// discarded duplicate), pair P belongs to wave P mod 4, and waves 1-3 run a discarded 7th pair
+// so that every wave has the same branch-free loop. The fragment reads of k-step kb+1 are issued
+// between the two halves of k-step kb's MFMAs (scheduling barriers keep them there): the LDS
+// latency hides behind the second half instead of an lgkmcnt drain in front of every k-step
+// (lgkmcnt counts to 15; a step has 22 reads). Both operands are pixel-major, read
+// transposed (ds_read_b64_tr_b16) with wgrad_patch's pixel order; a 16-lane group's patch read
+// covers 4 pixels x 2 taps x 8 channels in 128 contiguous bytes modulo the banks (row stride
+// 103 x 16 B keeps the pairs that straddle two kernel rows conflict-free too). Each block writes
+// its fp32 partial to a slab [block][64][392]; wgrad_reduce_kernel sums the slabs in block order
+// (deterministic).
+constexpr int SWP_TR = 4, SWP_TC = 48, SWP_KS = SWP_TC / 8, SWP_TPI = 44 / SWP_TR;
+constexpr int SWP_DYB = SWP_KS * 32 * 128, SWP_DYPIECE = SWP_DYB / 4096;
+constexpr int SWP_PR = 2 * SWP_TR + 5, SWP_PC = 103, SWP_SLOTS = SWP_PR * SWP_PC, SWP_RB = SWP_PC * 16;
+constexpr int SWP_PPIECE = (SWP_SLOTS + 255) / 256, SWP_PBYTES = SWP_PPIECE * 4096;
+constexpr int SWP_BUF = SWP_DYB + SWP_PBYTES, SWP_NBUF = 3, SWP_LDS = SWP_NBUF * SWP_BUF;
+constexpr int SWP_NP = SWP_DYPIECE + SWP_PPIECE, SWP_COLS = 392, SWP_PAIRS = 25;
+constexpr int SWP_JW = (SWP_PAIRS + 3) / 4;     // pairs per wave (7; pairs >= 25 are discarded)
+static_assert(SWP_LDS <= 160 * 1024 && SWP_DYB % 4096 == 0 && SWP_KS % 2 == 0, "stem weight-grad tile buffers");
+static_assert(2 * (SWP_TC - 1) + 6 - 3 < SWP_PC - 3 + 1 && SWP_NP % SWP_KS == 0, "patch width / DMA spread");
+
+AVSR_DEV int swp_toff(int t) {                 // patch byte offset of tap t = (kh, kw) (t > 48 -> 48)
+  t = t > 48 ? 48 : t;
+  const int kh = t / 7, kw = t - 7 * kh;
+  return kh * SWP_RB + kw * 16;
+}
+
+__global__ __launch_bounds__(256, 1) void stem_wgrad_patch_kernel(const bf16* __restrict__ xp, const bf16* __restrict__ dy,
+                                                                  uint32_t x_bytes, uint32_t dy_bytes, int nimg,
+                                                                  float* __restrict__ ws) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int ntiles = nimg * SWP_TPI;
+  const int ta = (int)((int64_t)ntiles * blockIdx.x / gridDim.x), tb = (int)((int64_t)ntiles * (blockIdx.x + 1) / gridDim.x);
+  const __amdgpu_buffer_rsrc_t rx = make_rsrc(xp, x_bytes), rdy = make_rsrc(dy, dy_bytes);
+  // per-lane DMA offsets relative to the tile's first dy pixel / input pixel (OOB: zeros)
+  uint32_t vdy[SWP_DYPIECE];
+  int vpt[SWP_PPIECE], ppr[SWP_PPIECE];
+#pragma unroll
+  for (int i = 0; i < SWP_DYPIECE; ++i) {
+    const int sl = (wave + 4 * i) * 64 + lane, row = sl >> 3;          // dy LDS row = kb * 32 + r * 8 + c
+    const int ch = (sl & 7) ^ whswz(row), k = row & 31, col = 8 * (row >> 5) + (k & 7);
+    vdy[i] = col < 44 ? (uint32_t)(((k >> 3) * 44 + col) * 128 + ch * 16) : gemmg::OOB;
+  }
+#pragma unroll
+  for (int i = 0; i < SWP_PPIECE; ++i) {
+    const int sl = (wave + 4 * i) * 64 + lane, pr = sl / SWP_PC, pc = sl - pr * SWP_PC;
+    const bool ok = sl < SWP_SLOTS && pc >= 3 && pc < 91;
+    vpt[i] = ((pr - 3) * 88 + pc - 3) * 16;
+    ppr[i] = ok ? pr - 3 : -1000;                   // input row offset of the slot (-1000: never valid)
+  }
+  auto issue = [&](int pc, int t, char* buf) {      // DMA piece pc of tile t (dy pieces, then patch)
+    const int img = t / SWP_TPI, oy0 = (t - img * SWP_TPI) * SWP_TR;
+    if (pc < SWP_DYPIECE) {
+      gemmg::bglds16(rdy, vdy[pc], (uint32_t)(img * 1936 + oy0 * 44) * 128u, buf + (wave + 4 * pc) * 1024);
+    } else {
+      const int i = pc - SWP_DYPIECE, y = 2 * oy0 + ppr[i];
+      const uint32_t vo = (uint32_t)y < 88u ? (uint32_t)(img * 123904 + oy0 * 2816 + vpt[i]) : gemmg::OOB;
+      gemmg::bglds16(rx, vo, 0u, buf + SWP_DYB + (wave + 4 * i) * 1024);
+    }
+  };
+  // fragment bases: lane group g holds k = 8g + j <-> pixel 16(g >> 1) + 4(g & 1) + (j & 3) + 8(j >> 2)
+  // of the k-step = row k >> 3, column 8 kb + (k & 7) of the tile
+  const int g = lane >> 4, qq = (lane & 15) >> 2, pp = lane & 3;
+  const int pxa = 16 * (g >> 1) + 4 * (g & 1) + qq;
+  const int sw = whswz(pxa);
+  int dA[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) dA[i] = pxa * 128 + (((2 * i + (pp >> 1)) ^ sw) << 4) + 8 * (pp & 1);
+  const int pbase = SWP_DYB + (2 * (pxa >> 3) * SWP_PC + 2 * (pxa & 7)) * 16;
+  int oB[SWP_JW];                                   // patch byte base of this lane per pair
+#pragma unroll
+  for (int j = 0; j < SWP_JW; ++j) oB[j] = pbase + swp_toff(2 * (wave + 4 * j) + (pp >> 1)) + 8 * (pp & 1);
+  f32x4 acc[4][SWP_JW];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < SWP_JW; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  constexpr int PD = SWP_NBUF - 1, PER = SWP_NP / SWP_KS;
+#pragma unroll
+  for (int d = 0; d < PD; ++d)
+    if (ta + d < tb)
+#pragma unroll
+      for (int pc = 0; pc < SWP_NP; ++pc) issue(pc, ta + d, smem + d * SWP_BUF);
+  struct Fr { bf16x8 a[4], b[SWP_JW]; };
+  // k-step kb: dy rows kb * 32 (+ 8: the next tile row), patch columns + 16 kb pixels (+ 2 rows)
+  auto load = [&](Fr& f, const char* buf, int kb) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) f.a[i] = trpair(buf + dA[i] + kb * 4096, buf + dA[i] + kb * 4096 + 1024);
+#pragma unroll
+    for (int j = 0; j < SWP_JW; ++j) f.b[j] = trpair(buf + oB[j] + kb * 256, buf + oB[j] + kb * 256 + 2 * SWP_RB);
+  };
+  auto mma = [&](const Fr& f, int h) {            // output-channel tiles 2h, 2h + 1
+#pragma unroll
+    for (int i = 2 * h; i < 2 * h + 2; ++i)
+#pragma unroll
+      for (int j = 0; j < SWP_JW; ++j) acc[i][j] = mfma16(f.a[i], f.b[j], acc[i][j]);
+  };
+  for (int t = ta; t < tb; ++t) {
+    const char* buf = smem + ((t - ta) % SWP_NBUF) * SWP_BUF;
+    char* nbuf = smem + ((t + PD - ta) % SWP_NBUF) * SWP_BUF;
+    const bool more = t + PD < tb;
+    if (t + 1 < tb) gemmg::wait_vmcnt<SWP_NP>();   // tile t landed; tile t+1's DMAs may fly
+    else gemmg::wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();                  // ... for every wave; every wave is done with tile t-1
+    asm volatile("" ::: "memory");
+    // two fragment sets in fixed roles (even / odd k-steps): no register copies
+    Fr f0, f1;
+    load(f0, buf, 0);
+#pragma unroll
+    for (int kb = 0; kb < SWP_KS; kb += 2) {
+      mma(f0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      load(f1, buf, kb + 1);
+      __builtin_amdgcn_sched_barrier(0);
+      mma(f0, 1);
+      if (more)
+#pragma unroll
+        for (int d = 0; d < PER; ++d) issue(kb * PER + d, t + PD, nbuf);
+      mma(f1, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      if (kb + 2 < SWP_KS) load(f0, buf, kb + 2);
+      __builtin_amdgcn_sched_barrier(0);
+      mma(f1, 1);
+      if (more)
+#pragma unroll
+        for (int d = 0; d < PER; ++d) issue((kb + 1) * PER + d, t + PD, nbuf);
+    }
+  }
+  // partial -> ws[block][co 64][392]: accumulator (i, j) register r = co 16i + 4g + r, column
+  // 16 * pair + (lane & 15) = (tap 2 * pair + ((lane >> 3) & 1)) * 8 + channel (lane & 7)
+  float* o = ws + (int64_t)blockIdx.x * 64 * SWP_COLS;
+#pragma unroll
+  for (int j = 0; j < SWP_JW; ++j) {
+    const int col = 16 * (wave + 4 * j) + (lane & 15);
+    if (col < SWP_COLS)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[(16 * i + 4 * g + r) * SWP_COLS + col] = acc[i][j][r];
+  }
+}
+
+// the stem geometry on the packed input, bf16, slab workspace, both tensors below the 2 GiB
+// buffer extent
+static bool stem_wpatch_ok(const avsr_conv_params* p) {
+  if (!avsr_opt(AVSR_OPT_STEM_WPATCH) || p->dtype != AVSR_BF16 || p->groups != 1 || p->splitk > 0) return false;
+  if (p->cin != 8 || p->ldx != 8 || p->cout != 64 || p->ldy != 64 || p->kh != 7 || p->kw != 7) return false;
+  if (p->sh != 2 || p->sw != 2 || p->ph != 3 || p->pw != 3 || p->hin != 88 || p->win != 88) return false;
+  if (p->hout != 44 || p->wout != 44) return false;
+  const int64_t dyb = (int64_t)p->nimg * 1936 * 128;
+  return dyb > 0 && dyb < (int64_t)gemmg::OOB - (1 << 20);
+}
+
+static int stem_wpatch_launch(const avsr_conv_params* p, hipStream_t st) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)stem_wgrad_patch_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, SWP_LDS);
+    attr = true;
+  }
+  const uint32_t xb = (uint32_t)((int64_t)p->nimg * 88 * 88 * 16), dyb = (uint32_t)((int64_t)p->nimg * 1936 * 128);
+  hipLaunchKernelGGL(stem_wgrad_patch_kernel, dim3(WP_BLOCKS), dim3(256), SWP_LDS, st, (const bf16*)p->x,
+                     (const bf16*)p->dy, xb, dyb, p->nimg, p->ws);
+  AVSR_CHECK_LAUNCH();
+  const int64_t mn = 64 * SWP_COLS;
+  const int xg = avsr_grid(mn / 4, 256, 1024);
+  const int chunks = 8;
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)xg, 1u, (unsigned)chunks), dim3(256), 0, st, p->ws, WP_BLOCKS,
+                     chunks, mn, p->dw, (int64_t)0);
+  AVSR_CHECK_LAUNCH();
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)xg, 1u, 1u), dim3(256), 0, st, p->ws, WP_BLOCKS, -chunks, mn,
+                     p->dw, (int64_t)0);
+  AVSR_CHECK_LAUNCH();
+  return 0;
+}
+
 // the patch-resident stage-1 kernel applies (bf16, 3x3 / stride 1 / pad 1, 64 -> 64 channels)
 static bool patch_ok(const avsr_conv_params* p, const ConvArgs& a) {
   if (!avsr_opt(AVSR_OPT_CONV_PATCH) || p->dtype != AVSR_BF16 || !conv_glds_enabled() || !a.a_bytes || p->groups != 1) return false;
@@ -1138,6 +1328,7 @@ extern "C" int avsr_conv_bwd_weight(const avsr_conv_params* p, void* stream) {
   a.M = p->cout; a.N = (int)ktot; a.K = p->nimg * p->hout * p->wout;
   if (a.K == 0) return 0;
   if (p->ws && wpatch_ok(p)) return wpatch_launch(p, (hipStream_t)stream);   // patch-resident, ordered slab reduce
+  if (p->ws && stem_wpatch_ok(p)) return stem_wpatch_launch(p, (hipStream_t)stream);
   set_extents(a, p, true, ((int64_t)p->nimg * p->hout * p->wout - 1) * p->ldy + p->cout,
               ((int64_t)p->nimg * p->hin * p->win - 1) * p->ldx + p->cin);
   const bool glds = p->dtype == AVSR_BF16 && conv_glds_enabled();
@@ -1173,6 +1364,7 @@ extern "C" int avsr_conv_bwd_weight(const avsr_conv_params* p, void* stream) {
 extern "C" int64_t avsr_conv_wgrad_ws(const avsr_conv_params* p) {
   if (!p || (p->dtype != AVSR_BF16 && p->dtype != AVSR_F32)) return 0;
   if (wpatch_ok(p)) return (int64_t)WP_BLOCKS * 64 * WP_COLS;
+  if (stem_wpatch_ok(p)) return (int64_t)WP_BLOCKS * 64 * SWP_COLS;
   const WgradPlan w = wgrad_plan(p, p->dtype == AVSR_BF16 && conv_glds_enabled(), true);
   if (!w.slab) return 0;
   return (int64_t)p->groups * w.splits * p->cout * ((int64_t)p->kh * p->kw * p->cin);

@@ -7,7 +7,7 @@ extern "C" const char* avsr_version(void) { return "avsr_hip 0.2.0 gfx950"; }
 
 namespace {
 // defaults = the production choices documented in avsr_hip.h
-std::atomic<int64_t> g_opt[AVSR_OPT_COUNT] = {{0}, {1}, {0}, {1}, {1}, {1}, {1}, {1}, {1}};
+std::atomic<int64_t> g_opt[AVSR_OPT_COUNT] = {{0}, {1}, {0}, {1}, {1}, {1}, {1}, {1}, {1}, {1}};
 
 bool opt_valid(int option, int64_t v) {
   switch (option) {
@@ -19,7 +19,8 @@ bool opt_valid(int option, int64_t v) {
     case AVSR_OPT_CONV_S2PHASE:
     case AVSR_OPT_CONV_PATCH:
     case AVSR_OPT_CONV_WPATCH:
-    case AVSR_OPT_STEM_POOL_2X2: return v == 0 || v == 1;
+    case AVSR_OPT_STEM_POOL_2X2:
+    case AVSR_OPT_STEM_WPATCH: return v == 0 || v == 1;
     default: return false;
   }
 }

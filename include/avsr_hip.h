@@ -58,6 +58,9 @@ const char* avsr_version(void);
  *                                 the general split-K weight-grad (fp32 re-association)
  *   AVSR_OPT_STEM_POOL_2X2  [1]  1: stem max-pool forward / backward apply over 2x2 output
  *                                 blocks; 0: one output pixel per thread (bit-identical)
+ *   AVSR_OPT_STEM_WPATCH    [1]  1: patch-resident stem weight-grad (packed 8-channel input,
+ *                                 7x7 / stride 2); 0: the general split-K weight-grad (fp32
+ *                                 re-association)
  * avsr_set_option returns 0, or AVSR_E_ARG for an unknown option or a value out of range;
  * avsr_get_option returns the value, or -1 for an unknown option.
  * ------------------------------------------------------------------------------------ */
@@ -71,7 +74,8 @@ enum {
   AVSR_OPT_CONV_PATCH = 6,
   AVSR_OPT_CONV_WPATCH = 7,
   AVSR_OPT_STEM_POOL_2X2 = 8,
-  AVSR_OPT_COUNT = 9
+  AVSR_OPT_STEM_WPATCH = 9,
+  AVSR_OPT_COUNT = 10
 };
 /* tile configurations of the bf16 GEMM core (AVSR_OPT_GEMM_TILE = k + 1) */
 enum {

@@ -254,3 +254,32 @@ def test_wgrad_patch_matches_general(dev, nimg, hw, c, monkeypatch, lib_opt):
     wr = torch.zeros(c, c, 3, 3, dtype=torch.float64, requires_grad=True)
     F.conv2d(xr, wr, padding=1).backward(dy.double().cpu().permute(0, 3, 1, 2))
     assert _rel(dw1 - init, wr.grad.permute(0, 2, 3, 1)) < 1e-4
+
+
+@pytest.mark.parametrize("nimg", [1, 13, 600])
+def test_stem_wgrad_patch_matches_general(dev, nimg, lib_opt):
+    """Patch-resident stem weight-grad (packed 8-channel input, 7 x 7 / stride 2 / pad 3,
+    persistent blocks over 4-row tiles, per-block slabs, ordered reduce) vs the general
+    implicit-GEMM weight-grad and fp64 torch: blocks without tiles (nimg = 1), tile ranges
+    spanning images, accumulation into a non-zero dw, run-to-run bit-identical."""
+    g = torch.Generator().manual_seed(nimg)
+    geom = ops.ConvGeom(nimg, 88, 88, 8, 64, 7, 7, (2, 2), (3, 3))
+    x = torch.randn(nimg, 88, 88, 8, generator=g)
+    x[..., 5:] = 0                                   # the packing's zero channels
+    xd = x.to(dev, torch.bfloat16)
+    dy = torch.randn(nimg * 44 * 44, 64, generator=g).to(dev, torch.bfloat16)
+    init = torch.randn(64, 7, 7, 8, generator=g).to(dev)
+    dw1 = init.clone()
+    ops.conv_bwd_weight(geom, xd, dy, dw1)
+    dw1b = init.clone()
+    ops.conv_bwd_weight(geom, xd, dy, dw1b)
+    assert torch.equal(dw1, dw1b)
+    lib_opt("stem_wpatch", 0)
+    dw2 = init.clone()
+    ops.conv_bwd_weight(geom, xd, dy, dw2)
+    assert _rel(dw1 - init, dw2 - init) < 1e-4
+    if nimg <= 13:
+        xr = xd.double().cpu().permute(0, 3, 1, 2)
+        wr = torch.zeros(64, 8, 7, 7, dtype=torch.float64, requires_grad=True)
+        F.conv2d(xr, wr, stride=2, padding=3).backward(dy.double().cpu().view(nimg, 44, 44, 64).permute(0, 3, 1, 2))
+        assert _rel(dw1 - init, wr.grad.permute(0, 2, 3, 1)) < 1e-5

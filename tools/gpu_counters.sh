@@ -19,6 +19,7 @@ for prog in ${PROGS:-probe wgrad attn stem cwgrad step}; do
     wgrad) CMD="python3 tools/gemm_one.py 4096 1024 6000 wgrad 20";;
     attn) CMD="python3 tools/attn_bench.py";;
     stem) CMD="python3 tools/stem_kbench.py 5";;
+    stemw) CMD="python3 tools/stem_wgrad_kbench.py 3";;
     cwgrad) CMD="python3 tools/wgrad_kb.py";;
     step) CMD="python3 bench.py --steps 2 --warmup 1 --quick --no-cpu-baseline --force-modality none";;
   esac
