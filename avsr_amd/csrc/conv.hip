@@ -720,7 +720,7 @@ __global__ __launch_bounds__(PCfg::NTH, 2) void conv_patch_kernel(ConvArgs a, Pa
 // dW[co][(kh, kw, ci)] = sum_p dy[p][co] * x[p + (kh-1, kw-1)][ci] for the 3x3 / stride 1 /
 // pad 1 convolutions of ResNet stages 1 (22 x 22 x 64) and 2 (11 x 11 x 128). The general
 // weight-grad re-gathers x for every tap (9 passes of the input through L2; at stage 1 its
-// 64 x 256 tiles are 1/4 padding). Here persistent blocks (one per CU) walk tiles of TR whole
+// 64 x 256 tiles are 1/4 padding). Here persistent blocks (WP_BLOCKS, below) walk tiles of TR whole
 // image rows; a block owns a 64 x 64 (co, ci) block of every tap. Per tile the block's dy
 // channels and the zero-padded (TR+2) x (W+2) patch of its x channels are DMA'd into LDS once,
 // double buffered, and all 9 taps read the patch at row offsets. Every tile has the same
@@ -756,7 +756,15 @@ struct WPGeo {
 // none (what the LDS allows)
 using WPStage1 = WPGeo<22, 11, 2, 2, 144>;   // half images: 242 pixels, 13 x 24 patch, double buffered
 using WPStage2 = WPGeo<11, 11, 1, 3, 160>;   // whole images: 121 pixels, 13 x 13 patch, 3 buffers (short tiles)
-constexpr int WP_BLOCKS = 256, WP_COLS = 576;
+// Persistent blocks of the stage-1 / stage-2 weight-grads: 128, one on every other CU. These run
+// on the side stream beside the ResNet backward's data-gradient chain, and a block holds up to
+// 152 KB of LDS, so at one block per CU (256) every chain kernel needing LDS waited for free CUs;
+// 128 blocks take longer on the side but the step is shorter (6 of 6 interleaved pairs, +0.3-0.5 %
+// value_expected; 64: slower; profiles/r05_wpatch_blocks_ab.txt). A/B builds may override.
+#ifndef AVSR_WP_BLOCKS
+#define AVSR_WP_BLOCKS 128
+#endif
+constexpr int WP_BLOCKS = AVSR_WP_BLOCKS, WP_COLS = 576;
 
 AVSR_DEV int whswz(int row) { return ((row >> 1) & 3) << 1; }
 AVSR_DEV bf16x8 trpair(const char* pa, const char* pb) {
@@ -998,6 +1006,7 @@ constexpr int SWP_PR = 2 * SWP_TR + 5, SWP_PC = 103, SWP_SLOTS = SWP_PR * SWP_PC
 constexpr int SWP_PPIECE = (SWP_SLOTS + 255) / 256, SWP_PBYTES = SWP_PPIECE * 4096;
 constexpr int SWP_BUF = SWP_DYB + SWP_PBYTES, SWP_NBUF = 3, SWP_LDS = SWP_NBUF * SWP_BUF;
 constexpr int SWP_NP = SWP_DYPIECE + SWP_PPIECE, SWP_COLS = 392, SWP_PAIRS = 25;
+constexpr int SWP_BLOCKS = 256;                  // persistent blocks, one per CU
 constexpr int SWP_JW = (SWP_PAIRS + 3) / 4;     // pairs per wave (7; pairs >= 25 are discarded)
 static_assert(SWP_LDS <= 160 * 1024 && SWP_DYB % 4096 == 0 && SWP_KS % 2 == 0, "stem weight-grad tile buffers");
 static_assert(2 * (SWP_TC - 1) + 6 - 3 < SWP_PC - 3 + 1 && SWP_NP % SWP_KS == 0, "patch width / DMA spread");
@@ -1142,16 +1151,16 @@ static int stem_wpatch_launch(const avsr_conv_params* p, hipStream_t st) {
     attr = true;
   }
   const uint32_t xb = (uint32_t)((int64_t)p->nimg * 88 * 88 * 16), dyb = (uint32_t)((int64_t)p->nimg * 1936 * 128);
-  hipLaunchKernelGGL(stem_wgrad_patch_kernel, dim3(WP_BLOCKS), dim3(256), SWP_LDS, st, (const bf16*)p->x,
+  hipLaunchKernelGGL(stem_wgrad_patch_kernel, dim3(SWP_BLOCKS), dim3(256), SWP_LDS, st, (const bf16*)p->x,
                      (const bf16*)p->dy, xb, dyb, p->nimg, p->ws);
   AVSR_CHECK_LAUNCH();
   const int64_t mn = 64 * SWP_COLS;
   const int xg = avsr_grid(mn / 4, 256, 1024);
   const int chunks = 8;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)xg, 1u, (unsigned)chunks), dim3(256), 0, st, p->ws, WP_BLOCKS,
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)xg, 1u, (unsigned)chunks), dim3(256), 0, st, p->ws, SWP_BLOCKS,
                      chunks, mn, p->dw, (int64_t)0);
   AVSR_CHECK_LAUNCH();
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)xg, 1u, 1u), dim3(256), 0, st, p->ws, WP_BLOCKS, -chunks, mn,
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)xg, 1u, 1u), dim3(256), 0, st, p->ws, SWP_BLOCKS, -chunks, mn,
                      p->dw, (int64_t)0);
   AVSR_CHECK_LAUNCH();
   return 0;
@@ -1364,7 +1373,7 @@ extern "C" int avsr_conv_bwd_weight(const avsr_conv_params* p, void* stream) {
 extern "C" int64_t avsr_conv_wgrad_ws(const avsr_conv_params* p) {
   if (!p || (p->dtype != AVSR_BF16 && p->dtype != AVSR_F32)) return 0;
   if (wpatch_ok(p)) return (int64_t)WP_BLOCKS * 64 * WP_COLS;
-  if (stem_wpatch_ok(p)) return (int64_t)WP_BLOCKS * 64 * SWP_COLS;
+  if (stem_wpatch_ok(p)) return (int64_t)SWP_BLOCKS * 64 * SWP_COLS;
   const WgradPlan w = wgrad_plan(p, p->dtype == AVSR_BF16 && conv_glds_enabled(), true);
   if (!w.slab) return 0;
   return (int64_t)p->groups * w.splits * p->cout * ((int64_t)p->kh * p->kw * p->cin);
