@@ -121,6 +121,7 @@ class FusedAdamW:
             for ps, pe, step in self._pieces(s, e):
                 if step is not None:
                     launch(ps, pe, wd, step)
+        self._early = False          # the early partial belongs to this step's gradients only
         if zero_grad:
             a.zero_grad()
         return lr
@@ -217,9 +218,12 @@ class ArenaAdamW(torch.optim.Optimizer):
         self._clip = 0.0
         st = self.state[self.arena.data]
         st["step"] = torch.tensor(float(f.step_count))
+        if f.layer_steps is not None:        # LayerDrop: each encoder layer's own AdamW step count
+            st["layer_steps"] = torch.tensor(f.layer_steps, dtype=torch.float32)
         return loss
 
     def zero_grad(self, set_to_none=True):
+        self.fused._early = False
         self.arena.zero_grad()
 
     def load_state_dict(self, state_dict):
@@ -230,3 +234,9 @@ class ArenaAdamW(torch.optim.Optimizer):
         a.exp_avg_sq.copy_(st["exp_avg_sq"])
         self.fused.step_count = int(float(st["step"]))
         self.state[a.data] = {"step": st["step"], "exp_avg": a.exp_avg, "exp_avg_sq": a.exp_avg_sq}
+        if "layer_steps" in st:             # torch casts saved state tensors to the parameter dtype
+            ls = st["layer_steps"]
+            self.fused.layer_steps = [int(round(float(v))) for v in ls.flatten().tolist()]
+            self.state[a.data]["layer_steps"] = ls.detach().cpu().float()
+        else:
+            self.fused.layer_steps = None

@@ -3,12 +3,14 @@
 0): modality_fuse='add' (avhubert.py:225-233,486-489), transformer_length_normalized_loss
 (label_smoothing_loss.py:61) and layerdrop (avhubert.py:709-712, with the optimizer skipping a
 dropped layer's parameters as torch.optim.AdamW skips parameters whose grad is None)."""
+import io
+
 import pytest
 import torch
 
 from avsr_amd.avhubert_avsr_model import AVHubertAVSR
 from avsr_amd.configuration_avhubert_avsr import AVHubertAVSRConfig
-from avsr_amd.optim import FusedAdamW
+from avsr_amd.optim import ArenaAdamW, FusedAdamW
 from oracle import avsr_oracle as O
 from oracle.weights import NO_DROPOUT, TINY_CONFIG
 from tests.oracle_util import (CFGVAR, LDROP_SEED, cfgvar_oracle_cfg, cfgvar_state, golden_batch, load_cfgvar,
@@ -69,16 +71,40 @@ def test_train_step(gv, batch, name):
         assert not any(".layers.1." in k for k in keys)
 
 
-def test_layerdrop_optimizer_skips_dropped_layers(gv, batch):
+def _arena_opt(eng):
+    return ArenaAdamW(eng.arena, lr=1e-3, eps=1e-3, weight_decay=0.05)
+
+
+def _resume(opt, eng):
+    """the HF Trainer checkpoint path: the optimizer state dict through torch.save /
+    torch.load(weights_only=True), loaded into a fresh ArenaAdamW whose moments were cleared"""
+    buf = io.BytesIO()
+    torch.save(opt.state_dict(), buf)
+    buf.seek(0)
+    sd = torch.load(buf, weights_only=True)
+    eng.arena.exp_avg.zero_()
+    eng.arena.exp_avg_sq.zero_()
+    new = _arena_opt(eng)
+    new.load_state_dict(sd)
+    return new
+
+
+@pytest.mark.parametrize("kind", ["fused", "arena_resume"])
+def test_layerdrop_optimizer_skips_dropped_layers(gv, batch, kind):
     """two AdamW steps with LayerDrop: step 1 drops layer 1 (draws 0.758 / 0.279), step 2 drops
     layer 0 (seed 0: 0.496 / 0.768). torch.optim.AdamW on the oracle with zero_grad(set_to_none)
     skips the dropped layer's parameters (grad None): no decay, no moment update, and its own
-    step count for the bias correction. The arena optimizer must land on the same parameters."""
+    step count for the bias correction. The arena optimizer must land on the same parameters —
+    also (kind arena_resume) when the Trainer's ArenaAdamW is checkpointed after step 1 and a
+    fresh one resumes from that checkpoint: the per-layer step counts travel in its state dict."""
     m = _model(gv, "ldrop").train()
     eng = m.avsr.engine()
     # eps 1e-3: Adam's normalisation would turn round-off-level gradient differences (signs of
     # near-zero elements) into +-lr updates; with this eps an update follows its gradient
-    opt = FusedAdamW(eng.arena, lr=1e-3, eps=1e-3, weight_decay=0.05, max_grad_norm=0.0)
+    if kind == "fused":
+        opt = FusedAdamW(eng.arena, lr=1e-3, eps=1e-3, weight_decay=0.05, max_grad_norm=0.0)
+    else:
+        opt = _arena_opt(eng)
     sd = O.to_torch_state(cfgvar_state(gv, "ldrop"), requires_grad=True)
     ocfg = cfgvar_oracle_cfg("ldrop")
     names = [k for k, _ in m.named_parameters()]
@@ -107,6 +133,9 @@ def test_layerdrop_optimizer_skips_dropped_layers(gv, batch):
         if seed == LDROP_SEED:       # layer 1 dropped: untouched, not even decayed
             for k, v in l1.items():
                 assert torch.equal(dict(m.named_parameters())[k].detach(), v), k
+            if kind == "arena_resume":
+                opt = _resume(opt, eng)
+                assert opt.fused.layer_steps == [1, 0]
     params = dict(m.named_parameters())
     for k in names:
         if zero_grad_by_symmetry(k):     # round-off gradients: Adam normalises their noise to +-lr
@@ -116,7 +145,7 @@ def test_layerdrop_optimizer_skips_dropped_layers(gv, batch):
         # ResNet: parity-mode gradients there differ by up to ~5e-3 (train-mode BatchNorm backward,
         # as in test_gpu_surface.py), which an Adam step passes on element by element
         assert d < (1e-2 if ".resnet." in k else 2e-3), (k, d)
-    assert opt.layer_steps == [1, 1]
+    assert (opt.layer_steps if kind == "fused" else opt.fused.layer_steps) == [1, 1]
 
 
 def test_early_gradient_norm_matches_full(gv, batch):

@@ -160,7 +160,8 @@ def test_encode_then_decode_end_to_end(g, trained_model, b):
 @pytest.mark.parametrize("beam", [1, 3, 5])
 def test_batched_decode_equals_per_utterance(g, model, beam):
     """decode_batch over utterances of different lengths returns, per utterance, exactly the
-    hypotheses of the one-utterance search (tokens and scores)."""
+    hypotheses of the one-utterance search: tokens identical, total and per-scorer scores equal
+    as floats (bit for bit, no rounding)."""
     bs = get_beam_search_decoder(model.avsr, TOKENS, ctc_weight=0.1, beam_size=beam)
     xs = [torch.from_numpy(g["dec_enc_0"]).cuda(), torch.from_numpy(g["dec_enc_1"]).cuda(),
           torch.from_numpy(g["dec_enc_0"][:11]).cuda(), torch.from_numpy(g["dec_enc_1"][3:17]).cuda()]
@@ -168,7 +169,10 @@ def test_batched_decode_equals_per_utterance(g, model, beam):
     for x, hyps in zip(xs, got):
         want = bs(x)
         assert [h.asdict()["yseq"] for h in hyps] == [h.asdict()["yseq"] for h in want]
-        assert [round(float(h.score), 4) for h in hyps] == [round(float(h.score), 4) for h in want]
+        assert [float(h.score) for h in hyps] == [float(h.score) for h in want]
+        for hb, hw in zip(hyps, want):
+            sb, sw = hb.asdict()["scores"], hw.asdict()["scores"]
+            assert sorted(sb) == sorted(sw) and all(float(sb[k]) == float(sw[k]) for k in sw), (sb, sw)
     if beam in (1, 3):                       # and the reference's own best hypothesis
         assert got[0][0].asdict()["yseq"] == g[f"yseq_b{beam}_0"].tolist()
 

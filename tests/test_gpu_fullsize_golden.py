@@ -234,7 +234,7 @@ def test_early_ending_beam_search(g, model, state, off, beam):
     before maxlen (end_detect, e2e_asr_common.py:18-48) and return hypotheses that ended at
     different lengths (beam_search.py:330-406). The engine's one-utterance search AND the
     batched search return the same ended list: token sequences identical, total / decoder /
-    CTC scores within 1e-4 (fp32)."""
+    CTC scores within 1e-4 (fp32) of the reference, and batched == one-utterance bit for bit."""
     from tests.golden.full_inputs import ENDBEAM
     from tests.oracle_util import endbeam_case, endbeam_state, load_golden_endbeam
     ge = load_golden_endbeam()
@@ -246,7 +246,12 @@ def test_early_ending_beam_search(g, model, state, off, beam):
     worst = 0.0
     for c, x, hb in zip(ENDBEAM["clips"], xs, batched):
         ref = endbeam_case(ge, off, beam, c)
-        for hyps in (bs(x), hb):
+        single = bs(x)
+        for h1, h2 in zip((h.asdict() for h in single), (h.asdict() for h in hb)):
+            assert h1["yseq"] == h2["yseq"] and float(h1["score"]) == float(h2["score"]), c
+            assert all(float(h1["scores"][k]) == float(h2["scores"][k]) for k in h1["scores"]), c
+        assert len(single) == len(hb)
+        for hyps in (single, hb):
             got = [h.asdict() for h in hyps]
             assert [h["yseq"] for h in got] == [r[0] for r in ref], (c, [len(h["yseq"]) for h in got])
             for h, r in zip(got, ref):
