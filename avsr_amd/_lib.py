@@ -116,7 +116,7 @@ class AttnParams(ctypes.Structure):
         ("drop_p", _f), ("seed", ctypes.c_uint64),
         ("dout", _c_p), ("lddo", _i64), ("delta", _c_p), ("dq", _c_p), ("lddq", _i64),
         ("dk", _c_p), ("lddk", _i64), ("dv", _c_p), ("lddv", _i64), ("dq_out", _c_p), ("lddq_out", _i64),
-        ("db", _c_p), ("db_ws", _c_p),
+        ("db", _c_p), ("db_ws", _c_p), ("drop_mask", _c_p),
     ]
 
 
@@ -272,6 +272,7 @@ SYMBOLS = {
     "avsr_debug_attn_stamps": ([_c_p], _i),
     "avsr_attn_bwd_prep": ([ctypes.POINTER(AttnParams), _c_p], _i),
     "avsr_attn_bwd": ([ctypes.POINTER(AttnParams), _c_p], _i),
+    "avsr_attn_dropmask": ([ctypes.POINTER(AttnParams), _c_p], _i),
     "avsr_row_lse": ([ctypes.POINTER(XentParams), _c_p], _i),
     "avsr_lsm_fwd": ([ctypes.POINTER(XentParams), _c_p], _i),
     "avsr_lsm_bwd": ([ctypes.POINTER(XentParams), _c_p], _i),
@@ -332,6 +333,8 @@ def load():
         raise AvsrLibError(f"{LIB_PATH} not built: run `python -c 'import __graft_entry__ as g; g.build()'`")
     lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
     for name, (argtypes, restype) in SYMBOLS.items():
+        if os.environ.get("AVSR_LIB_PATH_AB") and not hasattr(lib, name):
+            continue                # an older A/B build: entry points it predates stay unbound
         fn = getattr(lib, name)
         fn.argtypes = argtypes
         fn.restype = restype

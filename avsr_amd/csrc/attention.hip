@@ -117,7 +117,8 @@ struct AttnArgs {
   void* o; int64_t ldo; float* lse; const int* klen; int causal; float drop_p; uint64_t seed;
   const void* dout; int64_t lddo; float* delta; float* dq; int64_t lddq;
   void* dk; int64_t lddk; void* dv; int64_t lddv;
-  float* db_ws;                 // per-utterance q/k/v bias-gradient partials [B][3][H][64] or null
+  const uint64_t* mq;           // dropout keep masks (avsr_attn_dropmask, query on the lane) or null
+  int mnqb, mnkb;               // their 32-row query blocks / (even) 32-row key blocks per head
 };
 
 template <typename T> struct L {
@@ -148,15 +149,6 @@ AVSR_DEV void store_t(const f32x16& x0, const f32x16& x1, float mul, float* st, 
       stv(out + (int64_t)i * ld + cb + e, v);
     }
   }
-}
-
-// column sums of the wave's 32 x 64 slab (rows < nvalid) as store_t stored them (rounded to
-// T); lane l returns column l. Read after store_t by the same wave (LDS order), no barrier
-template <typename T> AVSR_DEV float slab_colsum(const float* st, int nvalid) {
-  const int l = threadIdx.x & 63, n = nvalid < 32 ? nvalid : 32;
-  float s = 0.f;
-  for (int i = 0; i < n; ++i) s += (float)from_f<T>(st[i * 65 + l]);
-  return s;
 }
 
 template <typename T>
@@ -839,6 +831,17 @@ AVSR_DEV void drop_tile_sel(f32x16& x, uint32_t tG, const AttnDrop& d, int hh) {
   }
 }
 
+// stored dropout masks (avsr_attn_dropmask): 16 lane masks per 32 x 32 tile, read through the
+// constant address space so that a wave-uniform tile address becomes scalar loads
+typedef const __attribute__((address_space(4))) uint64_t* smask_t;
+AVSR_DEV smask_t mask_tile(const uint64_t* base, int64_t tile) { return (smask_t)(base + tile * 16); }
+// x on the lanes whose bit of m is set, else 0: one v_cndmask with the scalar mask as condition
+AVSR_DEV float msel(float x, uint64_t m) {
+  float r;
+  asm("v_cndmask_b32_e64 %0, 0, %1, %2" : "=v"(r) : "v"(x), "s"(m));
+  return r;
+}
+
 __global__ __launch_bounds__(768) void attn_fwd_kernel(AttnArgs a) {
   extern __shared__ __attribute__((aligned(16))) bf16 sm[];
   stamp(0);
@@ -978,11 +981,13 @@ __global__ __launch_bounds__(768) void attn_fwd_kernel(AttnArgs a) {
   stamp(3);
 }
 
-template <int NT>
-__global__ __launch_bounds__(NT) void attn_bwd_dkdv_kernel(AttnArgs a) {
+// dK / dV (decoder shapes: causal self-attention, source attention), one workgroup per (b, h)
+// and up to 12 waves of 32 keys; dropout hashed per key pair
+__global__ __launch_bounds__(768) void attn_bwd_dkdv_kernel(AttnArgs a) {
   extern __shared__ __attribute__((aligned(16))) bf16 sm[];
   const int bh = blockIdx.x, b = bh / a.H, h = bh % a.H;
-  const int tid = threadIdx.x, nthr = blockDim.x, w = tid >> 6, l = tid & 63, c = l & 31, hh = l >> 5;
+  const int tid = threadIdx.x, nthr = blockDim.x, l = tid & 63, c = l & 31, hh = l >> 5;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int nq = (a.Lq + 31) & ~31;
   bf16* Qs = sm;
   bf16* dOs = sm + nq * ROW;
@@ -1042,11 +1047,16 @@ __global__ __launch_bounds__(NT) void attn_bwd_dkdv_kernel(AttnArgs a) {
   }
   const int klen = a.klen ? min(a.klen[b], a.Lk) : a.Lk;
   const float sl2 = a.scale * LOG2E;
-  const AttnDrop drop(a.drop_p, a.seed, a.B, a.H, a.Lq, a.Lk);
-  const uint32_t nG = drop.npair * GOLD;
-  const uint32_t keyG = ((uint32_t)bh * (uint32_t)a.Lq * drop.npair + (uint32_t)(min(key, a.Lk - 1) >> 1)) * GOLD;
+  const bool drop_on = a.drop_p > 0.f;
+  uint32_t thr = 0, pre = 0, nG = 0, keyG = 0;
+  float dscale = 1.f;
+  if (drop_on) {
+    const AttnDrop drop(a.drop_p, a.seed, a.B, a.H, a.Lq, a.Lk);
+    dscale = drop.scale;
+    thr = drop.thr; pre = drop.pre; nG = drop.npair * GOLD;
+    keyG = ((uint32_t)bh * (uint32_t)a.Lq * drop.npair + (uint32_t)(min(key, a.Lk - 1) >> 1)) * GOLD;
+  }
   const bool odd = c & 1;
-  const float dscale = a.drop_p > 0.f ? drop.scale : 1.f;
   __syncthreads();
   f32x16 dv0, dv1, dk0, dk1;
   zacc(dv0); zacc(dv1); zacc(dk0); zacc(dk1);
@@ -1069,28 +1079,30 @@ __global__ __launch_bounds__(NT) void attn_bwd_dkdv_kernel(AttnArgs a) {
       for (int i = 0; i < 4; ++i) {                 // registers 4i..4i+3 = queries qt0 + 8i + 4hh + 0..3
         const f32x4 ls = *(const f32x4*)&lss[qt0 + 8 * i + 4 * hh];
         const f32x4 ds = *(const f32x4*)&dls[qt0 + 8 * i + 4 * hh];
-        // dropout: this lane pair (keys 2j, 2j+1) splits the 4 queries' hashes: even lanes
-        // hash queries 0, 1, odd lanes 2, 3, then the two swap (static registers only)
-        // keep bits; P' = dropout(P) is stored unscaled (the 1/(1-p) factor goes on dV at the
-        // store), dP' = dropout(dP) scaled; the softmax scale of dS goes on dK at the store
-        bool kb[4] = {true, true, true, true};
-        if (a.drop_p > 0.f) {
+        // P' = dropout(P) is stored unscaled (the 1/(1-p) factor goes on dV at the store),
+        // dP' = dropout(dP) scaled; the softmax scale of dS goes on dK at the store
+        {
+          // hashed dropout: this lane pair (keys 2j, 2j+1) splits the 4 queries' hashes: even
+          // lanes hash queries 0, 1, odd lanes 2, 3, then the two swap (static registers only)
+          bool kb[4] = {true, true, true, true};
+          if (drop_on) {
 #pragma unroll
-          for (int u = 0; u < 2; ++u) {
-            const uint32_t mine = hashG(tG + (uint32_t)(8 * i + (odd ? 2 : 0) + u) * nG, drop.pre);
-            const uint32_t other = __shfl_xor(mine, 1, 64);
-            const uint32_t h0 = odd ? other : mine, h1 = odd ? mine : other;
-            kb[u] = (odd ? (h0 >> 16) : (h0 & 0xFFFFu)) >= drop.thr;
-            kb[u + 2] = (odd ? (h1 >> 16) : (h1 & 0xFFFFu)) >= drop.thr;
+            for (int u = 0; u < 2; ++u) {
+              const uint32_t mine = hashG(tG + (uint32_t)(8 * i + (odd ? 2 : 0) + u) * nG, pre);
+              const uint32_t other = __shfl_xor(mine, 1, 64);
+              const uint32_t h0 = odd ? other : mine, h1 = odd ? mine : other;
+              kb[u] = (odd ? (h0 >> 16) : (h0 & 0xFFFFu)) >= thr;
+              kb[u + 2] = (odd ? (h1 >> 16) : (h1 & 0xFFFFu)) >= thr;
+            }
           }
-        }
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int r = 4 * i + e, ql = qt0 + 8 * i + 4 * hh + e;
-          const bool ok = full || (kok & (ql < a.Lq) & (!a.causal | (key <= ql)));
-          const float p = ok ? fexp2(fmaf(sc[r], sl2, -ls[e])) : 0.f;
-          sc[r] = kb[e] ? p : 0.f;
-          dp[r] = p * ((kb[e] ? dp[r] * dscale : 0.f) - ds[e]);
+          for (int e = 0; e < 4; ++e) {
+            const int r = 4 * i + e, ql = qt0 + 8 * i + 4 * hh + e;
+            const bool ok = full || (kok & (ql < a.Lq) & (!a.causal | (key <= ql)));
+            const float p = ok ? fexp2(fmaf(sc[r], sl2, -ls[e])) : 0.f;
+            sc[r] = kb[e] ? p : 0.f;
+            dp[r] = p * fmaf(kb[e] ? dp[r] : 0.f, dscale, -ds[e]);
+          }
         }
       }
       const bf16x8 pa = accb(sc, 0), pb = accb(sc, 1), sa = accb(dp, 0), sb = accb(dp, 1);
@@ -1105,37 +1117,22 @@ __global__ __launch_bounds__(NT) void attn_bwd_dkdv_kernel(AttnArgs a) {
     }
   }
   __syncthreads();
-  // fused k / v bias gradients: each wave's column sums of what it stores, then wave 0 adds the
-  // waves' partials in wave order (the launch has one workgroup per (b, h) and every wave holds
-  // keys < Lk, so every wave reaches every barrier)
-  float* part = (float*)sm + (nthr >> 6) * 32 * 65;
   if (kb0 < a.Lk) {
     float* scr = (float*)sm + w * 32 * 65;
     bf16* DK = (bf16*)a.dk + ((int64_t)b * a.Lk + kb0) * a.lddk + h * DH;
     store_t<bf16>(dk0, dk1, a.scale, scr, DK, a.lddk, a.Lk - kb0);
-    if (a.db_ws) part[w * 128 + l] = slab_colsum<bf16>(scr, a.Lk - kb0);
     bf16* DV = (bf16*)a.dv + ((int64_t)b * a.Lk + kb0) * a.lddv + h * DH;
     store_t<bf16>(dv0, dv1, dscale, scr, DV, a.lddv, a.Lk - kb0);
-    if (a.db_ws) part[w * 128 + 64 + l] = slab_colsum<bf16>(scr, a.Lk - kb0);
-  }
-  if (a.db_ws) {
-    __syncthreads();
-    if (w == 0) {
-      const int nw = min(nthr >> 6, (a.Lk + 31) >> 5);
-      float sk = 0.f, sv = 0.f;
-      for (int i = 0; i < nw; ++i) { sk += part[i * 128 + l]; sv += part[i * 128 + 64 + l]; }
-      float* o = a.db_ws + (int64_t)b * 3 * a.H * DH + h * DH + l;
-      o[a.H * DH] = sk;
-      o[2 * a.H * DH] = sv;
-    }
   }
 }
 
+// dQ (decoder shapes), one workgroup per (b, h) and up to 12 waves of 32 queries
 template <typename OutT>
 __global__ __launch_bounds__(768) void attn_bwd_dq_kernel(AttnArgs a, OutT* dq, int64_t lddq) {
   extern __shared__ __attribute__((aligned(16))) bf16 sm[];
   const int bh = blockIdx.x, b = bh / a.H, h = bh % a.H;
-  const int tid = threadIdx.x, nthr = blockDim.x, w = tid >> 6, l = tid & 63, c = l & 31, hh = l >> 5;
+  const int tid = threadIdx.x, nthr = blockDim.x, l = tid & 63, c = l & 31, hh = l >> 5;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int nk = (a.Lk + 31) & ~31;
   bf16* Ks = sm;
   bf16* Vs = sm + nk * ROW;
@@ -1204,21 +1201,42 @@ __global__ __launch_bounds__(768) void attn_bwd_dq_kernel(AttnArgs a, OutT* dq, 
     }
   }
   __syncthreads();
-  float* part = (float*)sm + (nthr >> 6) * 32 * 65;
   if (q0 < a.Lq) {
     OutT* DQ = dq + ((int64_t)b * a.Lq + q0) * lddq + h * DH;
     store_t<OutT>(dq0, dq1, a.scale, (float*)sm + w * 32 * 65, DQ, lddq, a.Lq - q0);
-    if (a.db_ws) part[w * 64 + l] = slab_colsum<OutT>((float*)sm + w * 32 * 65, a.Lq - q0);
   }
-  if (a.db_ws) {                  // fused q bias gradient (as in the dK/dV kernel)
-    __syncthreads();
-    if (w == 0) {
-      const int nw = min(nthr >> 6, (a.Lq + 31) >> 5);
-      float sq = 0.f;
-      for (int i = 0; i < nw; ++i) sq += part[i * 64 + l];
-      a.db_ws[(int64_t)b * 3 * a.H * DH + h * DH + l] = sq;
+}
+
+// the keep masks of avsr_attn_dropmask: one wave per 32 x 32 tile (bh, qb, kb) writes the
+// tile's 16 lane masks, query on the lane (AttnDrop's bits, 0 past Lq / Lk). Register pair
+// (r, r + 1) of a lane holds keys 2j, 2j + 1: one hash per pair, 32-bit index arithmetic.
+__global__ __launch_bounds__(256) void attn_mask_kernel(AttnArgs a, uint64_t* mq, int ntiles) {
+  const int l = threadIdx.x & 63, c = l & 31, hh = l >> 5;
+  const int tile = __builtin_amdgcn_readfirstlane((int)blockIdx.x * 4 + (int)(threadIdx.x >> 6));
+  if (tile >= ntiles) return;                          // wave-uniform
+  const int kb = tile % a.mnkb, r1 = tile / a.mnkb, qb = r1 % a.mnqb, bh = r1 / a.mnqb;
+  const AttnDrop d(a.drop_p, a.seed, a.B, a.H, a.Lq, a.Lk);
+  const int q = qb * 32 + c;
+  // pair index of register pair (r, r + 1): row (bh, q), pair kb * 16 + ((r & 3) >> 1) + 4 (r >> 2) + 2 hh
+  const uint32_t gG = (((uint32_t)bh * (uint32_t)a.Lq + (uint32_t)min(q, a.Lq - 1)) * d.npair + (uint32_t)(kb * 16 + 2 * hh)) * GOLD;
+  const bool interior = qb * 32 + 32 <= a.Lq && kb * 32 + 32 <= a.Lk;
+  uint32_t wlo = 0, whi = 0;                           // lane r < 16: lane mask r
+#pragma unroll
+  for (int r = 0; r < 16; r += 2) {
+    const uint32_t hv = hashG(gG + (uint32_t)(((r & 3) >> 1) + 4 * (r >> 2)) * GOLD, d.pre);
+    bool k0 = (hv & 0xFFFFu) >= d.thr, k1 = (hv >> 16) >= d.thr;
+    if (!interior) {
+      const int k = kb * 32 + qrow(r, hh);
+      k0 = k0 & (q < a.Lq) & (k < a.Lk);
+      k1 = k1 & (q < a.Lq) & (k + 1 < a.Lk);
     }
+    const uint64_t b0 = __ballot(k0), b1 = __ballot(k1);
+    wlo = l == r ? (uint32_t)b0 : wlo;
+    whi = l == r ? (uint32_t)(b0 >> 32) : whi;
+    wlo = l == r + 1 ? (uint32_t)b1 : wlo;
+    whi = l == r + 1 ? (uint32_t)(b1 >> 32) : whi;
   }
+  if (l < 16) mq[(int64_t)tile * 16 + l] = ((uint64_t)whi << 32) | wlo;
 }
 
 // launch geometry: waves per workgroup (<= 12) covering `rows` 32-row blocks, grid.y chunks
@@ -1365,6 +1383,7 @@ AVSR_DEV int next_stage(int s) { return s + 1 == NS ? 0 : s + 1; }
 AVSR_DEV int prev_stage(int s) { return s == 0 ? NS - 1 : s - 1; }
 
 // ----------------------------------------------------------------------------- forward
+template <bool MASK>
 __global__ __launch_bounds__(256, 3) void attn_fwd_kernel(AttnArgs a, int nqb) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int id = xcd_id(blockIdx.x, gridDim.x);
@@ -1391,7 +1410,8 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_kernel(AttnArgs a, int nqb) {
   fo.init(l);
   const float sl2 = a.scale * LOG2E;
   const AttnDrop drop(a.drop_p, a.seed, a.B, a.H, a.Lq, a.Lk);
-  const uint32_t rowG = ((uint32_t)bh * (uint32_t)a.Lq + (uint32_t)min(qi, a.Lq - 1)) * drop.npair * GOLD;
+  const uint32_t rowG = MASK ? 0u : ((uint32_t)bh * (uint32_t)a.Lq + (uint32_t)min(qi, a.Lq - 1)) * drop.npair * GOLD;
+  const int64_t mrow = MASK ? ((int64_t)bh * a.mnqb + (q0 >> 5)) * a.mnkb : 0;
   f32x16 o0, o1;
   zacc(o0); zacc(o1);
   float lsum = 0.f, mb = -INFINITY;          // lazy reference max, as res::attn_fwd_kernel
@@ -1401,6 +1421,12 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_kernel(AttnArgs a, int nqb) {
     if (t + 2 < nt) ring.issue(smem + prev_stage(cs) * STAGEB, t + 2, w, l);
     const char* Ks = smem + cs * STAGEB;
     const char* Vs = Ks + IMGB;
+    uint64_t mw[32];
+    if (MASK && a.drop_p > 0.f) {
+      const smask_t mt = mask_tile(a.mq, mrow + 2 * t);
+#pragma unroll
+      for (int r = 0; r < 32; ++r) mw[r] = mt[r];
+    }
     f32x16 s0, s1;
     zacc(s0); zacc(s1);
 #pragma unroll
@@ -1447,8 +1473,16 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_kernel(AttnArgs a, int nqb) {
       for (int r = 0; r < w2; ++r) ts[r] += ts[r + w2];
     lsum += ts[0];
     if (a.drop_p > 0.f) {
-      drop_tile_sel(s0, rowG + (uint32_t)(k0 >> 1) * GOLD, drop, hh);
-      drop_tile_sel(s1, rowG + (uint32_t)((k0 + 32) >> 1) * GOLD, drop, hh);
+      if (MASK) {                            // the stored keep masks of key blocks 2t, 2t + 1
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          s0[r] = msel(s0[r], mw[r]);
+          s1[r] = msel(s1[r], mw[16 + r]);
+        }
+      } else {
+        drop_tile_sel(s0, rowG + (uint32_t)(k0 >> 1) * GOLD, drop, hh);
+        drop_tile_sel(s1, rowG + (uint32_t)((k0 + 32) >> 1) * GOLD, drop, hh);
+      }
     }
     const bf16x8 p0a = accb(s0, 0), p0b = accb(s0, 1), p1a = accb(s1, 0), p1b = accb(s1, 1);
     o0 = mfma32(ldT(Vs, 0, fo, 0), p0a, o0);
@@ -1469,24 +1503,51 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_kernel(AttnArgs a, int nqb) {
   store_t<bf16>(o0, o1, inv, (float*)smem + w * 32 * 65, O, a.ldo, a.Lq - q0);
 }
 
-// ----------------------------------------------------------------------------- dQ (+ delta)
-// per wave 32 queries on the lanes (Q, dO rows in registers; delta = rowsum(dO * O) computed
-// from this lane's O / dO halves and published for the dK / dV kernel, which runs after);
-// 64-key tiles of K, V: S^T = K Q^T, dP^T = V dO^T, dQ^T += K^T dS^T
-template <typename OutT>
-__global__ __launch_bounds__(256, 3) void attn_bwd_dq_kernel(AttnArgs a, int nqb, OutT* dq, int64_t lddq) {
+}  // namespace sq
+
+// =====================================================================================
+// Encoder backward (bf16, non-causal, 128 <= Lq, Lk <= 384): one 12-wave workgroup per (b, h),
+// the streamed operands of the head DMA'd (buffer_load ... lds, no staging registers) into
+// unpadded XOR-swizzled [384][64] LDS images in four rounds of 96 rows that are all issued up
+// front; the waves start on the first 32-row tiles while the later rounds are in flight. Every
+// fragment address is a per-lane FragOff offset plus a tile base (swz(32t + x) = swz(x)).
+//   dQ kernel (runs first): K, V images; per wave 32 queries (Q, dO rows in registers), delta =
+//     rowsum(dO * O) from this lane's dO / O half-rows, published for the dK / dV kernel.
+//   dK / dV kernel: Q, dO images, lse and delta rows, and each wave's own 32-row K image
+//     (K fragments re-read per tile instead of held: the register file then holds dK, dV,
+//     V and the tile without spilling at 3 waves per SIMD).
+// DM: 0 no dropout, 1 hashed per element (AttnDrop), 2 stored keep masks (a.mq).
+namespace rb {
+using namespace sq;
+constexpr int NTH = 768;                 // 12 waves
+constexpr int IMG384 = MAXR * 128;       // one swizzled [384][64] bf16 image
+
+// wave w's 8-row piece `piece` of a [n][64] operand (row stride ld) into a swizzled image; rows
+// past n lie outside the buffer extent and land as zeros
+AVSR_DEV void dma_piece(const bf16* base, int64_t ld, int n, char* img, int piece, int l) {
+  const int row = 8 * piece + (l >> 3), ch = (l & 7) ^ swz(row);
+  dma16(rsrc(base, (uint32_t)(((n - 1) * ld + DH) * 2)), (uint32_t)((row * ld + ch * 8) * 2), img + piece * 1024);
+}
+AVSR_DEV void round_barrier() {                    // LDS writes done, no vmcnt drain
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+template <typename OutT, int DM>
+__global__ __launch_bounds__(NTH) void attn_bwd_dq_kernel(AttnArgs a, OutT* dq, int64_t lddq) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int id = xcd_id(blockIdx.x, gridDim.x);
-  const int bh = id / nqb, qb = id - bh * nqb, b = bh / a.H, h = bh % a.H;
-  const int tid = threadIdx.x, w = __builtin_amdgcn_readfirstlane(tid >> 6), l = tid & 63, c = l & 31, hh = l >> 5;
-  const int q0 = qb * 128 + w * 32, qi = q0 + c;
+  char* Ks = smem;
+  char* Vs = smem + IMG384;
+  const int bh = xcd_id(blockIdx.x, gridDim.x), b = bh / a.H, h = bh % a.H;
+  const int tid = threadIdx.x, l = tid & 63, c = l & 31, hh = l >> 5;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int q0 = w * 32, qi = q0 + c;
   const bool qok = qi < a.Lq;
-  Ring ring;
-  ring.init((const bf16*)a.k + (int64_t)b * a.Lk * a.ldk + h * DH, a.ldk,
-            (const bf16*)a.v + (int64_t)b * a.Lk * a.ldv + h * DH, a.ldv, a.Lk, nullptr, nullptr, w, l);
-  const int klen = a.klen ? min(a.klen[b], a.Lk) : a.Lk;
-  const int nt = (klen + KT - 1) / KT;
-  if (nt > 0) ring.issue(smem, 0, w, l);
+  const bf16* Kg = (const bf16*)a.k + (int64_t)b * a.Lk * a.ldk + h * DH;
+  const bf16* Vg = (const bf16*)a.v + (int64_t)b * a.Lk * a.ldv + h * DH;
+  dma_piece(Kg, a.ldk, a.Lk, Ks, w, l);                    // round 0
+  dma_piece(Vg, a.ldv, a.Lk, Vs, w, l);
   const bf16* Q = (const bf16*)a.q + (int64_t)b * a.Lq * a.ldq + h * DH;
   const bf16* dO = (const bf16*)a.dout + (int64_t)b * a.Lq * a.lddo + h * DH;
   const bf16* Og = (const bf16*)a.o + (int64_t)b * a.Lq * a.ldo + h * DH;
@@ -1499,10 +1560,10 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_dq_kernel(AttnArgs a, int nqb
   }
   const int64_t bhq = (int64_t)bh * a.Lq + min(qi, a.Lq - 1);
   const float lq0 = a.lse[bhq];
+  // the compiler's wait for these loads (vmcnt(0), covering round 0) happens here, once
 #pragma unroll
   for (int s = 0; s < 4; ++s) asm volatile("" ::"v"(qf[s]), "v"(of[s]), "v"(ov[s]));
   asm volatile("" ::"v"(lq0));
-  if (nt > 1) ring.issue(smem + STAGEB, 1, w, l);
   float dsum = 0.f;
 #pragma unroll
   for (int s = 0; s < 4; ++s)
@@ -1510,127 +1571,179 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_dq_kernel(AttnArgs a, int nqb
     for (int j = 0; j < 8; ++j) dsum = fmaf((float)of[s][j], (float)ov[s][j], dsum);
   dsum = xor32_sum(dsum);
   if (hh == 0 && qok) a.delta[bhq] = dsum;
+#pragma unroll
+  for (int r = 1; r < 4; ++r) {                           // rounds 1..3 in flight from here on
+    dma_piece(Kg, a.ldk, a.Lk, Ks, 12 * r + w, l);
+    dma_piece(Vg, a.ldv, a.Lk, Vs, 12 * r + w, l);
+  }
   const float lq = qok ? lq0 * LOG2E : 0.f;
   const float dl = qok ? dsum : 0.f;
-  FragOff fo;
-  fo.init(l);
+  const int klen = a.klen ? min(a.klen[b], a.Lk) : a.Lk;
+  const int nt = (klen + 31) >> 5;
   const float sl2 = a.scale * LOG2E;
   const AttnDrop drop(a.drop_p, a.seed, a.B, a.H, a.Lq, a.Lk);
-  const uint32_t rowG = ((uint32_t)bh * (uint32_t)a.Lq + (uint32_t)min(qi, a.Lq - 1)) * drop.npair * GOLD;
-  const float dscale = drop.scale;
+  const float dscale = DM ? drop.scale : 1.f;
+  const uint32_t rowG = DM == 1 ? ((uint32_t)bh * (uint32_t)a.Lq + (uint32_t)min(qi, a.Lq - 1)) * drop.npair * GOLD : 0u;
+  const int64_t mrow = DM == 2 ? ((int64_t)bh * a.mnqb + w) * a.mnkb : 0;
+  FragOff fo;
+  fo.init(l);
   f32x16 dq0, dq1;
   zacc(dq0); zacc(dq1);
-  int cs = 0;
-  for (int t = 0; t < nt; ++t) {
-    ring.arrive(t, nt, w);
-    if (t + 2 < nt) ring.issue(smem + prev_stage(cs) * STAGEB, t + 2, w, l);
-    const char* Ks = smem + cs * STAGEB;
-    const char* Vs = Ks + IMGB;
+  int t = 0;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int k0 = t * KT + 32 * j;
-      f32x16 st, dpt;
-      zacc(st); zacc(dpt);
+  for (int r = 0; r < 4; ++r) {
+    if (r == 1) vmwait<4>();
+    if (r == 2) vmwait<2>();
+    if (r == 3) vmwait<0>();
+    round_barrier();                                       // round r of every wave has landed
+    const int tend = min(nt, 3 * r + 3);
+    if (q0 < a.Lq) {
+      for (; t < tend; ++t) {
+        uint64_t mw[16];
+        if (DM == 2) {
+          const smask_t mt = mask_tile(a.mq, mrow + t);
 #pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        st = mfma32(ldA(Ks + 4096 * j, fo.row[s]), qf[s], st);
-        dpt = mfma32(ldA(Vs + 4096 * j, fo.row[s]), of[s], dpt);
-      }
-      if (a.drop_p > 0.f) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) dpt[r] *= dscale;
-        drop_tile_sel(dpt, rowG + (uint32_t)(k0 >> 1) * GOLD, drop, hh);
-      }
-      if (k0 + 32 <= klen) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) dpt[r] = fexp2(fmaf(st[r], sl2, -lq)) * (dpt[r] - dl);
-      } else {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const float p = k0 + qrow(r, hh) < klen ? fexp2(fmaf(st[r], sl2, -lq)) : 0.f;
-          dpt[r] = p * (dpt[r] - dl);
+          for (int e = 0; e < 16; ++e) mw[e] = mt[e];
         }
-      }
-      const bf16x8 sa = accb(dpt, 0), sb = accb(dpt, 1);
-      dq0 = mfma32(ldT(Ks, 32 * j, fo, 0), sa, dq0);
-      dq1 = mfma32(ldT(Ks, 32 * j, fo, 1), sa, dq1);
-      dq0 = mfma32(ldT(Ks, 32 * j + 16, fo, 0), sb, dq0);
-      dq1 = mfma32(ldT(Ks, 32 * j + 16, fo, 1), sb, dq1);
-    }
-    cs = next_stage(cs);
-  }
-  __syncthreads();
-  OutT* DQ = dq + ((int64_t)b * a.Lq + q0) * lddq + h * DH;
-  store_t<OutT>(dq0, dq1, a.scale, (float*)smem + w * 32 * 65, DQ, lddq, a.Lq - q0);
-}
-
-// ----------------------------------------------------------------------------- dK / dV
-// per wave 32 keys on the lanes (K, V rows in registers); 64-query tiles of Q, dO and their
-// lse / delta streamed; per 32-query block S = Q K^T, dP = dO V^T with the key on the lane,
-// dV^T += dO^T P', dK^T += Q^T dS (as res::attn_bwd_dkdv_kernel, delta from the dQ kernel)
-__global__ __launch_bounds__(256, 3) void attn_bwd_dkdv_kernel(AttnArgs a, int nkb) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int id = xcd_id(blockIdx.x, gridDim.x);
-  const int bh = id / nkb, kbk = id - bh * nkb, b = bh / a.H, h = bh % a.H;
-  const int tid = threadIdx.x, w = __builtin_amdgcn_readfirstlane(tid >> 6), l = tid & 63, c = l & 31, hh = l >> 5;
-  const int kb0 = kbk * 128 + w * 32, key = kb0 + c;
-  Ring ring;
-  ring.init((const bf16*)a.q + (int64_t)b * a.Lq * a.ldq + h * DH, a.ldq,
-            (const bf16*)a.dout + (int64_t)b * a.Lq * a.lddo + h * DH, a.lddo, a.Lq,
-            a.lse + (int64_t)bh * a.Lq, a.delta + (int64_t)bh * a.Lq, w, l);
-  const int nt = (a.Lq + KT - 1) / KT;
-  if (nt > 0) ring.issue(smem, 0, w, l);
-  const bf16* K = (const bf16*)a.k + (int64_t)b * a.Lk * a.ldk + h * DH;
-  const bf16* V = (const bf16*)a.v + (int64_t)b * a.Lk * a.ldv + h * DH;
-  bf16x8 kf[4], vf[4];
-#pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    kf[s] = ldrow_sel(K, a.ldk, key, a.Lk, s * 16 + 8 * hh);
-    vf[s] = ldrow_sel(V, a.ldv, key, a.Lk, s * 16 + 8 * hh);
-  }
-#pragma unroll
-  for (int s = 0; s < 4; ++s) asm volatile("" ::"v"(kf[s]), "v"(vf[s]));
-  if (nt > 1) ring.issue(smem + STAGEB_F, 1, w, l);
-  FragOff fo;
-  fo.init(l);
-  const int klen = a.klen ? min(a.klen[b], a.Lk) : a.Lk;
-  const bool active = kb0 < klen;            // wave-uniform: a wave past klen only keeps the ring going
-  const bool kok = key < klen;
-  const float sl2 = a.scale * LOG2E;
-  const AttnDrop drop(a.drop_p, a.seed, a.B, a.H, a.Lq, a.Lk);
-  const uint32_t nG = drop.npair * GOLD;
-  const uint32_t keyG = ((uint32_t)bh * (uint32_t)a.Lq * drop.npair + (uint32_t)(min(key, a.Lk - 1) >> 1)) * GOLD;
-  const bool odd = c & 1;
-  const float dscale = a.drop_p > 0.f ? drop.scale : 1.f;
-  f32x16 dv0, dv1, dk0, dk1;
-  zacc(dv0); zacc(dv1); zacc(dk0); zacc(dk1);
-  int cs = 0;
-  for (int t = 0; t < nt; ++t) {
-    ring.arrive(t, nt, w);
-    if (t + 2 < nt) ring.issue(smem + prev_stage(cs) * STAGEB_F, t + 2, w, l);
-    if (active) {
-      const char* Qs = smem + cs * STAGEB_F;
-      const char* dOs = Qs + IMGB;
-      const float* lsS = (const float*)(Qs + STAGEB);
-      const float* dlS = lsS + KT;
-#pragma nounroll
-      for (int j = 0; j < 2; ++j) {
-        const int qt0 = t * KT + 32 * j;
-        f32x16 sc, dp;
-        zacc(sc); zacc(dp);
+        const char* Kt = Ks + t * 4096;
+        const char* Vt = Vs + t * 4096;
+        f32x16 st, dpt;
+        zacc(st); zacc(dpt);
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
-          sc = mfma32(ldA(Qs + 4096 * j, fo.row[s]), kf[s], sc);
-          dp = mfma32(ldA(dOs + 4096 * j, fo.row[s]), vf[s], dp);
+          st = mfma32(ldA(Kt, fo.row[s]), qf[s], st);
+          dpt = mfma32(ldA(Vt, fo.row[s]), of[s], dpt);
+        }
+        if (t * 32 + 32 > klen) {                          // wave-uniform: keys past klen
+#pragma unroll
+          for (int e = 0; e < 16; ++e) st[e] = t * 32 + qrow(e, hh) < klen ? st[e] : -INFINITY;
+        }
+        // dP' = dropout(dP) (kept x 1/(1-p), dropped 0); the softmax scale of dS goes on dQ at the store
+        if (DM == 1) {
+#pragma unroll
+          for (int e = 0; e < 16; ++e) dpt[e] *= dscale;
+          drop_tile_sel(dpt, rowG + (uint32_t)(t * 16) * GOLD, drop, hh);
+        }
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const float p = fexp2(fmaf(st[e], sl2, -lq));
+          const float d = DM == 2 ? msel(dpt[e] * dscale, mw[e]) : dpt[e];   // rounding as DM 1
+          dpt[e] = p * (d - dl);
+        }
+        const bf16x8 sa = accb(dpt, 0), sb = accb(dpt, 1);
+        dq0 = mfma32(ldT(Ks, 32 * t, fo, 0), sa, dq0);
+        dq0 = mfma32(ldT(Ks, 32 * t + 16, fo, 0), sb, dq0);
+        dq1 = mfma32(ldT(Ks, 32 * t, fo, 1), sa, dq1);
+        dq1 = mfma32(ldT(Ks, 32 * t + 16, fo, 1), sb, dq1);
+      }
+    }
+  }
+  __syncthreads();                                         // images no longer read: store slabs
+  if (q0 < a.Lq) {
+    OutT* DQ = dq + ((int64_t)b * a.Lq + q0) * lddq + h * DH;
+    store_t<OutT>(dq0, dq1, a.scale, (float*)smem + w * 32 * 65, DQ, lddq, a.Lq - q0);
+  }
+}
+
+template <int DM>
+__global__ __launch_bounds__(NTH) void attn_bwd_dkdv_kernel(AttnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* Qs = smem;
+  char* dOs = smem + IMG384;
+  float* lss = (float*)(smem + 2 * IMG384);                // lse, then lse * log2(e) (0 past Lq)
+  float* dls = lss + MAXR;                                 // delta (0 past Lq)
+  char* Kw = smem + 2 * IMG384 + 2 * MAXR * 4;             // this wave's [32][64] K image
+  const int bh = xcd_id(blockIdx.x, gridDim.x), b = bh / a.H, h = bh % a.H;
+  const int tid = threadIdx.x, l = tid & 63, c = l & 31, hh = l >> 5;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  Kw += w * 4096;
+  const int kb0 = w * 32, key = kb0 + c;
+  const bf16* Qg = (const bf16*)a.q + (int64_t)b * a.Lq * a.ldq + h * DH;
+  const bf16* dOg = (const bf16*)a.dout + (int64_t)b * a.Lq * a.lddo + h * DH;
+  const bf16* Kg = (const bf16*)a.k + ((int64_t)b * a.Lk + kb0) * a.ldk + h * DH;
+  const bf16* V = (const bf16*)a.v + (int64_t)b * a.Lk * a.ldv + h * DH;
+  // this wave's K rows (4 pieces; rows past Lk zero), round 0 of Q / dO, the lse / delta rows
+  if (kb0 < a.Lk) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) dma_piece(Kg, a.ldk, min(32, a.Lk - kb0), Kw, i, l);
+  }
+  dma_piece(Qg, a.ldq, a.Lq, Qs, w, l);
+  dma_piece(dOg, a.lddo, a.Lq, dOs, w, l);
+  {                                                        // 6 x 64 floats of each array
+    const float* f = (w < 6 ? a.lse : a.delta) + (int64_t)bh * a.Lq;
+    dma4(rsrc(f, (uint32_t)(a.Lq * 4)), (uint32_t)((64 * (w % 6) + l) * 4), (char*)((w < 6 ? lss : dls) + 64 * (w % 6)));
+  }
+  bf16x8 vf[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) vf[s] = ldrow_sel(V, a.ldv, key, a.Lk, s * 16 + 8 * hh);
+#pragma unroll
+  for (int s = 0; s < 4; ++s) asm volatile("" ::"v"(vf[s]));    // vmcnt(0) here, covering round 0
+#pragma unroll
+  for (int r = 1; r < 4; ++r) {
+    dma_piece(Qg, a.ldq, a.Lq, Qs, 12 * r + w, l);
+    dma_piece(dOg, a.lddo, a.Lq, dOs, 12 * r + w, l);
+  }
+  round_barrier();
+  if (tid < MAXR) lss[tid] *= LOG2E;
+  const int klen = a.klen ? min(a.klen[b], a.Lk) : a.Lk;
+  const bool active = kb0 < klen, kok = key < klen;
+  const float sl2 = a.scale * LOG2E;
+  const AttnDrop drop(a.drop_p, a.seed, a.B, a.H, a.Lq, a.Lk);
+  const float dscale = DM ? drop.scale : 1.f;
+  const uint32_t nG = DM == 1 ? drop.npair * GOLD : 0u;
+  const uint32_t keyG = DM == 1 ? ((uint32_t)bh * (uint32_t)a.Lq * drop.npair + (uint32_t)(min(key, a.Lk - 1) >> 1)) * GOLD : 0u;
+  const bool odd = c & 1;
+  // DM 2: key c of this wave is bit (q & 31) + 32 hh' of lane mask r' of each (query block t, key
+  // block w) tile of the query-on-the-lane masks, r' = (c & 3) + 4 (c >> 3), hh' = (c >> 2) & 1:
+  // one 8-byte load per lane per tile, the half for this key, shifted to this lane's 4 hh rows
+  const uint64_t* mp = DM == 2 ? a.mq + ((int64_t)bh * a.mnqb * a.mnkb + w) * 16 + ((c & 3) + 4 * (c >> 3)) : nullptr;
+  const int mstride = a.mnkb * 16;
+  const bool mhi = (c >> 2) & 1;
+  const int nt = (a.Lq + 31) >> 5;
+  FragOff fo;
+  fo.init(l);
+  f32x16 dv0, dv1, dk0, dk1;
+  zacc(dv0); zacc(dv1); zacc(dk0); zacc(dk1);
+  int t = 0;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    if (r == 1) vmwait<4>();
+    if (r == 2) vmwait<2>();
+    if (r == 3) vmwait<0>();
+    round_barrier();                       // round r landed (r = 0: the lse scaling is visible)
+    const int tend = min(nt, 3 * r + 3);
+    if (active) {
+      for (; t < tend; ++t) {
+        const int qt0 = t * 32;
+        uint32_t mbits = 0;
+        if (DM == 2) {
+          const uint64_t m64 = mp[(int64_t)t * mstride];
+          mbits = (mhi ? (uint32_t)(m64 >> 32) : (uint32_t)m64) >> (4 * hh);
+        }
+        const char* Qt = Qs + t * 4096;
+        const char* dOt = dOs + t * 4096;
+        f32x16 sc, dp;
+        zacc(sc); zacc(dp);
+        // K fragments re-read every tile: an opaque image base keeps the compiler from hoisting
+        // them out of the loop into 16 more live registers
+        const char* Kt = Kw;
+        asm volatile("" : "+v"(Kt));
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          sc = mfma32(ldA(Qt, fo.row[s]), ldA(Kt, fo.row[s]), sc);
+          dp = mfma32(ldA(dOt, fo.row[s]), vf[s], dp);
+        }
+        if (!(kb0 + 32 <= klen && qt0 + 32 <= a.Lq)) {     // wave-uniform: invalid keys / queries
+#pragma unroll
+          for (int e = 0; e < 16; ++e) sc[e] = kok & (qt0 + qrow(e, hh) < a.Lq) ? sc[e] : -INFINITY;
         }
         const uint32_t tG = keyG + (uint32_t)(qt0 + 4 * hh) * nG;
-        const bool full = kok && qt0 + 32 <= a.Lq;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {            // registers 4i..4i+3 = queries qt0 + 8i + 4hh + 0..3
-          const f32x4 ls = *(const f32x4*)&lsS[32 * j + 8 * i + 4 * hh] * LOG2E;
-          const f32x4 ds = *(const f32x4*)&dlS[32 * j + 8 * i + 4 * hh];
+        for (int i = 0; i < 4; ++i) {                      // registers 4i..4i+3 = queries qt0 + 8i + 4hh + 0..3
+          const f32x4 ls = *(const f32x4*)&lss[qt0 + 8 * i + 4 * hh];
+          const f32x4 ds = *(const f32x4*)&dls[qt0 + 8 * i + 4 * hh];
           bool kb[4] = {true, true, true, true};
-          if (a.drop_p > 0.f) {
+          if (DM == 1) {     // the key pair (2j, 2j+1) on lanes c, c^1 splits the 4 queries' hashes
 #pragma unroll
             for (int u = 0; u < 2; ++u) {
               const uint32_t mine = hashG(tG + (uint32_t)(8 * i + (odd ? 2 : 0) + u) * nG, drop.pre);
@@ -1640,36 +1753,47 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_dkdv_kernel(AttnArgs a, int n
               kb[u + 2] = (odd ? (h1 >> 16) : (h1 & 0xFFFFu)) >= drop.thr;
             }
           }
+          // P' = dropout(P) unscaled (1/(1-p) goes on dV at the store), dS = P (dP' - delta)
+          // with dP' = dropout(dP) / (1-p); the softmax scale goes on dK at the store
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            const int r = 4 * i + e, ql = qt0 + 8 * i + 4 * hh + e;
-            const bool ok = full || (kok & (ql < a.Lq));
-            const float p = ok ? fexp2(fmaf(sc[r], sl2, -ls[e])) : 0.f;
-            sc[r] = kb[e] ? p : 0.f;
-            dp[r] = p * ((kb[e] ? dp[r] * dscale : 0.f) - ds[e]);
+            const int r4 = 4 * i + e;
+            const float p = fexp2(fmaf(sc[r4], sl2, -ls[e]));
+            if (DM == 2) {
+              const bool kp = (mbits >> ((r4 & 3) + 8 * (r4 >> 2))) & 1u;
+              sc[r4] = kp ? p : 0.f;
+              dp[r4] = p * fmaf(kp ? dp[r4] : 0.f, dscale, -ds[e]);
+            } else {
+              sc[r4] = kb[e] ? p : 0.f;
+              dp[r4] = p * fmaf(kb[e] ? dp[r4] : 0.f, dscale, -ds[e]);
+            }
           }
         }
         const bf16x8 pa = accb(sc, 0), pb = accb(sc, 1), sa = accb(dp, 0), sb = accb(dp, 1);
-        dv0 = mfma32(ldT(dOs, 32 * j, fo, 0), pa, dv0);
-        dv1 = mfma32(ldT(dOs, 32 * j, fo, 1), pa, dv1);
-        dv0 = mfma32(ldT(dOs, 32 * j + 16, fo, 0), pb, dv0);
-        dv1 = mfma32(ldT(dOs, 32 * j + 16, fo, 1), pb, dv1);
-        dk0 = mfma32(ldT(Qs, 32 * j, fo, 0), sa, dk0);
-        dk1 = mfma32(ldT(Qs, 32 * j, fo, 1), sa, dk1);
-        dk0 = mfma32(ldT(Qs, 32 * j + 16, fo, 0), sb, dk0);
-        dk1 = mfma32(ldT(Qs, 32 * j + 16, fo, 1), sb, dk1);
+        dv0 = mfma32(ldT(dOs, qt0, fo, 0), pa, dv0);
+        dv0 = mfma32(ldT(dOs, qt0 + 16, fo, 0), pb, dv0);
+        dv1 = mfma32(ldT(dOs, qt0, fo, 1), pa, dv1);
+        dv1 = mfma32(ldT(dOs, qt0 + 16, fo, 1), pb, dv1);
+        dk0 = mfma32(ldT(Qs, qt0, fo, 0), sa, dk0);
+        dk0 = mfma32(ldT(Qs, qt0 + 16, fo, 0), sb, dk0);
+        dk1 = mfma32(ldT(Qs, qt0, fo, 1), sa, dk1);
+        dk1 = mfma32(ldT(Qs, qt0 + 16, fo, 1), sb, dk1);
       }
     }
-    cs = next_stage(cs);
   }
   __syncthreads();
-  float* scr = (float*)smem + w * 32 * 65;
-  bf16* DK = (bf16*)a.dk + ((int64_t)b * a.Lk + kb0) * a.lddk + h * DH;
-  store_t<bf16>(dk0, dk1, a.scale, scr, DK, a.lddk, a.Lk - kb0);
-  bf16* DV = (bf16*)a.dv + ((int64_t)b * a.Lk + kb0) * a.lddv + h * DH;
-  store_t<bf16>(dv0, dv1, dscale, scr, DV, a.lddv, a.Lk - kb0);
+  if (kb0 < a.Lk) {
+    float* scr = (float*)smem + w * 32 * 65;
+    bf16* DK = (bf16*)a.dk + ((int64_t)b * a.Lk + kb0) * a.lddk + h * DH;
+    store_t<bf16>(dk0, dk1, a.scale, scr, DK, a.lddk, a.Lk - kb0);
+    bf16* DV = (bf16*)a.dv + ((int64_t)b * a.Lk + kb0) * a.lddv + h * DH;
+    store_t<bf16>(dv0, dv1, dscale, scr, DV, a.lddv, a.Lk - kb0);
+  }
 }
-}  // namespace sq
+constexpr size_t DQ_LDS = 2 * IMG384 > NTH / 64 * 32 * 65 * 4 ? 2 * IMG384 : NTH / 64 * 32 * 65 * 4;
+constexpr size_t DKDV_LDS = 3 * IMG384 + 2 * MAXR * 4;
+static_assert(DKDV_LDS <= 160 * 1024 && NTH / 64 * 32 * 65 * 4 <= DKDV_LDS, "dK/dV LDS");
+}  // namespace rb
 
 AttnArgs args(const avsr_attn_params* p) {
   AttnArgs a;
@@ -1678,7 +1802,10 @@ AttnArgs args(const avsr_attn_params* p) {
   a.o = p->o; a.ldo = p->ldo; a.lse = p->lse; a.klen = p->klen; a.causal = p->causal;
   a.drop_p = p->drop_p; a.seed = p->seed; a.dout = p->dout; a.lddo = p->lddo; a.delta = p->delta;
   a.dq = p->dq; a.lddq = p->lddq; a.dk = p->dk; a.lddk = p->lddk; a.dv = p->dv; a.lddv = p->lddv;
-  a.db_ws = nullptr;            // set per kernel path by avsr_attn_bwd
+  a.mnqb = (p->Lq + 31) / 32;
+  a.mnkb = 2 * ((p->Lk + 63) / 64);
+  const bool m = p->drop_mask != nullptr && p->drop_p > 0.f && !p->causal && p->dtype == AVSR_BF16;
+  a.mq = m ? p->drop_mask : nullptr;
   return a;
 }
 
@@ -1712,8 +1839,12 @@ extern "C" int avsr_attn_fwd(const avsr_attn_params* p, void* stream) {
     const int nqb = (p->Lq + 127) / 128;
     const long nwg = (long)p->B * p->H * nqb;
     if (nwg > 0x7fffffffL) return AVSR_E_SHAPE;
-    hipLaunchKernelGGL(sq::attn_fwd_kernel, dim3((unsigned)nwg), dim3(256), sq::NS * sq::STAGEB, (hipStream_t)stream, a,
-                       nqb);
+    if (a.mq)
+      hipLaunchKernelGGL(sq::attn_fwd_kernel<true>, dim3((unsigned)nwg), dim3(256), sq::NS * sq::STAGEB, (hipStream_t)stream,
+                         a, nqb);
+    else
+      hipLaunchKernelGGL(sq::attn_fwd_kernel<false>, dim3((unsigned)nwg), dim3(256), sq::NS * sq::STAGEB, (hipStream_t)stream,
+                         a, nqb);
     AVSR_CHECK_LAUNCH();
     return 0;
   }
@@ -1733,16 +1864,28 @@ extern "C" int avsr_attn_fwd(const avsr_attn_params* p, void* stream) {
   return 0;
 }
 
-// the query-tiled bf16 backward computes delta in its dQ kernel (which runs first). Where the
-// resident kernels apply (Lq, Lk <= 384) they stay the default: isolated the tiled pair is
-// faster (C2 with dropout 93.7 vs 101.5 us), but inside the training step, beside the weight-
-// gradient GEMMs of the side stream, it took 144 vs 100 us per layer (profiles/r04_*)
-static bool sq_bwd(const avsr_attn_params* p) {
-  const bool force = avsr_opt(AVSR_OPT_ATTN_SQ_BWD) != 0;
-  return p->dtype == AVSR_BF16 && !p->causal && p->Lq >= 128 && p->Lk >= 128 && res::small_index(p) && sq_enabled() &&
-         (force || p->Lq > res::MAXR || p->Lk > res::MAXR);
+extern "C" int avsr_attn_dropmask(const avsr_attn_params* p, void* stream) {
+  if (!p || !p->drop_mask) return AVSR_E_ARG;
+  if (!(p->drop_p > 0.f) || !res::small_index(p)) return AVSR_E_ARG;
+  if (p->B * p->H == 0 || p->Lq == 0 || p->Lk == 0) return 0;
+  avsr_attn_params q = *p;
+  q.dtype = AVSR_BF16; q.causal = 0;                    // the layout args() fills for the mask readers
+  AttnArgs a = args(&q);
+  const int64_t ntiles = (int64_t)p->B * p->H * a.mnqb * a.mnkb;
+  if (ntiles > 0x7ffffff0L) return AVSR_E_SHAPE;
+  hipLaunchKernelGGL(res::attn_mask_kernel, dim3((unsigned)((ntiles + 3) / 4)), dim3(256), 0, (hipStream_t)stream, a,
+                     const_cast<uint64_t*>(a.mq), (int)ntiles);
+  AVSR_CHECK_LAUNCH();
+  return 0;
 }
-// the resident bf16 backward computes delta inside its dK/dV kernel (Q / dO already in LDS)
+
+// the encoder backward (rb::, bf16 non-causal 128..384 rows) computes delta in its dQ kernel,
+// the resident bf16 backward (decoder shapes, Lq, Lk <= 384) inside its dK/dV kernel (Q / dO
+// already in LDS); longer sequences take the tiled v2 kernels after avsr_attn_bwd_prep
+static bool enc_bwd(const avsr_attn_params* p) {
+  return p->dtype == AVSR_BF16 && !p->causal && p->Lq >= 128 && p->Lk >= 128 && p->Lq <= res::MAXR &&
+         p->Lk <= res::MAXR && res::small_index(p) && (p->lddo % 8) == 0;
+}
 static bool resident_bwd(const avsr_attn_params* p) {
   return p->dtype == AVSR_BF16 && p->Lq <= res::MAXR && p->Lk <= res::MAXR && res::small_index(p);
 }
@@ -1750,7 +1893,7 @@ static bool resident_bwd(const avsr_attn_params* p) {
 extern "C" int avsr_attn_bwd_prep(const avsr_attn_params* p, void* stream) {
   int rc = check(p);
   if (rc) return rc;
-  if (sq_bwd(p) || resident_bwd(p)) return 0;
+  if (enc_bwd(p) || resident_bwd(p)) return 0;
   AttnArgs a = args(p);
   const int g = avsr_grid((int64_t)p->B * p->Lq * p->H);
   if (p->dtype == AVSR_BF16) hipLaunchKernelGGL(attn_prep_kernel<bf16>, dim3(g), dim3(256), 0, (hipStream_t)stream, a);
@@ -1759,43 +1902,44 @@ extern "C" int avsr_attn_bwd_prep(const avsr_attn_params* p, void* stream) {
   return 0;
 }
 
-// the backward kernels of one call; fused = the q/k/v bias partials were written by them
-static int attn_bwd_kernels(const avsr_attn_params* p, hipStream_t st, bool& fused) {
+template <int DM>
+static void launch_enc_bwd(const avsr_attn_params* p, const AttnArgs& a, hipStream_t st) {
+  const dim3 g(p->B * p->H);
+  if (p->dq_out) {
+    res::allow_lds(rb::attn_bwd_dq_kernel<bf16, DM>);
+    hipLaunchKernelGGL((rb::attn_bwd_dq_kernel<bf16, DM>), g, dim3(rb::NTH), rb::DQ_LDS, st, a, (bf16*)p->dq_out,
+                       p->lddq_out);
+  } else {
+    res::allow_lds(rb::attn_bwd_dq_kernel<float, DM>);
+    hipLaunchKernelGGL((rb::attn_bwd_dq_kernel<float, DM>), g, dim3(rb::NTH), rb::DQ_LDS, st, a, p->dq, p->lddq);
+  }
+  res::allow_lds(rb::attn_bwd_dkdv_kernel<DM>);
+  hipLaunchKernelGGL(rb::attn_bwd_dkdv_kernel<DM>, g, dim3(rb::NTH), rb::DKDV_LDS, st, a);
+}
+
+static int attn_bwd_kernels(const avsr_attn_params* p, hipStream_t st) {
   AttnArgs a = args(p);
   dim3 grid((p->Lk + 127) / 128, p->B * p->H);
   if (p->dtype == AVSR_BF16) {
     if (p->dq_out && (p->lddq_out % 8 || !avsr_aligned16(p->dq_out))) return AVSR_E_ALIGN;
     if (!p->dq_out && (p->lddq % 4 || !avsr_aligned16(p->dq))) return AVSR_E_ALIGN;
-    if (sq_bwd(p)) {
-      const int nqb = (p->Lq + 127) / 128, nkb = (p->Lk + 127) / 128;
-      const long gq = (long)p->B * p->H * nqb, gk = (long)p->B * p->H * nkb;
-      if (gq > 0x7fffffffL || gk > 0x7fffffffL) return AVSR_E_SHAPE;
-      if (p->dq_out)
-        hipLaunchKernelGGL(sq::attn_bwd_dq_kernel<bf16>, dim3((unsigned)gq), dim3(256), sq::NS * sq::STAGEB, st, a, nqb,
-                           (bf16*)p->dq_out, p->lddq_out);
-      else
-        hipLaunchKernelGGL(sq::attn_bwd_dq_kernel<float>, dim3((unsigned)gq), dim3(256), sq::NS * sq::STAGEB, st, a, nqb,
-                           p->dq, p->lddq);
-      AVSR_CHECK_LAUNCH();
-      hipLaunchKernelGGL(sq::attn_bwd_dkdv_kernel, dim3((unsigned)gk), dim3(256), sq::NS * sq::STAGEB_F, st, a, nkb);
+    if (enc_bwd(p)) {
+      if (!(p->drop_p > 0.f)) launch_enc_bwd<0>(p, a, st);
+      else if (a.mq) launch_enc_bwd<2>(p, a, st);
+      else launch_enc_bwd<1>(p, a, st);
       AVSR_CHECK_LAUNCH();
       return 0;
     }
     if (resident_bwd(p)) {
-      // dK/dV: 12 waves (3 per SIMD; a few registers spill to scratch, measured 5 % faster than
-      // 8 spill-free waves at 2 per SIMD)
-      // (one workgroup per (b, h): grid.y = 1 for L <= 384) with the fused bias-gradient partials
-      const int nwk = std::min(res::nwaves(p->Lk), 12), nwq = res::nwaves(p->Lq);
-      a.db_ws = p->db ? p->db_ws : nullptr;
-      fused = p->db != nullptr;
-      const size_t ldk = std::max(res::img_lds(p->Lq) + (size_t)2 * ((p->Lq + 31) & ~31) * sizeof(float),
-                                  res::slab_lds(nwk) + (size_t)nwk * 128 * sizeof(float));
+      // dK/dV: one workgroup per (b, h) of up to 12 waves (3 per SIMD), grid.y = 1 for L <= 384
+      const int nwk = res::nwaves(p->Lk), nwq = res::nwaves(p->Lq);
+      const size_t ldk = std::max(res::img_lds(p->Lq) + (size_t)2 * ((p->Lq + 31) & ~31) * sizeof(float), res::slab_lds(nwk));
       const dim3 gk(p->B * p->H, (p->Lk + 32 * nwk - 1) / (32 * nwk));
-      res::allow_lds(res::attn_bwd_dkdv_kernel<768>);
-      hipLaunchKernelGGL(res::attn_bwd_dkdv_kernel<768>, gk, dim3(64 * nwk), ldk, st, a);
+      res::allow_lds(res::attn_bwd_dkdv_kernel);
+      hipLaunchKernelGGL(res::attn_bwd_dkdv_kernel, gk, dim3(64 * nwk), ldk, st, a);
       AVSR_CHECK_LAUNCH();
-      const size_t ldq = std::max(res::img_lds(p->Lk), res::slab_lds(nwq) + (size_t)nwq * 64 * sizeof(float));
-      dim3 gq(p->B * p->H, (p->Lq + 32 * nwq - 1) / (32 * nwq));
+      const size_t ldq = std::max(res::img_lds(p->Lk), res::slab_lds(nwq));
+      const dim3 gq(p->B * p->H, (p->Lq + 32 * nwq - 1) / (32 * nwq));
       if (p->dq_out) {
         res::allow_lds(res::attn_bwd_dq_kernel<bf16>);
         hipLaunchKernelGGL(res::attn_bwd_dq_kernel<bf16>, gq, dim3(64 * nwq), ldq, st, a, (bf16*)p->dq_out, p->lddq_out);
@@ -1843,11 +1987,10 @@ extern "C" int avsr_attn_bwd(const avsr_attn_params* p, void* stream) {
   if (p->db && !p->db_ws) return AVSR_E_ARG;
   if (p->B * p->H == 0 || p->Lk == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
-  bool fused = false;
-  rc = attn_bwd_kernels(p, st, fused);
+  rc = attn_bwd_kernels(p, st);
   if (rc || !p->db) return rc;
   const int HD = p->H * DH;
-  if (!fused) {
+  {
     const dim3 g((3 * HD + 255) / 256, p->B);
     if (p->dtype == AVSR_BF16 && p->dq_out)
       hipLaunchKernelGGL((attn_db_kernel<bf16, bf16>), g, dim3(256), 0, st, (const bf16*)p->dq_out, p->lddq_out,

@@ -42,11 +42,10 @@ _DB_FUSE = True
 _COLSUM_DEFER = True
 # bias gradients of operands only the side stream's weight-grads read run on the side stream
 _SIDE_BIAS = True
-# encoder q/k/v bias gradients written by the attention backward (avsr_attn_params.db) instead of
-# a column-sum pass over dqkv on the side stream: off — the fused form adds ~1 us per layer to the
-# data-gradient chain and removes ~27 us of side-stream work, and the step got 1 % slower
-# (131.2 vs 132.8 k AV-frames/s, 3 interleaved pairs, profiles/r05_attn_db_ab.txt)
-_ATTN_DB = False
+# encoder self-attention dropout from stored keep masks (avsr_attn_dropmask, generated for every
+# layer on the side stream while the step stream runs the frontends) instead of a hash per score
+# element in the forward, dK/dV and dQ kernels (same bits)
+ATTN_MASK = True
 # the CTC branch of the forward runs on the side stream beside the decoder forward
 _CTC_SIDE = True
 # bf16 stem conv straight from the video (stem.hip) instead of pack + general implicit GEMM
@@ -113,7 +112,11 @@ class _Seeds:
 
     def next(self):
         self.i += 1
-        return (self.base * 0x9E3779B97F4A7C15 + self.i * 0xBF58476D1CE4E5B9) & 0xFFFFFFFFFFFFFFFF
+        return self.peek(0)
+
+    def peek(self, k):
+        """the value next() returns k + 1 calls from now (k = 0: the last one drawn)"""
+        return (self.base * 0x9E3779B97F4A7C15 + (self.i + k) * 0xBF58476D1CE4E5B9) & 0xFFFFFFFFFFFFFFFF
 
 
 def positional_encoding(L_, d, device):
@@ -168,6 +171,8 @@ class Engine:
                      if self.device.type == "cuda" and SIDE_STREAM else None)
         # reused events: a stream wait binds the record that precedes it
         self._side_ev = [torch.cuda.Event() for _ in range(8)] if self.side is not None else []
+        self._amask, self._amask_wait = None, False     # encoder attention dropout masks (ATTN_MASK)
+        self._amask_ev = torch.cuda.Event() if self.side is not None else None
         self._side_i = 0
         # operands the side stream reads stay referenced until join_side() (instead of
         # record_stream, whose deferred frees keep the caching allocator growing for steps)
@@ -720,6 +725,16 @@ class Engine:
         M, D = B * T, self.D
         EN = "encoder."
         ctx = {"B": B, "T": T, "modality": modality}
+        # LayerDrop: one torch.rand([]) (CPU generator) per layer on every call, train or eval, as
+        # the reference draws them (avhubert.py:709-712; no other torch CPU draw happens between
+        # the reference's frontends and its layer loop); training skips a layer whose draw is below
+        # cfg.layerdrop (its context is None, the backward passes the gradient through)
+        draws = [float(torch.rand([])) for _ in range(self.nl)]
+        kept = [i for i in range(self.nl) if not (train and draws[i] < self.layerdrop)]
+        # the self-attention dropout masks of every kept layer, on the side stream beside the
+        # frontends (seeds: sd_in, sd_pc, then sd_att, sd_o, sd_a, sd_f per kept layer)
+        p_att = cfg.attention_dropout if train else 0.0
+        amask = self._attn_masks(B, T, p_att, {i: seeds.peek(3 + 4 * j) for j, i in enumerate(kept)})
         # audio / video frontends -> concat buffer [M][2D] (audio | video), or with
         # modality_fuse 'add' the sum [M][D] (avhubert.py:486-489: the video projection adds the
         # audio features as its residual)
@@ -778,16 +793,12 @@ class Engine:
                        norm=norm, pre=pre, sd_pc=sd_pc, p_h=p_h, vctx=vctx, feat=feat, klen=klen)
         x = y
         layers = []
-        # LayerDrop: one torch.rand([]) (CPU generator) per layer on every call, train or eval, as
-        # the reference draws them (avhubert.py:709-712); training skips a layer whose draw is below
-        # cfg.layerdrop (its context is None, the backward passes the gradient through)
-        draws = [float(torch.rand([])) for _ in range(self.nl)]
         for i in range(self.nl):
-            if train and draws[i] < self.layerdrop:
+            if i not in kept:
                 if save:
                     layers.append(None)
                 continue
-            x, lc = self._enc_layer_fwd(i, x, B, T, klen, train, save, seeds)
+            x, lc = self._enc_layer_fwd(i, x, B, T, klen, train, save, seeds, amask.get(i))
             if save:
                 layers.append(lc)
         E = "encoder.encoder."
@@ -796,7 +807,30 @@ class Engine:
             ctx.update(layers=layers, x_last=x, mf=mf, rf=rf)
         return out, ctx
 
-    def _enc_layer_fwd(self, i, x, B, T, klen, train, save, seeds):
+    def _attn_masks(self, B, T, p_att, seeds_by_layer):
+        """{layer: (seed, keep mask)} of the encoder self-attention dropout, generated on the side
+        stream into a persistent per-layer buffer; the step stream waits for them before its first
+        attention (ATTN_MASK, bf16 only)"""
+        H = self.H
+        if not (ATTN_MASK and p_att > 0 and self.dtype == torch.bfloat16 and seeds_by_layer
+                and B * H * T * ((T + 1) // 2) <= 0xFFFFFFFF):
+            return {}
+        words = ops.attn_mask_words(B, H, T, T)
+        if self._amask is None or self._amask.shape[1] != words:
+            self._amask = None
+            self._amask = torch.empty(self.nl, words, dtype=torch.int64, device=self.device)
+        buf = self._amask
+
+        def run():
+            for i, sd in seeds_by_layer.items():
+                ops.attn_dropmask(buf[i], B=B, H=H, Lq=T, Lk=T, drop_p=p_att, seed=sd)
+        self._on_side(run)
+        self._amask_wait = self.side is not None
+        if self._amask_wait:
+            self._amask_ev.record(self.side)
+        return {i: (sd, buf[i]) for i, sd in seeds_by_layer.items()}
+
+    def _enc_layer_fwd(self, i, x, B, T, klen, train, save, seeds, amask=None):
         cfg = self.cfg
         D, H = self.D, self.H
         M = B * T
@@ -810,8 +844,15 @@ class Engine:
         lse = self._e(B, H, T, dtype=torch.float32)
         sd_att = seeds.next()
         p_att = cfg.attention_dropout if train else 0.0
+        mask = None
+        if amask is not None:
+            assert amask[0] == sd_att, "attention mask seed out of step with the dropout sites"
+            mask = amask[1]
+            if self._amask_wait:            # the side stream's masks, once per forward
+                torch.cuda.current_stream(self.device).wait_event(self._amask_ev)
+                self._amask_wait = False
         ops.attn_fwd(qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:], o, lse, B=B, H=H, Lq=T, Lk=T, klen=klen,
-                     scale=0.125, drop_p=p_att, seed=sd_att)
+                     scale=0.125, drop_p=p_att, seed=sd_att, mask=mask)
         sd_o = seeds.next()
         p_h = cfg.hidden_dropout if train else 0.0
         x1 = ops.linear_fwd(o, self.w(a + "out_proj.weight"), self.arena.master(a + "out_proj.bias"), res=x,
@@ -828,7 +869,8 @@ class Engine:
                             drop_p=p_h, seed=sd_f)
         lc = None
         if save:
-            lc = dict(i=i, x=x, ln1=ln1, m1=m1, r1=r1, qkv=qkv, o=o, lse=lse, sd_att=sd_att, p_att=p_att, sd_o=sd_o, p_h=p_h,
+            lc = dict(i=i, x=x, ln1=ln1, m1=m1, r1=r1, qkv=qkv, o=o, lse=lse, sd_att=sd_att, p_att=p_att, mask=mask,
+                      sd_o=sd_o, p_h=p_h,
                       x1=x1, ln2=ln2, m2=m2, r2=r2, h=h, act=act, sd_a=sd_a, p_a=p_a, sd_f=sd_f)
         return x2, lc
 
@@ -871,16 +913,13 @@ class Engine:
         names_b = [a + "q_proj.bias", a + "k_proj.bias", a + "v_proj.bias"]
         names_w = [a + "q_proj.weight", a + "k_proj.weight", a + "v_proj.weight"]
         db_qkv = self.arena.span(names_b, buf="g")
-        # the q/k/v bias gradients (column sums of dqkv) come out of the attention backward's
-        # store epilogues (bf16) instead of a pass over dqkv
         ops.attn_bwd(do, qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:], lc["o"], lc["lse"], dq32, dqkv[:, D:2 * D],
                      dqkv[:, 2 * D:], delta, B=B, H=H, Lq=T, Lk=T, klen=klen, scale=0.125, drop_p=lc["p_att"],
-                     seed=lc["sd_att"], dq=None if dq32 is not None else dqkv[:, :D],
-                     db=db_qkv if _ATTN_DB else None)
+                     seed=lc["sd_att"], dq=None if dq32 is not None else dqkv[:, :D], mask=lc["mask"])
         if dq32 is not None:
             ops.cast(dq32, dqkv[:, :D])
-        if not _ATTN_DB:
-            self._bias_grad_side(dqkv, db_qkv)
+        # the q/k/v bias gradients (column sums of dqkv) on the side stream
+        self._bias_grad_side(dqkv, db_qkv)
         self._wgrad(dqkv, lc["ln1"], self.arena.span(names_w, buf="g"))
         dln1 = ops.linear_dgrad(dqkv, self.arena.span(names_w))
         ew = self._ew_next(lc_prev["i"], lc_prev, M) if lc_prev is not None else None

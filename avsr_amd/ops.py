@@ -544,19 +544,41 @@ def _attn_params(q, k, v, o, B, H, Lq, Lk, lse, klen, causal, scale, drop_p, see
                   lse=lse, klen=klen, causal=int(causal), drop_p=float(drop_p), seed=int(seed) & (2 ** 64 - 1))
 
 
-def attn_fwd(q, k, v, o, lse, *, B, H, Lq, Lk, klen=None, causal=False, scale=0.125, drop_p=0.0, seed=0):
+def attn_mask_words(B, H, Lq, Lk):
+    """AVSR_ATTN_MASK_WORDS: 64-bit words of one attention call's stored dropout keep mask"""
+    return B * H * ((Lq + 31) // 32) * (2 * ((Lk + 63) // 64)) * 16
+
+
+def attn_dropmask(mask, *, B, H, Lq, Lk, drop_p, seed):
+    """the keep decisions of the attention dropout (drop_p, seed) for (B, H, Lq, Lk) into mask
+    (int64, attn_mask_words(...) elements); data-independent, so it may run on any stream ahead
+    of the forward. Pass the same mask to attn_fwd / attn_bwd."""
+    assert mask.dtype == torch.int64 and mask.is_contiguous() and mask.numel() >= attn_mask_words(B, H, Lq, Lk)
+    p = L.fill(L.AttnParams, dtype=L.AVSR_BF16, B=B, H=H, Lq=Lq, Lk=Lk, drop_p=float(drop_p),
+               seed=int(seed) & (2 ** 64 - 1), drop_mask=mask)
+    _call("avsr_attn_dropmask", p)
+    return mask
+
+
+def attn_fwd(q, k, v, o, lse, *, B, H, Lq, Lk, klen=None, causal=False, scale=0.125, drop_p=0.0, seed=0, mask=None):
+    """mask: a keep mask from attn_dropmask for the same (B, H, Lq, Lk, drop_p, seed), or None
+    (the kernels hash the dropout per element; same result)"""
     p = _attn_params(q, k, v, o, B, H, Lq, Lk, lse, klen, causal, scale, drop_p, seed)
+    if mask is not None:
+        p.drop_mask = mask.data_ptr()
     _call("avsr_attn_fwd", p)
     return o
 
 
 def attn_bwd(dout, q, k, v, o, lse, dq32, dk, dv, delta, *, B, H, Lq, Lk, klen=None, causal=False,
-             scale=0.125, drop_p=0.0, seed=0, dq=None, db=None):
+             scale=0.125, drop_p=0.0, seed=0, dq=None, db=None, mask=None):
     """dq32: fp32 accumulator (zeroed by the caller), or None with dq (bf16 only): dQ written
     straight into dq in the activation dtype. dk/dv in the activation dtype. db (fp32, 3*H*64):
     += the column sums of the stored dQ | dK | dV (the fused q/k/v bias gradients), finalised
-    through the column-sum path (deferred within a training step's backward)."""
+    through the column-sum path (deferred within a training step's backward). mask: as attn_fwd."""
     p = _attn_params(q, k, v, o, B, H, Lq, Lk, lse, klen, causal, scale, drop_p, seed)
+    if mask is not None:
+        p.drop_mask = mask.data_ptr()
     p.dout, p.lddo = dout.data_ptr(), dout.stride(0)
     p.delta = delta.data_ptr()
     if dq is not None:

@@ -44,8 +44,8 @@ const char* avsr_version(void);
  *                                 tile configuration k (AVSR_TILE_* below) on the bf16 core
  *   AVSR_OPT_ATTN_SQ_FWD    [1]  1: query-tiled streamed self-attention forward for bf16,
  *                                 L >= 128; 0: the resident-K/V kernel (same rows to 1e-2)
- *   AVSR_OPT_ATTN_SQ_BWD    [0]  1: query-tiled backward also where the resident backward
- *                                 applies (L <= 384); 0: resident up to 384 frames
+ *   AVSR_OPT_ATTN_SQ_BWD    [0]  retired (round 6: the query-tiled backward was removed; the
+ *                                 value is accepted and has no effect)
  *   AVSR_OPT_WGRAD_DUAL     [1]  1: two-wave-group weight-gradient kernel (fp32 C, both
  *                                 operands r-contiguous); 0: the 4-wave core
  *   AVSR_OPT_CONV_192       [1]  1: 192x128 tiles for conv fwd / data-grad where they still
@@ -399,8 +399,19 @@ typedef struct {
    * flush). The resident bf16 kernels sum them in their store epilogues; other paths run one
    * extra pass over dq/dk/dv. NULL: off. */
   float* db; float* db_ws;
+  /* optional probability-dropout keep mask (bf16, non-causal): written once per (seed, shape)
+   * by avsr_attn_dropmask, then read by avsr_attn_fwd / avsr_attn_bwd in place of re-hashing
+   * the counter dropout per element (same bits: the mask IS the hash's keep decision). 64-bit
+   * lane masks, AVSR_ATTN_MASK_WORDS(B, H, Lq, Lk) words, per (b, h) and 32 x 32 tile (query
+   * block qb of 32, key block kb of 32, kb padded to an even count NKB = 2 * ceil(Lk / 64)), 16
+   * words per tile, query on the lane: word ((bh * NQB + qb) * NKB + kb) * 16 + r, bit l keeps
+   * (q = 32 qb + (l & 31), k = 32 kb + (r & 3) + 8 (r >> 2) + 4 (l >> 5)); 0 past Lq / Lk.
+   * NULL: the kernels hash (decoder attention, fp32). */
+  uint64_t* drop_mask;
 } avsr_attn_params;
 #define AVSR_ATTN_DB_WS(B, H) ((int64_t)(B) * 3 * (H) * 64)
+#define AVSR_ATTN_MASK_WORDS(B, H, Lq, Lk) \
+  ((int64_t)(B) * (H) * (((Lq) + 31) / 32) * (2 * (((Lk) + 63) / 64)) * 16)
 /* diagnostic (not product path): per-workgroup s_memrealtime stamps of the resident attention
  * forward into buf[6 * workgroups] (start, first K/V round, compute done, end, HW_ID, XCC_ID);
  * buf = NULL turns them off */
@@ -408,6 +419,11 @@ int avsr_debug_attn_stamps(unsigned long long* buf);
 int avsr_attn_fwd(const avsr_attn_params* p, void* stream);
 int avsr_attn_bwd_prep(const avsr_attn_params* p, void* stream);   /* delta = rowsum(dO * O) */
 int avsr_attn_bwd(const avsr_attn_params* p, void* stream);
+/* fills p->drop_mask (AVSR_ATTN_MASK_WORDS words) with the keep decisions of drop_p / seed for
+ * (B, H, Lq, Lk): the data-independent half of the attention dropout, runnable ahead of the
+ * forward on another stream. Same replacement as avsr_attn_fwd (the dropout of
+ * Wav2Vec2Attention / eager_attention_forward, avhubert.py:747-768). */
+int avsr_attn_dropmask(const avsr_attn_params* p, void* stream);
 
 /* ------------------------------------------------------------------------------------
  * Losses on logits [rows][ldx] (V valid columns; columns V..ldx-1 of every gradient row are

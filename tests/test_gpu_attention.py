@@ -2,6 +2,7 @@
 causal self-attention, decoder source attention, probability dropout)."""
 import math
 
+import numpy as np
 import pytest
 import torch
 
@@ -211,39 +212,6 @@ def test_attention_sq_matches_resident(dev, monkeypatch, B, H, L, klen, lib_opt)
     assert (l1 - l0).abs().max().item() < 1e-4
 
 
-@pytest.mark.parametrize("B,H,L,klen", [(2, 16, 375, [375, 301]), (3, 2, 200, [200, 129, 64])])
-def test_attention_sq_backward_matches_resident(dev, monkeypatch, B, H, L, klen, lib_opt):
-    """The query-tiled backward (dQ kernel computing delta, then dK / dV streaming Q, dO, lse,
-    delta; the default only past 384 frames) against the resident backward on the same bf16
-    inputs with dropout: dQ / dK / dV agree to bf16 rounding."""
-    D = H * 64
-    g = torch.Generator().manual_seed(L + 7)
-    bf = torch.bfloat16
-    qkv = torch.randn(B * L, 3 * D, generator=g).to(dev, bf)
-    q, k, v = qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:]
-    dout = torch.randn(B * L, D, generator=g).to(dev, bf)
-    kl = torch.tensor(klen, dtype=torch.int32, device=dev)
-    o = torch.empty(B * L, D, device=dev, dtype=bf)
-    lse = torch.empty(B, H, L, device=dev)
-    ops.attn_fwd(q, k, v, o, lse, B=B, H=H, Lq=L, Lk=L, klen=kl, scale=0.125, drop_p=0.1, seed=5)
-
-    def bwd():
-        dq = torch.empty(B * L, D, device=dev, dtype=bf)
-        dk = torch.empty(B * L, D, device=dev, dtype=bf)
-        dv = torch.empty(B * L, D, device=dev, dtype=bf)
-        delta = torch.empty(B, H, L, device=dev)
-        ops.attn_bwd(dout, q, k, v, o, lse, None, dk, dv, delta, B=B, H=H, Lq=L, Lk=L, klen=kl, scale=0.125,
-                     drop_p=0.1, seed=5, dq=dq)
-        return dq, dk, dv
-    ref = bwd()
-    lib_opt("attn_sq_bwd", 1)
-    got = bwd()
-    again = bwd()
-    for a_, b_, c_ in zip(got, ref, again):
-        assert torch.equal(a_, c_)
-        assert _rel(a_, b_) < 2e-2
-
-
 # ---------------------------------------------------------------------------------------------
 # Dropout mask identity (verdict r4 item 2): the kept / dropped pattern of every (query, key)
 # pair is recovered exactly from each kernel that applies or regenerates it, and must be the
@@ -282,12 +250,16 @@ def _onehot_rows(rows, H, L, c, n, col0, dev, dt):
     return x.view(rows, H * 64)
 
 
-def _masks(dev, dt, B, H, Lq, Lk, klen, causal, p, seed):
+def _masks(dev, dt, B, H, Lq, Lk, klen, causal, p, seed, stored=False):
     """(forward mask, dV mask, dQ mask, dK mask) recovered from the kernels the current library
-    options select, each restricted to the allowed pairs"""
+    options select, each restricted to the allowed pairs; stored: the kernels read the keep mask
+    of avsr_attn_dropmask instead of hashing"""
     D = H * 64
     kl = None if klen is None else torch.tensor(klen, dtype=torch.int32, device=dev)
     kw = dict(B=B, H=H, Lq=Lq, Lk=Lk, klen=kl, causal=causal, scale=0.125, drop_p=p, seed=seed)
+    if stored:
+        kw["mask"] = ops.attn_dropmask(torch.empty(ops.attn_mask_words(B, H, Lq, Lk), dtype=torch.int64, device=dev),
+                                       B=B, H=H, Lq=Lq, Lk=Lk, drop_p=p, seed=seed)
     allowed = _allowed(dev, B, H, Lq, Lk, klen, causal)
     lse = torch.empty(B, H, Lq, device=dev)
     zq, zk = torch.zeros(B * Lq, D, device=dev, dtype=dt), torch.zeros(B * Lk, D, device=dev, dtype=dt)
@@ -343,22 +315,22 @@ def _masks(dev, dt, B, H, Lq, Lk, klen, causal, p, seed):
 @pytest.mark.parametrize("case", MASK_CASES, ids=[c[0] for c in MASK_CASES])
 def test_attention_dropout_mask_bitexact(dev, lib_opt, case):
     """every attention kernel of the training step applies or regenerates exactly the same
-    dropout mask: the query-tiled and resident forwards, the resident and query-tiled backward
-    (dK/dV and dQ kernels), bf16 and the fp32 parity kernels — torch.equal on the recovered
-    kept / dropped pattern of every allowed (query, key) pair"""
+    dropout mask: the query-tiled and resident forwards, the resident backward (dK/dV and dQ
+    kernels), each hashing or reading the stored keep mask of avsr_attn_dropmask (the encoder's
+    production path; causal launches ignore it and hash), bf16 and the fp32 parity kernels —
+    torch.equal on the recovered kept / dropped pattern of every allowed (query, key) pair"""
     name, B, H, Lq, Lk, klen, causal = case
     p, seed = 0.1, 0x5EED + Lq
     bf = torch.bfloat16
     runs = {}
     for fwd_sq in (1, 0):
-        for bwd_sq in (0, 1):
+        for stored in (True, False):
             lib_opt("attn_sq_fwd", fwd_sq)
-            lib_opt("attn_sq_bwd", bwd_sq)
-            runs[f"bf16 fwd_sq={fwd_sq} bwd_sq={bwd_sq}"], allowed = _masks(dev, bf, B, H, Lq, Lk, klen, causal, p, seed)
+            runs[f"bf16 fwd_sq={fwd_sq} stored={stored}"], allowed = _masks(dev, bf, B, H, Lq, Lk, klen, causal, p, seed,
+                                                                            stored)
     lib_opt("attn_sq_fwd", 1)
-    lib_opt("attn_sq_bwd", 0)
     runs["fp32"], _ = _masks(dev, torch.float32, B, H, Lq, Lk, klen, causal, p, seed)
-    ref = runs["bf16 fwd_sq=1 bwd_sq=0"][0]          # the production forward's mask
+    ref = runs["bf16 fwd_sq=1 stored=True"][0]          # the production forward's mask
     frac = ref.sum().item() / allowed.sum().item()
     assert 0.88 < frac < 0.92, frac                  # keep probability 1 - p
     for label, masks in runs.items():
@@ -370,8 +342,8 @@ def test_attention_dropout_mask_bitexact(dev, lib_opt, case):
 @pytest.mark.parametrize("case", CASES)
 def test_attention_bias_grad(dev, dtype, case):
     """avsr_attn_params.db: += the column sums of the dQ | dK | dV the backward stores (the fused
-    q/k/v bias gradients; the resident bf16 kernels sum them in their store epilogues, the other
-    paths in a pass over the outputs) — against fp64 sums of the stored tensors, dropout on"""
+    q/k/v bias gradients, one pass over the outputs after the backward kernels) — against fp64
+    sums of the stored tensors, dropout on"""
     B, H, Lq, Lk, klen, causal = case
     D = H * 64
     g = torch.Generator().manual_seed(B * 7 + Lk)
@@ -401,3 +373,93 @@ def test_attention_bias_grad(dev, dtype, case):
         mag = torch.cat([t.double().abs().sum(0) for t in (dq, dk, dv)]).cpu()
         got = (db.double() - db0.double()).cpu()
         assert ((got - want).abs() <= 2e-6 * mag + 1e-5).all(), (mode, (got - want).abs().max().item())
+
+
+# ---------------------------------------------------------------------------------------------
+# Stored dropout keep masks (avsr_attn_dropmask): the layout of include/avsr_hip.h against a
+# numpy restatement of the attention dropout's counter hash (AttnDrop, attention.hip: pair index
+# g = ((b*H + h) * Lq + q) * ceil(Lk / 2) + k / 2, fmix32(g * 0x9E3779B1 ^ pre), 16-bit half by
+# key parity, kept iff >= round(p * 65536)); and kernel outputs with the stored mask == hashed.
+# ---------------------------------------------------------------------------------------------
+def _fmix32(h):
+    h = h ^ (h >> np.uint64(16)); h = (h * np.uint64(0x85EBCA6B)) & np.uint64(0xFFFFFFFF)
+    h = h ^ (h >> np.uint64(13)); h = (h * np.uint64(0xC2B2AE35)) & np.uint64(0xFFFFFFFF)
+    return h ^ (h >> np.uint64(16))
+
+
+def _keep_ref(B, H, Lq, Lk, p, seed):
+    """[B*H, Lq, Lk] bool keep decisions of the attention dropout (32-bit index form)"""
+    seed = np.uint64(seed)
+    lo, hi = seed & np.uint64(0xFFFFFFFF), seed >> np.uint64(32)
+    pre = lo ^ _fmix32(np.uint64(0) ^ hi ^ np.uint64(0x68E31DA4))
+    thr = int(np.float32(p) * np.float32(65536.0) + np.float32(0.5))
+    npair = (Lk + 1) // 2
+    bh = np.arange(B * H, dtype=np.uint64)[:, None, None]
+    q = np.arange(Lq, dtype=np.uint64)[None, :, None]
+    k = np.arange(Lk, dtype=np.uint64)[None, None, :]
+    g = ((bh * np.uint64(Lq) + q) * np.uint64(npair) + (k >> np.uint64(1))) & np.uint64(0xFFFFFFFF)
+    h = _fmix32(((g * np.uint64(0x9E3779B1)) & np.uint64(0xFFFFFFFF)) ^ pre)
+    u = np.where((k & np.uint64(1)) == 1, h >> np.uint64(16), h & np.uint64(0xFFFF))
+    return u >= thr
+
+
+def _unpack_mask(words, B, H, Lq, Lk):
+    """the lane-mask layout of AVSR_ATTN_MASK_WORDS back to [B*H, Lq, Lk] bools"""
+    NQB, NKB = -(-Lq // 32), 2 * (-(-Lk // 64))
+    w = words.view(np.uint64)
+    bits = ((w[:, None] >> np.arange(64, dtype=np.uint64)[None, :]) & np.uint64(1)).astype(bool)   # [W, 64]
+    r = np.arange(16)[:, None]
+    l = np.arange(64)[None, :]
+    qi = np.broadcast_to(l & 31, (16, 64))
+    ki = np.broadcast_to((r & 3) + 8 * (r >> 2) + 4 * (l >> 5), (16, 64))
+    t = bits.reshape(B * H, NQB, NKB, 16, 64)
+    full = np.zeros((B * H, NQB * 32, NKB * 32), dtype=bool)
+    for qb in range(NQB):
+        for kb in range(NKB):
+            full[:, 32 * qb + qi, 32 * kb + ki] = t[:, qb, kb]
+    return full[:, :Lq, :Lk]
+
+
+@pytest.mark.parametrize("B,H,Lq,Lk,p,seed", [(2, 3, 75, 70, 0.1, 0x1234ABCD5678), (1, 2, 41, 375, 0.3, 7),
+                                             (2, 1, 130, 200, 0.05, 2 ** 63 + 11)])
+def test_attention_dropmask_layout(dev, B, H, Lq, Lk, p, seed):
+    """avsr_attn_dropmask writes the documented lane-mask layout of exactly the hash's keep bits
+    (bits past Lq / Lk zero)"""
+    n = ops.attn_mask_words(B, H, Lq, Lk)
+    m = torch.full((n,), -1, dtype=torch.int64, device=dev)
+    ops.attn_dropmask(m, B=B, H=H, Lq=Lq, Lk=Lk, drop_p=p, seed=seed)
+    words = m.cpu().numpy()
+    want = _keep_ref(B, H, Lq, Lk, p, seed)
+    assert 0.9 * (1 - p) < want.mean() < 1.1 * (1 - p)
+    got = _unpack_mask(words, B, H, Lq, Lk)
+    assert np.array_equal(got, want), (got ^ want).sum()
+    assert np.unpackbits(words.view(np.uint8)).sum() == want.sum()            # nothing set past Lq / Lk
+
+
+@pytest.mark.parametrize("B,H,L,klen", [(16, 16, 375, [375, 301] * 8), (3, 2, 200, [200, 129, 64])])
+def test_attention_stored_mask_outputs_identical(dev, B, H, L, klen):
+    """the encoder's production path (bf16, keep mask from avsr_attn_dropmask) returns exactly the
+    forward output and the dQ / dK / dV of the hashing kernels: torch.equal"""
+    D = H * 64
+    g = torch.Generator().manual_seed(L + 3)
+    bf = torch.bfloat16
+    qkv = torch.randn(B * L, 3 * D, generator=g).to(dev, bf)
+    q, k, v = qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:]
+    dout = torch.randn(B * L, D, generator=g).to(dev, bf)
+    kl = torch.tensor(klen, dtype=torch.int32, device=dev)
+    kw = dict(B=B, H=H, Lq=L, Lk=L, klen=kl, scale=0.125, drop_p=0.1, seed=31337)
+    mask = ops.attn_dropmask(torch.empty(ops.attn_mask_words(B, H, L, L), dtype=torch.int64, device=dev),
+                             B=B, H=H, Lq=L, Lk=L, drop_p=0.1, seed=31337)
+    res = []
+    for mk in (None, mask):
+        o = torch.empty(B * L, D, device=dev, dtype=bf)
+        lse = torch.empty(B, H, L, device=dev)
+        ops.attn_fwd(q, k, v, o, lse, mask=mk, **kw)
+        dq = torch.empty(B * L, D, device=dev, dtype=bf)
+        dk = torch.empty(B * L, D, device=dev, dtype=bf)
+        dv = torch.empty(B * L, D, device=dev, dtype=bf)
+        delta = torch.empty(B, H, L, device=dev)
+        ops.attn_bwd(dout, q, k, v, o, lse, None, dk, dv, delta, dq=dq, mask=mk, **kw)
+        res.append((o, lse, dq, dk, dv))
+    for name, a, b in zip(("o", "lse", "dq", "dk", "dv"), *res):
+        assert torch.equal(a, b), (name, (a.float() - b.float()).abs().max().item())

@@ -1,6 +1,6 @@
-"""Encoder self-attention fwd / bwd timing at C2 (B=16, H=16, L=375, dh=64), with and without
-probability dropout; with `db` also the fused q/k/v bias-gradient variant of the backward against
-the separate column-sum pass. usage: python tools/attn_bench.py [db]"""
+"""Encoder self-attention fwd / bwd timing at C2 (B=16, H=16, L=375, dh=64), without and with
+probability dropout, the dropout hashed per element or read from the stored keep mask
+(avsr_attn_dropmask, also timed). usage: python tools/attn_bench.py"""
 import os
 import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -17,10 +17,11 @@ do = torch.randn_like(o)
 dq = torch.empty_like(o); dk = torch.empty_like(o); dv = torch.empty_like(o)
 delta = torch.empty(B * H * L, device=dev)
 klen = torch.full((B,), L, device=dev, dtype=torch.int32)
+mask = torch.empty(ops.attn_mask_words(B, H, L, L), device=dev, dtype=torch.int64)
 fl = 4.0 * B * H * L * L * D
 
 
-def tm(fn, n=20):
+def tm(fn, n=50):
     fn(); torch.cuda.synchronize()
     a = torch.cuda.Event(enable_timing=True); b = torch.cuda.Event(enable_timing=True)
     a.record()
@@ -30,18 +31,12 @@ def tm(fn, n=20):
     return a.elapsed_time(b) / n
 
 
-for p in (0.0, 0.1):
-    f = tm(lambda: ops.attn_fwd(q, k, v, o, lse, B=B, H=H, Lq=L, Lk=L, klen=klen, drop_p=p, seed=3))
+for p, stored in ((0.0, False), (0.1, False), (0.1, True)):
+    m = ops.attn_dropmask(mask, B=B, H=H, Lq=L, Lk=L, drop_p=p, seed=3) if stored else None
+    f = tm(lambda: ops.attn_fwd(q, k, v, o, lse, B=B, H=H, Lq=L, Lk=L, klen=klen, drop_p=p, seed=3, mask=m))
     g = tm(lambda: ops.attn_bwd(do, q, k, v, o, lse, None, dk, dv, delta, B=B, H=H, Lq=L, Lk=L, klen=klen,
-                                drop_p=p, seed=3, dq=dq))
-    print(f"drop {p}: fwd {f * 1e3:.1f} us ({fl / f / 1e9:.0f} TF/s)  bwd(prep+dkdv+dq) {g * 1e3:.1f} us "
-          f"({2.5 * fl / g / 1e9:.0f} TF/s)", flush=True)
-db = torch.zeros(3 * H * D, device=dev)
-for p in ((0.0, 0.1) if "db" in sys.argv[1:] else ()):   # `python tools/attn_bench.py db`
-    g0 = tm(lambda: ops.attn_bwd(do, q, k, v, o, lse, None, dk, dv, delta, B=B, H=H, Lq=L, Lk=L, klen=klen,
-                                 drop_p=p, seed=3, dq=dq))
-    g1 = tm(lambda: ops.attn_bwd(do, q, k, v, o, lse, None, dk, dv, delta, B=B, H=H, Lq=L, Lk=L, klen=klen,
-                                 drop_p=p, seed=3, dq=dq, db=db))
-    g2 = tm(lambda: ops.ew_bwd(qkv, db=db))
-    print(f"drop {p}: bwd {g0 * 1e3:.1f} us, with fused q/k/v bias grads {g1 * 1e3:.1f} us; "
-          f"separate column-sum pass over dqkv {g2 * 1e3:.1f} us", flush=True)
+                                drop_p=p, seed=3, dq=dq, mask=m))
+    print(f"drop {p} {'stored mask' if stored else 'hashed'}: fwd {f * 1e3:.1f} us ({fl / f / 1e9:.0f} TF/s)  "
+          f"bwd(dkdv+dq) {g * 1e3:.1f} us ({2.5 * fl / g / 1e9:.0f} TF/s)", flush=True)
+t = tm(lambda: ops.attn_dropmask(mask, B=B, H=H, Lq=L, Lk=L, drop_p=0.1, seed=3))
+print(f"dropmask ({mask.numel() * 8 / 1e6:.1f} MB): {t * 1e3:.1f} us", flush=True)

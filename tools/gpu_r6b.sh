@@ -1,0 +1,10 @@
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+O=gpurun_out/r6b; mkdir -p $O
+timeout -k 10 600 python -u -m pytest tests/test_gpu_attention.py -q -x -rf --timeout 300 --timeout-method thread > $O/tests.log 2>&1; rc=$?
+grep -E "^(FAILED|ERROR)|passed|failed" $O/tests.log | tail -15
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 120 python -u tools/attn_bench.py > $O/attn.log 2>&1 || { cat $O/attn.log; exit 1; }
+cat $O/attn.log
+REPS="1 2" timeout -k 10 900 bash tools/gpu_flag_ab.sh r6b/ab base ATTN_MASK=0
