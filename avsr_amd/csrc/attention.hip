@@ -15,6 +15,7 @@
 // fp32 storage ("parity mode") runs the same tiles on bf16 hi/lo splits (3 products).
 #include "common.h"
 #include <algorithm>
+#include <type_traits>
 #include <cstdlib>
 
 namespace {
@@ -746,6 +747,19 @@ AVSR_DEV void stamp(int slot) {
     }
   }
 }
+// the same per workgroup for a 1-D grid at buffer offset `part` x (6 x gridDim.x): the encoder
+// backward's dQ (part 0) and dK / dV (part 1) kernels
+AVSR_DEV void stamp_part(int slot, int part) {
+  unsigned long long* st = g_stamps;
+  if (st != nullptr && threadIdx.x == 0) {
+    unsigned long long* o = st + ((unsigned long long)part * gridDim.x + blockIdx.x) * 6;
+    o[slot] = __builtin_amdgcn_s_memrealtime();
+    if (slot == 0) {
+      o[4] = (unsigned long long)__builtin_amdgcn_s_getreg((4) | (0 << 6) | (31 << 11));
+      o[5] = (unsigned long long)__builtin_amdgcn_s_getreg((20) | (0 << 6) | (31 << 11));
+    }
+  }
+}
 constexpr int MAXR = 384;           // resident rows per (b, h)
 constexpr int MAXW = MAXR / 32;     // waves per workgroup (768 threads)
 constexpr uint32_t GOLD = 0x9E3779B1u;
@@ -1207,36 +1221,45 @@ __global__ __launch_bounds__(768) void attn_bwd_dq_kernel(AttnArgs a, OutT* dq, 
   }
 }
 
-// the keep masks of avsr_attn_dropmask: one wave per 32 x 32 tile (bh, qb, kb) writes the
-// tile's 16 lane masks, query on the lane (AttnDrop's bits, 0 past Lq / Lk). Register pair
-// (r, r + 1) of a lane holds keys 2j, 2j + 1: one hash per pair, 32-bit index arithmetic.
-__global__ __launch_bounds__(256) void attn_mask_kernel(AttnArgs a, uint64_t* mq, int ntiles) {
+// the keep masks of avsr_attn_dropmask: workgroup (qb, bh) of 4 waves, wave w writes the lane
+// masks of the tiles (bh, qb, kb = w, w + 4, ..), query on the lane (AttnDrop's bits, 0 past Lq /
+// Lk). Register pair (r, r + 1) of a lane holds keys 2j, 2j + 1: one hash per pair, 32-bit
+// index arithmetic, no divisions.
+__global__ __launch_bounds__(256) void attn_mask_kernel(AttnArgs a, uint64_t* mq) {
   const int l = threadIdx.x & 63, c = l & 31, hh = l >> 5;
-  const int tile = __builtin_amdgcn_readfirstlane((int)blockIdx.x * 4 + (int)(threadIdx.x >> 6));
-  if (tile >= ntiles) return;                          // wave-uniform
-  const int kb = tile % a.mnkb, r1 = tile / a.mnkb, qb = r1 % a.mnqb, bh = r1 / a.mnqb;
+  const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int qb = blockIdx.x, bh = blockIdx.y;
   const AttnDrop d(a.drop_p, a.seed, a.B, a.H, a.Lq, a.Lk);
   const int q = qb * 32 + c;
   // pair index of register pair (r, r + 1): row (bh, q), pair kb * 16 + ((r & 3) >> 1) + 4 (r >> 2) + 2 hh
-  const uint32_t gG = (((uint32_t)bh * (uint32_t)a.Lq + (uint32_t)min(q, a.Lq - 1)) * d.npair + (uint32_t)(kb * 16 + 2 * hh)) * GOLD;
-  const bool interior = qb * 32 + 32 <= a.Lq && kb * 32 + 32 <= a.Lk;
-  uint32_t wlo = 0, whi = 0;                           // lane r < 16: lane mask r
+  const uint32_t rowG = (((uint32_t)bh * (uint32_t)a.Lq + (uint32_t)min(q, a.Lq - 1)) * d.npair + (uint32_t)(2 * hh)) * GOLD;
+  uint64_t* out = mq + ((int64_t)bh * a.mnqb + qb) * a.mnkb * 16;
+  auto tile = [&](int kb, auto edge) {
+    const uint32_t gG = rowG + (uint32_t)(kb * 16) * GOLD;
+    // edge tiles: thresholds that reject keys past Lk and every key of a query past Lq
+    const int klim = q < a.Lq ? a.Lk - kb * 32 - 4 * hh : -1;
+    uint32_t wlo = 0, whi = 0;                         // lane r < 16: lane mask r
 #pragma unroll
-  for (int r = 0; r < 16; r += 2) {
-    const uint32_t hv = hashG(gG + (uint32_t)(((r & 3) >> 1) + 4 * (r >> 2)) * GOLD, d.pre);
-    bool k0 = (hv & 0xFFFFu) >= d.thr, k1 = (hv >> 16) >= d.thr;
-    if (!interior) {
-      const int k = kb * 32 + qrow(r, hh);
-      k0 = k0 & (q < a.Lq) & (k < a.Lk);
-      k1 = k1 & (q < a.Lq) & (k + 1 < a.Lk);
+    for (int r = 0; r < 16; r += 2) {
+      const uint32_t hv = hashG(gG + (uint32_t)(((r & 3) >> 1) + 4 * (r >> 2)) * GOLD, d.pre);
+      bool k0 = (hv & 0xFFFFu) >= d.thr, k1 = (hv >> 16) >= d.thr;
+      if (edge) {
+        const int kr = (r & 3) + 8 * (r >> 2);        // key offset in the tile, minus 4 hh
+        k0 = k0 & (kr < klim);
+        k1 = k1 & (kr + 1 < klim);
+      }
+      const uint64_t b0 = __ballot(k0), b1 = __ballot(k1);
+      wlo = l == r ? (uint32_t)b0 : wlo;
+      whi = l == r ? (uint32_t)(b0 >> 32) : whi;
+      wlo = l == r + 1 ? (uint32_t)b1 : wlo;
+      whi = l == r + 1 ? (uint32_t)(b1 >> 32) : whi;
     }
-    const uint64_t b0 = __ballot(k0), b1 = __ballot(k1);
-    wlo = l == r ? (uint32_t)b0 : wlo;
-    whi = l == r ? (uint32_t)(b0 >> 32) : whi;
-    wlo = l == r + 1 ? (uint32_t)b1 : wlo;
-    whi = l == r + 1 ? (uint32_t)(b1 >> 32) : whi;
+    if (l < 16) out[kb * 16 + l] = ((uint64_t)whi << 32) | wlo;
+  };
+  for (int kb = w; kb < a.mnkb; kb += 4) {
+    if (qb * 32 + 32 <= a.Lq && kb * 32 + 32 <= a.Lk) tile(kb, std::false_type());
+    else tile(kb, std::true_type());
   }
-  if (l < 16) mq[(int64_t)tile * 16 + l] = ((uint64_t)whi << 32) | wlo;
 }
 
 // launch geometry: waves per workgroup (<= 12) covering `rows` 32-row blocks, grid.y chunks
@@ -1293,8 +1316,14 @@ typedef short s4v __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) s4v lds_s4v;
 
 AVSR_DEV int swz(int row) { const int g = (row >> 1) & 7; return g ^ ((g & 1) << 2); }
+// base and extent are wave-uniform at every call; readfirstlane states it, so the descriptor
+// always lands in SGPRs (the DMA asm requires them)
 AVSR_DEV __amdgpu_buffer_rsrc_t rsrc(const void* base, uint32_t bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+  const uint64_t b = (uint64_t)(uintptr_t)base;
+  const uint64_t ub = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(b >> 32)) << 32) |
+                      (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)b);
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(uintptr_t)ub, (short)0, (int)__builtin_amdgcn_readfirstlane(bytes),
+                                           0x00020000);
 }
 // one wave-instruction: 64 lanes x 16 B (x4: 4 B) -> 1 KiB (256 B) of LDS at lds_wave_base.
 // Inline asm as gemm_glds.h bglds16: the compiler's waitcnt pass would otherwise drain the
@@ -1539,6 +1568,7 @@ __global__ __launch_bounds__(NTH) void attn_bwd_dq_kernel(AttnArgs a, OutT* dq, 
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* Ks = smem;
   char* Vs = smem + IMG384;
+  stamp_part(0, 0);
   const int bh = xcd_id(blockIdx.x, gridDim.x), b = bh / a.H, h = bh % a.H;
   const int tid = threadIdx.x, l = tid & 63, c = l & 31, hh = l >> 5;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1596,6 +1626,7 @@ __global__ __launch_bounds__(NTH) void attn_bwd_dq_kernel(AttnArgs a, OutT* dq, 
     if (r == 2) vmwait<2>();
     if (r == 3) vmwait<0>();
     round_barrier();                                       // round r of every wave has landed
+    if (r == 0) stamp_part(1, 0);
     const int tend = min(nt, 3 * r + 3);
     if (q0 < a.Lq) {
       for (; t < tend; ++t) {
@@ -1638,10 +1669,15 @@ __global__ __launch_bounds__(NTH) void attn_bwd_dq_kernel(AttnArgs a, OutT* dq, 
       }
     }
   }
+  stamp_part(2, 0);
   __syncthreads();                                         // images no longer read: store slabs
   if (q0 < a.Lq) {
     OutT* DQ = dq + ((int64_t)b * a.Lq + q0) * lddq + h * DH;
     store_t<OutT>(dq0, dq1, a.scale, (float*)smem + w * 32 * 65, DQ, lddq, a.Lq - q0);
+  }
+  if (g_stamps != nullptr) {
+    __syncthreads();
+    stamp_part(3, 0);
   }
 }
 
@@ -1653,6 +1689,7 @@ __global__ __launch_bounds__(NTH) void attn_bwd_dkdv_kernel(AttnArgs a) {
   float* lss = (float*)(smem + 2 * IMG384);                // lse, then lse * log2(e) (0 past Lq)
   float* dls = lss + MAXR;                                 // delta (0 past Lq)
   char* Kw = smem + 2 * IMG384 + 2 * MAXR * 4;             // this wave's [32][64] K image
+  stamp_part(0, 1);
   const int bh = xcd_id(blockIdx.x, gridDim.x), b = bh / a.H, h = bh % a.H;
   const int tid = threadIdx.x, l = tid & 63, c = l & 31, hh = l >> 5;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1711,6 +1748,7 @@ __global__ __launch_bounds__(NTH) void attn_bwd_dkdv_kernel(AttnArgs a) {
     if (r == 2) vmwait<2>();
     if (r == 3) vmwait<0>();
     round_barrier();                       // round r landed (r = 0: the lse scaling is visible)
+    if (r == 0) stamp_part(1, 1);
     const int tend = min(nt, 3 * r + 3);
     if (active) {
       for (; t < tend; ++t) {
@@ -1781,6 +1819,7 @@ __global__ __launch_bounds__(NTH) void attn_bwd_dkdv_kernel(AttnArgs a) {
       }
     }
   }
+  stamp_part(2, 1);
   __syncthreads();
   if (kb0 < a.Lk) {
     float* scr = (float*)smem + w * 32 * 65;
@@ -1788,6 +1827,10 @@ __global__ __launch_bounds__(NTH) void attn_bwd_dkdv_kernel(AttnArgs a) {
     store_t<bf16>(dk0, dk1, a.scale, scr, DK, a.lddk, a.Lk - kb0);
     bf16* DV = (bf16*)a.dv + ((int64_t)b * a.Lk + kb0) * a.lddv + h * DH;
     store_t<bf16>(dv0, dv1, dscale, scr, DV, a.lddv, a.Lk - kb0);
+  }
+  if (g_stamps != nullptr) {
+    __syncthreads();
+    stamp_part(3, 1);
   }
 }
 constexpr size_t DQ_LDS = 2 * IMG384 > NTH / 64 * 32 * 65 * 4 ? 2 * IMG384 : NTH / 64 * 32 * 65 * 4;
@@ -1871,10 +1914,9 @@ extern "C" int avsr_attn_dropmask(const avsr_attn_params* p, void* stream) {
   avsr_attn_params q = *p;
   q.dtype = AVSR_BF16; q.causal = 0;                    // the layout args() fills for the mask readers
   AttnArgs a = args(&q);
-  const int64_t ntiles = (int64_t)p->B * p->H * a.mnqb * a.mnkb;
-  if (ntiles > 0x7ffffff0L) return AVSR_E_SHAPE;
-  hipLaunchKernelGGL(res::attn_mask_kernel, dim3((unsigned)((ntiles + 3) / 4)), dim3(256), 0, (hipStream_t)stream, a,
-                     const_cast<uint64_t*>(a.mq), (int)ntiles);
+  if ((int64_t)p->B * p->H > 65535) return AVSR_E_SHAPE;
+  hipLaunchKernelGGL(res::attn_mask_kernel, dim3(a.mnqb, p->B * p->H), dim3(256), 0, (hipStream_t)stream, a,
+                     const_cast<uint64_t*>(a.mq));
   AVSR_CHECK_LAUNCH();
   return 0;
 }

@@ -412,9 +412,10 @@ typedef struct {
 #define AVSR_ATTN_DB_WS(B, H) ((int64_t)(B) * 3 * (H) * 64)
 #define AVSR_ATTN_MASK_WORDS(B, H, Lq, Lk) \
   ((int64_t)(B) * (H) * (((Lq) + 31) / 32) * (2 * (((Lk) + 63) / 64)) * 16)
-/* diagnostic (not product path): per-workgroup s_memrealtime stamps of the resident attention
- * forward into buf[6 * workgroups] (start, first K/V round, compute done, end, HW_ID, XCC_ID);
- * buf = NULL turns them off */
+/* diagnostic (not product path): per-workgroup s_memrealtime stamps (start, first round
+ * landed, compute done, end, HW_ID, XCC_ID) of the resident attention forward into
+ * buf[6 * workgroups], and of the encoder backward's dQ / dK-dV kernels into buf[6 * B * H]
+ * / buf[6 * B * H ..]; buf = NULL turns them off */
 int avsr_debug_attn_stamps(unsigned long long* buf);
 int avsr_attn_fwd(const avsr_attn_params* p, void* stream);
 int avsr_attn_bwd_prep(const avsr_attn_params* p, void* stream);   /* delta = rowsum(dO * O) */
