@@ -139,15 +139,19 @@ AVSR_DEV void store_t(const f32x16& x0, const f32x16& x1, float mul, float* st, 
     st[c * 65 + 32 + qrow(r, hh)] = x1[r] * mul;
   }
   __syncthreads();
-  const int i = l >> 1, cb = (l & 1) * 32;
-  constexpr int VE = 16 / (int)sizeof(T);
-  if (i < nvalid) {
+  // each store instruction writes whole 128-byte (bf16) / 256-byte (fp32) output rows: lane l
+  // takes row i0 + l / LPR, elements (l % LPR) * VE ..; the slab reads are conflict-free (row
+  // stride 65 floats)
+  constexpr int VE = 16 / (int)sizeof(T), LPR = 64 / VE, RPI = 64 / LPR;
+  const int rr = l / LPR, ch = (l % LPR) * VE;
 #pragma unroll
-    for (int e = 0; e < 32; e += VE) {
+  for (int i0 = 0; i0 < 32; i0 += RPI) {
+    const int i = i0 + rr;
+    if (i < nvalid) {
       float v[VE];
 #pragma unroll
-      for (int j = 0; j < VE; ++j) v[j] = st[i * 65 + cb + e + j];
-      stv(out + (int64_t)i * ld + cb + e, v);
+      for (int j = 0; j < VE; ++j) v[j] = st[i * 65 + ch + j];
+      stv(out + (int64_t)i * ld + ch, v);
     }
   }
 }
