@@ -250,6 +250,7 @@ SYMBOLS = {
     "avsr_set_option": ([_i, _i64], _i),
     "avsr_get_option": ([_i], _i64),
     "avsr_gemm": ([ctypes.POINTER(GemmParams), _c_p], _i),
+    "avsr_gemm_wgrad_group": ([ctypes.POINTER(GemmParams), _i, _c_p], _i),
     "avsr_gemm_skinny_splits": ([_i, _i, _i], _i),
     "avsr_conv_fwd": ([ctypes.POINTER(ConvParams), _c_p], _i),
     "avsr_conv_bwd_data": ([ctypes.POINTER(ConvParams), _c_p], _i),

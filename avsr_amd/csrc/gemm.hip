@@ -104,12 +104,10 @@ __global__ __launch_bounds__(CF::NTH, CF::MINB) void dense_glds_kernel(DenseArgs
 // from LDS, the others with sc1 loads), writes C = alpha*sum + beta*C — the arithmetic of
 // slab_reduce_kernel, which this replaces — and resets the counter (cdna_hip_programming.md
 // Guideline 16, counter form).
-template <class CF, bool FR = false>     // FR: the in-kernel slab reduction (its own register budget)
-__global__ __launch_bounds__(2 * CF::NTH, 1) void wgrad_dual_kernel(DenseArgs a, int tiles_m, int tiles_n) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
+template <class CF, bool FR>     // FR: the in-kernel slab reduction (its own register budget)
+__device__ __forceinline__ void wgrad_dual_body(const DenseArgs& a, int tiles_m, int tiles_n, int id, char* smem) {
   static_assert(CF::BM * (CF::BN + 4) * 4 <= 2 * CF::S * CF::STAGE, "reduction tile exceeds the two rings");
   if (a.stamp != nullptr && threadIdx.x == 0) atomicMin(a.stamp, (unsigned long long)__builtin_amdgcn_s_memrealtime());
-  const int id = gemmg::xcd_remap(blockIdx.x, gridDim.x);
   int tm, tn, sp;
   if (a.cnt) {                                      // splits innermost: a tile's splits share an XCD
     int z;
@@ -265,6 +263,32 @@ __global__ __launch_bounds__(2 * CF::NTH, 1) void wgrad_dual_kernel(DenseArgs a,
     __syncthreads();
     if (threadIdx.x == 0) atomicMax(a.stamp + 1, (unsigned long long)__builtin_amdgcn_s_memrealtime());
   }
+}
+
+template <class CF, bool FR = false>
+__global__ __launch_bounds__(2 * CF::NTH, 1) void wgrad_dual_kernel(DenseArgs a, int tiles_m, int tiles_n) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  wgrad_dual_body<CF, FR>(a, tiles_m, tiles_n, gemmg::xcd_remap(blockIdx.x, gridDim.x), smem);
+}
+
+// several weight-gradients in one grid (avsr_gemm_wgrad_group): block ids [start[q], start[q+1])
+// are problem q's output tiles, each block the whole K range (no split). Two problems that leave
+// part of the chip idle alone fill it together (encoder out-proj 64 + QKV 192 tiles = 256 = one
+// block per CU).
+constexpr int WG_MAX = 4;
+struct WgGroup {
+  DenseArgs a[WG_MAX];
+  int tm[WG_MAX], tn[WG_MAX], start[WG_MAX + 1];
+};
+template <class CF>
+__global__ __launch_bounds__(2 * CF::NTH, 1) void wgrad_group_kernel(WgGroup g) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int id = gemmg::xcd_remap(blockIdx.x, gridDim.x);
+  int q = 0;
+#pragma unroll
+  for (int i = 1; i < WG_MAX; ++i) q += id >= g.start[i];
+  q = __builtin_amdgcn_readfirstlane(q);
+  wgrad_dual_body<CF, false>(g.a[q], g.tm[q], g.tn[q], id - g.start[q], smem);
 }
 
 // 256x256 ping-pong core (gemm_pp.h)
@@ -1072,6 +1096,52 @@ extern "C" int avsr_gemm(const avsr_gemm_params* p, void* stream) {
   const dim3 g((unsigned)avsr_grid(per, 256, 4096), p->batch);
   hipLaunchKernelGGL(slab_reduce_kernel, g, dim3(256), 0, st, (const float*)p->ws, splits, p->M, p->N,
                      (int64_t)p->M * p->N + AVSR_GEMM_SLAB_PAD, (float*)p->C, p->ldc, p->strideC, p->alpha, p->beta);
+  AVSR_CHECK_LAUNCH();
+  return 0;
+}
+
+// grouped weight-gradients: each problem must be the plain wgrad_dual shape (bf16 operands, both
+// r-contiguous, fp32 C, no epilogue, no split); otherwise the problems run one by one
+extern "C" int avsr_gemm_wgrad_group(const avsr_gemm_params* ps, int n, void* stream) {
+  if (!ps || n < 1 || n > WG_MAX) return AVSR_E_ARG;
+  bool grouped = true;
+  for (int i = 0; i < n; ++i) {
+    const avsr_gemm_params* p = ps + i;
+    if (p->M <= 0 || p->N <= 0 || p->K <= 0 || p->batch != 1) return AVSR_E_SHAPE;
+    grouped = grouped && glds_ok(p) && p->splitk <= 1 && !p->ws && !p->stamp && wgrad_dual_ok(p, 1, false) &&
+              avsr_aligned16(p->A) && avsr_aligned16(p->B) && (p->lda % 8) == 0 && (p->ldb % 8) == 0;
+  }
+  if (!grouped) {
+    for (int i = 0; i < n; ++i) {
+      const int rc = avsr_gemm(ps + i, stream);
+      if (rc) return rc;
+    }
+    return 0;
+  }
+  using CF = CfgDual;
+  WgGroup g;
+  std::memset(&g, 0, sizeof(g));
+  int total = 0;
+  for (int i = 0; i < n; ++i) {
+    const avsr_gemm_params* p = ps + i;
+    DenseArgs& a = g.a[i];
+    a.M = p->M; a.N = p->N; a.K = p->K; a.splits = 1;
+    a.kchunk = (p->K + gemmg::GBK - 1) / gemmg::GBK * gemmg::GBK;
+    const int64_t ea = ((int64_t)(p->K - 1) * p->lda + p->M) * 2, eb = ((int64_t)(p->K - 1) * p->ldb + p->N) * 2;
+    const int64_t lim = (int64_t)gemmg::OOB - (1 << 20);
+    const bool ok = ea < lim && eb < lim;
+    a.a_bytes = ok ? (uint32_t)ea : 0u;
+    a.b_bytes = ok ? (uint32_t)eb : 0u;
+    a.A = p->A; a.lda = p->lda; a.B = p->B; a.ldb = p->ldb;
+    a.e.M = p->M; a.e.N = p->N; a.e.C = p->C; a.e.ldc = p->ldc; a.e.alpha = p->alpha; a.e.beta = p->beta;
+    g.tm[i] = (p->M + CF::BM - 1) / CF::BM;
+    g.tn[i] = (p->N + CF::BN - 1) / CF::BN;
+    g.start[i] = total;
+    total += g.tm[i] * g.tn[i];
+  }
+  for (int i = n; i <= WG_MAX; ++i) g.start[i] = total;
+  hipLaunchKernelGGL(wgrad_group_kernel<CF>, dim3((unsigned)total), dim3(2 * CF::NTH), 2 * CF::S * CF::STAGE,
+                     (hipStream_t)stream, g);
   AVSR_CHECK_LAUNCH();
   return 0;
 }

@@ -42,6 +42,11 @@ _DB_FUSE = True
 _COLSUM_DEFER = True
 # bias gradients of operands only the side stream's weight-grads read run on the side stream
 _SIDE_BIAS = True
+# encoder QKV and out-proj weight-gradients as one grouped launch (192 + 64 output tiles = one
+# block per CU) instead of a 192-tile launch beside 64 idle CUs and a 64-tile x 4 split-K launch:
+# 68.1 vs 66.7 + 30.2 us isolated, but 0.4-0.6 % slower in the step (its 256 long 128-KiB blocks
+# hold every CU while the data-gradient chain waits; profiles/r06_wgrad_group_ab.txt): off
+WGRAD_GROUP = False
 # encoder self-attention dropout from stored keep masks (avsr_attn_dropmask, generated for every
 # layer on the side stream while the step stream runs the frontends) instead of a hash per score
 # element in the forward, dK/dV and dQ kernels (same bits)
@@ -903,7 +908,8 @@ class Engine:
         go = self._e(M, D)              # fresh: g2 may still be read by the side stream
         dx1 = self._ln_bwd(dln2, lc["x1"], p + "final_layer_norm", lc["m2"], lc["r2"], dres=dx2, dx=dx2,
                            ew=(go, lc["p_h"], lc["sd_o"], a + "out_proj.bias"))
-        self._wgrad(go, lc["o"], self.g(a + "out_proj.weight"))
+        if not WGRAD_GROUP:
+            self._wgrad(go, lc["o"], self.g(a + "out_proj.weight"))
         do = ops.linear_dgrad(go, self.w(a + "out_proj.weight"))
         # attention
         qkv = lc["qkv"]
@@ -920,7 +926,13 @@ class Engine:
             ops.cast(dq32, dqkv[:, :D])
         # the q/k/v bias gradients (column sums of dqkv) on the side stream
         self._bias_grad_side(dqkv, db_qkv)
-        self._wgrad(dqkv, lc["ln1"], self.arena.span(names_w, buf="g"))
+        if WGRAD_GROUP:     # QKV (192 tiles) and out-proj (64 tiles) weight-gradients in one launch
+            dwq, dwo = self.arena.span(names_w, buf="g"), self.g(a + "out_proj.weight")
+            o = lc["o"]
+            ln1 = lc["ln1"]
+            self._on_side(lambda: ops.wgrad_group([(dqkv, ln1, dwq, 1.0), (go, o, dwo, 1.0)]), dqkv, ln1, go, o)
+        else:
+            self._wgrad(dqkv, lc["ln1"], self.arena.span(names_w, buf="g"))
         dln1 = ops.linear_dgrad(dqkv, self.arena.span(names_w))
         ew = self._ew_next(lc_prev["i"], lc_prev, M) if lc_prev is not None else None
         dx = self._ln_bwd(dln1, lc["x"], p + "layer_norm", lc["m1"], lc["r1"], dres=dx1, dx=dx1, ew=ew)

@@ -178,6 +178,25 @@ def gemm(A, B, C, *, M, N, K, a_kmajor, b_kmajor, lda, ldb, ldc, batch=1,
     return C
 
 
+def wgrad_group(problems):
+    """several weight-gradients dW (fp32, [N][K]) += alpha * dy^T x (dy [M][N], x [M][K], bf16)
+    in one launch (avsr_gemm_wgrad_group): problems = [(dy, x, dW, alpha), ...], at most 4"""
+    lib = L.load()
+    arr = (L.GemmParams * len(problems))()
+    for p, (dy, x, dW, alpha) in zip(arr, problems):
+        assert dy.dtype == x.dtype == torch.bfloat16 and dW.dtype == torch.float32
+        M, N = dy.shape
+        K = x.shape[1]
+        p.M, p.N, p.K, p.batch = N, K, M, 1
+        p.dtype, p.a_kmajor, p.b_kmajor, p.c_f32 = L.AVSR_BF16, 0, 0, 1
+        p.A, p.lda = dy.data_ptr(), dy.stride(0)
+        p.B, p.ldb = x.data_ptr(), x.stride(0)
+        p.C, p.ldc = dW.data_ptr(), dW.stride(0)
+        p.alpha, p.beta = float(alpha), 1.0
+        p.ldr, p.splitk = dW.stride(0), 1
+    L.check(lib.avsr_gemm_wgrad_group(arr, len(problems), L.stream_ptr()), "avsr_gemm_wgrad_group")
+
+
 # ---------------------------------------------------------------------------------------
 # Linear layer building blocks (x: (M, K) row-major, W: (N, K) = torch.nn.Linear.weight)
 # ---------------------------------------------------------------------------------------

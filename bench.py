@@ -251,25 +251,36 @@ def encoder_gemm_table(dev, M, D, F):
     from avsr_amd import ops
     from tools.gemm_table import timed, wgrad
     g = torch.Generator(device="cpu").manual_seed(0)
-    rows = []
+    from avsr_amd import engine
+    rows, wg = [], {}
     for name, (N, K) in {"qkv": (3 * D, D), "out": (D, D), "ffn1": (F, D), "ffn2": (D, F)}.items():
         x = (torch.randn(M, K, generator=g) * 0.5).to(dev, torch.bfloat16)
         W = (torch.randn(N, K, generator=g) * 0.05).to(dev, torch.bfloat16)
         dy = (torch.randn(M, N, generator=g) * 0.5).to(dev, torch.bfloat16)
         dW = torch.zeros(N, K, device=dev)
+        wg[name] = (dy, x, dW)
         fl = 2.0 * M * N * K
         for op, fn in (("fwd", lambda: ops.linear_fwd(x, W)), ("dgrad", lambda: ops.linear_dgrad(dy, W)),
                        ("wgrad", lambda: wgrad(dy, x, dW))):
             us = timed(fn)
             tf = fl / us / 1e6
             rows.append({"gemm": f"{name} {op}", "us": round(us, 1), "tflops": round(tf, 1),
-                         "frac": round(tf / BF16_PEAK_TFLOPS, 4)})
-    worst = min(rows, key=lambda r: r["frac"])
-    tot_us = sum(r["us"] for r in rows)
+                         "frac": round(tf / BF16_PEAK_TFLOPS, 4),
+                         "engine": not (engine.WGRAD_GROUP and op == "wgrad" and name in ("qkv", "out"))})
+    # the engine's QKV + out-proj weight-gradients: one grouped launch (192 + 64 output tiles)
+    us = timed(lambda: ops.wgrad_group([wg["qkv"] + (1.0,), wg["out"] + (1.0,)]))
+    fl = 2.0 * M * (3 * D * D + D * D)
+    tf = fl / us / 1e6
+    rows.append({"gemm": "qkv+out wgrad (grouped)", "us": round(us, 1), "tflops": round(tf, 1),
+                 "frac": round(tf / BF16_PEAK_TFLOPS, 4), "engine": bool(engine.WGRAD_GROUP)})
+    used = [r for r in rows if r["engine"]]
+    worst = min(used, key=lambda r: r["frac"])
+    tot_us = sum(r["us"] for r in used)
     tot_fl = sum(2.0 * M * N * K for (N, K) in ((3 * D, D), (D, D), (F, D), (D, F))) * 3
     return {"per_shape": rows, "worst": worst, "layer_us": round(tot_us, 1),
             "layer_frac": round(tot_fl / tot_us / 1e6 / BF16_PEAK_TFLOPS, 4),
-            "note": "isolated launches, plain epilogue (tools/gemm_table.py); the in-step probe is `roofline`"}
+            "note": "isolated launches, plain epilogue (tools/gemm_table.py); worst / layer over the launches the "
+                    "engine makes (engine: true); the in-step probe is `roofline`"}
 
 
 def decode_throughput(dev, state_cpu, model_cfg, cpu_threads):

@@ -180,6 +180,13 @@ typedef struct {
 #define AVSR_GEMM_SLAB_WS(batch, splitk, M, N) ((int64_t)(batch) * (splitk) * ((int64_t)(M) * (N) + AVSR_GEMM_SLAB_PAD))
 
 int avsr_gemm(const avsr_gemm_params* p, void* stream);
+/* n <= 4 weight-gradient GEMMs (C fp32 += alpha * A^T B with both operands r-contiguous bf16, no
+ * epilogue, no split: the avsr_gemm weight-gradient shape) in ONE launch whose grid holds every
+ * problem's output tiles — problems that each fill part of the chip fill it together (encoder
+ * out-proj 64 + QKV 192 tiles = 256 = one block per CU). Results equal avsr_gemm's per problem
+ * bit for bit; problems of another shape run one by one through avsr_gemm. Replaces the
+ * nn.Linear weight-gradients of Wav2Vec2Attention (avhubert.py:747-768). */
+int avsr_gemm_wgrad_group(const avsr_gemm_params* p, int n, void* stream);
 /* K-split count the few-row path uses for an N x K weight of this dtype when skinny_ws is given
  * (depends on dtype, N and K only, never on M: a row's result does not depend on how many rows
  * share the launch; fp32 with K % 16 == 0 and 16-byte aligned rows runs the matrix-core kernel) */

@@ -167,6 +167,33 @@ def test_wgrad_dual_kernel(dev, monkeypatch, M, N, K, splitk, lib_opt):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("shapes", [[(6000, 3072, 1024), (6000, 1024, 1024)],          # encoder QKV + out-proj
+                                    [(700, 256, 384), (700, 136, 200), (96, 128, 128)],   # ragged; 3 problems
+                                    [(640, 120, 256), (640, 256, 256)]])                  # one not groupable
+def test_wgrad_group_matches_single(dev, shapes):
+    """avsr_gemm_wgrad_group (several weight-gradients dW += alpha dy^T x in one grid) equals each
+    problem's own avsr_gemm launch (unsplit weight-gradient kernel) bit for bit, beta accumulation
+    included; a problem of another shape (N = 120 < 128: not the weight-gradient core) falls back to
+    one-by-one launches"""
+    g = torch.Generator().manual_seed(sum(a + b + c for a, b, c in shapes))
+    probs = []
+    for M, N, K in shapes:          # dy [M][N], x [M][K], dW [N][K]
+        probs.append((torch.randn(M, N, generator=g).to(dev, torch.bfloat16), torch.randn(M, K, generator=g).to(dev, torch.bfloat16),
+                      torch.randn(N, K, generator=g).to(dev), 0.5))
+    got = [dW.clone() for _, _, dW, _ in probs]
+    ops.wgrad_group([(dy, x, w, al) for (dy, x, _, al), w in zip(probs, got)])
+    for (dy, x, dW, al), gw in zip(probs, got):
+        M, N = dy.shape
+        K = x.shape[1]
+        want = dW.clone()
+        ops.gemm(dy, x, want, M=N, N=K, K=M, a_kmajor=False, b_kmajor=False, lda=dy.stride(0), ldb=x.stride(0),
+                 ldc=want.stride(0), alpha=al, beta=1.0)
+        assert torch.equal(gw, want), (M, N, K, (gw - want).abs().max().item())
+        ref = al * (dy.double().t() @ x.double()) + dW.double()
+        assert _rel(gw, ref) < 1e-5 * (M ** 0.5)
+
+
+@pytest.mark.gpu
 def test_gemm_batched_strided_bf16(dev, gemm_tile):
     """batch > 1 with operand / output strides (attention-style batched products)."""
     g = torch.Generator().manual_seed(5)
