@@ -44,8 +44,10 @@ const char* avsr_version(void);
  *                                 tile configuration k (AVSR_TILE_* below) on the bf16 core
  *   AVSR_OPT_ATTN_SQ_FWD    [1]  1: query-tiled streamed self-attention forward for bf16,
  *                                 L >= 128; 0: the resident-K/V kernel (same rows to 1e-2)
- *   AVSR_OPT_ATTN_SQ_BWD    [0]  retired (round 6: the query-tiled backward was removed; the
- *                                 value is accepted and has no effect)
+ *   AVSR_OPT_ATTN_SQ_BWD    [0]  1: the encoder backward's dQ as the small-footprint kernel
+ *                                 (3 workgroups of 4 waves per head, 24 KiB of LDS: fits beside a
+ *                                 weight-gradient block); 0: one 12-wave workgroup per head
+ *                                 (bit-identical)
  *   AVSR_OPT_WGRAD_DUAL     [1]  1: two-wave-group weight-gradient kernel (fp32 C, both
  *                                 operands r-contiguous); 0: the 4-wave core
  *   AVSR_OPT_CONV_192       [1]  1: 192x128 tiles for conv fwd / data-grad where they still
