@@ -735,27 +735,6 @@ __global__ __launch_bounds__(PCfg::NTH, 2) void conv_patch_kernel(ConvArgs a, Pa
 // 2 x 2), the blocks that share an XCD (ids b, b+8, ...) take the blocks of the same tile range,
 // so x and dy come from that XCD's L2 after the first read. Each block writes its fp32 partial
 // once to a slab [block][64][576]; wpatch_reduce_kernel sums them in block order (deterministic).
-template <int W_, int TR_, int TPI_, int NBUF_, int PST_>
-struct WPGeo {
-  static constexpr int W = W_, TR = TR_, TPI = TPI_, H = TR * TPI, NBUF = NBUF_, PST = PST_;
-  static constexpr int PX = TR * W;                  // pixels per tile
-  static constexpr int KS = (PX + 31) / 32;          // k-steps of 32 pixels
-  static constexpr int DYR = KS * 32;                // dy image rows (>= PX: zero)
-  static constexpr int WP = W + 2, PROWS = (TR + 2) * WP;
-  static constexpr int SLOTS = PST / 16;             // 16-byte slots per patch row (8 data + pad)
-  static constexpr int PPIECE = (PROWS * SLOTS + 255) / 256;   // patch DMA pieces per wave
-  static constexpr int PBYTES = PPIECE * 4 * 1024;
-  static constexpr int DYPIECE = DYR * 128 / 4096;   // dy DMA pieces per wave
-  static constexpr int DYB = DYR * 128;
-  static constexpr int BUF = DYB + PBYTES;
-  static constexpr int LDS = NBUF * BUF;
-  static constexpr int NP = DYPIECE + PPIECE;        // DMAs per wave per tile
-  static_assert(LDS <= 160 * 1024, "the tile buffers must fit the CU's LDS");
-};
-// patch row stride 144 B: one 2-way overlap among 8 consecutive rows' 32-byte windows; 160 B:
-// none (what the LDS allows)
-using WPStage1 = WPGeo<22, 11, 2, 2, 144>;   // half images: 242 pixels, 13 x 24 patch, double buffered
-using WPStage2 = WPGeo<11, 11, 1, 3, 160>;   // whole images: 121 pixels, 13 x 13 patch, 3 buffers (short tiles)
 // Persistent blocks of the stage-1 / stage-2 weight-grads: 128, one on every other CU. These run
 // on the side stream beside the ResNet backward's data-gradient chain, and a block holds up to
 // 152 KB of LDS, so at one block per CU (256) every chain kernel needing LDS waited for free CUs;
@@ -764,7 +743,48 @@ using WPStage2 = WPGeo<11, 11, 1, 3, 160>;   // whole images: 121 pixels, 13 x 1
 #ifndef AVSR_WP_BLOCKS
 #define AVSR_WP_BLOCKS 128
 #endif
-constexpr int WP_BLOCKS = AVSR_WP_BLOCKS, WP_COLS = 576;
+#ifndef AVSR_WP34          // A/B builds only: stages 3-4 on the general weight-grad
+#define AVSR_WP34 1
+#endif
+#ifndef AVSR_WP34_BLOCKS
+#define AVSR_WP34_BLOCKS 128
+#endif
+constexpr int WP_BLOCKS = AVSR_WP_BLOCKS, WP34_BLOCKS = AVSR_WP34_BLOCKS, WP_COLS = 576;
+
+// Stages 3 (6 x 6, 256 channels) and 4 (3 x 3, 512 channels): a tile is IPT whole images stacked
+// vertically in the patch with ONE shared zero row between neighbours (a tap above an image's
+// first row or below its last reads that row), so the 9 taps stay row offsets; IPT is chosen so
+// that IPT x H x W pixels nearly fill whole 32-pixel k-steps (180 of 192, 126 of 128). NBLK
+// persistent blocks; the next tile's DMAs are issued over the first SPREAD k-steps of the current
+// one (with few k-steps per tile, DMAs issued at the last one would have no time to land).
+template <int W_, int TR_, int TPI_, int NBUF_, int PST_, int IPT_ = 1, int NBLK_ = WP_BLOCKS, int SPREAD_ = 0>
+struct WPGeo {
+  static constexpr int W = W_, TR = TR_, TPI = TPI_, H = TR * TPI, NBUF = NBUF_, PST = PST_, IPT = IPT_, NBLK = NBLK_;
+  static constexpr int IMGT = TR * W;                // pixels of one image in a tile
+  static constexpr int PX = IPT * IMGT;              // pixels per tile
+  static constexpr int KS = (PX + 31) / 32;          // k-steps of 32 pixels
+  static constexpr int DYR = KS * 32;                // dy image rows (>= PX: zero)
+  static constexpr int WP = W + 2, PROWS = (IPT * (TR + 1) + 1) * WP;
+  static constexpr int SLOTS = PST / 16;             // 16-byte slots per patch row (8 data + pad)
+  static constexpr int PPIECE = (PROWS * SLOTS + 255) / 256;   // patch DMA pieces per wave
+  static constexpr int PBYTES = PPIECE * 4 * 1024;
+  static constexpr int DYPIECE = DYR * 128 / 4096;   // dy DMA pieces per wave
+  static constexpr int DYB = DYR * 128;
+  static constexpr int BUF = DYB + PBYTES;
+  static constexpr int LDS = NBUF * BUF;
+  static constexpr int NP = DYPIECE + PPIECE;        // DMAs per wave per tile
+  static constexpr int SPREAD = SPREAD_ > 0 ? SPREAD_ : KS;
+  static_assert(LDS <= 160 * 1024, "the tile buffers must fit the CU's LDS");
+  static_assert(IPT == 1 || TPI == 1, "a tile is part of one image or whole images");
+  static_assert(NBUF >= 2 && (NBUF - 2) * NP <= 63 && SPREAD <= KS, "vmcnt range / DMA spread");
+  static_assert(NBLK % 8 == 0, "blocks come in XCD groups of 8");
+};
+// patch row stride 144 B: one 2-way overlap among 8 consecutive rows' 32-byte windows; 160 B:
+// none (what the LDS allows)
+using WPStage1 = WPGeo<22, 11, 2, 2, 144>;   // half images: 242 pixels, 13 x 24 patch, double buffered
+using WPStage2 = WPGeo<11, 11, 1, 3, 160>;   // whole images: 121 pixels, 13 x 13 patch, 3 buffers (short tiles)
+using WPStage3 = WPGeo<6, 6, 1, 2, 144, 5, WP34_BLOCKS, 3>;    // 5 images: 180 pixels, 36 x 8 patch
+using WPStage4 = WPGeo<3, 3, 1, 2, 160, 14, WP34_BLOCKS, 2>;   // 14 images: 126 pixels, 57 x 5 patch
 
 AVSR_DEV int whswz(int row) { return ((row >> 1) & 3) << 1; }
 AVSR_DEV bf16x8 trpair(const char* pa, const char* pb) {
@@ -775,11 +795,31 @@ AVSR_DEV bf16x8 trpair(const char* pa, const char* pb) {
   return u.h;
 }
 
-// (co, ci) block q and tile range r of block b: the nq blocks with the same range sit at
-// ids b, b+8, ... (one XCD under round-robin placement); ranges per block kind = 256 / nq
-AVSR_DEV void wp_block(int b, int nq, int& q, int& r) {
-  q = (b >> 3) % nq;
-  r = ((b >> 3) / nq) * 8 + (b & 7);
+// (co, ci) block q and tile range r of block b among nblk: blocks b, b+8, ... share an XCD under
+// round-robin placement (S = nblk / 8 per XCD). nq <= S (S % nq == 0): the nq blocks with the same
+// range sit on one XCD; nq > S (nq % S == 0): a range's blocks fill nq / S XCDs. Ranges per
+// block kind: bpq = nblk / nq either way.
+AVSR_DEV void wp_block(int b, int nq, int nblk, int& q, int& r) {
+  const int x = b & 7, s = b >> 3, S = nblk >> 3;
+  if (nq <= S) {
+    q = s % nq;
+    r = (s / nq) * 8 + x;
+  } else {
+    const int k = nq / S;
+    r = x / k;
+    q = (x - r * k) * S + s;
+  }
+}
+
+// wait until at most min(ahead, K) tiles of NP DMAs each are still in flight (vmcnt is an immediate)
+template <int NP, int K>
+AVSR_DEV void wp_wait_ahead(int ahead) {
+  if constexpr (K == 0) {
+    gemmg::wait_vmcnt<0>();
+  } else {
+    if (ahead >= K) gemmg::wait_vmcnt<NP * K>();
+    else wp_wait_ahead<NP, K - 1>(ahead);
+  }
 }
 
 template <class G>
@@ -791,13 +831,13 @@ __global__ __launch_bounds__(256, 1) void conv_wgrad_patch_kernel(const bf16* __
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int ncih = cin / 64, nq = (cout / 64) * ncih, bpq = gridDim.x / nq;
   int q, rng;
-  wp_block(blockIdx.x, nq, q, rng);
+  wp_block(blockIdx.x, nq, gridDim.x, q, rng);
   const int coh = q / ncih, cih = q - coh * ncih;
-  const int ntiles = nimg * G::TPI;
+  const int ntiles = (nimg * G::TPI + G::IPT - 1) / G::IPT;   // a last part tile reads zeros past the end
   const int ta = (int)((int64_t)ntiles * rng / bpq), tb = (int)((int64_t)ntiles * (rng + 1) / bpq);
   const __amdgpu_buffer_rsrc_t rx = make_rsrc(x, x_bytes), rdy = make_rsrc(dy, dy_bytes);
   // DMA pieces of a tile (offsets recomputed per issue: compile-time divisors, no registers held)
-  auto tile_px = [&](int t) { return (t / G::TPI) * IMG + (t % G::TPI) * G::PX; };
+  auto tile_px = [&](int t) { return (t / G::TPI) * IMG * G::IPT + (t % G::TPI) * G::PX; };
   auto issue_dy = [&](int i, int t, char* buf) {
     const int s = (wave + 4 * i) * 64 + lane, row = s >> 3;
     const int c = (s & 7) ^ whswz(row);
@@ -807,10 +847,19 @@ __global__ __launch_bounds__(256, 1) void conv_wgrad_patch_kernel(const bf16* __
   auto issue_patch = [&](int i, int t, char* buf) {
     const int s = (wave + 4 * i) * 64 + lane, row = s / G::SLOTS, ch = s - row * G::SLOTS;
     const int py = row / G::WP, pxp = row - py * G::WP;
-    const int y = (t % G::TPI) * G::TR + py - 1;       // image row of this slot's patch row
-    const bool ok = ch < 8 && row < G::PROWS && pxp >= 1 && pxp <= G::W && y >= 0 && y < G::H;
-    const uint32_t vo = ok ? (uint32_t)(tile_px(t) + (py - 1) * G::W + pxp - 1) * (uint32_t)(cin * 2) + cih * 128 + ch * 16
-                           : gemmg::OOB;
+    bool ok;
+    int src;                                           // input pixel of this slot (relative to the tile's first)
+    if constexpr (G::IPT == 1) {
+      const int y = (t % G::TPI) * G::TR + py - 1;     // image row of this slot's patch row
+      ok = y >= 0 && y < G::H;
+      src = (py - 1) * G::W + pxp - 1;
+    } else {                                           // image i's rows 1 + i (H + 1) ..., shared zero rows between
+      const int i = (py - 1) / (G::TR + 1), yl = py - 1 - i * (G::TR + 1);
+      ok = py >= 1 && yl < G::TR;
+      src = i * G::IMGT + yl * G::W + pxp - 1;
+    }
+    ok = ok && ch < 8 && row < G::PROWS && pxp >= 1 && pxp <= G::W;
+    const uint32_t vo = ok ? (uint32_t)(tile_px(t) + src) * (uint32_t)(cin * 2) + cih * 128 + ch * 16 : gemmg::OOB;
     gemmg::bglds16(rx, vo, 0u, buf + G::DYB + (wave + 4 * i) * 1024);
   };
   // fragment bases: lane group g holds k = 8g + j <-> pixel 32kb + 16(g >> 1) + 4(g & 1) + (j & 3) + 8(j >> 2)
@@ -822,8 +871,8 @@ __global__ __launch_bounds__(256, 1) void conv_wgrad_patch_kernel(const bf16* __
   for (int i = 0; i < 4; ++i) dA[i] = pxa * 128 + (((2 * i + (pp >> 1)) ^ sw) << 4) + 8 * (pp & 1);
   auto prow = [&](int px) {                        // tile pixel -> patch row
     px = min(px, G::PX - 1);
-    const int yy = px / G::W, xx = px - yy * G::W;
-    return (yy + 1) * G::WP + xx + 1;
+    const int i = px / G::IMGT, r = px - i * G::IMGT, yy = r / G::W, xx = r - yy * G::W;
+    return (i * (G::TR + 1) + yy + 1) * G::WP + xx + 1;
   };
   int pA[G::KS], pB[G::KS];               // patch byte bases (tap (0, 0) = offset 0) per k-step
 #pragma unroll
@@ -845,18 +894,13 @@ __global__ __launch_bounds__(256, 1) void conv_wgrad_patch_kernel(const bf16* __
 #pragma unroll
       for (int i = 0; i < G::PPIECE; ++i) issue_patch(i, ta + d, smem + d * G::BUF);
     }
-  constexpr int PER = (G::DYPIECE + G::PPIECE + G::KS - 1) / G::KS;   // DMAs per k-step
+  constexpr int PER = (G::NP + G::SPREAD - 1) / G::SPREAD;   // DMAs per k-step
   for (int t = ta; t < tb; ++t) {
     const char* buf = smem + ((t - ta) % G::NBUF) * G::BUF;
     char* nbuf = smem + ((t + PD - ta) % G::NBUF) * G::BUF;
     const bool more = t + PD < tb;
     // tile t has landed: the DMAs of the (up to PD - 1) later tiles already issued may still fly
-    if constexpr (PD == 2) {
-      if (t + 1 < tb) gemmg::wait_vmcnt<G::NP>();
-      else gemmg::wait_vmcnt<0>();
-    } else {
-      gemmg::wait_vmcnt<0>();
-    }
+    wp_wait_ahead<G::NP, PD - 1>(tb - 1 - t);
     __builtin_amdgcn_s_barrier();         // ... for every wave; every wave is done with tile t-1
     asm volatile("" ::: "memory");
     const char* patch = buf + G::DYB;
@@ -878,7 +922,7 @@ __global__ __launch_bounds__(256, 1) void conv_wgrad_patch_kernel(const bf16* __
 #pragma unroll
     for (int kb = 0; kb < G::KS; ++kb) {
       if (kb + 1 < G::KS) load(nxt, kb + 1);
-      if (more) {
+      if (more && kb < G::SPREAD) {
 #pragma unroll
         for (int d = 0; d < PER; ++d) {
           const int pc = kb * PER + d;
@@ -904,29 +948,34 @@ __global__ __launch_bounds__(256, 1) void conv_wgrad_patch_kernel(const bf16* __
       for (int r = 0; r < 4; ++r) o[(16 * i + 4 * g + r) * WP_COLS + tp * 64 + 16 * wave + (lane & 15)] = acc[i][tp][r];
 }
 
-AVSR_DEV int wp_bid(int q, int r, int nq) { return ((((r >> 3) * nq) + q) << 3) + (r & 7); }   // inverse of wp_block
+AVSR_DEV int wp_bid(int q, int r, int nq, int nblk) {   // inverse of wp_block
+  const int S = nblk >> 3;
+  if (nq <= S) return ((((r >> 3) * nq) + q) << 3) + (r & 7);
+  const int k = nq / S;
+  return ((q % S) << 3) + r * k + q / S;
+}
 
 // dw[co][tap][ci] += sum over the tile ranges r of block kind q of ws[wp_bid(q, r)][co % 64][tap * 64 + ci % 64],
 // in range order (deterministic), in two passes: chunk c of WPR_CHUNKS folds its ranges into the
 // slab of its first range (in place); pass 2 (chunk < 0) adds the chunk heads in order to dw.
 // 4 consecutive ci per thread.
 constexpr int WPR_CHUNKS = 8;
-__global__ __launch_bounds__(256) void wpatch_reduce_kernel(float* __restrict__ ws, int bpq, int cin, int cout,
+__global__ __launch_bounds__(256) void wpatch_reduce_kernel(float* __restrict__ ws, int nblk, int cin, int cout,
                                                             float* dw, int pass2) {
-  const int ncih = cin / 64, nq = (cout / 64) * ncih;
+  const int ncih = cin / 64, nq = (cout / 64) * ncih, bpq = nblk / nq;
   const int e = (blockIdx.x * 256 + threadIdx.x) * 4;      // element of the 64 x 576 block
   const int q = blockIdx.y, c = blockIdx.z;
   if (e >= 64 * WP_COLS) return;
   f32x4 s = {0.f, 0.f, 0.f, 0.f};
   if (!pass2) {
     const int r0 = bpq * c / WPR_CHUNKS, r1 = bpq * (c + 1) / WPR_CHUNKS;
-    for (int r = r0; r < r1; ++r) s += *(const f32x4*)(ws + (int64_t)wp_bid(q, r, nq) * 64 * WP_COLS + e);
-    if (r1 > r0) *(f32x4*)(ws + (int64_t)wp_bid(q, r0, nq) * 64 * WP_COLS + e) = s;
+    for (int r = r0; r < r1; ++r) s += *(const f32x4*)(ws + (int64_t)wp_bid(q, r, nq, nblk) * 64 * WP_COLS + e);
+    if (r1 > r0) *(f32x4*)(ws + (int64_t)wp_bid(q, r0, nq, nblk) * 64 * WP_COLS + e) = s;
     return;
   }
   for (int k = 0; k < WPR_CHUNKS; ++k) {
     const int r0 = bpq * k / WPR_CHUNKS, r1 = bpq * (k + 1) / WPR_CHUNKS;
-    if (r1 > r0) s += *(const f32x4*)(ws + (int64_t)wp_bid(q, r0, nq) * 64 * WP_COLS + e);
+    if (r1 > r0) s += *(const f32x4*)(ws + (int64_t)wp_bid(q, r0, nq, nblk) * 64 * WP_COLS + e);
   }
   const int r = e / WP_COLS, col = e - r * WP_COLS, tap = col >> 6, ci = col & 63;
   const int coh = q / ncih, cih = q - coh * ncih;
@@ -936,7 +985,8 @@ __global__ __launch_bounds__(256) void wpatch_reduce_kernel(float* __restrict__ 
 }
 
 // the patch-resident weight-grad applies: bf16, slab workspace, automatic split, 3x3 / stride 1
-// / pad 1, one group, the stage-1 (22 x 22, 64 -> 64) or stage-2 (11 x 11, 128 -> 128) geometry
+// / pad 1, one group, the stage-1 (22 x 22, 64 -> 64), stage-2 (11 x 11, 128 -> 128), stage-3
+// (6 x 6, 256 -> 256) or stage-4 (3 x 3, 512 -> 512) geometry
 static bool wpatch_ok(const avsr_conv_params* p) {
   if (!avsr_opt(AVSR_OPT_CONV_WPATCH) || p->dtype != AVSR_BF16 || !conv_glds_enabled() || p->groups != 1 || p->splitk > 0)
     return false;
@@ -945,8 +995,11 @@ static bool wpatch_ok(const avsr_conv_params* p) {
   if (p->hin != p->win) return false;
   const int64_t bytes = (int64_t)p->nimg * p->hin * p->win * p->cin * 2;
   if (bytes <= 0 || bytes >= (int64_t)gemmg::OOB - (1 << 20)) return false;
+  if ((p->cin == 256 && p->hin == 6) || (p->cin == 512 && p->hin == 3)) return AVSR_WP34 != 0;
   return (p->cin == 64 && p->hin == 22) || (p->cin == 128 && p->hin == 11);
 }
+
+static int wpatch_blocks(const avsr_conv_params* p) { return p->cin >= 256 ? WP34_BLOCKS : WP_BLOCKS; }
 
 template <class G>
 static int wpatch_launch_g(const avsr_conv_params* p, hipStream_t st) {
@@ -956,23 +1009,27 @@ static int wpatch_launch_g(const avsr_conv_params* p, hipStream_t st) {
     attr = true;
   }
   const uint32_t bytes = (uint32_t)((int64_t)p->nimg * p->hin * p->win * p->cin * 2);
-  hipLaunchKernelGGL((conv_wgrad_patch_kernel<G>), dim3(WP_BLOCKS), dim3(256), G::LDS, st, (const bf16*)p->x,
+  static_assert(G::NBLK % 8 == 0, "");
+  const int nq = (p->cout / 64) * (p->cin / 64), S = G::NBLK / 8;
+  if (nq <= S ? S % nq != 0 : (nq % S != 0 || 8 % (nq / S) != 0)) return AVSR_E_SHAPE;   // wp_block's mapping
+  hipLaunchKernelGGL((conv_wgrad_patch_kernel<G>), dim3(G::NBLK), dim3(256), G::LDS, st, (const bf16*)p->x,
                      (const bf16*)p->dy, bytes, bytes, p->nimg, p->cin, p->cout, p->ws);
   AVSR_CHECK_LAUNCH();
-  const int nq = (p->cout / 64) * (p->cin / 64), bpq = WP_BLOCKS / nq;
   const unsigned gx = (64 * WP_COLS / 4 + 255) / 256;
-  hipLaunchKernelGGL(wpatch_reduce_kernel, dim3(gx, (unsigned)nq, (unsigned)WPR_CHUNKS), dim3(256), 0, st, p->ws, bpq,
-                     p->cin, p->cout, p->dw, 0);
+  hipLaunchKernelGGL(wpatch_reduce_kernel, dim3(gx, (unsigned)nq, (unsigned)WPR_CHUNKS), dim3(256), 0, st, p->ws,
+                     G::NBLK, p->cin, p->cout, p->dw, 0);
   AVSR_CHECK_LAUNCH();
-  hipLaunchKernelGGL(wpatch_reduce_kernel, dim3(gx, (unsigned)nq, 1u), dim3(256), 0, st, p->ws, bpq, p->cin, p->cout,
-                     p->dw, 1);
+  hipLaunchKernelGGL(wpatch_reduce_kernel, dim3(gx, (unsigned)nq, 1u), dim3(256), 0, st, p->ws, G::NBLK, p->cin,
+                     p->cout, p->dw, 1);
   AVSR_CHECK_LAUNCH();
   return 0;
 }
 
 static int wpatch_launch(const avsr_conv_params* p, hipStream_t st) {
   if (p->cin == 64) return wpatch_launch_g<WPStage1>(p, st);
-  return wpatch_launch_g<WPStage2>(p, st);
+  if (p->cin == 128) return wpatch_launch_g<WPStage2>(p, st);
+  if (p->cin == 256) return wpatch_launch_g<WPStage3>(p, st);
+  return wpatch_launch_g<WPStage4>(p, st);
 }
 
 // ---------------------------------------------------------------- patch-resident stem weight-grad
@@ -1372,7 +1429,7 @@ extern "C" int avsr_conv_bwd_weight(const avsr_conv_params* p, void* stream) {
 
 extern "C" int64_t avsr_conv_wgrad_ws(const avsr_conv_params* p) {
   if (!p || (p->dtype != AVSR_BF16 && p->dtype != AVSR_F32)) return 0;
-  if (wpatch_ok(p)) return (int64_t)WP_BLOCKS * 64 * WP_COLS;
+  if (wpatch_ok(p)) return (int64_t)wpatch_blocks(p) * 64 * WP_COLS;
   if (stem_wpatch_ok(p)) return (int64_t)SWP_BLOCKS * 64 * SWP_COLS;
   const WgradPlan w = wgrad_plan(p, p->dtype == AVSR_BF16 && conv_glds_enabled(), true);
   if (!w.slab) return 0;

@@ -228,11 +228,12 @@ def test_stem_conv_direct(dev, B, T):
     assert torch.equal(h, h2)
 
 
-@pytest.mark.parametrize("hw,c", [(22, 64), (11, 128)])
+@pytest.mark.parametrize("hw,c", [(22, 64), (11, 128), (6, 256), (3, 512)])
 @pytest.mark.parametrize("nimg", [1, 37, 600])
 def test_wgrad_patch_matches_general(dev, nimg, hw, c, monkeypatch, lib_opt):
-    """Patch-resident weight-grad of the stage-1 / stage-2 3x3 convolutions (persistent blocks,
-    per-block slabs, ordered reduce) vs the general implicit-GEMM weight-grad and fp64 torch;
+    """Patch-resident weight-grad of the stage-1..4 3x3 convolutions (persistent blocks,
+    per-block slabs, ordered reduce; stages 3-4: several images per tile, a part tile at the end
+    when nimg is not a multiple) vs the general implicit-GEMM weight-grad and fp64 torch;
     blocks without tiles (nimg = 1), accumulation into a non-zero dw, run-to-run bit-identical."""
     g = torch.Generator().manual_seed(nimg + c)
     geom = ops.ConvGeom(nimg, hw, hw, c, c, 3, 3, (1, 1), (1, 1))

@@ -18,10 +18,10 @@ def _tol(dtype, f32=2e-5, b16=2e-2):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("N,eps", [(1024, 1e-5), (2048, 1e-5), (256, 1e-12)])
-def test_layernorm(dev, dtype, N, eps):
+@pytest.mark.parametrize("N,eps,rows", [(1024, 1e-5, 777), (2048, 1e-5, 777), (256, 1e-12, 777), (1024, 1e-5, 3001)])
+def test_layernorm(dev, dtype, N, eps, rows):
+    """rows = 3001: each of the backward's 1024 waves walks 2-3 rows through both register stages"""
     g = torch.Generator().manual_seed(N)
-    rows = 777
     x = torch.randn(rows, N, generator=g) * 2 + 0.5
     gam = 1 + 0.1 * torch.randn(N, generator=g)
     bet = 0.1 * torch.randn(N, generator=g)
