@@ -1838,138 +1838,6 @@ __global__ __launch_bounds__(NTH) void attn_bwd_dkdv_kernel(AttnArgs a) {
     stamp_part(3, 1);
   }
 }
-// dQ with a small footprint (AVSR_OPT_ATTN_SQ_BWD = 1): 4 waves x 32 queries per workgroup, three
-// workgroups per head (XCD-adjacent), K / V streamed in 32-row tiles through a 3-stage LDS-DMA
-// ring of 8 KiB stages (24 KiB in all). It fits beside a side-stream weight-gradient block (128
-// KiB of LDS, 2 waves per SIMD), where the whole-head dQ kernel has to wait for an empty CU.
-// Same arithmetic per element as the whole-head kernel (results equal bit for bit).
-constexpr int QT = 32, QNS = 3, QIMG = QT * 128, QSTG = 2 * QIMG;
-template <typename OutT, int DM>
-__global__ __launch_bounds__(256) void attn_bwd_dq_small_kernel(AttnArgs a, int nqb, OutT* dq, int64_t lddq) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int id = xcd_id(blockIdx.x, gridDim.x);
-  const int bh = id / nqb, qb = id - bh * nqb, b = bh / a.H, h = bh % a.H;
-  const int tid = threadIdx.x, l = tid & 63, c = l & 31, hh = l >> 5;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int q0 = qb * 128 + w * 32, qi = q0 + c;
-  const bool qok = qi < a.Lq;
-  const bf16* Kg = (const bf16*)a.k + (int64_t)b * a.Lk * a.ldk + h * DH;
-  const bf16* Vg = (const bf16*)a.v + (int64_t)b * a.Lk * a.ldv + h * DH;
-  const int klen = a.klen ? min(a.klen[b], a.Lk) : a.Lk;
-  const int nt = (klen + QT - 1) / QT;
-  // tile t: rows 32t + 8w .. + 7 of K and V (rows past Lk land as zeros)
-  auto issue = [&](int t, char* stage) {
-    dma_piece(Kg + (int64_t)QT * t * a.ldk, a.ldk, a.Lk - QT * t, stage, w, l);
-    dma_piece(Vg + (int64_t)QT * t * a.ldv, a.ldv, a.Lk - QT * t, stage + QIMG, w, l);
-  };
-  if (nt > 0) issue(0, smem);
-  const bf16* Q = (const bf16*)a.q + (int64_t)b * a.Lq * a.ldq + h * DH;
-  const bf16* dO = (const bf16*)a.dout + (int64_t)b * a.Lq * a.lddo + h * DH;
-  const bf16* Og = (const bf16*)a.o + (int64_t)b * a.Lq * a.ldo + h * DH;
-  bf16x8 qf[4], of[4], ov[4];
-#pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    qf[s] = ldrow_sel(Q, a.ldq, qi, a.Lq, s * 16 + 8 * hh);
-    of[s] = ldrow_sel(dO, a.lddo, qi, a.Lq, s * 16 + 8 * hh);
-    ov[s] = ldrow_sel(Og, a.ldo, qi, a.Lq, s * 16 + 8 * hh);
-  }
-  const int64_t bhq = (int64_t)bh * a.Lq + min(qi, a.Lq - 1);
-  const float lq0 = a.lse[bhq];
-  // the compiler's wait for these loads (vmcnt(0), covering tile 0) happens here, once
-#pragma unroll
-  for (int s = 0; s < 4; ++s) asm volatile("" ::"v"(qf[s]), "v"(of[s]), "v"(ov[s]));
-  asm volatile("" ::"v"(lq0));
-  float dsum = 0.f;
-#pragma unroll
-  for (int s = 0; s < 4; ++s)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) dsum = fmaf((float)of[s][j], (float)ov[s][j], dsum);
-  dsum = xor32_sum(dsum);
-  if (hh == 0 && qok) a.delta[bhq] = dsum;
-  if (nt > 1) issue(1, smem + QSTG);
-  const float lq = qok ? lq0 * LOG2E : 0.f;
-  const float dl = qok ? dsum : 0.f;
-  const float sl2 = a.scale * LOG2E;
-  const AttnDrop drop(a.drop_p, a.seed, a.B, a.H, a.Lq, a.Lk);
-  const float dscale = DM ? drop.scale : 1.f;
-  const uint32_t rowG = DM == 1 ? ((uint32_t)bh * (uint32_t)a.Lq + (uint32_t)min(qi, a.Lq - 1)) * drop.npair * GOLD : 0u;
-  const int64_t mrow = DM == 2 ? ((int64_t)bh * a.mnqb + (q0 >> 5)) * a.mnkb : 0;
-  FragOff fo;
-  fo.init(l);
-  f32x16 dq0, dq1;
-  zacc(dq0); zacc(dq1);
-  int cs = 0;
-  for (int t = 0; t < nt; ++t) {
-    if (t + 1 < nt) vmwait<2>(); else vmwait<0>();         // tile t landed (t + 1 may be in flight)
-    round_barrier();                                         // ... for every wave; tile t - 1 is done
-    if (t + 2 < nt) issue(t + 2, smem + (cs == 0 ? QNS - 1 : cs - 1) * QSTG);
-    if (q0 < a.Lq) {
-      uint64_t mw[16];
-      if (DM == 2) {
-        const smask_t mt = mask_tile(a.mq, mrow + t);
-#pragma unroll
-        for (int e = 0; e < 16; ++e) mw[e] = mt[e];
-      }
-      const char* Kt = smem + cs * QSTG;
-      const char* Vt = Kt + QIMG;
-      f32x16 st, dpt;
-      zacc(st); zacc(dpt);
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        st = mfma32(ldA(Kt, fo.row[s]), qf[s], st);
-        dpt = mfma32(ldA(Vt, fo.row[s]), of[s], dpt);
-      }
-      if (t * 32 + 32 > klen) {                               // wave-uniform: keys past klen
-#pragma unroll
-        for (int e = 0; e < 16; ++e) st[e] = t * 32 + qrow(e, hh) < klen ? st[e] : -INFINITY;
-      }
-      if (DM == 1) {
-#pragma unroll
-        for (int e = 0; e < 16; ++e) dpt[e] *= dscale;
-        drop_tile_sel(dpt, rowG + (uint32_t)(t * 16) * GOLD, drop, hh);
-      }
-#pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const float p = fexp2(fmaf(st[e], sl2, -lq));
-        const float d = DM == 2 ? msel(dpt[e] * dscale, mw[e]) : dpt[e];
-        dpt[e] = p * (d - dl);
-      }
-      const bf16x8 sa = accb(dpt, 0), sb = accb(dpt, 1);
-      dq0 = mfma32(ldT(Kt, 0, fo, 0), sa, dq0);
-      dq0 = mfma32(ldT(Kt, 16, fo, 0), sb, dq0);
-      dq1 = mfma32(ldT(Kt, 0, fo, 1), sa, dq1);
-      dq1 = mfma32(ldT(Kt, 16, fo, 1), sb, dq1);
-    }
-    cs = cs + 1 == QNS ? 0 : cs + 1;
-  }
-  __syncthreads();                                           // the ring is free: half slabs per wave
-  if (q0 < a.Lq) {
-    float* sl = (float*)smem + w * 32 * 33;
-    OutT* DQ = dq + ((int64_t)b * a.Lq + q0) * lddq + h * DH;
-    constexpr int VE = 16 / (int)sizeof(OutT), LPR = 32 / VE, RPI = 64 / LPR;   // a half row: 32 values
-    const int rr = l / LPR, ch = (l % LPR) * VE, nvalid = a.Lq - q0;
-#pragma unroll
-    for (int half = 0; half < 2; ++half) {
-      const f32x16& x = half ? dq1 : dq0;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) sl[c * 33 + qrow(r, hh)] = x[r] * a.scale;
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");     // the wave's own slab: no barrier
-#pragma unroll
-      for (int i0 = 0; i0 < 32; i0 += RPI) {
-        const int i = i0 + rr;
-        if (i < nvalid) {
-          float v[VE];
-#pragma unroll
-          for (int j = 0; j < VE; ++j) v[j] = sl[i * 33 + ch + j];
-          stv(DQ + (int64_t)i * lddq + 32 * half + ch, v);
-        }
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    }
-  }
-}
-constexpr size_t DQS_LDS = QNS * QSTG;
-static_assert(4 * 32 * 33 * 4 <= DQS_LDS, "half slabs exceed the ring");
 
 constexpr size_t DQ_LDS = 2 * IMG384 > NTH / 64 * 32 * 65 * 4 ? 2 * IMG384 : NTH / 64 * 32 * 65 * 4;
 constexpr size_t DKDV_LDS = 3 * IMG384 + 2 * MAXR * 4;
@@ -2085,16 +1953,7 @@ extern "C" int avsr_attn_bwd_prep(const avsr_attn_params* p, void* stream) {
 template <int DM>
 static void launch_enc_bwd(const avsr_attn_params* p, const AttnArgs& a, hipStream_t st) {
   const dim3 g(p->B * p->H);
-  if (avsr_opt(AVSR_OPT_ATTN_SQ_BWD) != 0) {         // small-footprint dQ (3 workgroups per head)
-    const int nqb = (p->Lq + 127) / 128;
-    const dim3 gq(p->B * p->H * nqb);
-    if (p->dq_out)
-      hipLaunchKernelGGL((rb::attn_bwd_dq_small_kernel<bf16, DM>), gq, dim3(256), rb::DQS_LDS, st, a, nqb,
-                         (bf16*)p->dq_out, p->lddq_out);
-    else
-      hipLaunchKernelGGL((rb::attn_bwd_dq_small_kernel<float, DM>), gq, dim3(256), rb::DQS_LDS, st, a, nqb, p->dq,
-                         p->lddq);
-  } else if (p->dq_out) {
+  if (p->dq_out) {
     res::allow_lds(rb::attn_bwd_dq_kernel<bf16, DM>);
     hipLaunchKernelGGL((rb::attn_bwd_dq_kernel<bf16, DM>), g, dim3(rb::NTH), rb::DQ_LDS, st, a, (bf16*)p->dq_out,
                        p->lddq_out);

@@ -12,8 +12,8 @@ std::atomic<int64_t> g_opt[AVSR_OPT_COUNT] = {{0}, {1}, {0}, {1}, {1}, {1}, {1},
 bool opt_valid(int option, int64_t v) {
   switch (option) {
     case AVSR_OPT_GEMM_TILE: return v >= 0 && v <= AVSR_TILE_COUNT;
+    case AVSR_OPT_ATTN_SQ_BWD: return v == 0;        // retired (round 6): accepts its default only
     case AVSR_OPT_ATTN_SQ_FWD:
-    case AVSR_OPT_ATTN_SQ_BWD:
     case AVSR_OPT_WGRAD_DUAL:
     case AVSR_OPT_CONV_192:
     case AVSR_OPT_CONV_S2PHASE:

@@ -1085,27 +1085,43 @@ class Engine:
         dyn = self._e(R, D)
         ops.gemm(dlogits, self.arena.w_padded("decoder.output_layer.weight"), dyn, M=R, N=D, K=self.Vp, a_kmajor=True,
                  b_kmajor=False, lda=dlogits.stride(0), ldb=D, ldc=D)
-        dy = ops.layernorm_bwd(dyn, ctx["y_last"], self.arena.master("decoder.after_norm.weight"), ctx["mf"], ctx["rf"],
-                               dgamma=self.g("decoder.after_norm.weight"), dbeta=self.g("decoder.after_norm.bias"))
+        def ln_bwd(dn, x, name, m, r, dres, ew):
+            """LayerNorm backward (dx over the residual gradient dres, in place) with the dropout
+            backward + bias gradient of the sublayer whose output fed it fused in (ew = (seed, bias
+            name): g = ew_bwd(dx, drop_p, seed, db), as the encoder's _ln_bwd); returns (dx, g)"""
+            g = None if ew is None else self._e(R, D)      # fresh: the previous g may still be read by the side stream
+            if ew is not None and _LN_EW_FUSE:
+                dx = ops.layernorm_bwd(dn, x, self.arena.master(name + ".weight"), m, r, dx=dres, dres=dres,
+                                       dgamma=self.g(name + ".weight"), dbeta=self.g(name + ".bias"), g=g, drop_p=p_d,
+                                       seed=ew[0], db=self.g(ew[1]))
+                return dx, g
+            dx = ops.layernorm_bwd(dn, x, self.arena.master(name + ".weight"), m, r, dx=dres, dres=dres,
+                                   dgamma=self.g(name + ".weight"), dbeta=self.g(name + ".bias"))
+            if ew is not None:
+                ops.ew_bwd(dx, out=g, drop_p=p_d, seed=ew[0], db=self.g(ew[1]))
+            return dx, g
+
+        def ew_of(i, s, name):
+            return (ctx["layers"][i][s], f"decoder.decoders.{i}." + name)
+
+        top = self.dl - 1
+        dy, g = ln_bwd(dyn, ctx["y_last"], "decoder.after_norm", ctx["mf"], ctx["rf"], None,
+                       ew_of(top, "s6", "feed_forward.w_2.bias") if self.dl else None)
         for i in reversed(range(self.dl)):
             self._side_layer(True)              # flushes the previous layer's batch first
             lc = ctx["layers"][i]
             p = f"decoder.decoders.{i}."
             sa, ca, ff = p + "self_attn.", p + "src_attn.", p + "feed_forward."
-            # FFN (each g is a fresh buffer: the previous one may still be read by the side stream)
-            g = self._e(R, D)
-            ops.ew_bwd(dy, out=g, drop_p=p_d, seed=lc["s6"], db=self.g(ff + "w_2.bias"))
+            # FFN: g = the output dropout backward of dy (with w_2's bias gradient), fused into the
+            # LayerNorm backward that produced dy
             self._wgrad(g, lc["a"], self.g(ff + "w_2.weight"))
             dh = ops.linear_dgrad(g, self.w(ff + "w_2.weight"), gate=lc["h"], act=RELU, drop_p=p_d, seed=lc["s5"],
                                   db=self._fused_db(ff + "w_1.bias"))
             self._bias_grad(dh, self.g(ff + "w_1.bias"), fused=True)
             self._wgrad(dh, lc["n3"], self.g(ff + "w_1.weight"))
             dn3 = ops.linear_dgrad(dh, self.w(ff + "w_1.weight"))
-            dy = ops.layernorm_bwd(dn3, lc["y2"], self.arena.master(p + "norm3.weight"), lc["m3"], lc["r3"], dx=dy, dres=dy,
-                                   dgamma=self.g(p + "norm3.weight"), dbeta=self.g(p + "norm3.bias"))
+            dy, g = ln_bwd(dn3, lc["y2"], p + "norm3", lc["m3"], lc["r3"], dy, ew_of(i, "s4", "src_attn.linear_out.bias"))
             # source attention
-            g = self._e(R, D)
-            ops.ew_bwd(dy, out=g, drop_p=p_d, seed=lc["s4"], db=self.g(ca + "linear_out.bias"))
             self._wgrad(g, lc["o2"], self.g(ca + "linear_out.weight"))
             do2 = ops.linear_dgrad(g, self.w(ca + "linear_out.weight"))
             dkv = self._e(B * T, 2 * D)
@@ -1124,11 +1140,8 @@ class Engine:
             self._bias_grad(dkv, self.arena.span([ca + "linear_k.bias", ca + "linear_v.bias"], buf="g"))
             self._wgrad(dkv, enc, self.arena.span(kvw, buf="g"))
             ops.linear_dgrad(dkv, self.arena.span(kvw), out=denc, beta=1.0)
-            dy = ops.layernorm_bwd(dn2, lc["y1"], self.arena.master(p + "norm2.weight"), lc["m2"], lc["r2"], dx=dy, dres=dy,
-                                   dgamma=self.g(p + "norm2.weight"), dbeta=self.g(p + "norm2.bias"))
+            dy, g = ln_bwd(dn2, lc["y1"], p + "norm2", lc["m2"], lc["r2"], dy, ew_of(i, "s2", "self_attn.linear_out.bias"))
             # causal self attention
-            g = self._e(R, D)
-            ops.ew_bwd(dy, out=g, drop_p=p_d, seed=lc["s2"], db=self.g(sa + "linear_out.bias"))
             self._wgrad(g, lc["o1"], self.g(sa + "linear_out.weight"))
             do1 = ops.linear_dgrad(g, self.w(sa + "linear_out.weight"))
             dqkv = self._e(R, 3 * D)
@@ -1145,8 +1158,8 @@ class Engine:
             self._bias_grad(dqkv, self.arena.span(nb, buf="g"))
             self._wgrad(dqkv, lc["n1"], self.arena.span(nw, buf="g"))
             dn1 = ops.linear_dgrad(dqkv, self.arena.span(nw))
-            dy = ops.layernorm_bwd(dn1, lc["y"], self.arena.master(p + "norm1.weight"), lc["m1"], lc["r1"], dx=dy, dres=dy,
-                                   dgamma=self.g(p + "norm1.weight"), dbeta=self.g(p + "norm1.bias"))
+            dy, g = ln_bwd(dn1, lc["y"], p + "norm1", lc["m1"], lc["r1"], dy,
+                           ew_of(i - 1, "s6", "feed_forward.w_2.bias") if i > 0 else None)
         self._side_layer(False)
         ops.embed_bwd(bt["ys_in"], dy, math.sqrt(D), self.g("decoder.embed.0.weight"), L1, drop_p=p_d, seed=ctx["sd_e"])
 

@@ -44,10 +44,8 @@ const char* avsr_version(void);
  *                                 tile configuration k (AVSR_TILE_* below) on the bf16 core
  *   AVSR_OPT_ATTN_SQ_FWD    [1]  1: query-tiled streamed self-attention forward for bf16,
  *                                 L >= 128; 0: the resident-K/V kernel (same rows to 1e-2)
- *   AVSR_OPT_ATTN_SQ_BWD    [0]  1: the encoder backward's dQ as the small-footprint kernel
- *                                 (3 workgroups of 4 waves per head, 24 KiB of LDS: fits beside a
- *                                 weight-gradient block); 0: one 12-wave workgroup per head
- *                                 (bit-identical)
+ *   AVSR_OPT_ATTN_SQ_BWD    [0]  retired: accepts 0 only (the small-footprint dQ kernel it
+ *                                 selected measured 0.4 % slower in the step and was removed)
  *   AVSR_OPT_WGRAD_DUAL     [1]  1: two-wave-group weight-gradient kernel (fp32 C, both
  *                                 operands r-contiguous); 0: the 4-wave core
  *   AVSR_OPT_CONV_192       [1]  1: 192x128 tiles for conv fwd / data-grad where they still

@@ -329,10 +329,6 @@ def test_attention_dropout_mask_bitexact(dev, lib_opt, case):
             runs[f"bf16 fwd_sq={fwd_sq} stored={stored}"], allowed = _masks(dev, bf, B, H, Lq, Lk, klen, causal, p, seed,
                                                                             stored)
     lib_opt("attn_sq_fwd", 1)
-    for stored in (True, False):         # the small-footprint dQ kernel of the encoder backward
-        lib_opt("attn_sq_bwd", 1)
-        runs[f"bf16 dq_small stored={stored}"], _ = _masks(dev, bf, B, H, Lq, Lk, klen, causal, p, seed, stored)
-    lib_opt("attn_sq_bwd", 0)
     runs["fp32"], _ = _masks(dev, torch.float32, B, H, Lq, Lk, klen, causal, p, seed)
     ref = runs["bf16 fwd_sq=1 stored=True"][0]          # the production forward's mask
     frac = ref.sum().item() / allowed.sum().item()
@@ -469,38 +465,3 @@ def test_attention_stored_mask_outputs_identical(dev, B, H, L, klen):
         assert torch.equal(a, b), (name, (a.float() - b.float()).abs().max().item())
 
 
-@pytest.mark.parametrize("B,H,L,klen", [(16, 16, 375, [375, 301] * 8), (3, 2, 200, [200, 129, 64]),
-                                        (2, 2, 130, [130, 97])])
-@pytest.mark.parametrize("drop", ["none", "hashed", "stored"])
-def test_encoder_dq_small_matches_whole_head(dev, lib_opt, B, H, L, klen, drop):
-    """the small-footprint dQ kernel (library option attn_sq_bwd = 1: 3 workgroups of 4 waves per
-    head, K / V streamed through a 24 KiB ring) returns the whole-head kernel's dQ (bf16 and the
-    fp32 accumulator form) and delta bit for bit"""
-    D = H * 64
-    g = torch.Generator().manual_seed(L * 3 + H)
-    bf = torch.bfloat16
-    qkv = torch.randn(B * L, 3 * D, generator=g).to(dev, bf)
-    q, k, v = qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:]
-    dout = torch.randn(B * L, D, generator=g).to(dev, bf)
-    kl = torch.tensor(klen, dtype=torch.int32, device=dev)
-    p = 0.0 if drop == "none" else 0.1
-    kw = dict(B=B, H=H, Lq=L, Lk=L, klen=kl, scale=0.125, drop_p=p, seed=77)
-    if drop == "stored":
-        kw["mask"] = ops.attn_dropmask(torch.empty(ops.attn_mask_words(B, H, L, L), dtype=torch.int64, device=dev),
-                                       B=B, H=H, Lq=L, Lk=L, drop_p=p, seed=77)
-    o = torch.empty(B * L, D, device=dev, dtype=bf)
-    lse = torch.empty(B, H, L, device=dev)
-    ops.attn_fwd(q, k, v, o, lse, **kw)
-    res = []
-    for small in (0, 1):
-        lib_opt("attn_sq_bwd", small)
-        dq = torch.empty(B * L, D, device=dev, dtype=bf)
-        dq32 = torch.zeros(B * L, D, device=dev)
-        dk = torch.empty(B * L, D, device=dev, dtype=bf)
-        dv = torch.empty(B * L, D, device=dev, dtype=bf)
-        delta = torch.empty(B, H, L, device=dev)
-        ops.attn_bwd(dout, q, k, v, o, lse, None, dk, dv, delta, dq=dq, **kw)
-        ops.attn_bwd(dout, q, k, v, o, lse, dq32, dk, dv, delta, **kw)
-        res.append((dq, dq32, dk, dv, delta))
-    for name, a, b in zip(("dq", "dq32", "dk", "dv", "delta"), *res):
-        assert torch.equal(a, b), (name, (a.float() - b.float()).abs().max().item())

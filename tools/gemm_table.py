@@ -59,7 +59,10 @@ def main():
     cfgs = sys.argv[2].split(",") if len(sys.argv) > 2 else ["auto", "128", "128s3", "256x128", "128x256", "pp"]
     g = torch.Generator(device="cpu").manual_seed(0)
     rows = []
+    only = os.environ.get("GEMM_TABLE_LAYERS")       # e.g. "out": a subset of the layers
     for name, (N, K) in LAYERS.items():
+        if only and name not in only.split(","):
+            continue
         x = (torch.randn(M, K, generator=g) * 0.5).to(dev, torch.bfloat16)
         W = (torch.randn(N, K, generator=g) * 0.05).to(dev, torch.bfloat16)
         dy = (torch.randn(M, N, generator=g) * 0.5).to(dev, torch.bfloat16)
