@@ -115,6 +115,7 @@ class Arena:
         # them as torch.optim.AdamW skips parameters whose grad is None)
         self.ld_ranges = None
         self.ld_touched = set()
+        self.update_event = None     # an overlapped optimizer update in flight (wait_update)
         self.attach_grads(zero=False)
         self.sync_shadow()
 
@@ -221,7 +222,16 @@ class Arena:
         for n in missing:
             self.params[n].grad = self.grad_views[n]
 
+    def wait_update(self, stream=None):
+        """make `stream` (default: the current stream) wait for an overlapped optimizer update
+        still running on its own stream (FusedAdamW(overlap=True)); no-op otherwise. The event
+        stays set: every reader of parameters, moments or gradients may wait on it."""
+        ev = self.update_event
+        if ev is not None:
+            (stream or torch.cuda.current_stream(self.device)).wait_event(ev)
+
     def zero_grad(self):
+        self.wait_update()
         self.grad.zero_()
         self.attach_grads(zero=False)
         self.ld_touched.clear()

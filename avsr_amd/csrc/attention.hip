@@ -1623,7 +1623,6 @@ __global__ __launch_bounds__(NTH) void attn_bwd_dq_kernel(AttnArgs a, OutT* dq, 
   fo.init(l);
   f32x16 dq0, dq1;
   zacc(dq0); zacc(dq1);
-  int t = 0;
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     if (r == 1) vmwait<4>();
@@ -1631,9 +1630,11 @@ __global__ __launch_bounds__(NTH) void attn_bwd_dq_kernel(AttnArgs a, OutT* dq, 
     if (r == 3) vmwait<0>();
     round_barrier();                                       // round r of every wave has landed
     if (r == 0) stamp_part(1, 0);
-    const int tend = min(nt, 3 * r + 3);
     if (q0 < a.Lq) {
-      for (; t < tend; ++t) {
+#pragma unroll
+      for (int u = 0; u < 3; ++u) {                        // unrolled: tile offsets become immediates
+        const int t = 3 * r + u;
+        if (t >= nt) break;
         uint64_t mw[16];
         if (DM == 2) {
           const smask_t mt = mask_tile(a.mq, mrow + t);
@@ -1745,7 +1746,6 @@ __global__ __launch_bounds__(NTH) void attn_bwd_dkdv_kernel(AttnArgs a) {
   fo.init(l);
   f32x16 dv0, dv1, dk0, dk1;
   zacc(dv0); zacc(dv1); zacc(dk0); zacc(dk1);
-  int t = 0;
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     if (r == 1) vmwait<4>();
@@ -1753,9 +1753,13 @@ __global__ __launch_bounds__(NTH) void attn_bwd_dkdv_kernel(AttnArgs a) {
     if (r == 3) vmwait<0>();
     round_barrier();                       // round r landed (r = 0: the lse scaling is visible)
     if (r == 0) stamp_part(1, 1);
-    const int tend = min(nt, 3 * r + 3);
     if (active) {
-      for (; t < tend; ++t) {
+      // the round's 3 query tiles unrolled: tile offsets into the Q / dO images and the lse /
+      // delta rows become instruction offsets (no per-fragment address add)
+#pragma unroll
+      for (int u = 0; u < 3; ++u) {
+        const int t = 3 * r + u;
+        if (t >= nt) break;
         const int qt0 = t * 32;
         uint32_t mbits = 0;
         if (DM == 2) {

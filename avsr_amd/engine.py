@@ -65,6 +65,9 @@ SIDE_STREAM = True
 # single process: the optimizer's gradient-norm pass over everything but the ResNet frontend runs
 # on the side stream beside the ResNet backward (bench.py wires Engine.pre_video_grads)
 EARLY_NORM = True
+# training loops that own their optimizer (bench.py) update everything past the frontends on an
+# update stream beside the next step's frontend forward (FusedAdamW(overlap=True))
+OPT_OVERLAP = True
 
 
 _STEP_STREAMS = {}
@@ -362,7 +365,12 @@ class Engine:
             self.arena.zero_grad()
             return
         g = self.arena.grad
-        self._on_side(lambda: g.zero_(), g)
+        arena = self.arena
+
+        def clear():
+            arena.wait_update()         # an overlapped optimizer update still reads the gradients
+            g.zero_()
+        self._on_side(clear, g)
         self.arena.attach_grads(zero=False)
         self.arena.ld_touched.clear()
 
@@ -766,6 +774,9 @@ class Engine:
             ops.linear_fwd(feat, self.w(EN + "feature_extractor_video.proj.weight"),
                            self.arena.master(EN + "feature_extractor_video.proj.bias"),
                            res=fa if add and modality != "audio_off" else None, out=fcat if add else fcat[:, D:])
+        # an overlapped optimizer update of everything past the frontends (FusedAdamW(overlap=
+        # True)) ran beside the frontends' forward: the first read of those parameters waits here
+        self.arena.wait_update()
         ln0, m0, r0 = self._ln(fcat, EN + "layer_norm", 1e-5)
         sd_in = seeds.next()
         p_in = cfg.dropout_input if train else 0.0

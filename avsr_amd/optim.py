@@ -38,12 +38,27 @@ class LinearWarmupDecay:
 
 class FusedAdamW:
     """step(): gradient norm, then one fused clip + AdamW launch per weight-decay segment, all
-    on the current stream (an update overlapped with the next forward measured no gain in
-    round 3, profiles/r03_opt_overlap_ab.txt, and was removed)."""
+    on the current stream.
+
+    overlap=True: the update of the parameters the next training forward reads first (the audio
+    and video frontends: FRONT) runs on the current stream, the rest (encoder, decoder, CTC:
+    ~97 % of the arena) on an update stream that waits for the current one. The engine's next
+    training forward runs the frontends (the ResNet forward, several ms of single-stream work)
+    beside it and waits for the update (arena.update_event) before the first encoder parameter
+    is read; the gradient clear waits for it too. The update is elementwise, so results equal the
+    serial step bit for bit. Other readers of parameters, moments or gradients call sync() (or
+    arena.wait_update()) first. (Round 3 measured no gain from a similar overlap while the host
+    issued each step only just ahead of the GPU, profiles/r03_opt_overlap_ab.txt; the host now
+    runs 80-110 ms ahead, profiles/r06_host_lead.txt.)"""
+
+    FRONT = ("encoder.feature_extractor_audio.", "encoder.feature_extractor_video.")
 
     def __init__(self, arena, lr=1e-4, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.005, max_grad_norm=1.0,
-                 schedule=None):
+                 schedule=None, overlap=False):
         self.arena = arena
+        self.overlap = bool(overlap) and arena.device.type == "cuda"
+        self._ustream = torch.cuda.Stream(device=arena.device) if self.overlap else None
+        self._uevent = torch.cuda.Event() if self.overlap else None
         arena.init_optimizer()
         self.lr, self.betas, self.eps, self.wd, self.max_norm = lr, betas, eps, weight_decay, max_grad_norm
         self.schedule = schedule
@@ -117,14 +132,55 @@ class FusedAdamW:
             self._touched = union_touched(a.ld_touched, len(a.ld_ranges), a.device)
             for i in self._touched:
                 self.layer_steps[i] += 1
-        for (s, e), wd in (((d0, d1), self.wd), ((n0, n1), 0.0)):
-            for ps, pe, step in self._pieces(s, e):
-                if step is not None:
-                    launch(ps, pe, wd, step)
+        if not self.overlap:
+            for (s, e), wd in (((d0, d1), self.wd), ((n0, n1), 0.0)):
+                for ps, pe, step in self._pieces(s, e):
+                    if step is not None:
+                        launch(ps, pe, wd, step)
+        else:
+            a.wait_update()          # a previous overlapped update with no forward in between
+            front, rest = self._split()
+            for s, e, wd in front:
+                for ps, pe, step in self._pieces(s, e):
+                    if step is not None:
+                        launch(ps, pe, wd, step)
+            us = self._ustream
+            us.wait_stream(torch.cuda.current_stream(a.device))
+            with torch.cuda.stream(us):
+                for s, e, wd in rest:
+                    for ps, pe, step in self._pieces(s, e):
+                        if step is not None:
+                            launch(ps, pe, wd, step)
+                self._uevent.record(us)
+            a.update_event = self._uevent
         self._early = False          # the early partial belongs to this step's gradients only
         if zero_grad:
             a.zero_grad()
         return lr
+
+    def sync(self):
+        """current stream waits for an overlapped update (parameters, moments, gradients read)"""
+        self.arena.wait_update()
+
+    def _split(self):
+        """(front, rest): [start, end, weight decay] ranges of both segments, front = the FRONT
+        modules' parameters (the next forward reads them before any other), rest = the others"""
+        a = self.arena
+        fr = sorted(r for p in self.FRONT for r in a.ranges_of(p))
+        front, rest = [], []
+        for (s, e), wd in ((a.segments["decay"], self.wd), (a.segments["no_decay"], 0.0)):
+            pos = s
+            for r0, r1 in fr:
+                lo, hi = max(r0, s), min(r1, e)
+                if lo >= hi:
+                    continue
+                if pos < lo:
+                    rest.append((pos, lo, wd))
+                front.append((lo, hi, wd))
+                pos = hi
+            if pos < e:
+                rest.append((pos, e, wd))
+        return front, rest
 
     def _pieces(self, s, e):
         """[s, e) as (start, end, step) launches: without LayerDrop one piece at the global step;

@@ -401,8 +401,8 @@ def gpu_bench(args):
     # statistics broadcast, bucketed RCCL all-reduce overlapped with the backward; the 1/world
     # average is folded into the AdamW kernel (average=False, grad_scale below)
     ddp = parallel.ArenaDDP(model, average=False, compress=args.grad_compress)
-    opt = FusedAdamW(arena, lr=1e-4, weight_decay=0.005, max_grad_norm=1.0)
     from avsr_amd import engine as _engine
+    opt = FusedAdamW(arena, lr=1e-4, weight_decay=0.005, max_grad_norm=1.0, overlap=_engine.OPT_OVERLAP)
     if world == 1 and _engine.EARLY_NORM:   # gradient norm of all but the ResNet beside the ResNet backward
         eng.pre_video_grads = opt.early_sumsq
 

@@ -1,0 +1,87 @@
+"""FusedAdamW(overlap=True): the update of everything past the frontends on its own stream
+beside the next step's frontend forward (bench.py's training loop) gives the serial step's
+parameters, bf16 weights, moments and losses bit for bit, with and without LayerDrop (per-layer
+step counts), while the gradient clear of the next step runs on the engine's side stream."""
+import pytest
+import torch
+
+from avsr_amd.avhubert_avsr_model import AVHubertAVSR
+from avsr_amd.configuration_avhubert_avsr import AVHubertAVSRConfig
+from avsr_amd.optim import FusedAdamW
+from oracle.weights import TINY_CONFIG
+from tests.oracle_util import golden_batch, golden_state, load_golden
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(overlap, extra, steps=3):
+    g = load_golden()
+    torch.manual_seed(0)
+    m = AVHubertAVSR(AVHubertAVSRConfig(**TINY_CONFIG, **extra)).train()
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in golden_state(g).items()}, strict=True)
+    m.setup_engine(torch.device("cuda:0"), torch.bfloat16)
+    eng = m.avsr.engine()
+    b = golden_batch(g)
+    v, a = torch.from_numpy(b["videos"]).cuda(), torch.from_numpy(b["audios"]).cuda()
+    lens, lab = torch.from_numpy(b["video_lengths"]), torch.from_numpy(b["labels"])
+    mtl = eng.cfg.mtlalpha
+    d_ctc = torch.full((1,), mtl, device="cuda")
+    d_att = torch.full((1,), 1.0 - mtl, device="cuda")
+    opt = FusedAdamW(eng.arena, lr=1e-3, weight_decay=0.01, max_grad_norm=1.0, overlap=overlap)
+    eng.pre_video_grads = opt.early_sumsq
+    eng.force_modality = (None,)
+    torch.manual_seed(1)                  # LayerDrop draws (CPU generator)
+    losses = []
+    eng.arena.zero_grad()
+    for i in range(steps):
+        eng.zero_grad_async()
+        out4, ctx = eng.forward(v, a, lens, lab, train=True, need_grad=True, seed=100 + i)
+        eng.backward(ctx, d_ctc, d_att)
+        opt.step()
+        losses.append(out4.clone())
+    opt.sync()
+    torch.cuda.synchronize()
+    ar = eng.arena
+    return ([x.cpu() for x in losses], ar.data.cpu(), ar.shadow.cpu(), ar.exp_avg.cpu(), ar.exp_avg_sq.cpu(),
+            opt.layer_steps)
+
+
+@pytest.mark.parametrize("extra", [{}, {"layerdrop": 0.5}], ids=["plain", "layerdrop"])
+def test_overlapped_update_bit_identical(extra):
+    ser = _run(False, extra)
+    ovl = _run(True, extra)
+    for name, x, y in zip(("loss", "data", "shadow", "exp_avg", "exp_avg_sq"), ser[:5], ovl[:5]):
+        if name == "loss":
+            for i, (p, q) in enumerate(zip(x, y)):
+                assert torch.equal(p, q), (name, i, p, q)
+        else:
+            assert torch.equal(x, y), (name, (x.float() - y.float()).abs().max().item())
+    assert ser[5] == ovl[5]
+
+
+def test_overlap_splits_cover_the_arena():
+    """front + rest ranges tile both weight-decay segments exactly, front = the frontends"""
+    g = load_golden()
+    m = AVHubertAVSR(AVHubertAVSRConfig(**TINY_CONFIG))
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in golden_state(g).items()}, strict=True)
+    m.setup_engine(torch.device("cuda:0"), torch.bfloat16)
+    ar = m.avsr.engine().arena
+    opt = FusedAdamW(ar, overlap=True)
+    front, rest = opt._split()
+    cover = sorted((s, e) for s, e, _ in front + rest)
+    segs = sorted([ar.segments["decay"], ar.segments["no_decay"]])
+    pos = [segs[0][0]]
+    for s, e in cover:
+        assert s >= pos[-1]
+        pos.append(e)
+    total = sum(e - s for s, e in cover)
+    assert total == sum(e - s for s, e in segs)
+    fr = sorted(r for p in FusedAdamW.FRONT for r in ar.ranges_of(p))
+
+    def inside(s, e):
+        return any(r0 <= s and e <= r1 for r0, r1 in fr)
+
+    def touches(s, e):
+        return any(s < r1 and r0 < e for r0, r1 in fr)
+    assert front and all(inside(s, e) for s, e, _ in front)
+    assert rest and not any(touches(s, e) for s, e, _ in rest)
