@@ -689,7 +689,8 @@ extern "C" int avsr_adamw(const avsr_adamw_params* p, void* stream) {
   const int64_t nv = (p->n - head) / 4;
   const size_t ssz = p->shadow_dtype == AVSR_F32 ? 4 : 2;
   if (p->shadow && (((uintptr_t)p->shadow + head * ssz) & (4 * ssz - 1))) return AVSR_E_ALIGN;
-  const int g = avsr_grid(nv > 0 ? nv : 1, 256, 4096);
+  if (p->max_blocks < 0) return AVSR_E_ARG;
+  const int g = avsr_grid(nv > 0 ? nv : 1, 256, p->max_blocks > 0 && p->max_blocks < 4096 ? p->max_blocks : 4096);
   if (p->shadow_dtype == AVSR_F32) hipLaunchKernelGGL(adamw_kernel<float>, dim3(g), dim3(256), 0, (hipStream_t)stream, *p, head, nv);
   else hipLaunchKernelGGL(adamw_kernel<bf16>, dim3(g), dim3(256), 0, (hipStream_t)stream, *p, head, nv);
   AVSR_CHECK_LAUNCH();

@@ -68,6 +68,8 @@ EARLY_NORM = True
 # training loops that own their optimizer (bench.py) update everything past the frontends on an
 # update stream beside the next step's frontend forward (FusedAdamW(overlap=True))
 OPT_OVERLAP = True
+# grid cap of the overlapped update launches (FusedAdamW.overlap_blocks; 0: the whole chip)
+OPT_OVERLAP_BLOCKS = 256
 
 
 _STEP_STREAMS = {}

@@ -59,6 +59,10 @@ class FusedAdamW:
         self.overlap = bool(overlap) and arena.device.type == "cuda"
         self._ustream = torch.cuda.Stream(device=arena.device) if self.overlap else None
         self._uevent = torch.cuda.Event() if self.overlap else None
+        # grid cap of the overlapped launches: the update's grid-stride blocks live for the whole
+        # launch, and at the default 4096 blocks (8 resident per CU) they hold every wave slot, so
+        # the next forward's kernels (even its 5-us batch copy) wait for the update to finish
+        self.overlap_blocks = 256
         arena.init_optimizer()
         self.lr, self.betas, self.eps, self.wd, self.max_norm = lr, betas, eps, weight_decay, max_grad_norm
         self.schedule = schedule
@@ -119,12 +123,12 @@ class FusedAdamW:
         if self.max_norm and self.max_norm > 0 and not sumsq_ready:
             self.grad_sumsq()
 
-        def launch(s, e, wd, step):
+        def launch(s, e, wd, step, max_blocks=0):
             ops.adamw(a.data[s:e], a.grad[s:e], a.exp_avg[s:e], a.exp_avg_sq[s:e], lr=lr, beta1=self.betas[0],
                       beta2=self.betas[1], eps=self.eps, weight_decay=wd, step=step,
                       shadow=None if a.shadow is None else a.shadow[s:e],
                       sumsq_buf=self._sumsq if self.max_norm else None, max_norm=self.max_norm or 1.0,
-                      grad_scale=grad_scale)
+                      grad_scale=grad_scale, max_blocks=max_blocks)
 
         if a.ld_ranges is not None:
             if self.layer_steps is None:
@@ -150,7 +154,7 @@ class FusedAdamW:
                 for s, e, wd in rest:
                     for ps, pe, step in self._pieces(s, e):
                         if step is not None:
-                            launch(ps, pe, wd, step)
+                            launch(ps, pe, wd, step, self.overlap_blocks)
                 self._uevent.record(us)
             a.update_event = self._uevent
         self._early = False          # the early partial belongs to this step's gradients only

@@ -403,6 +403,7 @@ def gpu_bench(args):
     ddp = parallel.ArenaDDP(model, average=False, compress=args.grad_compress)
     from avsr_amd import engine as _engine
     opt = FusedAdamW(arena, lr=1e-4, weight_decay=0.005, max_grad_norm=1.0, overlap=_engine.OPT_OVERLAP)
+    opt.overlap_blocks = _engine.OPT_OVERLAP_BLOCKS
     if world == 1 and _engine.EARLY_NORM:   # gradient norm of all but the ResNet beside the ResNet backward
         eng.pre_video_grads = opt.early_sumsq
 

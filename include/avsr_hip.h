@@ -576,6 +576,10 @@ typedef struct {
   float bias_corr1, bias_corr2;          /* 1 - beta^t */
   const float* sumsq; float max_norm;    /* clip: coef = min(1, max_norm / (sqrt(*sumsq) + 1e-6)); sumsq NULL = no clip */
   float grad_scale;                      /* extra multiplier on the gradient (1/accumulation etc.) */
+  int max_blocks;                        /* grid cap (0: 4096 = the whole chip). An update running
+                                            beside other work on another stream takes fewer, so its
+                                            grid-stride blocks leave CU slots to that work; the
+                                            result does not depend on it */
 } avsr_adamw_params;
 int avsr_adamw(const avsr_adamw_params* p, void* stream);
 

@@ -260,6 +260,28 @@ def test_adamw_clip(dev):
     assert _rel(sh, pd) < 1e-2
 
 
+def test_adamw_grid_cap_bit_identical(dev):
+    """avsr_adamw_params.max_blocks (the overlapped update's grid cap) changes only the grid:
+    parameters, moments and the bf16 shadow equal the full-grid launch bit for bit (unaligned
+    head elements included)"""
+    n = 3_000_003
+    g = torch.Generator().manual_seed(3)
+    base = [torch.randn(n, generator=g) for _ in range(4)]
+    base[3] = base[3].abs()
+    out = []
+    for cap in (0, 64, 512):
+        p, gr, m, v = (t.to(dev) for t in base)
+        sh = torch.zeros(n, device=dev, dtype=torch.bfloat16)     # element 0 is outside the update
+        ss = torch.zeros(1, device=dev)
+        ops.sumsq(gr, ss)                       # (16-byte aligned input; the value only sets the clip)
+        ops.adamw(p[1:], gr[1:], m[1:], v[1:], lr=1e-3, beta1=0.9, beta2=0.999, eps=1e-8, weight_decay=0.01,
+                  step=3, shadow=sh[1:], sumsq_buf=ss, max_norm=1.0, max_blocks=cap)
+        out.append((p.cpu(), m.cpu(), v.cpu(), sh.cpu()))
+    for other in out[1:]:
+        for a, b in zip(out[0], other):
+            assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_stem_pack_exact(dev, dtype):
     """time-stacked stem input: channel c of frame t = frame t + c - 2 (zero outside the clip,

@@ -19,12 +19,25 @@ import json
 import sys
 
 lay = json.load(open(sys.argv[1]))
+
+def step_ends(rows, gap_ns=5_000_000):
+    """row indices closing each training step: the last optimizer (adamw_kernel) launch of each
+    cluster of launches that start within gap_ns of the previous one (2 per step serial, 4 with
+    the overlapped update: front segments on the step stream, the rest on the update stream)"""
+    ad = [i for i, r in enumerate(rows) if "adamw_kernel" in r["Kernel_Name"]]
+    ends = []
+    for j, i in enumerate(ad):
+        nxt = ad[j + 1] if j + 1 < len(ad) else None
+        if nxt is None or int(rows[nxt]["Start_Timestamp"]) - int(rows[i]["Start_Timestamp"]) > gap_ns:
+            ends.append(i)
+    return ends
+
 path = sys.argv[2]
 arg = lambda k, d: type(d)(sys.argv[sys.argv.index(k) + 1]) if k in sys.argv else d  # noqa: E731
 skip, world, bmib = arg("--skip", 0), arg("--world", 8), arg("--bucket-mib", 64)
 rows = list(csv.DictReader(gzip.open(path, "rt") if path.endswith(".gz") else open(path)))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-ends = [i for i, r in enumerate(rows) if "adamw_kernel" in r["Kernel_Name"]][1::2]
+ends = step_ends(rows)
 if skip:
     ends = ends[:-skip]
 step = rows[ends[-2] + 1: ends[-1] + 1]

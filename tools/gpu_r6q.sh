@@ -1,0 +1,9 @@
+# overlapped update grid cap: tests, then in-step A/B of the cap (and the serial update).
+# Usage: gpurun -- bash tools/gpu_r6q.sh TAG
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+O=gpurun_out/${1:-r6q}; mkdir -p $O
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_opt_overlap.py tests/test_gpu_loss_misc.py > $O/tests.log 2>&1 || { echo tests failed; tail -40 $O/tests.log; exit 1; }
+tail -2 $O/tests.log
+REPS="1 2" bash tools/gpu_abx.sh ${1:-r6q}/ab "base|-" "base|OPT_OVERLAP_BLOCKS=256" "base|OPT_OVERLAP_BLOCKS=0" "base|OPT_OVERLAP=0"

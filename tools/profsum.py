@@ -9,6 +9,19 @@ import csv
 import sys
 from collections import defaultdict
 
+
+def step_ends(rows, gap_ns=5_000_000):
+    """row indices closing each training step: the last optimizer (adamw_kernel) launch of each
+    cluster of launches that start within gap_ns of the previous one (2 per step serial, 4 with
+    the overlapped update: front segments on the step stream, the rest on the update stream)"""
+    ad = [i for i, r in enumerate(rows) if "adamw_kernel" in r["Kernel_Name"]]
+    ends = []
+    for j, i in enumerate(ad):
+        nxt = ad[j + 1] if j + 1 < len(ad) else None
+        if nxt is None or int(rows[nxt]["Start_Timestamp"]) - int(rows[i]["Start_Timestamp"]) > gap_ns:
+            ends.append(i)
+    return ends
+
 path = sys.argv[1]
 last = int(sys.argv[2]) if len(sys.argv) > 2 else 3
 top = int(sys.argv[3]) if len(sys.argv) > 3 else 30
@@ -26,9 +39,7 @@ def load_rows(path):
 
 
 rows = sorted(load_rows(path), key=lambda r: int(r["Start_Timestamp"]))
-ends = [i for i, r in enumerate(rows) if "adamw_kernel" in r["Kernel_Name"]]
-# two adamw launches (decay / no-decay segments) per step
-ends = ends[1::2]
+ends = step_ends(rows)
 # --skip S: leave out the last S steps (bench --quick appends 12 per-variant steps: none x4,
 # audio_off x4, video_off x4, one lead-in + 3 timed each; the forced timed steps are the 4 before them)
 skip = int(sys.argv[sys.argv.index("--skip") + 1]) if "--skip" in sys.argv else 0

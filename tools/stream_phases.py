@@ -7,11 +7,23 @@ import csv
 import sys
 from collections import defaultdict
 
+
+def step_ends(rows, gap_ns=5_000_000):
+    """row indices closing each training step: the last optimizer (adamw_kernel) launch of each
+    cluster of launches that start within gap_ns of the previous one (2 per step serial, 4 with
+    the overlapped update: front segments on the step stream, the rest on the update stream)"""
+    ad = [i for i, r in enumerate(rows) if "adamw_kernel" in r["Kernel_Name"]]
+    ends = []
+    for j, i in enumerate(ad):
+        nxt = ad[j + 1] if j + 1 < len(ad) else None
+        if nxt is None or int(rows[nxt]["Start_Timestamp"]) - int(rows[i]["Start_Timestamp"]) > gap_ns:
+            ends.append(i)
+    return ends
+
 rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
 last = int(sys.argv[2]) if len(sys.argv) > 2 and sys.argv[2] != "--skip" else 3
 skip = int(sys.argv[sys.argv.index("--skip") + 1]) if "--skip" in sys.argv else 0
-ad = [i for i, r in enumerate(rows) if "adamw_kernel" in r["Kernel_Name"]]
-ends = ad[1::2]                  # decay + no-decay launch per step: the second closes a step
+ends = step_ends(rows)
 if skip:
     ends = ends[:-skip]
 steps = list(zip(ends[:-1], ends[1:]))[-last:]
