@@ -69,7 +69,7 @@ EARLY_NORM = True
 # update stream beside the next step's frontend forward (FusedAdamW(overlap=True))
 OPT_OVERLAP = True
 # grid cap of the overlapped update launches (FusedAdamW.overlap_blocks; 0: the whole chip)
-OPT_OVERLAP_BLOCKS = 256
+OPT_OVERLAP_BLOCKS = 128
 
 
 _STEP_STREAMS = {}

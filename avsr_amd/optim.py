@@ -62,7 +62,7 @@ class FusedAdamW:
         # grid cap of the overlapped launches: the update's grid-stride blocks live for the whole
         # launch, and at the default 4096 blocks (8 resident per CU) they hold every wave slot, so
         # the next forward's kernels (even its 5-us batch copy) wait for the update to finish
-        self.overlap_blocks = 256
+        self.overlap_blocks = 128
         arena.init_optimizer()
         self.lr, self.betas, self.eps, self.wd, self.max_norm = lr, betas, eps, weight_decay, max_grad_norm
         self.schedule = schedule

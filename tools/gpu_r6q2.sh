@@ -1,5 +1,9 @@
-# overlapped update grid cap, second sweep. Usage: gpurun -- bash tools/gpu_r6q2.sh TAG
+# overlapped update grid cap and side-stream column-sum row blocks: engine tests, then in-step A/B.
+# Usage: gpurun -- bash tools/gpu_r6q2.sh TAG
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-REPS="1 2" bash tools/gpu_abx.sh ${1:-r6q2}/ab "base|-" "base|OPT_OVERLAP_BLOCKS=128" "base|OPT_OVERLAP_BLOCKS=192" "base|OPT_OVERLAP_BLOCKS=384"
+O=gpurun_out/${1:-r6q2}; mkdir -p $O
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_opt_overlap.py > $O/tests.log 2>&1 || { echo tests failed; tail -40 $O/tests.log; exit 1; }
+tail -2 $O/tests.log
+REPS="1 2" bash tools/gpu_abx.sh ${1:-r6q2}/ab "base|-" "base|OPT_OVERLAP_BLOCKS=64" "base|OPT_OVERLAP_BLOCKS=256"
