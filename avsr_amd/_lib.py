@@ -158,7 +158,7 @@ class AdamWParams(ctypes.Structure):
         ("n", _i64), ("param", _c_p), ("grad", _c_p), ("exp_avg", _c_p), ("exp_avg_sq", _c_p),
         ("shadow", _c_p), ("shadow_dtype", _i), ("lr", _f), ("beta1", _f), ("beta2", _f), ("eps", _f),
         ("weight_decay", _f), ("bias_corr1", _f), ("bias_corr2", _f), ("sumsq", _c_p), ("max_norm", _f),
-        ("grad_scale", _f), ("max_blocks", _i),
+        ("grad_scale", _f), ("max_blocks", _i), ("grad_clear", _c_p),
     ]
 
 

@@ -116,6 +116,7 @@ class Arena:
         self.ld_ranges = None
         self.ld_touched = set()
         self.update_event = None     # an overlapped optimizer update in flight (wait_update)
+        self.grads_cleared = False   # that update also zeroed the gradients (Engine.zero_grad_async)
         self.attach_grads(zero=False)
         self.sync_shadow()
 

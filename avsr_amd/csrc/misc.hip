@@ -399,6 +399,7 @@ __global__ __launch_bounds__(256) void adamw_kernel(avsr_adamw_params p, int hea
       const float w = adam_elem(p, c, p.grad[i], p.param[i], m, v);
       p.exp_avg[i] = m; p.exp_avg_sq[i] = v; p.param[i] = w;
       if (p.shadow) ((S*)p.shadow)[i] = from_f<S>(w);
+      if (p.grad_clear) p.grad_clear[i] = 0.f;
     }
   }
   float* P = p.param + head; const float* G = p.grad + head;
@@ -413,6 +414,7 @@ __global__ __launch_bounds__(256) void adamw_kernel(avsr_adamw_params p, int hea
       m[j] = mj; v[j] = vj;
     }
     *(f32x4*)(P + 4 * q) = w; *(f32x4*)(M + 4 * q) = m; *(f32x4*)(V + 4 * q) = v;
+    if (p.grad_clear) *(f32x4*)(p.grad_clear + head + 4 * q) = f32x4{0.f, 0.f, 0.f, 0.f};
     if (p.shadow) {
       S* sh = (S*)p.shadow + head + 4 * q;
       if constexpr (sizeof(S) == 2) {
@@ -690,6 +692,7 @@ extern "C" int avsr_adamw(const avsr_adamw_params* p, void* stream) {
   const size_t ssz = p->shadow_dtype == AVSR_F32 ? 4 : 2;
   if (p->shadow && (((uintptr_t)p->shadow + head * ssz) & (4 * ssz - 1))) return AVSR_E_ALIGN;
   if (p->max_blocks < 0) return AVSR_E_ARG;
+  if (p->grad_clear && p->grad_clear != p->grad) return AVSR_E_ARG;
   const int g = avsr_grid(nv > 0 ? nv : 1, 256, p->max_blocks > 0 && p->max_blocks < 4096 ? p->max_blocks : 4096);
   if (p->shadow_dtype == AVSR_F32) hipLaunchKernelGGL(adamw_kernel<float>, dim3(g), dim3(256), 0, (hipStream_t)stream, *p, head, nv);
   else hipLaunchKernelGGL(adamw_kernel<bf16>, dim3(g), dim3(256), 0, (hipStream_t)stream, *p, head, nv);

@@ -70,6 +70,8 @@ EARLY_NORM = True
 OPT_OVERLAP = True
 # grid cap of the overlapped update launches (FusedAdamW.overlap_blocks; 0: the whole chip)
 OPT_OVERLAP_BLOCKS = 128
+# ... and those launches zero the gradients they read (the next step's gradient clear)
+OPT_CLEAR_IN_UPDATE = True
 
 
 _STEP_STREAMS = {}
@@ -368,10 +370,13 @@ class Engine:
             return
         g = self.arena.grad
         arena = self.arena
+        done = arena.grads_cleared      # the overlapped update zeroes what it reads
+        arena.grads_cleared = False
 
         def clear():
             arena.wait_update()         # an overlapped optimizer update still reads the gradients
-            g.zero_()
+            if not done:
+                g.zero_()
         self._on_side(clear, g)
         self.arena.attach_grads(zero=False)
         self.arena.ld_touched.clear()

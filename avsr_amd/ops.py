@@ -852,13 +852,14 @@ def sumsq(x, out, ws=None):
 
 
 def adamw(param, grad, exp_avg, exp_avg_sq, *, lr, beta1, beta2, eps, weight_decay, step, shadow=None,
-          sumsq_buf=None, max_norm=1.0, grad_scale=1.0, max_blocks=0):
+          sumsq_buf=None, max_norm=1.0, grad_scale=1.0, max_blocks=0, clear_grad=False):
     _call("avsr_adamw", L.fill(L.AdamWParams, n=param.numel(), param=param, grad=grad, exp_avg=exp_avg,
                                 exp_avg_sq=exp_avg_sq, shadow=shadow,
                                 shadow_dtype=L.AVSR_BF16 if shadow is None else dtype_code(shadow),
                                 lr=lr, beta1=beta1, beta2=beta2, eps=eps, weight_decay=weight_decay,
                                 bias_corr1=1 - beta1 ** step, bias_corr2=1 - beta2 ** step,
-                                sumsq=sumsq_buf, max_norm=max_norm, grad_scale=grad_scale, max_blocks=max_blocks))
+                                sumsq=sumsq_buf, max_norm=max_norm, grad_scale=grad_scale, max_blocks=max_blocks,
+                                grad_clear=grad if clear_grad else None))
 
 
 # ---------------------------------------------------------------------------------------

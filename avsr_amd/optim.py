@@ -42,7 +42,9 @@ class FusedAdamW:
 
     overlap=True: the update of the parameters the next training forward reads first (the audio
     and video frontends: FRONT) runs on the current stream, the rest (encoder, decoder, CTC:
-    ~97 % of the arena) on an update stream that waits for the current one. The engine's next
+    ~97 % of the arena) on an update stream that waits for the current one, on a capped grid
+    (overlap_blocks); each launch also zeroes the gradients it has read (the next step's
+    gradient clear, arena.grads_cleared). The engine's next
     training forward runs the frontends (the ResNet forward, several ms of single-stream work)
     beside it and waits for the update (arena.update_event) before the first encoder parameter
     is read; the gradient clear waits for it too. The update is elementwise, so results equal the
@@ -63,6 +65,7 @@ class FusedAdamW:
         # launch, and at the default 4096 blocks (8 resident per CU) they hold every wave slot, so
         # the next forward's kernels (even its 5-us batch copy) wait for the update to finish
         self.overlap_blocks = 128
+        self.clear_in_update = True      # overlapped launches zero the gradients they read
         arena.init_optimizer()
         self.lr, self.betas, self.eps, self.wd, self.max_norm = lr, betas, eps, weight_decay, max_grad_norm
         self.schedule = schedule
@@ -128,7 +131,7 @@ class FusedAdamW:
                       beta2=self.betas[1], eps=self.eps, weight_decay=wd, step=step,
                       shadow=None if a.shadow is None else a.shadow[s:e],
                       sumsq_buf=self._sumsq if self.max_norm else None, max_norm=self.max_norm or 1.0,
-                      grad_scale=grad_scale, max_blocks=max_blocks)
+                      grad_scale=grad_scale, max_blocks=max_blocks, clear_grad=self.overlap and self.clear_in_update)
 
         if a.ld_ranges is not None:
             if self.layer_steps is None:
@@ -157,6 +160,9 @@ class FusedAdamW:
                             launch(ps, pe, wd, step, self.overlap_blocks)
                 self._uevent.record(us)
             a.update_event = self._uevent
+            # every gradient the update read is zero again (the ranges it skips — LayerDrop layers no
+            # backward touched — were never written): the next gradient clear has nothing to do
+            a.grads_cleared = self.clear_in_update
         self._early = False          # the early partial belongs to this step's gradients only
         if zero_grad:
             a.zero_grad()

@@ -404,6 +404,7 @@ def gpu_bench(args):
     from avsr_amd import engine as _engine
     opt = FusedAdamW(arena, lr=1e-4, weight_decay=0.005, max_grad_norm=1.0, overlap=_engine.OPT_OVERLAP)
     opt.overlap_blocks = _engine.OPT_OVERLAP_BLOCKS
+    opt.clear_in_update = _engine.OPT_CLEAR_IN_UPDATE
     if world == 1 and _engine.EARLY_NORM:   # gradient norm of all but the ResNet beside the ResNet backward
         eng.pre_video_grads = opt.early_sumsq
 

@@ -580,6 +580,9 @@ typedef struct {
                                             beside other work on another stream takes fewer, so its
                                             grid-stride blocks leave CU slots to that work; the
                                             result does not depend on it */
+  float* grad_clear;                     /* NULL, or = grad: each gradient element is set to 0 after the
+                                            update has read it (the next step's gradient clear done
+                                            by the update, e.g. while it overlaps the next forward) */
 } avsr_adamw_params;
 int avsr_adamw(const avsr_adamw_params* p, void* stream);
 

@@ -280,6 +280,16 @@ def test_adamw_grid_cap_bit_identical(dev):
     for other in out[1:]:
         for a, b in zip(out[0], other):
             assert torch.equal(a, b)
+    # avsr_adamw_params.grad_clear: the same update, and every gradient element it read is 0 after
+    p, gr, m, v = (t.to(dev) for t in base)
+    sh = torch.zeros(n, device=dev, dtype=torch.bfloat16)
+    ss = torch.zeros(1, device=dev)
+    ops.sumsq(gr, ss)
+    ops.adamw(p[1:], gr[1:], m[1:], v[1:], lr=1e-3, beta1=0.9, beta2=0.999, eps=1e-8, weight_decay=0.01,
+              step=3, shadow=sh[1:], sumsq_buf=ss, max_norm=1.0, max_blocks=128, clear_grad=True)
+    for a, b in zip(out[0], (p.cpu(), m.cpu(), v.cpu(), sh.cpu())):
+        assert torch.equal(a, b)
+    assert gr[1:].abs().max().item() == 0.0 and gr[0].item() == base[1][0].item()
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])

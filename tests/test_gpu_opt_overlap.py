@@ -42,6 +42,8 @@ def _run(overlap, extra, steps=3):
     opt.sync()
     torch.cuda.synchronize()
     ar = eng.arena
+    if overlap:       # the overlapped update zeroed every gradient it read (the next step's clear)
+        assert ar.grads_cleared and ar.grad.abs().max().item() == 0.0
     return ([x.cpu() for x in losses], ar.data.cpu(), ar.shadow.cpu(), ar.exp_avg.cpu(), ar.exp_avg_sq.cpu(),
             opt.layer_steps)
 

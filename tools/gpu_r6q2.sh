@@ -4,6 +4,6 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 O=gpurun_out/${1:-r6q2}; mkdir -p $O
-timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_opt_overlap.py > $O/tests.log 2>&1 || { echo tests failed; tail -40 $O/tests.log; exit 1; }
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_opt_overlap.py tests/test_gpu_loss_misc.py tests/test_gpu_cfgvar.py > $O/tests.log 2>&1 || { echo tests failed; tail -40 $O/tests.log; exit 1; }
 tail -2 $O/tests.log
-REPS="1 2" bash tools/gpu_abx.sh ${1:-r6q2}/ab "base|-" "base|OPT_OVERLAP_BLOCKS=64" "base|OPT_OVERLAP_BLOCKS=256"
+REPS="1 2" bash tools/gpu_abx.sh ${1:-r6q2}/ab "base|-" "base|OPT_CLEAR_IN_UPDATE=0"
