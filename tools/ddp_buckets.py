@@ -20,7 +20,7 @@ import sys
 
 lay = json.load(open(sys.argv[1]))
 
-def step_ends(rows, gap_ns=5_000_000):
+def step_ends(rows, gap_ns=15_000_000):
     """row indices closing each training step: the last optimizer (adamw_kernel) launch of each
     cluster of launches that start within gap_ns of the previous one (2 per step serial, 4 with
     the overlapped update: front segments on the step stream, the rest on the update stream)"""
