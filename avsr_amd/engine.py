@@ -47,6 +47,12 @@ _SIDE_BIAS = True
 # 68.1 vs 66.7 + 30.2 us isolated, but 0.4-0.6 % slower in the step (its 256 long 128-KiB blocks
 # hold every CU while the data-gradient chain waits; profiles/r06_wgrad_group_ab.txt): off
 WGRAD_GROUP = False
+# position of the encoder out-proj weight-gradient in its layer's side-stream batch: "first"
+# (ahead of the FFN weight-gradients: its 8-wave blocks then run beside the next layer's FFN
+# data-gradients instead of holding the CUs the whole-CU dQ kernel waits for) measured +0.3 % over
+# "mid" (where its operand becomes ready) in 5 interleaved pairs, "last" -0.7 %
+# (profiles/r06_side_order_ab.txt)
+SIDE_OUT_POS = "first"
 # encoder self-attention dropout from stored keep masks (avsr_attn_dropmask, generated for every
 # layer on the side stream while the step stream runs the frontends) instead of a hash per score
 # element in the forward, dK/dV and dQ kernels (same bits)
@@ -927,7 +933,14 @@ class Engine:
         dx1 = self._ln_bwd(dln2, lc["x1"], p + "final_layer_norm", lc["m2"], lc["r2"], dres=dx2, dx=dx2,
                            ew=(go, lc["p_h"], lc["sd_o"], a + "out_proj.bias"))
         if not WGRAD_GROUP:
+            n0 = len(self._side_defer) if self._side_defer is not None else None
             self._wgrad(go, lc["o"], self.g(a + "out_proj.weight"))
+            if n0 is not None and SIDE_OUT_POS != "mid" and len(self._side_defer) == n0 + 1:
+                item = self._side_defer.pop()
+                if SIDE_OUT_POS == "first":
+                    self._side_defer.insert(0, item)
+                else:
+                    self._out_last = item
         do = ops.linear_dgrad(go, self.w(a + "out_proj.weight"))
         # attention
         qkv = lc["qkv"]
@@ -951,6 +964,9 @@ class Engine:
             self._on_side(lambda: ops.wgrad_group([(dqkv, ln1, dwq, 1.0), (go, o, dwo, 1.0)]), dqkv, ln1, go, o)
         else:
             self._wgrad(dqkv, lc["ln1"], self.arena.span(names_w, buf="g"))
+        if getattr(self, "_out_last", None) is not None:      # SIDE_OUT_POS "last"
+            self._side_defer.append(self._out_last)
+            self._out_last = None
         dln1 = ops.linear_dgrad(dqkv, self.arena.span(names_w))
         ew = self._ew_next(lc_prev["i"], lc_prev, M) if lc_prev is not None else None
         dx = self._ln_bwd(dln1, lc["x"], p + "layer_norm", lc["m1"], lc["r1"], dres=dx1, dx=dx1, ew=ew)
