@@ -47,12 +47,13 @@ _SIDE_BIAS = True
 # 68.1 vs 66.7 + 30.2 us isolated, but 0.4-0.6 % slower in the step (its 256 long 128-KiB blocks
 # hold every CU while the data-gradient chain waits; profiles/r06_wgrad_group_ab.txt): off
 WGRAD_GROUP = False
-# position of the encoder out-proj weight-gradient in its layer's side-stream batch: "first"
-# (ahead of the FFN weight-gradients: its 8-wave blocks then run beside the next layer's FFN
-# data-gradients instead of holding the CUs the whole-CU dQ kernel waits for) measured +0.3 % over
-# "mid" (where its operand becomes ready) in 5 interleaved pairs, "last" -0.7 %
-# (profiles/r06_side_order_ab.txt)
-SIDE_OUT_POS = "first"
+# order of an encoder layer's side-stream batch (f2 / f1: FFN output / input weight-gradients,
+# o: out-proj weight-gradient, c: q/k/v bias column sums, q: QKV weight-gradient). The batch of
+# layer i runs beside layer i-1's data-gradient chain. "o,f2,f1,c,q" (the out-proj weight-gradient
+# ahead of the FFN ones, its 8-wave blocks then beside the next layer's FFN data-gradients rather
+# than the whole-CU dQ kernel) measured +0.3 % over the issue order "f2,f1,o,c,q"; o second
+# -1.7 %, o last -0.7 % (profiles/r06_side_order_ab.txt). Results do not depend on it.
+SIDE_ORDER = "o,f2,f1,c,q"
 # encoder self-attention dropout from stored keep masks (avsr_attn_dropmask, generated for every
 # layer on the side stream while the step stream runs the frontends) instead of a hash per score
 # element in the forward, dK/dV and dQ kernels (same bits)
@@ -922,25 +923,28 @@ class Engine:
         if g2 is None:
             g2 = self._e(M, D)
             ops.ew_bwd(dx2, out=g2, drop_p=lc["p_h"], seed=lc["sd_f"], db=self.g(ff + "output_dense.bias"))
+        # side-stream items of this layer, tagged as issued (reordered by SIDE_ORDER at the end)
+        base = len(self._side_defer) if self._side_defer is not None else None
+        tags = [] if base is not None else None
+
+        def tag(t):
+            if tags is not None and len(self._side_defer) == base + len(tags) + 1:
+                tags.append(t)
         self._wgrad(g2, lc["act"], self.g(ff + "output_dense.weight"))
+        tag("f2")
         dh = ops.linear_dgrad(g2, self.w(ff + "output_dense.weight"), gate=lc["h"], act=GELU, drop_p=lc["p_a"],
                               seed=lc["sd_a"], db=self._fused_db(ff + "intermediate_dense.bias"))
         self._bias_grad(dh, self.g(ff + "intermediate_dense.bias"), fused=True)
         self._wgrad(dh, lc["ln2"], self.g(ff + "intermediate_dense.weight"))
+        tag("f1")
         dln2 = ops.linear_dgrad(dh, self.w(ff + "intermediate_dense.weight"))
         # x1 = x + drop(o Wo^T + bo): the out-proj dropout backward rides on this LN backward
         go = self._e(M, D)              # fresh: g2 may still be read by the side stream
         dx1 = self._ln_bwd(dln2, lc["x1"], p + "final_layer_norm", lc["m2"], lc["r2"], dres=dx2, dx=dx2,
                            ew=(go, lc["p_h"], lc["sd_o"], a + "out_proj.bias"))
         if not WGRAD_GROUP:
-            n0 = len(self._side_defer) if self._side_defer is not None else None
             self._wgrad(go, lc["o"], self.g(a + "out_proj.weight"))
-            if n0 is not None and SIDE_OUT_POS != "mid" and len(self._side_defer) == n0 + 1:
-                item = self._side_defer.pop()
-                if SIDE_OUT_POS == "first":
-                    self._side_defer.insert(0, item)
-                else:
-                    self._out_last = item
+            tag("o")
         do = ops.linear_dgrad(go, self.w(a + "out_proj.weight"))
         # attention
         qkv = lc["qkv"]
@@ -957,6 +961,7 @@ class Engine:
             ops.cast(dq32, dqkv[:, :D])
         # the q/k/v bias gradients (column sums of dqkv) on the side stream
         self._bias_grad_side(dqkv, db_qkv)
+        tag("c")
         if WGRAD_GROUP:     # QKV (192 tiles) and out-proj (64 tiles) weight-gradients in one launch
             dwq, dwo = self.arena.span(names_w, buf="g"), self.g(a + "out_proj.weight")
             o = lc["o"]
@@ -964,9 +969,14 @@ class Engine:
             self._on_side(lambda: ops.wgrad_group([(dqkv, ln1, dwq, 1.0), (go, o, dwo, 1.0)]), dqkv, ln1, go, o)
         else:
             self._wgrad(dqkv, lc["ln1"], self.arena.span(names_w, buf="g"))
-        if getattr(self, "_out_last", None) is not None:      # SIDE_OUT_POS "last"
-            self._side_defer.append(self._out_last)
-            self._out_last = None
+        tag("q")
+        if tags is not None and SIDE_ORDER:
+            items = self._side_defer[base:]
+            if len(tags) == len(items):
+                by = dict(zip(tags, items))
+                order = [t for t in SIDE_ORDER.replace(".", ",").split(",") if t in by]
+                order += [t for t in tags if t not in order]
+                self._side_defer[base:] = [by[t] for t in order]
         dln1 = ops.linear_dgrad(dqkv, self.arena.span(names_w))
         ew = self._ew_next(lc_prev["i"], lc_prev, M) if lc_prev is not None else None
         dx = self._ln_bwd(dln1, lc["x"], p + "layer_norm", lc["m1"], lc["r1"], dres=dx1, dx=dx1, ew=ew)
